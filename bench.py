@@ -1,0 +1,196 @@
+#!/usr/bin/env python
+"""bench.py — the hot-path benchmark the driver runs (one JSON line on rank 0).
+
+Workload (BASELINE.json metric "Mpoints/s neighbor-search + sparse-conv fwd";
+config 1 shape): every GPU holds `--scenes` independent scenes of 65,536
+U[0,1)^3 fp32 points (seed = rank*100003 + scene) batched through row splits,
+r = 0.05, L2, int32 indices.  One step = the full Open3D
+`layers.FixedRadiusSearch` forward on that batch: spatial hash build + count +
+scan + host read of the total + fill.  Inputs are resident in HBM before the
+timed region.  value = queries processed by all ranks / wall time (Mpoints/s).
+
+Multi-GPU: one process per GPU (torchrun), scenes are independent, so there is
+no data-path collective ("scaling": "weak"); the only collectives are the
+timing barrier and the max-over-ranks of the elapsed time.
+
+roofline: the dominant kernel (frs fill) timed with events on the stream the
+library launches on; achieved = SURVEY §8d algorithmic bytes
+(12+12+4+8+4m per query) x queries / kernel time.  traffic: HBM bytes per launch
+from the committed rocprofv3 PMC summary (profiles/), if present.
+cpu_baseline: the C oracle (oracle/, OpenMP) on a bounded sample, rank 0, N=1.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "open3d-ml_amd"), os.path.join(ROOT, "oracle")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+N_POINTS = 65536
+RADIUS = 0.05
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scenes", type=int, default=64, help="C1-shaped scenes per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-reps", type=int, default=20)
+    return ap.parse_args()
+
+
+def make_batch(rank, scenes, dev):
+    pts = np.concatenate([
+        np.random.default_rng(rank * 100003 + s).random((N_POINTS, 3), dtype=np.float32)
+        for s in range(scenes)])
+    rs = np.arange(scenes + 1, dtype=np.int64) * N_POINTS
+    return torch.from_numpy(pts).to(dev), torch.from_numpy(rs)
+
+
+def time_fill_kernel(pts, rs, reps):
+    """Average duration of one o3dml_fixed_radius_search_fill launch (HIP events
+    on the library's stream = torch's current stream)."""
+    from o3dml_amd import _lib, ops
+    from o3dml_amd._util import ptr, stream_handle, workspace
+    dev = pts.device
+    lib = _lib.load()
+    n = pts.shape[0]
+    ht = ops.build_spatial_hash_table(pts, RADIUS, rs)
+    prs_d = rs.to(dev)
+    hts_d = ht.hash_table_splits.to(dev)
+    B = rs.numel() - 1
+    st = stream_handle(dev)
+    out_rs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ws = workspace(lib.o3dml_fixed_radius_search_workspace_size(n, n), dev)
+    common = (ptr(pts), n, ptr(pts), n, RADIUS, B, ptr(prs_d), ptr(prs_d), ptr(hts_d), ptr(ht.hash_table_index),
+              ptr(ht.hash_table_cell_splits), ptr(ht.hash_table_index), 1, 0)
+    _lib.call("o3dml_fixed_radius_search_count", *common, ptr(out_rs), ptr(ws), ws.numel(), st)
+    total = int(out_rs[-1].item())
+    idx = torch.empty(total, dtype=torch.int32, device=dev)
+    fill = lambda: _lib.call("o3dml_fixed_radius_search_fill", *common, ptr(out_rs), 32, ptr(idx), None,  # noqa
+                             ptr(ws), ws.numel(), st)
+    fill()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fill()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    mean_nbrs = total / n
+    alg_bytes = n * (12 + 12 + 4 + 8 + 4 * mean_nbrs)
+    return ms, alg_bytes, mean_nbrs
+
+
+def load_traffic():
+    path = os.path.join(ROOT, "profiles", "pmc_frs_fill.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline():
+    import oracle as O
+    threads = O.default_threads()
+    pts = np.random.default_rng(0).random((N_POINTS, 3), dtype=np.float32)
+    O.fixed_radius_search(pts, pts, RADIUS, nthreads=threads)  # warm (builds the oracle if needed)
+    times = []
+    for _ in range(3):
+        t = time.perf_counter()
+        O.fixed_radius_search(pts, pts, RADIUS, nthreads=threads)
+        times.append(time.perf_counter() - t)
+    return {"value": round(N_POINTS / float(np.median(times)) / 1e6, 4), "unit": "Mpoints/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle fixed_radius_search (hash build + count + fill), one 65,536-pt C1 scene, "
+                      f"median of 3, {threads} OpenMP threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from o3dml_amd import layers
+    pts, rs = make_batch(rank, args.scenes, dev)
+    nns = layers.FixedRadiusSearch()
+    step = lambda: nns(pts, pts, RADIUS, rs, rs)  # noqa: E731
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    pairs = int(res.neighbors_row_splits[-1].item())
+
+    out = None
+    if rank == 0:
+        queries_total = world * args.scenes * N_POINTS * args.steps
+        value = queries_total / elapsed / 1e6
+        ms, alg_bytes, mean_nbrs = time_fill_kernel(pts, rs, args.kernel_reps)
+        achieved = alg_bytes / (ms * 1e-3) / 1e9
+        out = {
+            "metric": "Mpoints/s neighbor-search + sparse-conv fwd; RandLA-Net frames/s",
+            "value": round(value, 2),
+            "unit": "Mpoints/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": "C1 fixed_radius_search: layers.FixedRadiusSearch forward (hash build + search) "
+                            f"over {args.scenes} scenes/GPU x 65,536 U[0,1)^3 pts, r=0.05, L2, int32 idx",
+                "scenes_per_gpu": args.scenes, "points_per_scene": N_POINTS, "radius": RADIUS,
+                "pairs_per_step_rank0": pairs, "parallelism": f"scene-dp{world}"},
+            "roofline": {"bound": "hbm", "kernel": "frs_kernel<L2,fill>", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic(), "kernel_ms": round(ms, 5),
+                         "alg_bytes_per_launch": int(alg_bytes), "mean_neighbors": round(mean_nbrs, 3)},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,159 @@
+// common.hpp — error plumbing, launch helpers and wave-level utilities shared
+// by every kernel family of libo3dml_amd.so (gfx950 / CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/o3dml_amd.h"
+
+#define O3DML_API extern "C" __attribute__((visibility("default")))
+
+namespace o3dml {
+
+// Thread-local last error, read back through o3dml_last_error().
+void set_error(const char* fmt, ...);
+const char* last_error();
+
+struct Error {
+    int code;
+};
+
+#define O3DML_CHECK_HIP(expr)                                                   \
+    do {                                                                        \
+        hipError_t _e = (expr);                                                 \
+        if (_e != hipSuccess) {                                                 \
+            ::o3dml::set_error("%s:%d: %s -> %s", __FILE__, __LINE__, #expr,    \
+                               hipGetErrorString(_e));                          \
+            throw ::o3dml::Error{1};                                            \
+        }                                                                       \
+    } while (0)
+
+#define O3DML_REQUIRE(cond, ...)                                                \
+    do {                                                                        \
+        if (!(cond)) {                                                          \
+            ::o3dml::set_error(__VA_ARGS__);                                    \
+            throw ::o3dml::Error{2};                                            \
+        }                                                                       \
+    } while (0)
+
+#define O3DML_LAUNCH_CHECK() O3DML_CHECK_HIP(hipGetLastError())
+
+// Wrap a C-ABI entry point body: returns 0 on success, nonzero on error.
+#define O3DML_GUARD_BEGIN try {
+#define O3DML_GUARD_END                                                         \
+    }                                                                           \
+    catch (const ::o3dml::Error& e) {                                           \
+        return e.code;                                                          \
+    }                                                                           \
+    catch (...) {                                                               \
+        ::o3dml::set_error("unknown C++ exception");                            \
+        return 3;                                                               \
+    }                                                                           \
+    return 0;
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Grid size for grid-stride streaming kernels: enough workgroups to fill the
+// 256 CUs several times over, capped (cdna_hip_programming.md Guideline 11).
+inline unsigned stream_grid(int64_t n, int block, int64_t cap = 256 * 8) {
+    int64_t g = ceil_div(n, block);
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return static_cast<unsigned>(g);
+}
+
+// Bump allocator over a caller-provided device workspace (no hipMalloc in
+// any launch function: everything stays capturable into a hipGraph).
+struct Workspace {
+    char* base;
+    size_t size;
+    size_t used = 0;
+    Workspace(void* b, size_t s) : base(static_cast<char*>(b)), size(s) {}
+    template <class T>
+    T* take(int64_t count) {
+        size_t bytes = (static_cast<size_t>(count < 0 ? 0 : count) * sizeof(T) + 255) & ~size_t(255);
+        O3DML_REQUIRE(base != nullptr || bytes == 0, "workspace is null");
+        O3DML_REQUIRE(used + bytes <= size, "workspace too small: need %zu more bytes (have %zu of %zu)",
+                      bytes, size - used, size);
+        T* p = reinterpret_cast<T*>(base + used);
+        used += bytes;
+        return p;
+    }
+};
+
+// Bytes a Workspace::take<T>(count) will consume (used by *_workspace_size).
+template <class T>
+inline size_t ws_bytes(int64_t count) {
+    return (static_cast<size_t>(count < 0 ? 0 : count) * sizeof(T) + 255) & ~size_t(255);
+}
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const int l = lane_id();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+template <class T>
+__device__ __forceinline__ T wave_inclusive_scan(T v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T t = __shfl_up(v, d, 64);
+        if (lane_id() >= d) v += t;
+    }
+    return v;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Squared L2 distance with the contraction pattern shared with the oracle:
+// fma(dz,dz, fma(dy,dy, dx*dx)), dx = p - q.
+__device__ __forceinline__ float dist_l2(float px, float py, float pz, float qx, float qy, float qz) {
+    const float dx = px - qx, dy = py - qy, dz = pz - qz;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+}
+
+enum Metric { kL1 = 0, kL2 = 1, kLinf = 2 };
+
+template <int METRIC>
+__device__ __forceinline__ float dist_metric(float px, float py, float pz, float qx, float qy, float qz) {
+    if constexpr (METRIC == kL2) {
+        return dist_l2(px, py, pz, qx, qy, qz);
+    } else {
+        const float ax = fabsf(px - qx), ay = fabsf(py - qy), az = fabsf(pz - qz);
+        if constexpr (METRIC == kL1) {
+            return (ax + ay) + az;
+        } else {
+            const float m = ax > ay ? ax : ay;
+            return m > az ? m : az;
+        }
+    }
+}
+
+// Index of the batch item containing element i (row_splits sorted, size B+1).
+__device__ __forceinline__ int batch_of(int64_t i, const int64_t* __restrict__ splits, int n_batch) {
+    int lo = 0, hi = n_batch - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (splits[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+}  // namespace o3dml

@@ -1,0 +1,263 @@
+// primitives.hpp — device-wide building blocks used by the hot-path kernels:
+//   * scan():            tiled reduce-then-scan (deterministic, in-place safe)
+//   * radix_sort_pairs(): stable LSD radix sort (8-bit digits) of u32/u64 keys
+//                         with u32 payloads; stability is what gives the
+//                         canonical "ascending point id within a bin / voxel"
+//                         order the oracle defines.
+// Header-only templates, instantiated per translation unit (no -fgpu-rdc).
+#pragma once
+
+#include "common.hpp"
+
+namespace o3dml {
+namespace prim {
+
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanBlock * kScanItems;  // 2048 elements per workgroup
+
+template <class TIn>
+__global__ void __launch_bounds__(kScanBlock) scan_tile_sums(const TIn* __restrict__ in, int64_t n,
+                                                             int64_t* __restrict__ sums) {
+    const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
+    int64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int64_t i = base + k * kScanBlock + threadIdx.x;
+        if (i < n) s += static_cast<int64_t>(in[i]);
+    }
+    s = wave_sum(s);
+    __shared__ int64_t ws[kScanBlock / 64];
+    if (lane_id() == 0) ws[wave_id()] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t = 0;
+#pragma unroll
+        for (int w = 0; w < kScanBlock / 64; ++w) t += ws[w];
+        sums[blockIdx.x] = t;
+    }
+}
+
+// Scan one tile (striped coalesced load -> LDS -> blocked per-thread scan).
+// offsets (nullable): exclusive carry-in per tile.
+template <class TIn, class TOut>
+__global__ void __launch_bounds__(kScanBlock) scan_tile_apply(const TIn* in, TOut* out, int64_t n,
+                                                              const int64_t* __restrict__ offsets,
+                                                              int inclusive) {
+    // +1 pad per 8 elements keeps the blocked LDS reads off one bank
+    __shared__ int64_t tile[kScanTile + kScanTile / 8];
+    __shared__ int64_t wsum[kScanBlock / 64];
+    const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int e = k * kScanBlock + t;
+        const int64_t i = base + e;
+        tile[e + (e >> 3)] = i < n ? static_cast<int64_t>(in[i]) : 0;
+    }
+    __syncthreads();
+    int64_t v[kScanItems];
+    int64_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+        const int e = t * kScanItems + j;
+        v[j] = tile[e + (e >> 3)];
+        acc += v[j];
+    }
+    const int64_t incl = wave_inclusive_scan(acc);
+    if (lane_id() == 63) wsum[wave_id()] = incl;
+    __syncthreads();
+    int64_t run = incl - acc + (offsets ? offsets[blockIdx.x] : 0);
+    for (int w = 0; w < wave_id(); ++w) run += wsum[w];
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+        const int e = t * kScanItems + j;
+        const int64_t x = v[j];
+        tile[e + (e >> 3)] = inclusive ? run + x : run;
+        run += x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int e = k * kScanBlock + t;
+        const int64_t i = base + e;
+        if (i < n) out[i] = static_cast<TOut>(tile[e + (e >> 3)]);
+    }
+}
+
+inline size_t scan_workspace_bytes(int64_t n) {
+    size_t b = 0;
+    int64_t tiles = ceil_div(n, kScanTile);
+    while (tiles > 1) {
+        b += ws_bytes<int64_t>(tiles);
+        tiles = ceil_div(tiles, kScanTile);
+    }
+    return b;
+}
+
+// out[i] = sum_{j<=i} in[j] (inclusive) or sum_{j<i} in[j] (exclusive).
+// in == out is allowed.
+template <class TIn, class TOut>
+void scan(const TIn* in, TOut* out, int64_t n, bool inclusive, Workspace& ws, hipStream_t st) {
+    if (n <= 0) return;
+    const int64_t tiles = ceil_div(n, kScanTile);
+    if (tiles == 1) {
+        scan_tile_apply<TIn, TOut><<<1, kScanBlock, 0, st>>>(in, out, n, nullptr, inclusive);
+        O3DML_LAUNCH_CHECK();
+        return;
+    }
+    int64_t* sums = ws.take<int64_t>(tiles);
+    scan_tile_sums<TIn><<<static_cast<unsigned>(tiles), kScanBlock, 0, st>>>(in, n, sums);
+    O3DML_LAUNCH_CHECK();
+    scan<int64_t, int64_t>(sums, sums, tiles, false, ws, st);
+    scan_tile_apply<TIn, TOut><<<static_cast<unsigned>(tiles), kScanBlock, 0, st>>>(in, out, n, sums,
+                                                                                   inclusive);
+    O3DML_LAUNCH_CHECK();
+}
+
+// ---------------------------------------------------------------------------
+// Stable LSD radix sort, 8-bit digits, 2048-key tiles.
+// ---------------------------------------------------------------------------
+constexpr int kRsBlock = 256;
+constexpr int kRsItems = 8;
+constexpr int kRsTile = kRsBlock * kRsItems;
+constexpr int kRsWaves = kRsBlock / 64;
+
+template <class K>
+__global__ void __launch_bounds__(kRsBlock) radix_hist(const K* __restrict__ keys, int64_t n, int shift,
+                                                       uint32_t* __restrict__ hist, int64_t tiles) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile;
+#pragma unroll
+    for (int k = 0; k < kRsItems; ++k) {
+        const int64_t i = base + k * kRsBlock + threadIdx.x;
+        if (i < n) atomicAdd(&h[static_cast<uint32_t>(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[static_cast<int64_t>(threadIdx.x) * tiles + blockIdx.x] = h[threadIdx.x];
+}
+
+// Stable scatter: rows of 256 keys are ranked in order; inside a row the
+// rank is (earlier waves) + (earlier lanes with the same digit), found with
+// eight 64-bit ballots per key.
+template <class K>
+__global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                          K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                          int64_t n, int shift,
+                                                          const int64_t* __restrict__ offsets,
+                                                          int64_t tiles) {
+    __shared__ uint32_t wcnt[kRsWaves][256];
+    __shared__ uint32_t running[256];
+    __shared__ int64_t goff[256];
+    const int t = threadIdx.x;
+    const int w = wave_id();
+    running[t] = 0;
+    goff[t] = offsets[static_cast<int64_t>(t) * tiles + blockIdx.x];
+#pragma unroll
+    for (int ww = 0; ww < kRsWaves; ++ww) wcnt[ww][t] = 0;
+    __syncthreads();
+    const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile;
+    const uint64_t lt = lanemask_lt();
+    for (int r = 0; r < kRsItems; ++r) {
+        const int64_t i = base + r * kRsBlock + t;
+        const bool valid = i < n;
+        const K key = valid ? kin[i] : K(0);
+        const uint32_t val = valid ? (vin ? vin[i] : static_cast<uint32_t>(i)) : 0u;
+        const uint32_t d = static_cast<uint32_t>(key >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t rank = __popcll(peers & lt);
+        if (valid && rank == 0) wcnt[w][d] = __popcll(peers);
+        __syncthreads();
+        {
+            uint32_t acc = running[t];
+#pragma unroll
+            for (int ww = 0; ww < kRsWaves; ++ww) {
+                const uint32_t c = wcnt[ww][t];
+                wcnt[ww][t] = acc;
+                acc += c;
+            }
+            running[t] = acc;
+        }
+        __syncthreads();
+        if (valid) {
+            const int64_t pos = goff[d] + wcnt[w][d] + rank;
+            kout[pos] = key;
+            vout[pos] = val;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ww = 0; ww < kRsWaves; ++ww) wcnt[ww][t] = 0;
+        __syncthreads();
+    }
+}
+
+template <class K>
+__global__ void copy_pairs(const K* __restrict__ kin, const uint32_t* __restrict__ vin, K* __restrict__ kout,
+                           uint32_t* __restrict__ vout, int64_t n) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        kout[i] = kin[i];
+        vout[i] = vin ? vin[i] : static_cast<uint32_t>(i);
+    }
+}
+
+inline int bits_needed(uint64_t max_key) {
+    int b = 0;
+    while (b < 64 && (max_key >> b) != 0) ++b;
+    return b;
+}
+
+template <class K>
+size_t radix_sort_workspace_bytes(int64_t n) {
+    const int64_t tiles = ceil_div(n > 0 ? n : 1, kRsTile);
+    return ws_bytes<K>(n) + ws_bytes<uint32_t>(n) + ws_bytes<uint32_t>(256 * tiles) +
+           ws_bytes<int64_t>(256 * tiles) + scan_workspace_bytes(256 * tiles);
+}
+
+// Sorts (keys_in, vals_in) by key bits [0, end_bit) into (keys_out, vals_out).
+// vals_in == nullptr means the payload is the element index (iota).
+// keys_in must not alias keys_out.
+template <class K>
+void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, uint32_t* vals_out,
+                      int64_t n, int end_bit, Workspace& ws, hipStream_t st) {
+    if (n <= 0) return;
+    const int passes = (end_bit + 7) / 8;
+    if (passes == 0 || n == 1) {
+        copy_pairs<K><<<stream_grid(n, 256), 256, 0, st>>>(keys_in, vals_in, keys_out, vals_out, n);
+        O3DML_LAUNCH_CHECK();
+        return;
+    }
+    const int64_t tiles = ceil_div(n, kRsTile);
+    K* ktmp = ws.take<K>(n);
+    uint32_t* vtmp = ws.take<uint32_t>(n);
+    uint32_t* hist = ws.take<uint32_t>(256 * tiles);
+    int64_t* offs = ws.take<int64_t>(256 * tiles);
+    const K* ksrc = keys_in;
+    const uint32_t* vsrc = vals_in;
+    for (int p = 0; p < passes; ++p) {
+        const bool to_out = ((passes - 1 - p) % 2) == 0;
+        K* kdst = to_out ? keys_out : ktmp;
+        uint32_t* vdst = to_out ? vals_out : vtmp;
+        const int shift = 8 * p;
+        radix_hist<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(ksrc, n, shift, hist, tiles);
+        O3DML_LAUNCH_CHECK();
+        Workspace sws = ws;  // scan scratch is transient per pass
+        scan<uint32_t, int64_t>(hist, offs, 256 * tiles, false, sws, st);
+        radix_scatter<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift,
+                                                                          offs, tiles);
+        O3DML_LAUNCH_CHECK();
+        ksrc = kdst;
+        vsrc = vdst;
+    }
+}
+
+}  // namespace prim
+}  // namespace o3dml

@@ -1,0 +1,77 @@
+"""ctypes binding of libo3dml_amd.so (the C ABI declared in include/o3dml_amd.h).
+
+The library is built in-tree by ``make -C open3d-ml_amd/csrc`` (or
+``__graft_entry__.build()``).  There is deliberately NO fallback: if the
+shared library or a ROCm GPU is missing, every op raises ``RuntimeError``.
+torch is imported first so that the HIP runtime torch ships is the one the
+library binds to (both carry the soname libamdhip64.so.7), which makes torch's
+streams and allocations valid handles inside the library.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before the HIP library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "O3DML_AMD_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libo3dml_amd.so"))
+
+_lib = None
+
+c_i64, c_i32, c_u64, c_f32, c_f64, c_p, c_sz = (
+    ctypes.c_int64, ctypes.c_int, ctypes.c_uint64, ctypes.c_float,
+    ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t)
+
+# name -> (restype, [argtypes]); must match include/o3dml_amd.h
+SIGNATURES = {
+    "o3dml_last_error": (ctypes.c_char_p, []),
+    "o3dml_version": (c_i32, []),
+    "o3dml_device_info": (c_i32, [c_i32, c_p, c_p, c_p]),
+    # nns_hash.hip
+    "o3dml_hash_table_splits": (c_i64, [c_i64, c_p, c_f64, c_i64, c_p]),
+    "o3dml_build_spatial_hash_table_workspace_size": (c_sz, [c_i64, c_i64]),
+    "o3dml_build_spatial_hash_table": (c_i32, [c_p, c_i64, c_f32, c_i64, c_p, c_p, c_i64, c_p, c_p,
+                                               c_p, c_sz, c_p]),
+    "o3dml_fixed_radius_search_workspace_size": (c_sz, [c_i64, c_i64]),
+    "o3dml_fixed_radius_search_count": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p,
+                                                c_p, c_p, c_p, c_i32, c_i32, c_p, c_p, c_sz, c_p]),
+    "o3dml_fixed_radius_search_fill": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p,
+                                               c_p, c_p, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p,
+                                               c_p, c_sz, c_p]),
+    # ragged.hip
+    "o3dml_ragged_to_dense": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p]),
+    "o3dml_reduce_subarrays_sum": (c_i32, [c_p, c_p, c_i64, c_p, c_p]),
+}
+
+
+def load():
+    """Load the library (idempotent).  Raises RuntimeError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"o3dml_amd: HIP library not found at {LIB_PATH}; build it with "
+            "`make -C open3d-ml_amd/csrc` (or __graft_entry__.build()).")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def check(status, what):
+    if status != 0:
+        msg = load().o3dml_last_error().decode(errors="replace")
+        raise RuntimeError(f"o3dml_amd.{what} failed: {msg}")
+
+
+def call(name, *args):
+    """Call a status-returning entry point and raise on failure."""
+    check(getattr(load(), name)(*args), name)

@@ -1,0 +1,101 @@
+"""Host-side plumbing shared by the op wrappers: device placement, streams,
+workspaces and row-split handling.  PyTorch is used only for device memory and
+streams; every computation runs in libo3dml_amd.so."""
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            "o3dml_amd: no ROCm GPU is visible. This build has no CPU fallback "
+            "(the CPU restatement in oracle/ is test infrastructure only).")
+
+
+def gpu_device(*tensors):
+    """The GPU the op runs on: that of the first CUDA input, else the current one."""
+    for t in tensors:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            return t.device
+    require_gpu()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_handle(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def to_dev(t, device, dtype=None):
+    """Contiguous copy (or view) of t on device with dtype."""
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(np.asarray(t))
+    if dtype is not None and t.dtype != dtype:
+        t = t.to(dtype)
+    return t.to(device, non_blocking=False).contiguous()
+
+
+def workspace(nbytes, device):
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def row_splits_host(rs, n):
+    """int64 numpy row splits; None means one batch item [0, n]."""
+    if rs is None:
+        return np.array([0, n], np.int64)
+    if isinstance(rs, torch.Tensor):
+        rs = rs.detach().cpu().numpy()
+    rs = np.ascontiguousarray(np.asarray(rs, dtype=np.int64))
+    if rs.ndim != 1 or len(rs) < 2:
+        raise RuntimeError("row_splits must be a 1-D tensor with at least 2 entries")
+    if rs[0] != 0 or rs[-1] != n or np.any(np.diff(rs) < 0):
+        raise RuntimeError(
+            f"row_splits must start at 0, end at {n} and be non-decreasing (got {rs[0]}..{rs[-1]})")
+    return rs
+
+
+def scalar(x):
+    if isinstance(x, torch.Tensor):
+        return float(x.detach().cpu().reshape(-1)[0])
+    return float(x)
+
+
+def back_to(t, like):
+    """Return t on the device of `like` (ops given CPU tensors return CPU tensors)."""
+    if isinstance(like, torch.Tensor) and not like.is_cuda:
+        return t.cpu()
+    return t
+
+
+def check_points(name, t, dims=3):
+    if t.dim() != 2 or t.shape[1] != dims:
+        raise RuntimeError(f"{name} must have shape [N, {dims}], got {list(t.shape)}")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32, got {t.dtype}")
+
+
+INDEX_DTYPES = {torch.int32: 32, torch.int64: 64, 3: 32, 4: 64, "int32": 32, "int64": 64}
+
+
+def index_bits(index_dtype):
+    if index_dtype in INDEX_DTYPES:
+        return INDEX_DTYPES[index_dtype]
+    raise RuntimeError(f"index_dtype must be torch.int32 or torch.int64, got {index_dtype}")
+
+
+METRICS = {"L1": 0, "L2": 1, "Linf": 2}
+
+
+def metric_code(metric):
+    if metric not in METRICS:
+        raise RuntimeError(f"metric must be one of {list(METRICS)}, got {metric!r}")
+    return METRICS[metric]
+
+
+__all__ = ["require_gpu", "gpu_device", "stream_handle", "ptr", "to_dev", "workspace",
+           "row_splits_host", "scalar", "back_to", "check_points", "index_bits", "metric_code", "_lib"]

@@ -1,0 +1,739 @@
+/*
+ * o3d_oracle.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the Open3D-ML point-cloud hot path (the ops that
+ * /root/reference calls through `open3d.ml.torch.ops`, `open3d.ml.torch.layers`,
+ * `open3d.ml.contrib` and `open3d.core.nns`).  It is the parity checker for the
+ * HIP library in open3d-ml_amd/csrc and the timed CPU baseline in bench.py.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it; the product path never does.
+ *
+ * Pinning status: the arithmetic of these ops lives in
+ * Open3D (C++/CUDA, un-vendored, version unpinned — SURVEY.md §0.2, §8c), which
+ * is absent from /root/reference and from this image.  The reference repo's
+ * own tests pin shapes only (tests/test_models.py:73,146,228).  This oracle is
+ * therefore pinned against INDEPENDENT exact oracles (scipy cKDTree neighbour
+ * sets, numpy integer voxel maths; tests/golden/make_golden.py) and against the
+ * reference's own Python call sites where they hold arithmetic (kpconv.py,
+ * sparseconvnet.py, point_pillars.py).  Against Open3D itself parity is
+ * "unpinned": the ORDER conventions below are this build's documented
+ * canonical order (DESIGN.md §Canonical order).
+ *
+ * Float conventions shared bit-for-bit with the HIP kernels:
+ *   squared L2 distance  d2 = fmaf(dz,dz, fmaf(dy,dy, dx*dx))   (dx = p - q)
+ *   (the contracted form nvcc/hipcc emit for the pointnet2 kernels; the C
+ *   library fmaf is correctly rounded, so both sides agree exactly).
+ *   This file must be compiled with -ffp-contract=off (see oracle/Makefile).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_API __attribute__((visibility("default")))
+
+enum { ORC_L1 = 0, ORC_L2 = 1, ORC_LINF = 2 };
+
+static inline float orc_dist(int metric, float px, float py, float pz, float qx,
+                             float qy, float qz) {
+    float dx = px - qx, dy = py - qy, dz = pz - qz;
+    if (metric == ORC_L2) return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+    float ax = fabsf(dx), ay = fabsf(dy), az = fabsf(dz);
+    if (metric == ORC_L1) return (ax + ay) + az;
+    float m = ax > ay ? ax : ay;
+    return m > az ? m : az;
+}
+
+static inline float orc_threshold(int metric, float r) {
+    return metric == ORC_L2 ? r * r : r;
+}
+
+static void set_threads(int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
+}
+
+/* ------------------------------------------------------------------------ */
+/* Spatial hash table (Open3D ops.build_spatial_hash_table, used by          */
+/* layers.FixedRadiusSearch; reference caller kpconv.py:2021-2023 via         */
+/* concat_batcher.py:228,257,261).                          */
+/* ------------------------------------------------------------------------ */
+
+/* Open3D SpatialHash(x,y,z) = x*73856096 ^ y*193649663 ^ z*83492791 evaluated
+ * in 32-bit int and returned as size_t (sign-extending), then % table size. */
+static inline uint64_t orc_spatial_hash(int32_t x, int32_t y, int32_t z) {
+    uint32_t h = ((uint32_t)x * 73856096u) ^ ((uint32_t)y * 193649663u) ^
+                 ((uint32_t)z * 83492791u);
+    return (uint64_t)(int64_t)(int32_t)h;
+}
+
+static inline void orc_voxel_index(float x, float y, float z, float inv,
+                                   int32_t* v) {
+    v[0] = (int32_t)floorf(x * inv);
+    v[1] = (int32_t)floorf(y * inv);
+    v[2] = (int32_t)floorf(z * inv);
+}
+
+/* Table size per batch item: min(max(trunc(factor * n_b), 1), max_size)
+ * (Open3D BuildSpatialHashTableOps).  Writes the [B+1] prefix sums and
+ * returns the total number of bins. */
+ORC_API int64_t orc_hash_table_splits(int64_t n_batch,
+                                      const int64_t* points_row_splits,
+                                      double factor, int64_t max_size,
+                                      uint32_t* hash_table_splits) {
+    hash_table_splits[0] = 0;
+    for (int64_t b = 0; b < n_batch; ++b) {
+        int64_t nb = points_row_splits[b + 1] - points_row_splits[b];
+        int64_t t = (int64_t)(factor * (double)nb);
+        if (t < 1) t = 1;
+        if (t > max_size) t = max_size;
+        hash_table_splits[b + 1] = hash_table_splits[b] + (uint32_t)t;
+    }
+    return hash_table_splits[n_batch];
+}
+
+/* Counting sort of point ids by bin; within a bin ids are ascending (the
+ * order of Open3D's CPU build when run on one thread — canonical order). */
+ORC_API void orc_build_spatial_hash_table(
+        const float* points, int64_t n, float radius, int64_t n_batch,
+        const int64_t* points_row_splits, const uint32_t* hash_table_splits,
+        uint32_t* hash_table_index, uint32_t* hash_table_cell_splits) {
+    const float voxel_size = 2.0f * radius;
+    const float inv = 1.0f / voxel_size;
+    const int64_t T = hash_table_splits[n_batch];
+    uint32_t* bin = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
+    memset(hash_table_cell_splits, 0, sizeof(uint32_t) * (size_t)(T + 1));
+    for (int64_t b = 0; b < n_batch; ++b) {
+        const uint64_t tsize = hash_table_splits[b + 1] - hash_table_splits[b];
+        const uint32_t first = hash_table_splits[b];
+        for (int64_t i = points_row_splits[b]; i < points_row_splits[b + 1]; ++i) {
+            int32_t v[3];
+            orc_voxel_index(points[3 * i], points[3 * i + 1], points[3 * i + 2], inv, v);
+            uint32_t h = first + (uint32_t)(orc_spatial_hash(v[0], v[1], v[2]) % tsize);
+            bin[i] = h;
+            hash_table_cell_splits[h + 1]++;
+        }
+    }
+    for (int64_t t = 0; t < T; ++t)
+        hash_table_cell_splits[t + 1] += hash_table_cell_splits[t];
+    uint32_t* fillp = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(T > 0 ? T : 1));
+    memcpy(fillp, hash_table_cell_splits, sizeof(uint32_t) * (size_t)T);
+    /* points outside every batch range are not hashed (Open3D loops over
+     * the row splits only) */
+    for (int64_t b = 0; b < n_batch; ++b)
+        for (int64_t i = points_row_splits[b]; i < points_row_splits[b + 1]; ++i)
+            hash_table_index[fillp[bin[i]]++] = (uint32_t)i;
+    free(fillp);
+    free(bin);
+}
+
+static int cmp_u32(const void* a, const void* b) {
+    uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return (x > y) - (x < y);
+}
+
+/* The (sorted, de-duplicated) bins a query visits: its own voxel plus the
+ * voxels of the 8 corners q + r*(±1,±1,±1) (Open3D FixedRadiusSearch CPU:
+ * std::set iteration = ascending bin). Returns the number of bins. */
+static int orc_query_bins(float qx, float qy, float qz, float radius, float inv,
+                          uint64_t tsize, uint32_t first, uint32_t* bins) {
+    int nb = 0;
+    int32_t v[3];
+    orc_voxel_index(qx, qy, qz, inv, v);
+    bins[nb++] = first + (uint32_t)(orc_spatial_hash(v[0], v[1], v[2]) % tsize);
+    for (int dz = -1; dz <= 1; dz += 2)
+        for (int dy = -1; dy <= 1; dy += 2)
+            for (int dx = -1; dx <= 1; dx += 2) {
+                float cx = qx + radius * (float)dx;
+                float cy = qy + radius * (float)dy;
+                float cz = qz + radius * (float)dz;
+                orc_voxel_index(cx, cy, cz, inv, v);
+                bins[nb++] = first + (uint32_t)(orc_spatial_hash(v[0], v[1], v[2]) % tsize);
+            }
+    qsort(bins, (size_t)nb, sizeof(uint32_t), cmp_u32);
+    int u = 0;
+    for (int i = 0; i < nb; ++i)
+        if (u == 0 || bins[i] != bins[u - 1]) bins[u++] = bins[i];
+    return u;
+}
+
+static int64_t orc_batch_of(int64_t i, int64_t n_batch, const int64_t* splits) {
+    int64_t lo = 0, hi = n_batch - 1;
+    while (lo < hi) {
+        int64_t mid = (lo + hi + 1) / 2;
+        if (splits[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+/* ops.fixed_radius_search.  phase 0: writes
+ * neighbors_row_splits[M+1] (count + exclusive scan).  phase 1: fills
+ * index (int32 or int64) and, if dist != NULL, distances (squared for L2),
+ * using the row splits from phase 0.  Neighbour order per query: bins in
+ * ascending order, ascending point id within a bin. */
+ORC_API void orc_fixed_radius_search(
+        const float* points, int64_t n_points, const float* queries,
+        int64_t n_queries, float radius, int64_t n_batch,
+        const int64_t* points_row_splits, const int64_t* queries_row_splits,
+        const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
+        const uint32_t* hash_table_cell_splits, int metric,
+        int ignore_query_point, int64_t* neighbors_row_splits, int32_t* idx32,
+        int64_t* idx64, float* dist, int nthreads, int phase) {
+    (void)n_points;
+    (void)points_row_splits;
+    const float inv = 1.0f / (2.0f * radius);
+    const float thr = orc_threshold(metric, radius);
+    set_threads(nthreads);
+    if (phase == 0) neighbors_row_splits[0] = 0;
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t q = 0; q < n_queries; ++q) {
+        int64_t b = orc_batch_of(q, n_batch, queries_row_splits);
+        if (q < queries_row_splits[b] || q >= queries_row_splits[b + 1]) {
+            if (phase == 0) neighbors_row_splits[q + 1] = 0;
+            continue;
+        }
+        uint64_t tsize = hash_table_splits[b + 1] - hash_table_splits[b];
+        uint32_t bins[9];
+        float qx = queries[3 * q], qy = queries[3 * q + 1], qz = queries[3 * q + 2];
+        int nb = orc_query_bins(qx, qy, qz, radius, inv, tsize, hash_table_splits[b], bins);
+        int64_t cnt = 0;
+        int64_t out = phase == 1 ? neighbors_row_splits[q] : 0;
+        for (int k = 0; k < nb; ++k) {
+            for (uint32_t j = hash_table_cell_splits[bins[k]];
+                 j < hash_table_cell_splits[bins[k] + 1]; ++j) {
+                uint32_t p = hash_table_index[j];
+                float px = points[3 * (size_t)p], py = points[3 * (size_t)p + 1],
+                      pz = points[3 * (size_t)p + 2];
+                if (ignore_query_point && px == qx && py == qy && pz == qz) continue;
+                float d = orc_dist(metric, px, py, pz, qx, qy, qz);
+                if (d <= thr) {
+                    if (phase == 1) {
+                        if (idx32) idx32[out] = (int32_t)p;
+                        if (idx64) idx64[out] = (int64_t)p;
+                        if (dist) dist[out] = d;
+                        ++out;
+                    }
+                    ++cnt;
+                }
+            }
+        }
+        if (phase == 0) neighbors_row_splits[q + 1] = cnt;
+    }
+    if (phase == 0)
+        for (int64_t q = 0; q < n_queries; ++q)
+            neighbors_row_splits[q + 1] += neighbors_row_splits[q];
+}
+
+/* ------------------------------------------------------------------------ */
+/* kNN (ops.knn_search / core.nns.NearestNeighborSearch.knn_search;         */
+/* dataprocessing.py:87-103 ← randlanet.py:220,224; point_transformer.py:724)*/
+/* k nearest per query within its batch item, ascending (distance, index).   */
+/* count = min(k, eligible points).  Brute force: the definition itself.     */
+/* ------------------------------------------------------------------------ */
+static inline int lex_less(float da, int64_t ia, float db, int64_t ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+ORC_API void orc_knn_search(const float* points, int64_t n_points,
+                            const float* queries, int64_t n_queries, int64_t k,
+                            int64_t n_batch, const int64_t* points_row_splits,
+                            const int64_t* queries_row_splits, int metric,
+                            int ignore_query_point, int64_t* neighbors_row_splits,
+                            int32_t* idx32, int64_t* idx64, float* dist,
+                            int nthreads, int phase) {
+    (void)n_points;
+    set_threads(nthreads);
+    if (phase == 0) neighbors_row_splits[0] = 0;
+#pragma omp parallel
+    {
+        float* bd = (float*)malloc(sizeof(float) * (size_t)(k > 0 ? k : 1));
+        int64_t* bi = (int64_t*)malloc(sizeof(int64_t) * (size_t)(k > 0 ? k : 1));
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t q = 0; q < n_queries; ++q) {
+            int64_t b = orc_batch_of(q, n_batch, queries_row_splits);
+            float qx = queries[3 * q], qy = queries[3 * q + 1], qz = queries[3 * q + 2];
+            int64_t cnt = 0;
+            for (int64_t p = points_row_splits[b]; p < points_row_splits[b + 1]; ++p) {
+                float px = points[3 * p], py = points[3 * p + 1], pz = points[3 * p + 2];
+                if (ignore_query_point && px == qx && py == qy && pz == qz) continue;
+                float d = orc_dist(metric, px, py, pz, qx, qy, qz);
+                if (cnt < k) {
+                    int64_t j = cnt++;
+                    while (j > 0 && lex_less(d, p, bd[j - 1], bi[j - 1])) {
+                        bd[j] = bd[j - 1]; bi[j] = bi[j - 1]; --j;
+                    }
+                    bd[j] = d; bi[j] = p;
+                } else if (k > 0 && lex_less(d, p, bd[k - 1], bi[k - 1])) {
+                    int64_t j = k - 1;
+                    while (j > 0 && lex_less(d, p, bd[j - 1], bi[j - 1])) {
+                        bd[j] = bd[j - 1]; bi[j] = bi[j - 1]; --j;
+                    }
+                    bd[j] = d; bi[j] = p;
+                }
+            }
+            if (phase == 0) {
+                neighbors_row_splits[q + 1] = cnt;
+            } else {
+                int64_t o = neighbors_row_splits[q];
+                for (int64_t j = 0; j < cnt; ++j) {
+                    if (idx32) idx32[o + j] = (int32_t)bi[j];
+                    if (idx64) idx64[o + j] = bi[j];
+                    if (dist) dist[o + j] = bd[j];
+                }
+            }
+        }
+        free(bd);
+        free(bi);
+    }
+    if (phase == 0)
+        for (int64_t q = 0; q < n_queries; ++q)
+            neighbors_row_splits[q + 1] += neighbors_row_splits[q];
+}
+
+/* ops.radius_search (per-query radius; Open3D ml ops API completeness,
+ * SURVEY §2.2).  Canonical order: ascending (distance, index).  If
+ * normalize_distances, distances are divided by the query radius (squared
+ * radius for L2). */
+typedef struct { float d; int64_t i; } orc_pair;
+static int cmp_pair(const void* a, const void* b) {
+    const orc_pair* x = (const orc_pair*)a;
+    const orc_pair* y = (const orc_pair*)b;
+    if (lex_less(x->d, x->i, y->d, y->i)) return -1;
+    if (lex_less(y->d, y->i, x->d, x->i)) return 1;
+    return 0;
+}
+
+ORC_API void orc_radius_search(const float* points, int64_t n_points,
+                               const float* queries, int64_t n_queries,
+                               const float* radii, int64_t n_batch,
+                               const int64_t* points_row_splits,
+                               const int64_t* queries_row_splits, int metric,
+                               int ignore_query_point, int normalize_distances,
+                               int64_t* neighbors_row_splits, int32_t* idx32,
+                               int64_t* idx64, float* dist, int nthreads, int phase) {
+    (void)n_points;
+    set_threads(nthreads);
+    if (phase == 0) neighbors_row_splits[0] = 0;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t q = 0; q < n_queries; ++q) {
+        int64_t b = orc_batch_of(q, n_batch, queries_row_splits);
+        float qx = queries[3 * q], qy = queries[3 * q + 1], qz = queries[3 * q + 2];
+        float thr = orc_threshold(metric, radii[q]);
+        int64_t nb = points_row_splits[b + 1] - points_row_splits[b];
+        orc_pair* buf = phase == 1 ? (orc_pair*)malloc(sizeof(orc_pair) * (size_t)(nb > 0 ? nb : 1)) : NULL;
+        int64_t cnt = 0;
+        for (int64_t p = points_row_splits[b]; p < points_row_splits[b + 1]; ++p) {
+            float px = points[3 * p], py = points[3 * p + 1], pz = points[3 * p + 2];
+            if (ignore_query_point && px == qx && py == qy && pz == qz) continue;
+            float d = orc_dist(metric, px, py, pz, qx, qy, qz);
+            if (d <= thr) {
+                if (buf) { buf[cnt].d = d; buf[cnt].i = p; }
+                ++cnt;
+            }
+        }
+        if (phase == 0) {
+            neighbors_row_splits[q + 1] = cnt;
+        } else {
+            qsort(buf, (size_t)cnt, sizeof(orc_pair), cmp_pair);
+            int64_t o = neighbors_row_splits[q];
+            for (int64_t j = 0; j < cnt; ++j) {
+                if (idx32) idx32[o + j] = (int32_t)buf[j].i;
+                if (idx64) idx64[o + j] = buf[j].i;
+                if (dist) dist[o + j] = normalize_distances ? buf[j].d / thr : buf[j].d;
+            }
+            free(buf);
+        }
+    }
+    if (phase == 0)
+        for (int64_t q = 0; q < n_queries; ++q)
+            neighbors_row_splits[q + 1] += neighbors_row_splits[q];
+}
+
+/* ------------------------------------------------------------------------ */
+/* Ragged helpers.                                       */
+/* ------------------------------------------------------------------------ */
+
+/* ops.reduce_subarrays_sum (sparseconvnet.py:319-324): left-to-right fp32. */
+ORC_API void orc_reduce_subarrays_sum(const float* values, const int64_t* row_splits,
+                                      int64_t n_rows, float* out) {
+    for (int64_t r = 0; r < n_rows; ++r) {
+        float s = 0.0f;
+        for (int64_t j = row_splits[r]; j < row_splits[r + 1]; ++j) s += values[j];
+        out[r] = s;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* ops.voxelize (point_pillars.py:352-357, sparseconvnet.py:293-298;         */
+/* SURVEY §8a A9).  Canonical semantics:                         */
+/*   inv = 1/vs (double), extent_d = (int32)((max_d - min_d) * inv_d)         */
+/*   coord_d = floor((p_d - min_d) * inv_d) in double                         */
+/*   valid iff 0 <= coord_d < extent_d for every d                            */
+/*   key = b*prod(extent) + sum_d coord_d * stride_d  (dim 0 fastest)         */
+/*   voxels ordered by key, points within a voxel by index; the first        */
+/*   max_voxels voxels of each batch item and the first                      */
+/*   max_points_per_voxel points of each voxel are kept.                     */
+/* phase 0 -> counts[0] = V, counts[1] = P.  phase 1 -> fills outputs.        */
+/* ------------------------------------------------------------------------ */
+typedef struct { int64_t key; int64_t idx; } orc_kv;
+static int cmp_kv(const void* a, const void* b) {
+    const orc_kv* x = (const orc_kv*)a;
+    const orc_kv* y = (const orc_kv*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return (x->idx > y->idx) - (x->idx < y->idx);
+}
+
+ORC_API void orc_voxelize(const float* points, int64_t n, int ndim, int64_t n_batch,
+                          const int64_t* row_splits, const float* voxel_size,
+                          const float* range_min, const float* range_max,
+                          int64_t max_points_per_voxel, int64_t max_voxels,
+                          int64_t* counts, int32_t* voxel_coords,
+                          int64_t* voxel_point_indices, int64_t* voxel_point_row_splits,
+                          int64_t* voxel_batch_splits, int phase) {
+    double inv[8];
+    int64_t ext[8], stride[8];
+    int64_t batch_hash = 1;
+    for (int d = 0; d < ndim; ++d) {
+        inv[d] = 1.0 / (double)voxel_size[d];
+        ext[d] = (int32_t)(((double)range_max[d] - (double)range_min[d]) * inv[d]);
+        stride[d] = batch_hash;
+        batch_hash *= ext[d];
+    }
+    orc_kv* kv = (orc_kv*)malloc(sizeof(orc_kv) * (size_t)(n > 0 ? n : 1));
+    int64_t nv = 0;
+    for (int64_t b = 0; b < n_batch; ++b) {
+        for (int64_t i = row_splits[b]; i < row_splits[b + 1]; ++i) {
+            int ok = 1;
+            int64_t key = b * batch_hash;
+            for (int d = 0; d < ndim; ++d) {
+                double c = floor(((double)points[i * ndim + d] - (double)range_min[d]) * inv[d]);
+                if (!(c >= 0.0 && c < (double)ext[d])) { ok = 0; break; }
+                key += (int64_t)c * stride[d];
+            }
+            if (ok) { kv[nv].key = key; kv[nv].idx = i; ++nv; }
+        }
+    }
+    qsort(kv, (size_t)nv, sizeof(orc_kv), cmp_kv);
+    int64_t V = 0, P = 0;
+    int64_t cur_batch = -1, vox_in_batch = 0;
+    if (phase == 1) voxel_batch_splits[0] = 0;
+    int64_t bsplit_filled = 0; /* batch splits written up to this batch */
+    for (int64_t s = 0; s < nv;) {
+        int64_t e = s;
+        while (e < nv && kv[e].key == kv[s].key) ++e;
+        int64_t b = kv[s].key / batch_hash;
+        if (b != cur_batch) { cur_batch = b; vox_in_batch = 0; }
+        if (vox_in_batch < max_voxels) {
+            int64_t take = e - s;
+            if (take > max_points_per_voxel) take = max_points_per_voxel;
+            if (phase == 1) {
+                while (bsplit_filled < b) voxel_batch_splits[++bsplit_filled] = V;
+                int64_t rem = kv[s].key - b * batch_hash;
+                for (int d = ndim - 1; d >= 0; --d) {
+                    voxel_coords[V * ndim + d] = (int32_t)(rem / stride[d]);
+                    rem -= (rem / stride[d]) * stride[d];
+                }
+                voxel_point_row_splits[V] = P;
+                for (int64_t j = 0; j < take; ++j) voxel_point_indices[P + j] = kv[s + j].idx;
+            }
+            ++V;
+            P += take;
+            ++vox_in_batch;
+        }
+        s = e;
+    }
+    if (phase == 1) {
+        voxel_point_row_splits[V] = P;
+        while (bsplit_filled < n_batch) voxel_batch_splits[++bsplit_filled] = V;
+    }
+    counts[0] = V;
+    counts[1] = P;
+    free(kv);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Grid subsampling (contrib.subsample / subsample_batch; dataprocessing.py: */
+/* 13-49 ← randlanet.py:133-139; kpconv.py:2037-2164).     */
+/* KPConv grid_subsampling arithmetic in fp32:                               */
+/*   origin = floor(min * (1/dl)) * dl                                       */
+/*   nX = (size_t)floor((max.x - origin.x)/dl) + 1 (same for nY)              */
+/*   i* = (size_t)floor((p - origin)/dl); key = iX + nX*iY + nX*nY*iZ         */
+/*   point  = (fp32 running sum in input order) * (float)(1.0/count)          */
+/*   feat   = (fp32 running sum) / (float)count                               */
+/*   label  = majority; ties -> smallest label (canonical)                    */
+/* Output order: ascending key (canonical).                                  */
+/* ------------------------------------------------------------------------ */
+typedef struct { uint64_t key; int64_t idx; } orc_ukv;
+static int cmp_ukv(const void* a, const void* b) {
+    const orc_ukv* x = (const orc_ukv*)a;
+    const orc_ukv* y = (const orc_ukv*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return (x->idx > y->idx) - (x->idx < y->idx);
+}
+static int cmp_i32(const void* a, const void* b) {
+    int32_t x = *(const int32_t*)a, y = *(const int32_t*)b;
+    return (x > y) - (x < y);
+}
+
+ORC_API int64_t orc_grid_subsample(const float* points, int64_t n, const float* feat,
+                                   int64_t fdim, const int32_t* classes, int64_t ldim,
+                                   float dl, int64_t max_p, float* out_points,
+                                   float* out_feat, int32_t* out_classes, int phase) {
+    if (n <= 0) return 0;
+    float mn[3] = {points[0], points[1], points[2]};
+    float mx[3] = {points[0], points[1], points[2]};
+    for (int64_t i = 1; i < n; ++i)
+        for (int d = 0; d < 3; ++d) {
+            float v = points[3 * i + d];
+            if (v < mn[d]) mn[d] = v;
+            if (v > mx[d]) mx[d] = v;
+        }
+    const float inv = 1.0f / dl;
+    float org[3];
+    for (int d = 0; d < 3; ++d) org[d] = floorf(mn[d] * inv) * dl;
+    uint64_t nX = (uint64_t)floorf((mx[0] - org[0]) / dl) + 1;
+    uint64_t nY = (uint64_t)floorf((mx[1] - org[1]) / dl) + 1;
+    orc_ukv* kv = (orc_ukv*)malloc(sizeof(orc_ukv) * (size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        uint64_t ix = (uint64_t)floorf((points[3 * i] - org[0]) / dl);
+        uint64_t iy = (uint64_t)floorf((points[3 * i + 1] - org[1]) / dl);
+        uint64_t iz = (uint64_t)floorf((points[3 * i + 2] - org[2]) / dl);
+        kv[i].key = ix + nX * iy + nX * nY * iz;
+        kv[i].idx = i;
+    }
+    qsort(kv, (size_t)n, sizeof(orc_ukv), cmp_ukv);
+    int64_t S = 0;
+    int32_t* lab = ldim > 0 ? (int32_t*)malloc(sizeof(int32_t) * (size_t)n) : NULL;
+    for (int64_t s = 0; s < n;) {
+        int64_t e = s;
+        while (e < n && kv[e].key == kv[s].key) ++e;
+        if (max_p > 0 && S >= max_p) break;
+        if (phase == 1) {
+            int64_t cnt = e - s;
+            float sx = 0.f, sy = 0.f, sz = 0.f;
+            for (int64_t j = s; j < e; ++j) {
+                int64_t i = kv[j].idx;
+                sx += points[3 * i]; sy += points[3 * i + 1]; sz += points[3 * i + 2];
+            }
+            float a = (float)(1.0 / (double)cnt);
+            out_points[3 * S] = sx * a;
+            out_points[3 * S + 1] = sy * a;
+            out_points[3 * S + 2] = sz * a;
+            for (int64_t c = 0; c < fdim; ++c) {
+                float f = 0.f;
+                for (int64_t j = s; j < e; ++j) f += feat[kv[j].idx * fdim + c];
+                out_feat[S * fdim + c] = f / (float)cnt;
+            }
+            for (int64_t c = 0; c < ldim; ++c) {
+                int64_t m = 0;
+                for (int64_t j = s; j < e; ++j) lab[m++] = classes[kv[j].idx * ldim + c];
+                qsort(lab, (size_t)m, sizeof(int32_t), cmp_i32);
+                int32_t best = lab[0];
+                int64_t bestc = 0;
+                for (int64_t a0 = 0; a0 < m;) {
+                    int64_t a1 = a0;
+                    while (a1 < m && lab[a1] == lab[a0]) ++a1;
+                    if (a1 - a0 > bestc) { bestc = a1 - a0; best = lab[a0]; }
+                    a0 = a1;
+                }
+                out_classes[S * ldim + c] = best;
+            }
+        }
+        ++S;
+        s = e;
+    }
+    free(lab);
+    free(kv);
+    return S;
+}
+
+/* ------------------------------------------------------------------------ */
+/* PointNet++ ops (pointnet2_utils.py:39-278).           */
+/* ------------------------------------------------------------------------ */
+
+/* furthest_point_sampling: greedy from index 0, min-dist initialised 1e10,
+ * argmax ties -> smallest index (canonical; the CUDA tree reduce is
+ * block-size dependent). */
+ORC_API void orc_furthest_point_sampling(const float* xyz, int64_t B, int64_t N,
+                                         int64_t m, int32_t* out) {
+    float* temp = (float*)malloc(sizeof(float) * (size_t)(N > 0 ? N : 1));
+    for (int64_t b = 0; b < B; ++b) {
+        const float* x = xyz + b * N * 3;
+        int32_t* o = out + b * m;
+        if (m <= 0) continue;
+        for (int64_t i = 0; i < N; ++i) temp[i] = 1e10f;
+        int64_t old = 0;
+        o[0] = 0;
+        for (int64_t j = 1; j < m; ++j) {
+            float x1 = x[old * 3], y1 = x[old * 3 + 1], z1 = x[old * 3 + 2];
+            float best = -1.f;
+            int64_t besti = 0;
+            for (int64_t k = 0; k < N; ++k) {
+                float d = orc_dist(ORC_L2, x[k * 3], x[k * 3 + 1], x[k * 3 + 2], x1, y1, z1);
+                float d2 = d < temp[k] ? d : temp[k];
+                temp[k] = d2;
+                if (d2 > best) { best = d2; besti = k; }
+            }
+            old = besti;
+            o[j] = (int32_t)old;
+        }
+    }
+    free(temp);
+}
+
+/* ball_query(xyz [B,N,3], center [B,M,3], radius, nsample) -> [B,M,nsample]:
+ * first nsample points in index order with d2 < r2 (strict), padded with
+ * the first hit, 0 when there is none. */
+ORC_API void orc_ball_query(const float* xyz, const float* center, int64_t B, int64_t N,
+                            int64_t M, float radius, int64_t nsample, int32_t* out) {
+    float r2 = radius * radius;
+    for (int64_t b = 0; b < B; ++b)
+        for (int64_t j = 0; j < M; ++j) {
+            const float* c = center + (b * M + j) * 3;
+            int32_t* o = out + (b * M + j) * nsample;
+            for (int64_t l = 0; l < nsample; ++l) o[l] = 0;
+            int64_t cnt = 0;
+            for (int64_t k = 0; k < N && cnt < nsample; ++k) {
+                const float* p = xyz + (b * N + k) * 3;
+                float d2 = orc_dist(ORC_L2, p[0], p[1], p[2], c[0], c[1], c[2]);
+                if (d2 < r2) {
+                    if (cnt == 0)
+                        for (int64_t l = 0; l < nsample; ++l) o[l] = (int32_t)k;
+                    o[cnt++] = (int32_t)k;
+                }
+            }
+        }
+}
+
+/* three_nn(unknown [B,n,3], known [B,m,3]) -> dist2 [B,n,3], idx [B,n,3]:
+ * the 3 smallest by (d2, index); missing slots: dist2 = 1e40 (inf in fp32),
+ * idx 0. */
+ORC_API void orc_three_nn(const float* unknown, const float* known, int64_t B,
+                          int64_t n, int64_t m, float* dist2, int32_t* idx) {
+    for (int64_t b = 0; b < B; ++b)
+        for (int64_t i = 0; i < n; ++i) {
+            const float* u = unknown + (b * n + i) * 3;
+            double b1 = 1e40, b2 = 1e40, b3 = 1e40;
+            int32_t i1 = 0, i2 = 0, i3 = 0;
+            for (int64_t k = 0; k < m; ++k) {
+                const float* p = known + (b * m + k) * 3;
+                float d = orc_dist(ORC_L2, p[0], p[1], p[2], u[0], u[1], u[2]);
+                if (d < b1) { b3 = b2; i3 = i2; b2 = b1; i2 = i1; b1 = d; i1 = (int32_t)k; }
+                else if (d < b2) { b3 = b2; i3 = i2; b2 = d; i2 = (int32_t)k; }
+                else if (d < b3) { b3 = d; i3 = (int32_t)k; }
+            }
+            float* dd = dist2 + (b * n + i) * 3;
+            int32_t* ii = idx + (b * n + i) * 3;
+            dd[0] = (float)b1; dd[1] = (float)b2; dd[2] = (float)b3;
+            ii[0] = i1; ii[1] = i2; ii[2] = i3;
+        }
+}
+
+/* three_interpolate(features [B,C,m], idx [B,n,3], weight [B,n,3]) -> [B,C,n]:
+ * out = fma(w2,f2, fma(w1,f1, w0*f0)). */
+ORC_API void orc_three_interpolate(const float* feat, const int32_t* idx, const float* w,
+                                   int64_t B, int64_t C, int64_t m, int64_t n, float* out) {
+    for (int64_t b = 0; b < B; ++b)
+        for (int64_t c = 0; c < C; ++c)
+            for (int64_t i = 0; i < n; ++i) {
+                const int32_t* ii = idx + (b * n + i) * 3;
+                const float* ww = w + (b * n + i) * 3;
+                const float* f = feat + (b * C + c) * m;
+                out[(b * C + c) * n + i] = fmaf(ww[2], f[ii[2]], fmaf(ww[1], f[ii[1]], ww[0] * f[ii[0]]));
+            }
+}
+
+/* three_interpolate_grad(grad_out [B,C,n], idx, weight, m) -> [B,C,m]
+ * (accumulated in double; GPU uses fp32 atomics -> tolerance test). */
+ORC_API void orc_three_interpolate_grad(const float* grad, const int32_t* idx,
+                                        const float* w, int64_t B, int64_t C, int64_t n,
+                                        int64_t m, float* out) {
+    double* acc = (double*)calloc((size_t)(B * C * m > 0 ? B * C * m : 1), sizeof(double));
+    for (int64_t b = 0; b < B; ++b)
+        for (int64_t c = 0; c < C; ++c)
+            for (int64_t i = 0; i < n; ++i) {
+                const int32_t* ii = idx + (b * n + i) * 3;
+                const float* ww = w + (b * n + i) * 3;
+                double g = grad[(b * C + c) * n + i];
+                for (int t = 0; t < 3; ++t) acc[(b * C + c) * m + ii[t]] += g * ww[t];
+            }
+    for (int64_t t = 0; t < B * C * m; ++t) out[t] = (float)acc[t];
+    free(acc);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Sparse convolution (ops.sparse_conv / layers.SparseConv; sparseconvnet.py */
+/* :344-482).  Accumulated in double.                    */
+/*   out[o] = sum_{n in rows(o)} W[kidx_n]^T (in[idx_n] * s_n) / norm_o       */
+/*   s_n = inp_importance[idx_n] (if given) * nbr_importance[n] (if given)    */
+/*   norm_o = count (or sum nbr_importance) if normalize and != 0, else 1     */
+/* filters: [K, Cin, Cout] row-major (the [k,k,k,Cin,Cout] kernel flattened). */
+/* ------------------------------------------------------------------------ */
+ORC_API void orc_sparse_conv(const float* filters, int64_t K, int64_t cin, int64_t cout,
+                             const float* inp, const float* inp_importance,
+                             const int32_t* nbr_index, const int32_t* nbr_kernel_index,
+                             const float* nbr_importance, const int64_t* row_splits,
+                             int64_t n_out, int normalize, float* out, int nthreads) {
+    set_threads(nthreads);
+    (void)K;
+#pragma omp parallel
+    {
+        double* acc = (double*)malloc(sizeof(double) * (size_t)(cout > 0 ? cout : 1));
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t o = 0; o < n_out; ++o) {
+            for (int64_t c = 0; c < cout; ++c) acc[c] = 0.0;
+            double norm = 0.0;
+            for (int64_t e = row_splits[o]; e < row_splits[o + 1]; ++e) {
+                int64_t i = nbr_index[e];
+                int64_t k = nbr_kernel_index[e];
+                double s = 1.0;
+                if (inp_importance) s *= inp_importance[i];
+                double ni = nbr_importance ? nbr_importance[e] : 1.0;
+                s *= ni;
+                norm += ni;
+                const float* w = filters + k * cin * cout;
+                const float* x = inp + i * cin;
+                for (int64_t a = 0; a < cin; ++a) {
+                    double xa = (double)x[a] * s;
+                    for (int64_t c = 0; c < cout; ++c) acc[c] += xa * (double)w[a * cout + c];
+                }
+            }
+            double div = (normalize && norm != 0.0) ? norm : 1.0;
+            for (int64_t c = 0; c < cout; ++c) out[o * cout + c] = (float)(acc[c] / div);
+        }
+        free(acc);
+    }
+}
+
+/* Rulebook for layers.SparseConv (sparseconvnet.py:344-441): kernel index of
+ * each (query q, input p) pair: per axis floor((p - q)/vs + k/2), clamped to
+ * [0,k), linearised x-fastest: (iz*k1 + iy)*k2 + ix (filter dims are
+ * [depth(z), height(y), width(x)]).  mirror=1 gives the transposed layer's
+ * index floor(k/2 - (p - q)/vs). */
+ORC_API void orc_kernel_index(const float* inp_pos, const float* query_pos,
+                              const int32_t* nbr_index, const int64_t* row_splits,
+                              int64_t n_query, const int32_t* ksize, float voxel_size,
+                              int mirror, int32_t* kidx) {
+    float inv = 1.0f / voxel_size;
+    for (int64_t q = 0; q < n_query; ++q)
+        for (int64_t e = row_splits[q]; e < row_splits[q + 1]; ++e) {
+            const float* p = inp_pos + 3 * (int64_t)nbr_index[e];
+            int32_t id[3];
+            for (int d = 0; d < 3; ++d) {
+                const int32_t kd = ksize[2 - d]; /* axis x<->dim 2, z<->dim 0 */
+                float rel = (p[d] - query_pos[3 * q + d]) * inv;
+                float h = 0.5f * (float)kd;
+                int32_t v = (int32_t)floorf(mirror ? h - rel : rel + h);
+                if (v < 0) v = 0;
+                if (v >= kd) v = kd - 1;
+                id[d] = v;
+            }
+            kidx[e] = (id[2] * ksize[1] + id[1]) * ksize[2] + id[0];
+        }
+}

@@ -1,0 +1,50 @@
+"""CPU checks of the C ABI: the library exists, loads, and exports every symbol
+include/o3dml_amd.h declares (no compute calls without a GPU)."""
+import ctypes
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "o3dml_amd.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(o3dml_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_matches_binding():
+    from o3dml_amd import _lib
+    assert sorted(_lib.exported_symbols()) == declared_symbols()
+
+
+def test_library_loads_and_exports_all():
+    from o3dml_amd import _lib
+    lib = _lib.load()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.o3dml_version() >= 1
+
+
+def test_hash_table_splits_host_helper():
+    import numpy as np
+    from o3dml_amd import _lib
+    import oracle as O
+    rs = np.array([0, 10, 10, 5000, 70000], np.int64)
+    a = np.zeros(5, np.uint32)
+    t = _lib.load().o3dml_hash_table_splits(4, rs.ctypes.data, 1 / 64, 33554432, a.ctypes.data)
+    b = np.zeros(5, np.uint32)
+    t2 = O.lib().orc_hash_table_splits(ctypes.c_int64(4), rs.ctypes.data_as(ctypes.c_void_p),
+                                       ctypes.c_double(1 / 64), ctypes.c_int64(33554432),
+                                       b.ctypes.data_as(ctypes.c_void_p))
+    assert t == t2 and np.array_equal(a, b)
+
+
+def test_ops_fail_loudly_without_gpu():
+    import pytest
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from o3dml_amd import ops
+    with pytest.raises(RuntimeError, match="no ROCm GPU"):
+        ops.fixed_radius_search(torch.zeros(4, 3), torch.zeros(4, 3), 0.1)

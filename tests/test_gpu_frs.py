@@ -1,0 +1,106 @@
+"""GPU parity: fixed-radius search + spatial hash build vs the oracle
+(bit-exact indices, row splits, hash tables; distances bit-exact too since both
+sides use the same fmaf contraction)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _cloud(n, seed=0, scale=1.0):
+    return (np.random.default_rng(seed).random((n, 3), dtype=np.float32) * scale).astype(np.float32)
+
+
+def test_hash_table_bit_exact(cuda):
+    from o3dml_amd import ops
+    pts = _cloud(20000, 1)
+    rs = np.array([0, 7000, 7000, 20000], np.int64)  # includes an empty batch item
+    ht = ops.build_spatial_hash_table(torch.from_numpy(pts).to(cuda), 0.05, torch.from_numpy(rs))
+    oi, oc, osp = O.build_spatial_hash_table(pts, 0.05, rs)
+    assert np.array_equal(ht.hash_table_splits.numpy().astype(np.uint32), osp)
+    assert np.array_equal(ht.hash_table_cell_splits.cpu().numpy().astype(np.uint32), oc)
+    assert np.array_equal(ht.hash_table_index.cpu().numpy().astype(np.uint32), oi)
+
+
+@pytest.mark.parametrize("metric", ["L2", "L1", "Linf"])
+@pytest.mark.parametrize("ignore", [False, True])
+def test_frs_self_search(cuda, metric, ignore):
+    from o3dml_amd import layers
+    pts = _cloud(16384, 0)
+    pts[100] = pts[50]  # an exact duplicate exercises ignore_query_point
+    nns = layers.FixedRadiusSearch(metric=metric, ignore_query_point=ignore, return_distances=True)
+    t = torch.from_numpy(pts).to(cuda)
+    res = nns(t, t, 0.06)
+    oi, ors, od = O.fixed_radius_search(pts, pts, 0.06, metric=metric, ignore_query_point=ignore,
+                                        return_distances=True)
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+    assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
+
+
+def test_frs_batched_queries_differ(cuda):
+    from o3dml_amd import layers
+    pts = _cloud(12000, 2, 2.0) - 0.5  # negative coordinates -> negative voxel ids
+    qry = _cloud(5000, 3, 2.0) - 0.5
+    prs = torch.LongTensor([0, 4000, 12000])
+    qrs = torch.LongTensor([0, 3000, 5000])
+    nns = layers.FixedRadiusSearch(index_dtype=torch.int64)
+    res = nns(torch.from_numpy(pts).to(cuda), torch.from_numpy(qry).to(cuda), 0.1, prs, qrs)
+    oi, ors, _ = O.fixed_radius_search(pts, qry, 0.1, prs.numpy(), qrs.numpy(), index_dtype=np.int64)
+    assert res.neighbors_index.dtype == torch.int64
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+
+
+def test_frs_c1_config(cuda):
+    """BASELINE config 1: 65,536 U[0,1)^3 points (seed 0), r = 0.05."""
+    from o3dml_amd import layers
+    pts = np.random.default_rng(0).random((65536, 3), dtype=np.float32)
+    t = torch.from_numpy(pts).to(cuda)
+    res = layers.FixedRadiusSearch()(t, t, 0.05)
+    oi, ors, _ = O.fixed_radius_search(pts, pts, 0.05)
+    assert int(ors[-1]) == int(res.neighbors_row_splits[-1])
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+
+
+def test_frs_cpu_tensors_roundtrip(cuda):
+    """The reference calls the op with CPU tensors (kpconv.py:2021); results come back on CPU."""
+    from o3dml_amd import layers
+    pts = _cloud(3000, 5)
+    res = layers.FixedRadiusSearch()(torch.from_numpy(pts), torch.from_numpy(pts), 0.08)
+    assert not res.neighbors_index.is_cuda
+    oi, ors, _ = O.fixed_radius_search(pts, pts, 0.08)
+    assert np.array_equal(res.neighbors_index.numpy(), oi)
+
+
+def test_frs_empty(cuda):
+    from o3dml_amd import layers
+    pts = torch.from_numpy(_cloud(100, 6)).to(cuda)
+    empty = torch.zeros((0, 3), dtype=torch.float32, device=cuda)
+    r1 = layers.FixedRadiusSearch()(pts, empty, 0.1)
+    assert r1.neighbors_row_splits.cpu().tolist() == [0] and r1.neighbors_index.numel() == 0
+    r2 = layers.FixedRadiusSearch()(empty, pts, 0.1)
+    assert r2.neighbors_row_splits.cpu().numpy().tolist() == [0] * 101
+
+
+def test_ragged_to_dense_and_reduce(cuda):
+    from o3dml_amd import ops
+    rng = np.random.default_rng(7)
+    lens = rng.integers(0, 9, 500)
+    rs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    vals = rng.integers(0, 1000, rs[-1]).astype(np.int32)
+    out = ops.ragged_to_dense(torch.from_numpy(vals.reshape(-1, 1)).to(cuda), torch.from_numpy(rs).to(cuda), 6,
+                              torch.tensor([-7], dtype=torch.int32))
+    ref = O.ragged_to_dense(vals.reshape(-1, 1), rs, 6, np.array([-7], np.int32))
+    assert np.array_equal(out.cpu().numpy(), ref)
+    v64 = torch.from_numpy(vals.astype(np.int64)).to(cuda)
+    out2 = ops.ragged_to_dense(v64, torch.from_numpy(rs).to(cuda), 32, torch.tensor(-1)) + 1
+    ref2 = O.ragged_to_dense(vals.astype(np.int64), rs, 32, np.int64(-1)) + 1
+    assert np.array_equal(out2.cpu().numpy(), ref2)
+    f = rng.standard_normal(rs[-1]).astype(np.float32)
+    s = ops.reduce_subarrays_sum(torch.from_numpy(f).to(cuda), torch.from_numpy(rs).to(cuda))
+    assert np.array_equal(s.cpu().numpy(), O.reduce_subarrays_sum(f, rs))
