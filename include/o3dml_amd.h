@@ -73,6 +73,79 @@ int o3dml_fixed_radius_search_fill(const float* points, int64_t n_points, const 
                                    int index_bits, void* neighbors_index, float* neighbors_distance,
                                    void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- kNN: replaces open3d.ml.torch.ops.knn_search / layers.KNNSearch
+ * (ml3d/torch/models/point_transformer.py:724-729) and
+ * open3d.core.nns.NearestNeighborSearch.knn_search
+ * (ml3d/datasets/utils/dataprocessing.py:99-101 <- randlanet.py:218-229).
+ * Per query the min(k, N_b) nearest points of its batch item, ascending
+ * (distance, index); distances squared for L2.  k <= 64: grid ring search;
+ * k > 64: per-query full sort (few queries, e.g. the patch crop).
+ * The *_host row splits are host copies (grid planning); self_search = 1
+ * when queries are the points themselves (same splits). ------------------- */
+size_t o3dml_knn_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t k, int64_t n_batch);
+int o3dml_knn_search_count(const float* points, int64_t n_points, const float* queries, int64_t n_queries, int64_t k,
+                           int64_t n_batch, const int64_t* points_row_splits, const int64_t* queries_row_splits,
+                           const int64_t* points_row_splits_host, const int64_t* queries_row_splits_host, int metric,
+                           int ignore_query_point, int self_search, int64_t* neighbors_row_splits, void* workspace,
+                           size_t workspace_bytes, void* stream);
+int o3dml_knn_search_fill(const float* points, int64_t n_points, const float* queries, int64_t n_queries, int64_t k,
+                          int64_t n_batch, const int64_t* points_row_splits_host,
+                          const int64_t* queries_row_splits_host, int metric, const int64_t* neighbors_row_splits,
+                          int index_bits, void* neighbors_index, float* neighbors_distance, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
+/* ---- voxelize: replaces open3d.ml.torch.ops.voxelize
+ * (ml3d/torch/models/point_pillars.py:352-357, sparseconvnet.py:293-298).
+ * points f32 [N, ndim] (ndim <= 8); voxel_size / range_min / range_max are
+ * HOST arrays of ndim floats.  Canonical semantics: coord_d =
+ * floor((p_d - min_d) / vs_d) in double, valid iff 0 <= coord_d < extent_d,
+ * voxels ordered by (batch, linear id with dim 0 fastest), points of a voxel
+ * by index; first max_voxels voxels per batch item, first
+ * max_points_per_voxel points per voxel.  _count writes counts_host[0] = V,
+ * counts_host[1] = P.  Outputs: voxel_coords int32 [V, ndim],
+ * voxel_point_indices int64 [P], voxel_point_row_splits int64 [V+1],
+ * voxel_batch_splits int64 [B+1]. ------------------------------------------ */
+size_t o3dml_voxelize_workspace_size(int64_t n_points, int64_t n_batch);
+int o3dml_voxelize_count(const float* points, int64_t n_points, int ndim, int64_t n_batch, const int64_t* row_splits,
+                         const float* voxel_size_host, const float* range_min_host, const float* range_max_host,
+                         int64_t max_points_per_voxel, int64_t max_voxels, int64_t* counts_host, void* workspace,
+                         size_t workspace_bytes, void* stream);
+int o3dml_voxelize_fill(int64_t n_points, int ndim, int64_t n_batch, const float* voxel_size_host,
+                        const float* range_min_host, const float* range_max_host, int64_t n_voxels,
+                        int32_t* voxel_coords, int64_t* voxel_point_indices, int64_t* voxel_point_row_splits,
+                        int64_t* voxel_batch_splits, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- grid subsampling: replaces open3d.ml.contrib.subsample / subsample_batch
+ * (ml3d/datasets/utils/dataprocessing.py:33-49 <- randlanet.py:133-139;
+ * kpconv.py:2099-2155 <- dataloaders/concat_batcher.py:245-247).  KPConv
+ * grid_subsampling fp32 arithmetic; cells in ascending key order per batch
+ * item, first max_p cells kept (max_p <= 0: all). _count writes the number of
+ * output points to *n_out_host. -------------------------------------------- */
+size_t o3dml_grid_subsample_workspace_size(int64_t n_points, int64_t n_batch);
+int o3dml_grid_subsample_count(const float* points, int64_t n_points, int64_t n_batch, const int64_t* row_splits,
+                               const int64_t* row_splits_host, float dl, int64_t max_p, int64_t* n_out_host,
+                               void* workspace, size_t workspace_bytes, void* stream);
+int o3dml_grid_subsample_fill(const float* points, int64_t n_points, int64_t n_batch, const float* features, int fdim,
+                              const int32_t* classes, int ldim, float* out_points, float* out_features,
+                              int32_t* out_classes, int64_t* out_lengths, void* workspace, size_t workspace_bytes,
+                              void* stream);
+
+/* ---- PointNet++ ops: replace open3d.ml.torch.ops.furthest_point_sampling,
+ * ball_query, three_nn, three_interpolate, three_interpolate_grad
+ * (ml3d/torch/utils/pointnet/pointnet2_utils.py:33-36, 55, 94, 129, 162, 184,
+ * 212; point_transformer.py:518). ------------------------------------------ */
+size_t o3dml_furthest_point_sampling_workspace_size(int64_t B, int64_t n);
+int o3dml_furthest_point_sampling(const float* xyz, int64_t B, int64_t n, int64_t m, int32_t* out, void* workspace,
+                                  size_t workspace_bytes, void* stream);
+int o3dml_ball_query(const float* xyz, const float* center, int64_t B, int64_t n, int64_t m, float radius,
+                     int64_t nsample, int32_t* out, void* stream);
+int o3dml_three_nn(const float* unknown, const float* known, int64_t B, int64_t n, int64_t m, float* dist2,
+                   int32_t* idx, void* stream);
+int o3dml_three_interpolate(const float* features, const int32_t* idx, const float* weight, int64_t B, int64_t C,
+                            int64_t m, int64_t n, float* out, void* stream);
+int o3dml_three_interpolate_grad(const float* grad_out, const int32_t* idx, const float* weight, int64_t B, int64_t C,
+                                 int64_t n, int64_t m, float* grad_features, void* stream);
+
 /* ---- ragged helpers ------------------------------------------------------
  * o3dml_ragged_to_dense replaces open3d.ml.torch.ops.ragged_to_dense
  * (kpconv.py:2030-2032, point_pillars.py:364-366): values [P, inner] of

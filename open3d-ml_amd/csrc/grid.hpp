@@ -1,0 +1,213 @@
+// grid.hpp — dense per-batch uniform grid over a point cloud, used by the
+// kNN / radius / ball-query kernels (not by fixed_radius_search, which must
+// use Open3D's hash-table semantics).
+//
+// Build: per-batch bounding box (one workgroup per batch item) -> host picks a
+// cell size h giving ~`target` points per cell, capped at `cap_factor*N_b+64`
+// cells -> cell key per point -> stable radix sort (key, id) -> CSR
+// cell_splits + points re-laid out as float4 (x,y,z,id) in cell order, so a
+// cell scan is one contiguous 16-B-per-point stream.
+#pragma once
+
+#include <cmath>
+#include <vector>
+
+#include "primitives.hpp"
+
+namespace o3dml {
+
+struct GridBatch {
+    float ox, oy, oz, h;   // origin, cell size
+    float inv_h;
+    int dx, dy, dz;        // cells per axis
+    uint32_t offset;       // first global cell id of this batch item
+    uint32_t pad[3];
+};
+
+// Kernels defined in this header get internal linkage (one copy per TU).
+namespace {
+
+__global__ void __launch_bounds__(256) bbox_kernel(const float* __restrict__ pts, const int64_t* __restrict__ rs,
+                                                   float* __restrict__ out /*[B][6]*/) {
+    const int b = blockIdx.x;
+    const int64_t s = rs[b], e = rs[b + 1];
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const float v = pts[3 * i + d];
+            mn[d] = fminf(mn[d], v);
+            mx[d] = fmaxf(mx[d], v);
+        }
+    }
+    __shared__ float red[6][4];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            mn[d] = fminf(mn[d], __shfl_xor(mn[d], o, 64));
+            mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o, 64));
+        }
+    }
+    if (lane_id() == 0) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            red[d][wave_id()] = mn[d];
+            red[3 + d][wave_id()] = mx[d];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int d = threadIdx.x;
+        float v = red[d][0];
+        for (int w = 1; w < (int)(blockDim.x / 64); ++w) v = d < 3 ? fminf(v, red[d][w]) : fmaxf(v, red[d][w]);
+        out[6 * b + d] = v;
+    }
+}
+
+__device__ __forceinline__ int grid_axis(float p, float o, float inv_h, int n) {
+    int c = static_cast<int>(floorf((p - o) * inv_h));
+    return c < 0 ? 0 : (c >= n ? n - 1 : c);
+}
+
+__global__ void grid_key_kernel(const float* __restrict__ pts, int64_t n, const int64_t* __restrict__ rs, int nb,
+                                const GridBatch* __restrict__ g, uint32_t* __restrict__ keys) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const GridBatch gb = g[batch_of(i, rs, nb)];
+        const int cx = grid_axis(pts[3 * i], gb.ox, gb.inv_h, gb.dx);
+        const int cy = grid_axis(pts[3 * i + 1], gb.oy, gb.inv_h, gb.dy);
+        const int cz = grid_axis(pts[3 * i + 2], gb.oz, gb.inv_h, gb.dz);
+        keys[i] = gb.offset + static_cast<uint32_t>(cx + gb.dx * (cy + gb.dy * cz));
+    }
+}
+
+// CSR splits from sorted keys: splits[c] = first position with key >= c.
+__global__ void key_boundaries_kernel(const uint32_t* __restrict__ skeys, int64_t n, int64_t n_cells,
+                                      uint32_t* __restrict__ splits) {
+    if (n == 0) {
+        for (int64_t c = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; c <= n_cells;
+             c += static_cast<int64_t>(gridDim.x) * blockDim.x)
+            splits[c] = 0;
+        return;
+    }
+    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
+         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t k = skeys[j];
+        const int64_t kp = j == 0 ? -1 : static_cast<int64_t>(skeys[j - 1]);
+        for (int64_t c = kp + 1; c <= k; ++c) splits[c] = static_cast<uint32_t>(j);
+        if (j == n - 1)
+            for (int64_t c = k + 1; c <= n_cells; ++c) splits[c] = static_cast<uint32_t>(n);
+    }
+}
+
+__global__ void gather_float4_kernel(const float* __restrict__ pts, const uint32_t* __restrict__ order, int64_t n,
+                                     float4* __restrict__ out) {
+    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
+         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t i = order[j];
+        out[j] = make_float4(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], __uint_as_float(static_cast<uint32_t>(i)));
+    }
+}
+
+}  // namespace
+
+// Host: choose per-batch grids from the bounding boxes.
+inline std::vector<GridBatch> plan_grid(const float* bbox, const int64_t* rs_host, int nb, double target,
+                                        double cap_factor, int64_t* total_cells) {
+    std::vector<GridBatch> g(nb);
+    int64_t off = 0;
+    for (int b = 0; b < nb; ++b) {
+        const int64_t n = rs_host[b + 1] - rs_host[b];
+        GridBatch& gb = g[b];
+        double ext[3];
+        double vol = 1.0, maxe = 0.0;
+        for (int d = 0; d < 3; ++d) {
+            const double lo = n > 0 ? bbox[6 * b + d] : 0.0, hi = n > 0 ? bbox[6 * b + 3 + d] : 0.0;
+            ext[d] = std::isfinite(hi - lo) ? (hi - lo) : 0.0;
+            maxe = std::max(maxe, ext[d]);
+        }
+        if (maxe <= 0.0) maxe = 1.0;
+        for (int d = 0; d < 3; ++d) vol *= std::max(ext[d], maxe * 1e-3);
+        double h = std::cbrt(vol * target / std::max<int64_t>(n, 1));
+        h = std::max(h, maxe / 1024.0);
+        const int64_t cap = static_cast<int64_t>(cap_factor * static_cast<double>(n)) + 64;
+        int64_t dims[3], cells = 1;
+        for (int it = 0; it < 64; ++it) {
+            cells = 1;
+            for (int d = 0; d < 3; ++d) {
+                dims[d] = static_cast<int64_t>(std::floor(ext[d] / h)) + 1;
+                cells *= dims[d];
+            }
+            if (cells <= cap) break;
+            h *= std::cbrt(static_cast<double>(cells) / static_cast<double>(cap)) * 1.01;
+        }
+        gb.ox = n > 0 ? bbox[6 * b] : 0.f;
+        gb.oy = n > 0 ? bbox[6 * b + 1] : 0.f;
+        gb.oz = n > 0 ? bbox[6 * b + 2] : 0.f;
+        gb.h = static_cast<float>(h);
+        gb.inv_h = static_cast<float>(1.0 / h);
+        gb.dx = static_cast<int>(dims[0]);
+        gb.dy = static_cast<int>(dims[1]);
+        gb.dz = static_cast<int>(dims[2]);
+        gb.offset = static_cast<uint32_t>(off);
+        off += cells;
+    }
+    *total_cells = off;
+    return g;
+}
+
+inline int64_t grid_cells_cap(int64_t n, int nb, double cap_factor) {
+    return static_cast<int64_t>(cap_factor * static_cast<double>(n)) + 64 * static_cast<int64_t>(nb) + 64;
+}
+
+// Device-side index produced by build_grid().
+struct GridIndex {
+    GridBatch* params;    // [nb]
+    uint32_t* splits;     // [cells+1]
+    float4* sorted;       // [n] (x,y,z,id) in cell order
+    uint32_t* order;      // [n] point ids in cell order
+    int64_t cells;
+};
+
+inline size_t grid_workspace_bytes(int64_t n, int nb, double cap_factor) {
+    return ws_bytes<GridBatch>(nb) + ws_bytes<float>(6 * nb) + ws_bytes<uint32_t>(grid_cells_cap(n, nb, cap_factor) + 1) +
+           ws_bytes<float4>(n) + 3 * ws_bytes<uint32_t>(n) + prim::radix_sort_workspace_bytes<uint32_t>(n);
+}
+
+// Builds the grid; synchronises the stream once (bounding boxes -> host).
+inline GridIndex build_grid(const float* pts, int64_t n, const int64_t* rs_dev, const int64_t* rs_host, int nb,
+                            double target, double cap_factor, Workspace& ws, hipStream_t st) {
+    GridIndex gi;
+    gi.params = ws.take<GridBatch>(nb);
+    float* bbox_d = ws.take<float>(6 * nb);
+    const int64_t cap = grid_cells_cap(n, nb, cap_factor);
+    gi.splits = ws.take<uint32_t>(cap + 1);
+    gi.sorted = ws.take<float4>(n);
+    uint32_t* keys = ws.take<uint32_t>(n);
+    uint32_t* skeys = ws.take<uint32_t>(n);
+    gi.order = ws.take<uint32_t>(n);
+    bbox_kernel<<<nb, 256, 0, st>>>(pts, rs_dev, bbox_d);
+    O3DML_LAUNCH_CHECK();
+    std::vector<float> bbox(6 * nb);
+    O3DML_CHECK_HIP(hipMemcpyAsync(bbox.data(), bbox_d, sizeof(float) * 6 * nb, hipMemcpyDeviceToHost, st));
+    O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    std::vector<GridBatch> plan = plan_grid(bbox.data(), rs_host, nb, target, cap_factor, &gi.cells);
+    O3DML_REQUIRE(gi.cells <= cap, "grid plan exceeds capacity");
+    O3DML_CHECK_HIP(hipMemcpyAsync(gi.params, plan.data(), sizeof(GridBatch) * nb, hipMemcpyHostToDevice, st));
+    // the plan lives in pageable host memory owned by this frame: wait for the copy
+    O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    if (n > 0) {
+        grid_key_kernel<<<stream_grid(n, 256), 256, 0, st>>>(pts, n, rs_dev, nb, gi.params, keys);
+        O3DML_LAUNCH_CHECK();
+        prim::radix_sort_pairs<uint32_t>(keys, nullptr, skeys, gi.order, n,
+                                         prim::bits_needed(static_cast<uint64_t>(gi.cells - 1)), ws, st);
+        gather_float4_kernel<<<stream_grid(n, 256), 256, 0, st>>>(pts, gi.order, n, gi.sorted);
+        O3DML_LAUNCH_CHECK();
+    }
+    key_boundaries_kernel<<<stream_grid(n > 0 ? n : gi.cells + 1, 256), 256, 0, st>>>(skeys, n, gi.cells, gi.splits);
+    O3DML_LAUNCH_CHECK();
+    return gi;
+}
+
+}  // namespace o3dml

@@ -1,0 +1,346 @@
+// nns_knn.hip — exact k-nearest-neighbour search (Open3D ops.knn_search /
+// layers.KNNSearch and core.nns.NearestNeighborSearch.knn_search; reference
+// callers ml3d/datasets/utils/dataprocessing.py:87-103 <- randlanet.py:218-229,
+// point_transformer.py:724-729).
+//
+// k <= 64: dense per-batch grid (grid.hpp, ~k/2 points per cell); one lane per
+// query walks Chebyshev rings of cells around its cell, keeping the k best
+// (distance, id) pairs sorted in registers, and stops once the k-th distance
+// is strictly below a conservative lower bound on every unvisited point.
+// Queries are processed in cell order (self search: the grid order itself),
+// so the lanes of a wave scan overlapping cells through L1/L2.
+// k > 64 (the sampler's single-centre patch crop): all distances
+// of the query's batch item + stable radix sort on the distance bits.
+// Result order per query: ascending (distance, index) — exact ties by index.
+#include <algorithm>
+#include <vector>
+
+#include "grid.hpp"
+
+namespace o3dml {
+
+__device__ __forceinline__ bool lex_less(float da, uint32_t ia, float db, uint32_t ib) {
+    return da < db || (da == db && ia < ib);
+}
+
+template <int K, int METRIC, bool IGNORE>
+__global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict__ sorted, const uint32_t* __restrict__ splits,
+                                                       const GridBatch* __restrict__ grids, const float* __restrict__ queries,
+                                                       int64_t m, const uint32_t* __restrict__ qorder,
+                                                       const int64_t* __restrict__ qrs, int nb, int k,
+                                                       int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
+                                                       int64_t* __restrict__ counts) {
+    for (int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; t < m;
+         t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t q = qorder ? static_cast<int64_t>(qorder[t]) : t;
+        const GridBatch g = grids[batch_of(q, qrs, nb)];
+        const float qx = queries[3 * q], qy = queries[3 * q + 1], qz = queries[3 * q + 2];
+        const int cx = grid_axis(qx, g.ox, g.inv_h, g.dx);
+        const int cy = grid_axis(qy, g.oy, g.inv_h, g.dy);
+        const int cz = grid_axis(qz, g.oz, g.inv_h, g.dz);
+        float bd[K];
+        uint32_t bi[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            bd[j] = INFINITY;
+            bi[j] = 0xffffffffu;
+        }
+        float kd = INFINITY;
+        uint32_t ki = 0xffffffffu;
+        int cnt = 0;
+        auto visit = [&](int x, int y, int z) {
+            const uint32_t c = g.offset + static_cast<uint32_t>(x + g.dx * (y + g.dy * z));
+            const uint32_t s = splits[c], e = splits[c + 1];
+            for (uint32_t j = s; j < e; ++j) {
+                const float4 p = sorted[j];
+                if (IGNORE && p.x == qx && p.y == qy && p.z == qz) continue;
+                const float d = dist_metric<METRIC>(p.x, p.y, p.z, qx, qy, qz);
+                const uint32_t id = __float_as_uint(p.w);
+                if (!lex_less(d, id, kd, ki)) continue;
+                ++cnt;
+#pragma unroll
+                for (int r = K - 1; r >= 0; --r) {
+                    const bool lt_prev = r > 0 && lex_less(d, id, bd[r > 0 ? r - 1 : 0], bi[r > 0 ? r - 1 : 0]);
+                    const bool lt_cur = lex_less(d, id, bd[r], bi[r]);
+                    if (lt_prev) {
+                        bd[r] = bd[r - 1];
+                        bi[r] = bi[r - 1];
+                    } else if (lt_cur) {
+                        bd[r] = d;
+                        bi[r] = id;
+                    }
+                }
+                if (cnt >= k) {
+#pragma unroll
+                    for (int r = 0; r < K; ++r)
+                        if (r == k - 1) {
+                            kd = bd[r];
+                            ki = bi[r];
+                        }
+                }
+            }
+        };
+        for (int R = 0;; ++R) {
+            const int x0 = cx - R, x1 = cx + R, y0 = cy - R, y1 = cy + R, z0 = cz - R, z1 = cz + R;
+            const int za = max(z0, 0), zb = min(z1, g.dz - 1);
+            const int ya = max(y0, 0), yb = min(y1, g.dy - 1);
+            const int xa = max(x0, 0), xb = min(x1, g.dx - 1);
+            for (int z = za; z <= zb; ++z) {
+                for (int y = ya; y <= yb; ++y) {
+                    if (z == z0 || z == z1 || y == y0 || y == y1) {
+                        for (int x = xa; x <= xb; ++x) visit(x, y, z);
+                    } else {
+                        if (x0 >= 0) visit(x0, y, z);
+                        if (x1 < g.dx) visit(x1, y, z);
+                    }
+                }
+            }
+            const bool lo_x = x0 <= 0, hi_x = x1 >= g.dx - 1, lo_y = y0 <= 0, hi_y = y1 >= g.dy - 1;
+            const bool lo_z = z0 <= 0, hi_z = z1 >= g.dz - 1;
+            if (lo_x && hi_x && lo_y && hi_y && lo_z && hi_z) break;  // every cell visited
+            if (cnt >= k) {
+                // distance from q to the unvisited region (faces not on the grid boundary)
+                float lb = INFINITY;
+                if (!lo_x) lb = fminf(lb, qx - (g.ox + static_cast<float>(x0) * g.h));
+                if (!hi_x) lb = fminf(lb, (g.ox + static_cast<float>(x1 + 1) * g.h) - qx);
+                if (!lo_y) lb = fminf(lb, qy - (g.oy + static_cast<float>(y0) * g.h));
+                if (!hi_y) lb = fminf(lb, (g.oy + static_cast<float>(y1 + 1) * g.h) - qy);
+                if (!lo_z) lb = fminf(lb, qz - (g.oz + static_cast<float>(z0) * g.h));
+                if (!hi_z) lb = fminf(lb, (g.oz + static_cast<float>(z1 + 1) * g.h) - qz);
+                // conservative against float cell-assignment rounding
+                lb = lb - 1e-3f * g.h - 1e-6f * (fabsf(qx) + fabsf(qy) + fabsf(qz));
+                if (lb > 0.f) {
+                    const float bound = METRIC == kL2 ? lb * lb : lb;
+                    if (kd < bound) break;
+                }
+            }
+        }
+        const int c = cnt < k ? cnt : k;
+        counts[q] = c;
+        int32_t* oi = out_idx + q * static_cast<int64_t>(k);
+        float* od = out_dist + q * static_cast<int64_t>(k);
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            if (r < c) {
+                oi[r] = static_cast<int32_t>(bi[r]);
+                od[r] = bd[r];
+            }
+        }
+    }
+}
+
+template <int K>
+static void launch_knn_k(int metric, bool ignore, unsigned grid, hipStream_t st, const GridIndex& gi, const float* q,
+                         int64_t m, const uint32_t* qorder, const int64_t* qrs, int nb, int k, int32_t* oi, float* od,
+                         int64_t* counts) {
+#define O3DML_KNN(M, I)                                                                                          \
+    knn_grid_kernel<K, M, I><<<grid, 256, 0, st>>>(gi.sorted, gi.splits, gi.params, q, m, qorder, qrs, nb, k, oi, od, \
+                                                   counts)
+    if (metric == kL2) {
+        if (ignore) O3DML_KNN(kL2, true); else O3DML_KNN(kL2, false);
+    } else if (metric == kL1) {
+        if (ignore) O3DML_KNN(kL1, true); else O3DML_KNN(kL1, false);
+    } else {
+        if (ignore) O3DML_KNN(kLinf, true); else O3DML_KNN(kLinf, false);
+    }
+#undef O3DML_KNN
+    O3DML_LAUNCH_CHECK();
+}
+
+__global__ void compact_rows_kernel(const int32_t* __restrict__ si, const float* __restrict__ sd, int64_t m, int k,
+                                    const int64_t* __restrict__ rs, int bits, void* __restrict__ out_idx,
+                                    float* __restrict__ out_dist) {
+    const int64_t total = m * k;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t q = e / k;
+        const int64_t j = e - q * k;
+        const int64_t s = rs[q];
+        if (s + j < rs[q + 1]) {
+            if (bits == 32)
+                static_cast<int32_t*>(out_idx)[s + j] = si[e];
+            else
+                static_cast<int64_t*>(out_idx)[s + j] = si[e];
+            if (out_dist) out_dist[s + j] = sd[e];
+        }
+    }
+}
+
+// ---- k > 64: one query at a time, full sort of its batch item's distances ----
+template <int METRIC>
+__global__ void dist_keys_kernel(const float* __restrict__ pts, int64_t s, int64_t n, float qx, float qy, float qz,
+                                 uint32_t* __restrict__ keys) {
+    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
+         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t i = s + j;
+        keys[j] = __float_as_uint(dist_metric<METRIC>(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], qx, qy, qz));
+    }
+}
+
+__global__ void write_bigk_kernel(const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sidx, int64_t cnt,
+                                  int64_t base_id, int64_t out_off, int bits, void* __restrict__ out_idx,
+                                  float* __restrict__ out_dist) {
+    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < cnt;
+         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t id = base_id + sidx[j];
+        if (bits == 32)
+            static_cast<int32_t*>(out_idx)[out_off + j] = static_cast<int32_t>(id);
+        else
+            static_cast<int64_t*>(out_idx)[out_off + j] = id;
+        if (out_dist) out_dist[out_off + j] = __uint_as_float(skeys[j]);
+    }
+}
+
+}  // namespace o3dml
+
+using namespace o3dml;
+
+static int knn_bucket(int64_t k) {
+    if (k <= 1) return 1;
+    if (k <= 4) return 4;
+    if (k <= 8) return 8;
+    if (k <= 16) return 16;
+    if (k <= 32) return 32;
+    if (k <= 64) return 64;
+    return 0;
+}
+
+static constexpr double kKnnCapFactor = 2.0;
+
+O3DML_API size_t o3dml_knn_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t k, int64_t n_batch) {
+    if (knn_bucket(k) == 0) {
+        int64_t maxn = n_points;
+        return 3 * ws_bytes<uint32_t>(maxn) + prim::radix_sort_workspace_bytes<uint32_t>(maxn);
+    }
+    return grid_workspace_bytes(n_points, static_cast<int>(n_batch), kKnnCapFactor) +
+           3 * ws_bytes<uint32_t>(n_queries) + prim::radix_sort_workspace_bytes<uint32_t>(n_queries) +
+           ws_bytes<int32_t>(n_queries * k) + ws_bytes<float>(n_queries * k) + ws_bytes<int64_t>(n_queries) +
+           prim::scan_workspace_bytes(n_queries);
+}
+
+// Phase 1: search; writes neighbors_row_splits [M+1] (device) and keeps the
+// per-query results in the workspace for o3dml_knn_search_fill.
+// Row-split arrays: *_host copies are needed to plan the grid.
+O3DML_API int o3dml_knn_search_count(const float* points, int64_t n_points, const float* queries, int64_t n_queries,
+                                     int64_t k, int64_t n_batch, const int64_t* points_row_splits,
+                                     const int64_t* queries_row_splits, const int64_t* points_row_splits_host,
+                                     const int64_t* queries_row_splits_host, int metric, int ignore_query_point,
+                                     int self_search, int64_t* neighbors_row_splits, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(k >= 1, "k must be >= 1");
+    O3DML_REQUIRE(metric >= 0 && metric <= 2, "metric must be L1(0), L2(1) or Linf(2)");
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    const int nb = static_cast<int>(n_batch);
+    const int K = knn_bucket(k);
+    if (K == 0) {
+        O3DML_REQUIRE(!ignore_query_point, "ignore_query_point is not supported for k > 64");
+        // rows: min(k, N_b) per query; computed on the host
+        std::vector<int64_t> rs(n_queries + 1, 0);
+        for (int b = 0; b < nb; ++b) {
+            const int64_t nbp = points_row_splits_host[b + 1] - points_row_splits_host[b];
+            for (int64_t q = queries_row_splits_host[b]; q < queries_row_splits_host[b + 1]; ++q)
+                rs[q + 1] = std::min<int64_t>(k, nbp);
+        }
+        for (int64_t q = 0; q < n_queries; ++q) rs[q + 1] += rs[q];
+        O3DML_CHECK_HIP(hipMemcpyAsync(neighbors_row_splits, rs.data(), sizeof(int64_t) * (n_queries + 1),
+                                       hipMemcpyHostToDevice, st));
+        O3DML_CHECK_HIP(hipStreamSynchronize(st));
+        return 0;
+    }
+    // per-query results first: o3dml_knn_search_fill finds them at the same offsets
+    int32_t* si = ws.take<int32_t>(n_queries * k);
+    float* sd = ws.take<float>(n_queries * k);
+    int64_t* counts = ws.take<int64_t>(n_queries);
+    GridIndex gi = build_grid(points, n_points, points_row_splits, points_row_splits_host, nb, std::max(2.0, k / 2.0),
+                              kKnnCapFactor, ws, st);
+    uint32_t* qkeys = ws.take<uint32_t>(n_queries);
+    uint32_t* qskeys = ws.take<uint32_t>(n_queries);
+    uint32_t* qorder = ws.take<uint32_t>(n_queries);
+    O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
+    if (n_queries == 0) return 0;
+    const uint32_t* order = nullptr;
+    if (self_search) {
+        order = gi.order;
+    } else if (n_points > 0) {
+        // process queries in cell order for wave coherence
+        grid_key_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(queries, n_queries, queries_row_splits, nb,
+                                                                    gi.params, qkeys);
+        O3DML_LAUNCH_CHECK();
+        Workspace sws = ws;
+        prim::radix_sort_pairs<uint32_t>(qkeys, nullptr, qskeys, qorder, n_queries,
+                                         prim::bits_needed(static_cast<uint64_t>(std::max<int64_t>(gi.cells - 1, 0))),
+                                         sws, st);
+        order = qorder;
+    }
+    const unsigned grid = stream_grid(n_queries, 256, 1 << 20);
+    const bool ig = ignore_query_point != 0;
+    switch (K) {
+        case 1: launch_knn_k<1>(metric, ig, grid, st, gi, queries, n_queries, order, queries_row_splits, nb, (int)k, si, sd, counts); break;
+        case 4: launch_knn_k<4>(metric, ig, grid, st, gi, queries, n_queries, order, queries_row_splits, nb, (int)k, si, sd, counts); break;
+        case 8: launch_knn_k<8>(metric, ig, grid, st, gi, queries, n_queries, order, queries_row_splits, nb, (int)k, si, sd, counts); break;
+        case 16: launch_knn_k<16>(metric, ig, grid, st, gi, queries, n_queries, order, queries_row_splits, nb, (int)k, si, sd, counts); break;
+        case 32: launch_knn_k<32>(metric, ig, grid, st, gi, queries, n_queries, order, queries_row_splits, nb, (int)k, si, sd, counts); break;
+        default: launch_knn_k<64>(metric, ig, grid, st, gi, queries, n_queries, order, queries_row_splits, nb, (int)k, si, sd, counts); break;
+    }
+    prim::scan<int64_t, int64_t>(counts, neighbors_row_splits + 1, n_queries, true, ws, st);
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_knn_search_fill(const float* points, int64_t n_points, const float* queries, int64_t n_queries,
+                                    int64_t k, int64_t n_batch, const int64_t* points_row_splits_host,
+                                    const int64_t* queries_row_splits_host, int metric,
+                                    const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
+                                    float* neighbors_distance, void* workspace, size_t workspace_bytes,
+                                    void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    const int nb = static_cast<int>(n_batch);
+    const int K = knn_bucket(k);
+    if (n_queries == 0) return 0;
+    if (K == 0) {
+        uint32_t* keys = ws.take<uint32_t>(n_points);
+        uint32_t* skeys = ws.take<uint32_t>(n_points);
+        uint32_t* sidx = ws.take<uint32_t>(n_points);
+        std::vector<float> qh(3 * n_queries);
+        O3DML_CHECK_HIP(hipMemcpyAsync(qh.data(), queries, sizeof(float) * 3 * n_queries, hipMemcpyDeviceToHost, st));
+        O3DML_CHECK_HIP(hipStreamSynchronize(st));
+        int64_t off = 0;
+        for (int b = 0; b < nb; ++b) {
+            const int64_t ps = points_row_splits_host[b], pn = points_row_splits_host[b + 1] - ps;
+            const int64_t cnt = std::min<int64_t>(k, pn);
+            for (int64_t q = queries_row_splits_host[b]; q < queries_row_splits_host[b + 1]; ++q) {
+                if (cnt == 0) continue;
+                const unsigned g = stream_grid(pn, 256);
+                if (metric == kL2)
+                    dist_keys_kernel<kL2><<<g, 256, 0, st>>>(points, ps, pn, qh[3 * q], qh[3 * q + 1], qh[3 * q + 2], keys);
+                else if (metric == kL1)
+                    dist_keys_kernel<kL1><<<g, 256, 0, st>>>(points, ps, pn, qh[3 * q], qh[3 * q + 1], qh[3 * q + 2], keys);
+                else
+                    dist_keys_kernel<kLinf><<<g, 256, 0, st>>>(points, ps, pn, qh[3 * q], qh[3 * q + 1], qh[3 * q + 2], keys);
+                O3DML_LAUNCH_CHECK();
+                Workspace sws = ws;
+                prim::radix_sort_pairs<uint32_t>(keys, nullptr, skeys, sidx, pn, 32, sws, st);
+                write_bigk_kernel<<<stream_grid(cnt, 256), 256, 0, st>>>(skeys, sidx, cnt, ps, off, index_bits,
+                                                                        neighbors_index, neighbors_distance);
+                O3DML_LAUNCH_CHECK();
+                off += cnt;
+            }
+        }
+        return 0;
+    }
+    // same workspace layout as _count (results at the front)
+    (void)points;
+    (void)queries;
+    (void)metric;
+    const int32_t* si = ws.take<int32_t>(n_queries * k);
+    const float* sd = ws.take<float>(n_queries * k);
+    compact_rows_kernel<<<stream_grid(n_queries * k, 256), 256, 0, st>>>(si, sd, n_queries, (int)k,
+                                                                        neighbors_row_splits, index_bits,
+                                                                        neighbors_index, neighbors_distance);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}

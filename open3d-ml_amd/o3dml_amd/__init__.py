@@ -7,7 +7,7 @@ point-cloud hot path behind the ``open3d.ml.torch`` ops/layers API.
 ``open3d.core.nns`` resolve to this package, so reference model code runs
 unchanged.
 """
-from . import _lib, layers, ops  # noqa: F401
+from . import _lib, contrib, core, layers, ops  # noqa: F401
 
 __version__ = "0.1.0"
 

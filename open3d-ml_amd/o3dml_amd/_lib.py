@@ -38,6 +38,28 @@ SIGNATURES = {
     "o3dml_fixed_radius_search_fill": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p,
                                                c_p, c_p, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p,
                                                c_p, c_sz, c_p]),
+    # nns_knn.hip
+    "o3dml_knn_search_workspace_size": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
+    "o3dml_knn_search_count": (c_i32, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i32, c_i32,
+                                       c_i32, c_p, c_p, c_sz, c_p]),
+    "o3dml_knn_search_fill": (c_i32, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_i32, c_p, c_i32, c_p,
+                                      c_p, c_p, c_sz, c_p]),
+    # voxel.hip
+    "o3dml_voxelize_workspace_size": (c_sz, [c_i64, c_i64]),
+    "o3dml_voxelize_count": (c_i32, [c_p, c_i64, c_i32, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_sz,
+                                     c_p]),
+    "o3dml_voxelize_fill": (c_i32, [c_i64, c_i32, c_i64, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "o3dml_grid_subsample_workspace_size": (c_sz, [c_i64, c_i64]),
+    "o3dml_grid_subsample_count": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_f32, c_i64, c_p, c_p, c_sz, c_p]),
+    "o3dml_grid_subsample_fill": (c_i32, [c_p, c_i64, c_i64, c_p, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_sz,
+                                          c_p]),
+    # pointnet2.hip
+    "o3dml_furthest_point_sampling_workspace_size": (c_sz, [c_i64, c_i64]),
+    "o3dml_furthest_point_sampling": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_p, c_sz, c_p]),
+    "o3dml_ball_query": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_i64, c_p, c_p]),
+    "o3dml_three_nn": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
+    "o3dml_three_interpolate": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
+    "o3dml_three_interpolate_grad": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     # ragged.hip
     "o3dml_ragged_to_dense": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p]),
     "o3dml_reduce_subarrays_sum": (c_i32, [c_p, c_p, c_i64, c_p, c_p]),

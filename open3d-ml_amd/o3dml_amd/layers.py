@@ -36,3 +36,25 @@ class FixedRadiusSearch(torch.nn.Module):
                                        index_dtype=self.index_dtype, metric=self.metric,
                                        ignore_query_point=self.ignore_query_point,
                                        return_distances=self.return_distances)
+
+
+class KNNSearch(torch.nn.Module):
+    """Open3D ``layers.KNNSearch`` (point_transformer.py:724-729)."""
+
+    def __init__(self, metric="L2", ignore_query_point=False, return_distances=False,
+                 index_dtype=torch.int32, **kwargs):
+        super().__init__()
+        self.metric = metric
+        self.ignore_query_point = ignore_query_point
+        self.return_distances = return_distances
+        self.index_dtype = index_dtype
+
+    def forward(self, points, queries, k, points_row_splits=None, queries_row_splits=None):
+        if points_row_splits is None:
+            points_row_splits = torch.LongTensor([0, points.shape[0]])
+        if queries_row_splits is None:
+            queries_row_splits = torch.LongTensor([0, queries.shape[0]])
+        return ops.knn_search(points, queries, k, points_row_splits, queries_row_splits,
+                              index_dtype=self.index_dtype, metric=self.metric,
+                              ignore_query_point=self.ignore_query_point,
+                              return_distances=self.return_distances)

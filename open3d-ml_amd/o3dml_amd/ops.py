@@ -22,6 +22,9 @@ FixedRadiusSearchResult = namedtuple(
     "fixed_radius_search", ["neighbors_index", "neighbors_row_splits", "neighbors_distance"])
 KnnSearchResult = namedtuple("knn_search", ["neighbors_index", "neighbors_row_splits", "neighbors_distance"])
 RadiusSearchResult = namedtuple("radius_search", ["neighbors_index", "neighbors_row_splits", "neighbors_distance"])
+VoxelizeResult = namedtuple(
+    "voxelize", ["voxel_coords", "voxel_point_indices", "voxel_point_row_splits", "voxel_batch_splits"])
+GridSubsampleResult = namedtuple("grid_subsample", ["points", "lengths", "features", "classes"])
 
 
 # ---------------------------------------------------------------------------
@@ -116,6 +119,49 @@ def fixed_radius_search(points, queries, radius, points_row_splits=None, queries
 
 
 # ---------------------------------------------------------------------------
+# kNN
+# ---------------------------------------------------------------------------
+def knn_search(points, queries, k, points_row_splits=None, queries_row_splits=None,
+               index_dtype=torch.int32, metric="L2", ignore_query_point=False, return_distances=False):
+    """Open3D ``ops.knn_search``: per query the min(k, N_b) nearest points of
+    its batch item, ascending (distance, index); distances squared for L2.
+    Returns (neighbors_index [P], neighbors_row_splits int64 [M+1],
+    neighbors_distance [P] or [0]).  Reference callers:
+    point_transformer.py:724-729 (and, through core.nns, randlanet.py:218-229)."""
+    dev = gpu_device(points, queries)
+    check_points("points", points)
+    check_points("queries", queries)
+    bits = index_bits(index_dtype)
+    mcode = metric_code(metric)
+    k = int(k)
+    if k < 1:
+        raise RuntimeError("k must be >= 1")
+    lib = _lib.load()
+    n, m = points.shape[0], queries.shape[0]
+    prs = row_splits_host(points_row_splits, n)
+    qrs = row_splits_host(queries_row_splits, m)
+    if len(prs) != len(qrs):
+        raise RuntimeError("points_row_splits and queries_row_splits must have the same length")
+    same = _same_cloud(points, queries, prs, qrs)
+    pts = to_dev(points, dev)
+    qry = pts if same else to_dev(queries, dev)
+    prs_d = torch.from_numpy(prs).to(dev)
+    qrs_d = prs_d if same else torch.from_numpy(qrs).to(dev)
+    B = len(prs) - 1
+    st = stream_handle(dev)
+    rs = torch.empty(m + 1, dtype=torch.int64, device=dev)
+    ws = workspace(lib.o3dml_knn_search_workspace_size(n, m, k, B), dev)
+    _lib.call("o3dml_knn_search_count", ptr(pts), n, ptr(qry), m, k, B, ptr(prs_d), ptr(qrs_d), prs.ctypes.data,
+              qrs.ctypes.data, mcode, int(bool(ignore_query_point)), int(same), ptr(rs), ptr(ws), ws.numel(), st)
+    total = int(rs[-1].item())
+    idx = torch.empty(total, dtype=torch.int32 if bits == 32 else torch.int64, device=dev)
+    dist = torch.empty(total if return_distances else 0, dtype=torch.float32, device=dev)
+    _lib.call("o3dml_knn_search_fill", ptr(pts), n, ptr(qry), m, k, B, prs.ctypes.data, qrs.ctypes.data, mcode,
+              ptr(rs), bits, ptr(idx), ptr(dist) if return_distances else None, ptr(ws), ws.numel(), st)
+    return KnnSearchResult(back_to(idx, points), back_to(rs, points), back_to(dist, points))
+
+
+# ---------------------------------------------------------------------------
 # ragged helpers (SURVEY §8a A6, A10)
 # ---------------------------------------------------------------------------
 def ragged_to_dense(values, row_splits, out_col_size, default_value):
@@ -152,3 +198,167 @@ def reduce_subarrays_sum(values, row_splits):
     out = torch.empty(M, dtype=torch.float32, device=dev)
     _lib.call("o3dml_reduce_subarrays_sum", ptr(vals), ptr(rs), M, ptr(out), stream_handle(dev))
     return back_to(out, values)
+
+
+# ---------------------------------------------------------------------------
+# voxelize
+# ---------------------------------------------------------------------------
+def _host_f32(x, ndim, name):
+    a = np.ascontiguousarray(np.asarray(x.detach().cpu() if isinstance(x, torch.Tensor) else x,
+                                        dtype=np.float32).reshape(-1))
+    if a.size != ndim:
+        raise RuntimeError(f"{name} must have {ndim} entries, got {a.size}")
+    return a
+
+
+def voxelize(points, row_splits, voxel_size, points_range_min, points_range_max,
+             max_points_per_voxel=9223372036854775807, max_voxels=9223372036854775807):
+    """Open3D ``ops.voxelize`` (point_pillars.py:352-357, sparseconvnet.py:293-298).
+    Returns (voxel_coords int32 [V,D], voxel_point_indices int64 [P],
+    voxel_point_row_splits int64 [V+1], voxel_batch_splits int64 [B+1]).
+    Voxels ordered by (batch, linear id, dim 0 fastest); points of a voxel by
+    index; caps keep the first voxels / points in that order."""
+    dev = gpu_device(points)
+    if points.dim() != 2 or points.dtype != torch.float32:
+        raise RuntimeError("voxelize: points must be float32 [N, D]")
+    lib = _lib.load()
+    n, ndim = points.shape
+    rs = row_splits_host(row_splits, n)
+    B = len(rs) - 1
+    vs = _host_f32(voxel_size, ndim, "voxel_size")
+    mn = _host_f32(points_range_min, ndim, "points_range_min")
+    mx = _host_f32(points_range_max, ndim, "points_range_max")
+    pts = to_dev(points, dev)
+    rs_d = torch.from_numpy(rs).to(dev)
+    st = stream_handle(dev)
+    ws = workspace(lib.o3dml_voxelize_workspace_size(n, B), dev)
+    counts = np.zeros(2, np.int64)
+    _lib.call("o3dml_voxelize_count", ptr(pts), n, ndim, B, ptr(rs_d), vs.ctypes.data, mn.ctypes.data,
+              mx.ctypes.data, int(max_points_per_voxel), int(max_voxels), counts.ctypes.data, ptr(ws), ws.numel(), st)
+    V, P = int(counts[0]), int(counts[1])
+    coords = torch.empty((V, ndim), dtype=torch.int32, device=dev)
+    pidx = torch.empty(P, dtype=torch.int64, device=dev)
+    prs = torch.empty(V + 1, dtype=torch.int64, device=dev)
+    bsp = torch.empty(B + 1, dtype=torch.int64, device=dev)
+    _lib.call("o3dml_voxelize_fill", n, ndim, B, vs.ctypes.data, mn.ctypes.data, mx.ctypes.data, V, ptr(coords),
+              ptr(pidx), ptr(prs), ptr(bsp), ptr(ws), ws.numel(), st)
+    return VoxelizeResult(back_to(coords, points), back_to(pidx, points), back_to(prs, points), back_to(bsp, points))
+
+
+# ---------------------------------------------------------------------------
+# grid subsampling (SURVEY §8a A7/A8) — backend of contrib.subsample(_batch)
+# ---------------------------------------------------------------------------
+def grid_subsample(points, lengths, sampleDl, features=None, classes=None, max_p=0):
+    """KPConv grid subsampling per batch element (lengths int64 [B]).
+    Returns (points [S,3], lengths int64 [B], features [S,F] | None,
+    classes int32 [S,L] | None); cells in ascending key order, first max_p
+    cells per element."""
+    dev = gpu_device(points)
+    check_points("points", points)
+    lib = _lib.load()
+    n = points.shape[0]
+    lengths = np.asarray(lengths.cpu() if isinstance(lengths, torch.Tensor) else lengths, np.int64).reshape(-1)
+    rs = np.zeros(len(lengths) + 1, np.int64)
+    rs[1:] = np.cumsum(lengths)
+    rs = row_splits_host(rs, n)
+    B = len(rs) - 1
+    pts = to_dev(points, dev)
+    rs_d = torch.from_numpy(rs).to(dev)
+    st = stream_handle(dev)
+    ws = workspace(lib.o3dml_grid_subsample_workspace_size(n, B), dev)
+    nout = np.zeros(1, np.int64)
+    _lib.call("o3dml_grid_subsample_count", ptr(pts), n, B, ptr(rs_d), rs.ctypes.data, float(sampleDl), int(max_p),
+              nout.ctypes.data, ptr(ws), ws.numel(), st)
+    S = int(nout[0])
+    fd = 0 if features is None else int(features.reshape(n, -1).shape[1])
+    ld = 0 if classes is None else int(classes.reshape(n, -1).shape[1])
+    f = None if features is None else to_dev(features.reshape(n, fd), dev, torch.float32)
+    c = None if classes is None else to_dev(classes.reshape(n, ld), dev, torch.int32)
+    out_p = torch.empty((S, 3), dtype=torch.float32, device=dev)
+    out_f = torch.empty((S, fd), dtype=torch.float32, device=dev) if fd else None
+    out_c = torch.empty((S, ld), dtype=torch.int32, device=dev) if ld else None
+    out_l = torch.empty(B, dtype=torch.int64, device=dev)
+    _lib.call("o3dml_grid_subsample_fill", ptr(pts), n, B, ptr(f), fd, ptr(c), ld, ptr(out_p), ptr(out_f),
+              ptr(out_c), ptr(out_l), ptr(ws), ws.numel(), st)
+    return GridSubsampleResult(back_to(out_p, points), back_to(out_l, points),
+                               None if out_f is None else back_to(out_f, points),
+                               None if out_c is None else back_to(out_c, points))
+
+
+# ---------------------------------------------------------------------------
+# PointNet++ ops (SURVEY §8a A15-A17)
+# ---------------------------------------------------------------------------
+def _check_bn3(name, t):
+    if t.dim() != 3 or t.shape[2] != 3 or t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32 [B, N, 3], got {t.dtype} {list(t.shape)}")
+
+
+def furthest_point_sampling(points, sample_size):
+    """Open3D ``ops.furthest_point_sampling`` (pointnet2_utils.py:55): points
+    [B,N,3] -> int32 [B, sample_size]; greedy from index 0, squared L2, ties
+    -> smallest index."""
+    dev = gpu_device(points)
+    _check_bn3("points", points)
+    lib = _lib.load()
+    B, N, _ = points.shape
+    m = int(sample_size)
+    pts = to_dev(points, dev)
+    out = torch.empty((B, m), dtype=torch.int32, device=dev)
+    ws = workspace(lib.o3dml_furthest_point_sampling_workspace_size(B, N), dev)
+    _lib.call("o3dml_furthest_point_sampling", ptr(pts), B, N, m, ptr(out), ptr(ws), ws.numel(), stream_handle(dev))
+    return back_to(out, points)
+
+
+def ball_query(xyz, center, radius, nsample):
+    """Open3D ``ops.ball_query`` (pointnet2_utils.py:212): first nsample points
+    (index order) with d^2 < r^2, padded with the first hit, 0 if none."""
+    dev = gpu_device(xyz, center)
+    _check_bn3("xyz", xyz)
+    _check_bn3("center", center)
+    B, N, _ = xyz.shape
+    M = center.shape[1]
+    x, c = to_dev(xyz, dev), to_dev(center, dev)
+    out = torch.empty((B, M, int(nsample)), dtype=torch.int32, device=dev)
+    _lib.call("o3dml_ball_query", ptr(x), ptr(c), B, N, M, float(radius), int(nsample), ptr(out), stream_handle(dev))
+    return back_to(out, xyz)
+
+
+def three_nn(query_pts, data_pts):
+    """Open3D ``ops.three_nn`` (pointnet2_utils.py:129): -> (dist2 [B,n,3], idx int32 [B,n,3])."""
+    dev = gpu_device(query_pts, data_pts)
+    _check_bn3("query_pts", query_pts)
+    _check_bn3("data_pts", data_pts)
+    B, n, _ = query_pts.shape
+    m = data_pts.shape[1]
+    q, d = to_dev(query_pts, dev), to_dev(data_pts, dev)
+    dist = torch.empty((B, n, 3), dtype=torch.float32, device=dev)
+    idx = torch.empty((B, n, 3), dtype=torch.int32, device=dev)
+    _lib.call("o3dml_three_nn", ptr(q), ptr(d), B, n, m, ptr(dist), ptr(idx), stream_handle(dev))
+    return back_to(dist, query_pts), back_to(idx, query_pts)
+
+
+def three_interpolate(feats, idx, weights):
+    """Open3D ``ops.three_interpolate`` (pointnet2_utils.py:162): feats [B,C,m],
+    idx/weights [B,n,3] -> [B,C,n]."""
+    dev = gpu_device(feats, idx, weights)
+    B, C, m = feats.shape
+    n = idx.shape[1]
+    f = to_dev(feats, dev, torch.float32)
+    i = to_dev(idx, dev, torch.int32)
+    w = to_dev(weights, dev, torch.float32)
+    out = torch.empty((B, C, n), dtype=torch.float32, device=dev)
+    _lib.call("o3dml_three_interpolate", ptr(f), ptr(i), ptr(w), B, C, m, n, ptr(out), stream_handle(dev))
+    return back_to(out, feats)
+
+
+def three_interpolate_grad(grad_out, idx, weights, M):
+    """Open3D ``ops.three_interpolate_grad`` (pointnet2_utils.py:184):
+    grad_out [B,C,n] -> [B,C,M] (fp32 atomic accumulation)."""
+    dev = gpu_device(grad_out, idx, weights)
+    B, C, n = grad_out.shape
+    g = to_dev(grad_out, dev, torch.float32)
+    i = to_dev(idx, dev, torch.int32)
+    w = to_dev(weights, dev, torch.float32)
+    out = torch.empty((B, C, int(M)), dtype=torch.float32, device=dev)
+    _lib.call("o3dml_three_interpolate_grad", ptr(g), ptr(i), ptr(w), B, C, n, int(M), ptr(out), stream_handle(dev))
+    return back_to(out, grad_out)
