@@ -146,6 +146,39 @@ int o3dml_three_interpolate(const float* features, const int32_t* idx, const flo
 int o3dml_three_interpolate_grad(const float* grad_out, const int32_t* idx, const float* weight, int64_t B, int64_t C,
                                  int64_t n, int64_t m, float* grad_features, void* stream);
 
+/* ---- sparse convolution: replaces open3d.ml.torch.ops.sparse_conv,
+ * sparse_conv_transpose and their gradients, bound by layers.SparseConv /
+ * layers.SparseConvTranspose (ml3d/torch/models/sparseconvnet.py:344-482;
+ * filters [k,k,k,Cin,Cout] per load_unet_wts :660-677).
+ * 1) o3dml_sparse_conv_build_map: CSR pairs (over OUTPUT points) -> dense
+ *    kernel map [n_out*K] (+ inverse map for the input gradient) in
+ *    `workspace`; status_host[0] bit0 = duplicate (o,k), bit1 = bad index.
+ * 2) o3dml_sparse_conv_forward: implicit GEMM on fp32 MFMA.
+ * 3) o3dml_sparse_conv_backward: grad_inp (inverse map, W^T) and
+ *    grad_filters (per-offset pair lists, split-K slabs, fixed-order reduce).
+ * o3dml_sparse_conv_kernel_index: the layer's rulebook — kernel index of
+ * each (query, input) pair, per axis floor((p-q)/vs + k/2) (mirror:
+ * floor(k/2 - (p-q)/vs)), linearised (z*k1 + y)*k2 + x. -------------------- */
+size_t o3dml_sparse_conv_map_workspace_size(int64_t n_out, int64_t n_in, int K);
+int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const int32_t* neighbors_kernel_index,
+                                const float* neighbors_importance, const int64_t* neighbors_row_splits, int64_t n_out,
+                                int64_t n_in, int K, int normalize, const float* out_importance, int want_inverse,
+                                int* status_host, void* workspace, size_t workspace_bytes, void* stream);
+int o3dml_sparse_conv_forward(const float* filters, int K, int cin, int cout, const float* inp_features, int64_t n_in,
+                              const float* inp_importance, int has_neighbors_importance, int use_out_scale,
+                              const float* bias, int64_t n_out, float* out_features, void* map_workspace,
+                              size_t map_workspace_bytes, void* stream);
+size_t o3dml_sparse_conv_backward_workspace_size(int64_t n_out, int K, int cin, int cout);
+int o3dml_sparse_conv_backward(const float* filters, int K, int cin, int cout, const float* inp_features, int64_t n_in,
+                               const float* inp_importance, int has_neighbors_importance, int use_out_scale,
+                               const float* grad_out, int64_t n_out, float* grad_inp, float* grad_filters,
+                               void* map_workspace, size_t map_workspace_bytes, void* workspace,
+                               size_t workspace_bytes, void* stream);
+int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* query_positions,
+                                   const int32_t* neighbors_index, const int64_t* neighbors_row_splits,
+                                   int64_t n_query, const int32_t* ksize_host, float voxel_size, int mirror,
+                                   int32_t* kernel_index, void* stream);
+
 /* ---- ragged helpers ------------------------------------------------------
  * o3dml_ragged_to_dense replaces open3d.ml.torch.ops.ragged_to_dense
  * (kpconv.py:2030-2032, point_pillars.py:364-366): values [P, inner] of

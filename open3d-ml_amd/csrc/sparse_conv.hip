@@ -1,0 +1,514 @@
+// sparse_conv.hip — SparseConv / SparseConvTranspose gather-GEMM-scatter on
+// MFMA, replacing open3d.ml.torch.ops.sparse_conv,
+// sparse_conv_transpose and their gradients as bound by layers.SparseConv /
+// layers.SparseConvTranspose (ml3d/torch/models/sparseconvnet.py:344-482).
+//
+// Data flow (all device):
+//   CSR pairs (neighbors_index, neighbors_kernel_index, neighbors_row_splits)
+//     -> dense kernel map  map[o*K + k] = input row or -1   (build_kernel_map)
+//   forward  out[o,:] = oscale[o] * sum_k (src[map[o,k],:] * sscale[i] * pscale[o,k]) @ W[k] + bias
+//            output-stationary implicit GEMM: a workgroup owns TM output rows x
+//            TN output channels, walks the K offsets (skipping offsets no row of
+//            the tile uses) and Cin in KC=32 chunks; the gathered rows and the
+//            W[k] chunk are staged in LDS and multiplied with
+//            v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains; 4 waves, 32x32 each).
+//            No atomics: every output row is written once -> deterministic.
+//   dIn      the same kernel on the inverse map inv[i*K+k] = o with W^T.
+//   dW       per offset k the pair list (o, i) (k-major compaction of the map);
+//            dW[k] = sum_j src[i_j]^T g[o_j] as split-K MFMA tiles into partial
+//            slabs, reduced in a fixed order (deterministic).
+// Roofline: MFMA fp32 (157 TF/s dense) for Cin*Cout >= ~64^2, gather/HBM bound
+// below that.
+#include <vector>
+
+#include "primitives.hpp"
+
+namespace o3dml {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kKC = 32;           // Cin chunk per LDS stage
+constexpr int kGemmThreads = 256; // 4 waves
+
+// --------------------------------------------------------------------------
+// kernel maps
+// --------------------------------------------------------------------------
+__global__ void build_kernel_map_kernel(const int32_t* __restrict__ nbr, const int32_t* __restrict__ kidx,
+                                        const float* __restrict__ nimp, const int64_t* __restrict__ rs, int64_t n_out,
+                                        int K, int32_t* __restrict__ map, float* __restrict__ pscale,
+                                        float* __restrict__ norm, int* __restrict__ dup) {
+    for (int64_t o = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; o < n_out;
+         o += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        float s = 0.f;
+        for (int64_t e = rs[o], ee = rs[o + 1]; e < ee; ++e) {
+            const int k = kidx[e];
+            if (k < 0 || k >= K) {
+                atomicOr(dup, 2);
+                continue;
+            }
+            int32_t* slot = map + o * K + k;
+            if (*slot >= 0) {
+                atomicOr(dup, 1);  // two pairs share (o, k): dense map impossible
+                continue;
+            }
+            *slot = nbr[e];
+            const float w = nimp ? nimp[e] : 1.f;
+            if (pscale) pscale[o * K + k] = w;
+            s += w;
+        }
+        if (norm) norm[o] = s;
+    }
+}
+
+__global__ void build_inverse_map_kernel(const int32_t* __restrict__ map, const float* __restrict__ pscale,
+                                         int64_t n_out, int K, int32_t* __restrict__ inv,
+                                         float* __restrict__ ipscale, int* __restrict__ dup) {
+    const int64_t total = n_out * K;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int32_t i = map[e];
+        if (i < 0) continue;
+        const int64_t o = e / K;
+        const int k = static_cast<int>(e - o * K);
+        const int32_t prev = atomicCAS(inv + static_cast<int64_t>(i) * K + k, -1, static_cast<int32_t>(o));
+        if (prev != -1) atomicOr(dup, 1);
+        if (ipscale && pscale) ipscale[static_cast<int64_t>(i) * K + k] = pscale[e];
+    }
+}
+
+__global__ void recip_norm_kernel(const float* __restrict__ norm, const float* __restrict__ mul, int64_t n,
+                                  float* __restrict__ out) {
+    for (int64_t o = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; o < n;
+         o += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        float s = norm ? (norm[o] != 0.f ? 1.f / norm[o] : 1.f) : 1.f;
+        if (mul) s *= mul[o];
+        out[o] = s;
+    }
+}
+
+// W [K][Cin][Cout] -> Wt [K][Cout][Cin]
+__global__ void transpose_filters_kernel(const float* __restrict__ w, int K, int cin, int cout, float* __restrict__ wt) {
+    const int64_t total = static_cast<int64_t>(K) * cin * cout;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t k = e / (static_cast<int64_t>(cin) * cout);
+        const int64_t r = e - k * cin * cout;
+        const int64_t a = r / cout, c = r - a * cout;
+        wt[(k * cout + c) * cin + a] = w[e];
+    }
+}
+
+// --------------------------------------------------------------------------
+// implicit GEMM (forward / dIn)
+// --------------------------------------------------------------------------
+template <int TN, bool VEC4>
+__global__ void __launch_bounds__(kGemmThreads)
+implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, const float* __restrict__ src,
+                     const float* __restrict__ sscale, const float* __restrict__ pscale,
+                     const float* __restrict__ W /*[K][cin][cout]*/, int cin, int cout,
+                     const float* __restrict__ oscale, const float* __restrict__ bias, float* __restrict__ out) {
+    constexpr int WN = TN / 32;           // waves along N
+    constexpr int WM = 4 / WN;            // waves along M
+    constexpr int TM = 32 * WM;           // rows per workgroup
+    constexpr int KMAX = 32;
+    __shared__ float As[TM][kKC + 1];
+    __shared__ float Bs[kKC][TN];
+    __shared__ int32_t Ms[TM][KMAX];
+    __shared__ float Ps[TM][KMAX];
+    __shared__ unsigned used_mask;
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const int w = t >> 6;
+    const int wr = w / WN, wc = w % WN;
+    const int64_t o0 = static_cast<int64_t>(blockIdx.x) * TM;
+    const int n0 = blockIdx.y * TN;
+    if (t == 0) used_mask = 0u;
+    __syncthreads();
+    for (int e = t; e < TM * K; e += kGemmThreads) {
+        const int r = e / K, k = e - r * K;
+        const int64_t o = o0 + r;
+        const int32_t i = o < n_out ? map[o * K + k] : -1;
+        Ms[r][k] = i;
+        Ps[r][k] = (i >= 0 && pscale) ? pscale[o * K + k] : 1.f;
+        if (i >= 0) atomicOr(&used_mask, 1u << k);
+    }
+    __syncthreads();
+    const unsigned mask = used_mask;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int k = 0; k < K; ++k) {
+        if (!((mask >> k) & 1u)) continue;  // no row of this tile uses offset k
+        const float* Wk = W + static_cast<int64_t>(k) * cin * cout;
+        for (int c0 = 0; c0 < cin; c0 += kKC) {
+            // gather A: TM rows x KC channels (scaled), zero for missing pairs
+            if constexpr (VEC4) {
+                for (int e = t; e < TM * (kKC / 4); e += kGemmThreads) {
+                    const int r = e / (kKC / 4), c4 = (e - r * (kKC / 4)) * 4;
+                    const int32_t i = Ms[r][k];
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (i >= 0 && c0 + c4 < cin) {
+                        v = *reinterpret_cast<const float4*>(src + static_cast<int64_t>(i) * cin + c0 + c4);
+                        const float s = (sscale ? sscale[i] : 1.f) * Ps[r][k];
+                        v.x *= s; v.y *= s; v.z *= s; v.w *= s;
+                    }
+                    As[r][c4] = v.x; As[r][c4 + 1] = v.y; As[r][c4 + 2] = v.z; As[r][c4 + 3] = v.w;
+                }
+            } else {
+                for (int e = t; e < TM * kKC; e += kGemmThreads) {
+                    const int r = e / kKC, c = e - r * kKC;
+                    const int32_t i = Ms[r][k];
+                    float v = 0.f;
+                    if (i >= 0 && c0 + c < cin)
+                        v = src[static_cast<int64_t>(i) * cin + c0 + c] * ((sscale ? sscale[i] : 1.f) * Ps[r][k]);
+                    As[r][c] = v;
+                }
+            }
+            // B: W[k][c0 .. c0+KC)[n0 .. n0+TN)
+            for (int e = t; e < kKC * TN; e += kGemmThreads) {
+                const int r = e / TN, c = e - r * TN;
+                Bs[r][c] = (c0 + r < cin && n0 + c < cout) ? Wk[static_cast<int64_t>(c0 + r) * cout + n0 + c] : 0.f;
+            }
+            __syncthreads();
+            const int ar = wr * 32 + (lane & 31);
+            const int bc = wc * 32 + (lane & 31);
+            const int kh = lane >> 5;
+#pragma unroll
+            for (int s = 0; s < kKC / 2; ++s)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[ar][2 * s + kh], Bs[2 * s + kh][bc], acc, 0, 0, 0);
+            __syncthreads();
+        }
+    }
+    // epilogue: C/D map row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31
+    const int col = n0 + wc * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int64_t o = o0 + wr * 32 + row;
+        if (o < n_out && col < cout) {
+            float v = acc[r];
+            if (oscale) v *= oscale[o];
+            if (bias) v += bias[col];
+            out[o * cout + col] = v;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// dW: per offset pair lists, split-K slabs
+// --------------------------------------------------------------------------
+// k-major flags: flag[k*n_out + o] = map[o*K+k] >= 0
+__global__ void pair_flags_kernel(const int32_t* __restrict__ map, int64_t n_out, int K, int64_t* __restrict__ flags) {
+    const int64_t total = n_out * K;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t k = e / n_out, o = e - k * n_out;
+        flags[e] = map[o * K + k] >= 0 ? 1 : 0;
+    }
+}
+
+__global__ void pair_lists_kernel(const int32_t* __restrict__ map, int64_t n_out, int K, const int64_t* __restrict__ incl,
+                                  int32_t* __restrict__ po, int64_t* __restrict__ kstart) {
+    const int64_t total = n_out * K;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t k = e / n_out, o = e - k * n_out;
+        if (map[o * K + k] >= 0) po[incl[e] - 1] = static_cast<int32_t>(o);
+        if (o == 0) kstart[k] = e == 0 ? 0 : incl[e - 1];
+        if (e == total - 1) kstart[K] = incl[e];
+    }
+}
+
+// part[(k*nchunk + ch)][cin][cout] for tile (ci0, co0) of 64x64.
+__global__ void __launch_bounds__(kGemmThreads)
+dweight_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ po, const int64_t* __restrict__ kstart, int K,
+               int nchunk, const float* __restrict__ src, const float* __restrict__ sscale,
+               const float* __restrict__ pscale, const float* __restrict__ g, const float* __restrict__ oscale, int cin,
+               int cout, float* __restrict__ part) {
+    __shared__ float As[64][kKC + 1];  // [ci][pair]
+    __shared__ float Bs[kKC][64];      // [pair][co]
+    __shared__ int32_t Ri[kKC], Ro[kKC];
+    __shared__ float Rs[kKC], Ro_s[kKC];
+    const int k = blockIdx.z / nchunk, ch = blockIdx.z % nchunk;
+    const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
+    const int64_t s = kstart[k], e = kstart[k + 1];
+    const int64_t len = (e - s + nchunk - 1) / nchunk;
+    const int64_t js = s + ch * len;
+    const int64_t je = min(e, js + len);
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int64_t j0 = js; j0 < je; j0 += kKC) {
+        if (t < kKC) {
+            const int64_t j = j0 + t;
+            if (j < je) {
+                const int32_t o = po[j];
+                const int32_t i = map[static_cast<int64_t>(o) * K + k];
+                Ro[t] = o;
+                Ri[t] = i;
+                Rs[t] = (sscale ? sscale[i] : 1.f) * (pscale ? pscale[static_cast<int64_t>(o) * K + k] : 1.f);
+                Ro_s[t] = oscale ? oscale[o] : 1.f;
+            } else {
+                Ro[t] = -1;
+                Ri[t] = -1;
+                Rs[t] = 0.f;
+                Ro_s[t] = 0.f;
+            }
+        }
+        __syncthreads();
+        for (int x = t; x < 64 * kKC; x += kGemmThreads) {
+            const int p = x / 64, c = x - p * 64;  // consecutive threads -> consecutive channels
+            const int32_t i = Ri[p];
+            As[c][p] = (i >= 0 && ci0 + c < cin) ? src[static_cast<int64_t>(i) * cin + ci0 + c] * Rs[p] : 0.f;
+            const int32_t o = Ro[p];
+            Bs[p][c] = (o >= 0 && co0 + c < cout) ? g[static_cast<int64_t>(o) * cout + co0 + c] * Ro_s[p] : 0.f;
+        }
+        __syncthreads();
+        const int ar = wr * 32 + (lane & 31), bc = wc * 32 + (lane & 31), kh = lane >> 5;
+#pragma unroll
+        for (int ss = 0; ss < kKC / 2; ++ss)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[ar][2 * ss + kh], Bs[2 * ss + kh][bc], acc, 0, 0, 0);
+        __syncthreads();
+    }
+    float* P = part + static_cast<int64_t>(blockIdx.z) * cin * cout;
+    const int col = co0 + wc * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = ci0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < cin && col < cout) P[static_cast<int64_t>(row) * cout + col] = acc[r];
+    }
+}
+
+__global__ void reduce_slabs_kernel(const float* __restrict__ part, int K, int nchunk, int64_t slab,
+                                    float* __restrict__ dw) {
+    const int64_t total = static_cast<int64_t>(K) * slab;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t k = e / slab, r = e - k * slab;
+        float s = 0.f;
+        for (int c = 0; c < nchunk; ++c) s += part[(k * nchunk + c) * slab + r];
+        dw[e] = s;
+    }
+}
+
+// kernel index of each (query, input) pair (the rulebook of layers.SparseConv)
+__global__ void kernel_index_kernel(const float* __restrict__ inp_pos, const float* __restrict__ qpos,
+                                    const int32_t* __restrict__ nbr, const int64_t* __restrict__ rs, int64_t n_query,
+                                    int k0, int k1, int k2, float inv_vs, int mirror, int32_t* __restrict__ kidx) {
+    for (int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; q < n_query;
+         q += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const float qx = qpos[3 * q], qy = qpos[3 * q + 1], qz = qpos[3 * q + 2];
+        for (int64_t e = rs[q], ee = rs[q + 1]; e < ee; ++e) {
+            const int64_t i = nbr[e];
+            const float qq[3] = {qx, qy, qz};
+            const int kd[3] = {k2, k1, k0};  // x <-> filter dim 2, z <-> dim 0
+            int id[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const float rel = (inp_pos[3 * i + d] - qq[d]) * inv_vs;
+                const float h = 0.5f * static_cast<float>(kd[d]);
+                int v = static_cast<int>(floorf(mirror ? h - rel : rel + h));
+                v = v < 0 ? 0 : (v >= kd[d] ? kd[d] - 1 : v);
+                id[d] = v;
+            }
+            kidx[e] = (id[2] * k1 + id[1]) * k2 + id[0];
+        }
+    }
+}
+
+template <int TN>
+static void launch_gemm(bool vec4, dim3 g, hipStream_t st, const int32_t* map, int K, int64_t n_out, const float* src,
+                        const float* sscale, const float* pscale, const float* W, int cin, int cout,
+                        const float* oscale, const float* bias, float* out) {
+    if (vec4)
+        implicit_gemm_kernel<TN, true><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
+                                                                   oscale, bias, out);
+    else
+        implicit_gemm_kernel<TN, false><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
+                                                                    oscale, bias, out);
+    O3DML_LAUNCH_CHECK();
+}
+
+static void run_gemm(hipStream_t st, const int32_t* map, int K, int64_t n_out, const float* src, const float* sscale,
+                     const float* pscale, const float* W, int cin, int cout, const float* oscale, const float* bias,
+                     float* out) {
+    if (n_out == 0 || cout == 0) return;
+    const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0;
+    if (cout <= 32) {
+        dim3 g(static_cast<unsigned>(ceil_div(n_out, 128)), 1);
+        launch_gemm<32>(vec4, g, st, map, K, n_out, src, sscale, pscale, W, cin, cout, oscale, bias, out);
+    } else {
+        dim3 g(static_cast<unsigned>(ceil_div(n_out, 64)), static_cast<unsigned>(ceil_div(cout, 64)));
+        launch_gemm<64>(vec4, g, st, map, K, n_out, src, sscale, pscale, W, cin, cout, oscale, bias, out);
+    }
+}
+
+}  // namespace o3dml
+
+using namespace o3dml;
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+O3DML_API size_t o3dml_sparse_conv_map_workspace_size(int64_t n_out, int64_t n_in, int K) {
+    return ws_bytes<int32_t>(n_out * K) + ws_bytes<float>(n_out * K) + ws_bytes<float>(n_out) +
+           ws_bytes<float>(n_out) + ws_bytes<int32_t>(n_in * K) + ws_bytes<float>(n_in * K) + ws_bytes<int>(4);
+}
+
+// Builds the dense kernel map (and, with want_inverse, the inverse map used by
+// the input gradient) from CSR pairs.  Results live at the front of
+// `workspace` (layout: map[n_out*K] i32, pscale[n_out*K] f32, norm[n_out],
+// oscale[n_out], inv[n_in*K] i32, ipscale[n_in*K] f32, status[4]) and are
+// consumed by o3dml_sparse_conv_forward / _backward with the same workspace.
+// status_host[0]: bit0 = duplicate (o,k) pair, bit1 = kernel index out of
+// range (the dense path cannot represent the neighbourhood).
+O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const int32_t* neighbors_kernel_index,
+                                          const float* neighbors_importance, const int64_t* neighbors_row_splits,
+                                          int64_t n_out, int64_t n_in, int K, int normalize,
+                                          const float* out_importance, int want_inverse, int* status_host,
+                                          void* workspace, size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(K >= 1 && K <= 32, "sparse_conv: kernel volume must be in [1, 32] (got %d)", K);
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    int32_t* map = ws.take<int32_t>(n_out * K);
+    float* pscale = ws.take<float>(n_out * K);
+    float* norm = ws.take<float>(n_out);
+    float* oscale = ws.take<float>(n_out);
+    int32_t* inv = ws.take<int32_t>(n_in * K);
+    float* ipscale = ws.take<float>(n_in * K);
+    int* status = ws.take<int>(4);
+    O3DML_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, st));
+    if (n_out > 0) {
+        O3DML_CHECK_HIP(hipMemsetAsync(map, 0xff, sizeof(int32_t) * n_out * K, st));
+        build_kernel_map_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(
+                neighbors_index, neighbors_kernel_index, neighbors_importance, neighbors_row_splits, n_out, K, map,
+                neighbors_importance ? pscale : nullptr, norm, status);
+        O3DML_LAUNCH_CHECK();
+        recip_norm_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(normalize ? norm : nullptr, out_importance, n_out,
+                                                                  oscale);
+        O3DML_LAUNCH_CHECK();
+    }
+    if (want_inverse && n_in > 0) {
+        O3DML_CHECK_HIP(hipMemsetAsync(inv, 0xff, sizeof(int32_t) * n_in * K, st));
+        if (n_out > 0) {
+            build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(
+                    map, neighbors_importance ? pscale : nullptr, n_out, K, inv,
+                    neighbors_importance ? ipscale : nullptr, status);
+            O3DML_LAUNCH_CHECK();
+        }
+    }
+    O3DML_CHECK_HIP(hipMemcpyAsync(status_host, status, sizeof(int), hipMemcpyDeviceToHost, st));
+    O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    O3DML_GUARD_END
+}
+
+static void map_views(void* workspace, size_t bytes, int64_t n_out, int64_t n_in, int K, int32_t** map,
+                      float** pscale, float** oscale, int32_t** inv, float** ipscale) {
+    Workspace ws(workspace, bytes);
+    *map = ws.take<int32_t>(n_out * K);
+    *pscale = ws.take<float>(n_out * K);
+    ws.take<float>(n_out);
+    *oscale = ws.take<float>(n_out);
+    *inv = ws.take<int32_t>(n_in * K);
+    *ipscale = ws.take<float>(n_in * K);
+}
+
+// out [n_out, cout] = oscale * sum_k gather(inp) @ W[k] (+ bias).  filters:
+// [K][cin][cout].  inp_importance (nullable) scales input rows; pair
+// importance / normalisation / out_importance come from the map workspace.
+O3DML_API int o3dml_sparse_conv_forward(const float* filters, int K, int cin, int cout, const float* inp_features,
+                                        int64_t n_in, const float* inp_importance, int has_neighbors_importance,
+                                        int use_out_scale, const float* bias, int64_t n_out, float* out_features,
+                                        void* map_workspace, size_t map_workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    int32_t *map, *inv;
+    float *pscale, *oscale, *ipscale;
+    map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale);
+    run_gemm(as_stream(stream), map, K, n_out, inp_features, inp_importance, has_neighbors_importance ? pscale : nullptr,
+             filters, cin, cout, use_out_scale ? oscale : nullptr, bias, out_features);
+    O3DML_GUARD_END
+}
+
+O3DML_API size_t o3dml_sparse_conv_backward_workspace_size(int64_t n_out, int K, int cin, int cout) {
+    const int nchunk = 16;
+    return ws_bytes<float>(static_cast<int64_t>(K) * cin * cout) + ws_bytes<float>(n_out * cout) +
+           ws_bytes<int64_t>(n_out * K) * 2 + ws_bytes<int32_t>(n_out * K) + ws_bytes<int64_t>(K + 1) +
+           ws_bytes<float>(static_cast<int64_t>(K) * nchunk * cin * cout) + prim::scan_workspace_bytes(n_out * K);
+}
+
+// grad_out [n_out, cout] -> grad_inp [n_in, cin] (nullable) and grad_filters
+// [K][cin][cout] (nullable).  Uses the inverse map (build_map with
+// want_inverse = 1) for grad_inp.
+O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, int cout, const float* inp_features,
+                                         int64_t n_in, const float* inp_importance, int has_neighbors_importance,
+                                         int use_out_scale, const float* grad_out, int64_t n_out, float* grad_inp,
+                                         float* grad_filters, void* map_workspace, size_t map_workspace_bytes,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    hipStream_t st = as_stream(stream);
+    int32_t *map, *inv;
+    float *pscale, *oscale, *ipscale;
+    map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale);
+    Workspace ws(workspace, workspace_bytes);
+    float* wt = ws.take<float>(static_cast<int64_t>(K) * cin * cout);
+    float* g = ws.take<float>(n_out * cout);  // unused slot kept for layout stability
+    (void)g;
+    const float* os = use_out_scale ? oscale : nullptr;
+    if (grad_inp && n_in > 0) {
+        // dIn[i] = sscale[i] * sum_k (g[inv[i,k]] * oscale[o] * pscale) @ W[k]^T
+        transpose_filters_kernel<<<stream_grid(static_cast<int64_t>(K) * cin * cout, 256), 256, 0, st>>>(
+                filters, K, cin, cout, wt);
+        O3DML_LAUNCH_CHECK();
+        // the per-row out-scale belongs to the gathered rows (source = grad_out):
+        // fold it in as sscale; pair importance via the inverse pscale.
+        run_gemm(st, inv, K, n_in, grad_out, os, has_neighbors_importance ? ipscale : nullptr, wt, cout, cin,
+                 inp_importance, nullptr, grad_inp);
+    }
+    if (grad_filters) {
+        const int64_t KC = static_cast<int64_t>(K) * cin * cout;
+        if (n_out == 0) {
+            O3DML_CHECK_HIP(hipMemsetAsync(grad_filters, 0, sizeof(float) * KC, st));
+            return 0;
+        }
+        int64_t* flags = ws.take<int64_t>(n_out * K);
+        int64_t* incl = ws.take<int64_t>(n_out * K);
+        int32_t* po = ws.take<int32_t>(n_out * K);
+        int64_t* kstart = ws.take<int64_t>(K + 1);
+        const int nchunk = 16;
+        float* part = ws.take<float>(static_cast<int64_t>(K) * nchunk * cin * cout);
+        pair_flags_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, n_out, K, flags);
+        O3DML_LAUNCH_CHECK();
+        Workspace sws = ws;
+        prim::scan<int64_t, int64_t>(flags, incl, n_out * K, true, sws, st);
+        pair_lists_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, n_out, K, incl, po, kstart);
+        O3DML_LAUNCH_CHECK();
+        dim3 gg(static_cast<unsigned>(ceil_div(cin, 64)), static_cast<unsigned>(ceil_div(cout, 64)),
+                static_cast<unsigned>(K * nchunk));
+        dweight_kernel<<<gg, kGemmThreads, 0, st>>>(map, po, kstart, K, nchunk, inp_features, inp_importance,
+                                                    has_neighbors_importance ? pscale : nullptr, grad_out, os, cin,
+                                                    cout, part);
+        O3DML_LAUNCH_CHECK();
+        reduce_slabs_kernel<<<stream_grid(KC, 256), 256, 0, st>>>(part, K, nchunk,
+                                                                  static_cast<int64_t>(cin) * cout, grad_filters);
+        O3DML_LAUNCH_CHECK();
+    }
+    O3DML_GUARD_END
+}
+
+// ksize_host[3] = filter dims (k0,k1,k2) = (z,y,x) extents.
+O3DML_API int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* query_positions,
+                                             const int32_t* neighbors_index, const int64_t* neighbors_row_splits,
+                                             int64_t n_query, const int32_t* ksize_host, float voxel_size,
+                                             int mirror, int32_t* kernel_index, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(voxel_size > 0.f, "voxel_size must be > 0");
+    if (n_query == 0) return 0;
+    const float inv = 1.0f / voxel_size;
+    kernel_index_kernel<<<stream_grid(n_query, 256), 256, 0, as_stream(stream)>>>(
+            inp_positions, query_positions, neighbors_index, neighbors_row_splits, n_query, ksize_host[0],
+            ksize_host[1], ksize_host[2], inv, mirror, kernel_index);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}

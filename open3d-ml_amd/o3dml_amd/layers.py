@@ -2,6 +2,7 @@
 import torch
 
 from . import ops
+from . import sparse_conv as sc
 
 
 class FixedRadiusSearch(torch.nn.Module):
@@ -58,3 +59,91 @@ class KNNSearch(torch.nn.Module):
                               index_dtype=self.index_dtype, metric=self.metric,
                               ignore_query_point=self.ignore_query_point,
                               return_distances=self.return_distances)
+
+
+def _voxel_size_scalar(voxel_size, like):
+    if isinstance(voxel_size, torch.Tensor):
+        if voxel_size.dim() != 0 and voxel_size.numel() != 1:
+            raise Exception("voxel_size must be a scalar")
+        return float(voxel_size.reshape(-1)[0])
+    return float(voxel_size)
+
+
+class SparseConv(torch.nn.Module):
+    """Open3D ``layers.SparseConv`` (sparseconvnet.py:344-441).
+
+    Neighbours: FixedRadiusSearch(metric='Linf') of the input positions around
+    queries out_positions - offset*voxel_size with radius kernel_size*vs/2;
+    kernel index of each pair from the relative position; then the MFMA
+    gather-GEMM (ops.sparse_conv) with bias/activation.  Parameters:
+    ``kernel`` [*kernel_size, Cin, Cout], ``bias`` [Cout], ``offset`` [3]
+    (state_dict layout of the reference, load_unet_wts :660-677)."""
+
+    def __init__(self, in_channels, filters, kernel_size, activation=None, use_bias=True,
+                 kernel_initializer=torch.nn.init.xavier_uniform_, bias_initializer=torch.nn.init.zeros_,
+                 normalize=False, offset=None, max_temp_mem_MB=64, **kwargs):
+        super().__init__()
+        self.in_channels = in_channels
+        self.filters = filters
+        self.kernel_size = list(kernel_size)
+        if len(set(self.kernel_size)) != 1 or len(self.kernel_size) != 3:
+            raise ValueError("SparseConv: only cubic 3-D kernels are supported")
+        self.activation = activation
+        self.use_bias = use_bias
+        self.normalize = normalize
+        self.max_temp_mem_MB = max_temp_mem_MB
+        if offset is None:
+            offset = torch.zeros((3,), dtype=torch.float32)
+        self.offset = torch.nn.Parameter(torch.as_tensor(offset, dtype=torch.float32).reshape(3),
+                                         requires_grad=False)
+        self.kernel = torch.nn.Parameter(torch.empty(*self.kernel_size, in_channels, filters))
+        kernel_initializer(self.kernel)
+        if use_bias:
+            self.bias = torch.nn.Parameter(torch.empty(filters))
+            bias_initializer(self.bias)
+        else:
+            self.bias = None
+        self.nns = FixedRadiusSearch(metric="Linf", ignore_query_point=False, return_distances=False)
+
+    def _rulebook(self, inp_positions, out_positions, voxel_size, hash_table, mirror, sign):
+        vs = _voxel_size_scalar(voxel_size, inp_positions)
+        queries = (out_positions - sign * self.offset.to(out_positions.device) * vs).contiguous()
+        radius = 0.5 * vs * self.kernel_size[0]
+        nb = self.nns(inp_positions, queries, radius, hash_table=hash_table)
+        kidx = sc.kernel_index(inp_positions, queries, nb.neighbors_index, nb.neighbors_row_splits,
+                               self.kernel_size, vs, mirror=mirror)
+        self._avg_neighbors = nb.neighbors_index.shape[0] / max(1, out_positions.shape[0])
+        return nb, kidx
+
+    def forward(self, inp_features, inp_positions, out_positions, voxel_size, inp_importance=None,
+                fixed_radius_search_hash_table=None):
+        nb, kidx = self._rulebook(inp_positions, out_positions, voxel_size, fixed_radius_search_hash_table,
+                                  False, 1.0)
+        out = sc.conv_with_bias(self.kernel, self.bias, inp_features, nb.neighbors_index, kidx,
+                                nb.neighbors_row_splits, inp_importance=inp_importance,
+                                normalize=self.normalize)
+        if self.activation:
+            out = self.activation(out)
+        return out
+
+
+class SparseConvTranspose(SparseConv):
+    """Open3D ``layers.SparseConvTranspose`` (sparseconvnet.py:447-482): the
+    adjoint of SparseConv with the same filter indexing — output o receives
+    input i with kernel index k exactly when SparseConv(out->in) would pair
+    them; queries out_positions + offset*voxel_size, mirrored kernel index."""
+
+    def forward(self, inp_features, inp_positions, out_positions, voxel_size, out_importance=None,
+                fixed_radius_search_hash_table=None):
+        if self.normalize:
+            raise NotImplementedError("SparseConvTranspose(normalize=True) is not supported")
+        nb, kidx = self._rulebook(inp_positions, out_positions, voxel_size, fixed_radius_search_hash_table,
+                                  True, -1.0)
+        out = sc.sparse_conv_transpose(self.kernel, out_importance, inp_features, None, None, None,
+                                       nb.neighbors_index, kidx, None, nb.neighbors_row_splits,
+                                       normalize=False)
+        if self.bias is not None:
+            out = out + self.bias
+        if self.activation:
+            out = self.activation(out)
+        return out

@@ -362,3 +362,9 @@ def three_interpolate_grad(grad_out, idx, weights, M):
     out = torch.empty((B, C, int(M)), dtype=torch.float32, device=dev)
     _lib.call("o3dml_three_interpolate_grad", ptr(g), ptr(i), ptr(w), B, C, n, int(M), ptr(out), stream_handle(dev))
     return back_to(out, grad_out)
+
+
+# ---------------------------------------------------------------------------
+# sparse convolution — see sparse_conv.py
+# ---------------------------------------------------------------------------
+from .sparse_conv import sparse_conv, sparse_conv_transpose  # noqa: E402,F401

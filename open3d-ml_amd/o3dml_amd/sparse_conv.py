@@ -1,0 +1,148 @@
+"""Sparse convolution ops with autograd, mirroring
+Open3D's ``ops.sparse_conv`` / ``ops.sparse_conv_transpose`` signatures.
+
+The neighbourhood arrives as CSR pairs over OUTPUT points (neighbors_index,
+neighbors_kernel_index, neighbors_row_splits); the HIP library turns it into a
+dense kernel map and runs the MFMA implicit GEMM (forward), the inverse-map
+GEMM with W^T (input gradient) and split-K slabs (filter gradient)."""
+import numpy as np
+import torch
+
+from . import _lib
+from ._util import gpu_device, ptr, stream_handle, to_dev, workspace
+
+
+def _opt(t, dev, dtype=torch.float32):
+    if t is None or (isinstance(t, torch.Tensor) and t.numel() == 0):
+        return None
+    return to_dev(t, dev, dtype)
+
+
+class _ConvFn(torch.autograd.Function):
+    """out = oscale * sum_k gather(x * sscale * pscale) @ W[k] (+ bias)."""
+
+    @staticmethod
+    def forward(ctx, filters, inp_features, bias, nidx, kidx, nimp, rs, sscale, normalize, out_importance):
+        dev = inp_features.device
+        lib = _lib.load()
+        K = int(np.prod(filters.shape[:-2]))
+        cin, cout = int(filters.shape[-2]), int(filters.shape[-1])
+        if inp_features.dim() != 2 or inp_features.shape[1] != cin:
+            raise RuntimeError(f"sparse_conv: inp_features must be [N, {cin}], got {list(inp_features.shape)}")
+        n_in = inp_features.shape[0]
+        n_out = rs.shape[0] - 1
+        st = stream_handle(dev)
+        mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
+        status = np.zeros(1, np.int32)
+        want_inv = int(inp_features.requires_grad or filters.requires_grad)
+        _lib.call("o3dml_sparse_conv_build_map", ptr(nidx), ptr(kidx), ptr(nimp), ptr(rs), n_out, n_in, K,
+                  int(bool(normalize)), ptr(out_importance), want_inv, status.ctypes.data, ptr(mws), mws.numel(), st)
+        if status[0] & 2:
+            raise RuntimeError("sparse_conv: neighbors_kernel_index out of range for the filter")
+        if status[0] & 1:
+            raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index "
+                               "(non-lattice neighbourhood); not representable by the dense kernel map")
+        W = filters.detach().contiguous()
+        x = inp_features.detach().contiguous()
+        out = torch.empty((n_out, cout), dtype=torch.float32, device=dev)
+        use_os = int(bool(normalize) or out_importance is not None)
+        _lib.call("o3dml_sparse_conv_forward", ptr(W), K, cin, cout, ptr(x), n_in, ptr(sscale), int(nimp is not None),
+                  use_os, ptr(bias.detach().contiguous() if bias is not None else None), n_out, ptr(out), ptr(mws),
+                  mws.numel(), st)
+        ctx.save_for_backward(W, x, mws, sscale if sscale is not None else torch.empty(0, device=dev))
+        ctx.meta = (K, cin, cout, n_in, n_out, nimp is not None, use_os, sscale is not None, bias is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        W, x, mws, sscale = ctx.saved_tensors
+        K, cin, cout, n_in, n_out, has_nimp, use_os, has_ss, has_bias = ctx.meta
+        dev = grad_out.device
+        lib = _lib.load()
+        g = grad_out.contiguous().float()
+        need_x, need_w = ctx.needs_input_grad[1], ctx.needs_input_grad[0]
+        gx = torch.empty((n_in, cin), dtype=torch.float32, device=dev) if need_x else None
+        gw = torch.empty(W.shape, dtype=torch.float32, device=dev) if need_w else None
+        ws = workspace(lib.o3dml_sparse_conv_backward_workspace_size(n_out, K, cin, cout), dev)
+        _lib.call("o3dml_sparse_conv_backward", ptr(W), K, cin, cout, ptr(x), n_in, ptr(sscale) if has_ss else None,
+                  int(has_nimp), use_os, ptr(g), n_out, ptr(gx), ptr(gw), ptr(mws), mws.numel(), ptr(ws), ws.numel(),
+                  stream_handle(dev))
+        gb = g.sum(0) if (has_bias and ctx.needs_input_grad[2]) else None
+        return gw, gx, gb, None, None, None, None, None, None, None
+
+
+def _conv(filters, inp_features, bias, neighbors_index, neighbors_kernel_index, neighbors_importance,
+          neighbors_row_splits, sscale, normalize, out_importance):
+    dev = gpu_device(inp_features, filters)
+    back_cpu = not inp_features.is_cuda
+    f = filters.to(dev) if not filters.is_cuda else filters
+    x = inp_features.to(dev) if back_cpu else inp_features
+    if f.dtype != torch.float32 or x.dtype != torch.float32:
+        raise RuntimeError("sparse_conv: filters and features must be float32")
+    nidx = to_dev(neighbors_index, dev, torch.int32)
+    kidx = to_dev(neighbors_kernel_index, dev, torch.int32)
+    rs = to_dev(neighbors_row_splits, dev, torch.int64)
+    nimp = _opt(neighbors_importance, dev)
+    oimp = _opt(out_importance, dev)
+    b = None if bias is None else (bias.to(dev) if not bias.is_cuda else bias)
+    out = _ConvFn.apply(f, x, b, nidx, kidx, nimp, rs, sscale, bool(normalize), oimp)
+    return out.cpu() if back_cpu else out
+
+
+def sparse_conv(filters, inp_features, inp_importance, neighbors_index, neighbors_kernel_index,
+                neighbors_importance, neighbors_row_splits, normalize=False, max_temp_mem_MB=64):
+    """Open3D ``ops.sparse_conv``: out[o] = sum over o's neighbours n of
+    W[kidx_n]^T (in[idx_n] * inp_importance[idx_n] * neighbors_importance[n]),
+    divided by the neighbour count (or importance sum) if normalize.
+    filters [*kernel_size, Cin, Cout]; empty importance tensors mean none."""
+    dev = gpu_device(inp_features, filters)
+    ss = _opt(inp_importance, dev)
+    return _conv(filters, inp_features, None, neighbors_index, neighbors_kernel_index, neighbors_importance,
+                 neighbors_row_splits, ss, normalize, None)
+
+
+def sparse_conv_transpose(filters, out_importance, inp_features, inp_neighbors_index,
+                          inp_neighbors_importance_sum, inp_neighbors_row_splits, neighbors_index,
+                          neighbors_kernel_index, neighbors_importance, neighbors_row_splits, normalize=False,
+                          max_temp_mem_MB=64):
+    """Open3D ``ops.sparse_conv_transpose``.  neighbors_* is the CSR over the
+    OUTPUT points (their input neighbours, with the kernel index of the pair);
+    inp_neighbors_* is the same relation per INPUT point and, with normalize,
+    each input's contribution is divided by its importance sum (or neighbour
+    count).  out_importance scales the outputs."""
+    dev = gpu_device(inp_features, filters)
+    n_in = inp_features.shape[0]
+    ss = None
+    if normalize:
+        s = _opt(inp_neighbors_importance_sum, dev)
+        if s is None:
+            irs = to_dev(inp_neighbors_row_splits, dev, torch.int64)
+            s = (irs[1:] - irs[:-1]).float()
+        ss = torch.where(s != 0, 1.0 / s, torch.ones_like(s)).contiguous()
+        if ss.numel() != n_in:
+            raise RuntimeError("sparse_conv_transpose: inp_neighbors_* must describe every input point")
+    return _conv(filters, inp_features, None, neighbors_index, neighbors_kernel_index, neighbors_importance,
+                 neighbors_row_splits, ss, False, out_importance)
+
+
+def conv_with_bias(filters, bias, inp_features, neighbors_index, neighbors_kernel_index, neighbors_row_splits,
+                   inp_importance=None, normalize=False):
+    """Fused forward used by the layers: bias added in the MFMA epilogue."""
+    dev = gpu_device(inp_features, filters)
+    return _conv(filters, inp_features, bias, neighbors_index, neighbors_kernel_index, None, neighbors_row_splits,
+                 _opt(inp_importance, dev), normalize, None)
+
+
+def kernel_index(inp_positions, query_positions, neighbors_index, neighbors_row_splits, kernel_size, voxel_size,
+                 mirror=False):
+    """Rulebook of layers.SparseConv: kernel index of every (query, input) pair."""
+    dev = gpu_device(inp_positions, query_positions)
+    ip = to_dev(inp_positions, dev, torch.float32)
+    qp = to_dev(query_positions, dev, torch.float32)
+    ni = to_dev(neighbors_index, dev, torch.int32)
+    rs = to_dev(neighbors_row_splits, dev, torch.int64)
+    ks = np.ascontiguousarray(np.asarray(kernel_size, np.int32).reshape(3))
+    out = torch.empty(ni.shape[0], dtype=torch.int32, device=dev)
+    _lib.call("o3dml_sparse_conv_kernel_index", ptr(ip), ptr(qp), ptr(ni), ptr(rs), qp.shape[0], ks.ctypes.data,
+              float(voxel_size), int(bool(mirror)), ptr(out), stream_handle(dev))
+    return out
