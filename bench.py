@@ -13,9 +13,10 @@ Multi-GPU: one process per GPU (torchrun), scenes are independent, so there is
 no data-path collective ("scaling": "weak"); the only collectives are the
 timing barrier and the max-over-ranks of the elapsed time.
 
-roofline: the dominant kernel (frs fill) timed with events on the stream the
-library launches on; achieved = SURVEY §8d algorithmic bytes
-(12+12+4+8+4m per query) x queries / kernel time.  traffic: HBM bytes per launch
+roofline: per-kernel HIP-event timing inside the library (events recorded on
+the stream each kernel is launched on, o3dml_timing_*); the dominant kernel's
+achieved = SURVEY §8d algorithmic bytes (12+12+4+8+4m per query) x queries /
+its average duration.  traffic: HBM bytes per launch
 from the committed rocprofv3 PMC summary (profiles/), if present.
 cpu_baseline: the C oracle (oracle/, OpenMP) on a bounded sample, rank 0, N=1.
 """
@@ -46,7 +47,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--scenes", type=int, default=64, help="C1-shaped scenes per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel-reps", type=int, default=20)
+    ap.add_argument("--kernel-reps", type=int, default=5)
     return ap.parse_args()
 
 
@@ -58,40 +59,26 @@ def make_batch(rank, scenes, dev):
     return torch.from_numpy(pts).to(dev), torch.from_numpy(rs)
 
 
-def time_fill_kernel(pts, rs, reps):
-    """Average duration of one o3dml_fixed_radius_search_fill launch (HIP events
-    on the library's stream = torch's current stream)."""
-    from o3dml_amd import _lib, ops
-    from o3dml_amd._util import ptr, stream_handle, workspace
-    dev = pts.device
+KERNELS = ("frs_fine_search", "frs_row_sort")
+
+
+def kernel_profile(step, n_queries, pairs, reps):
+    """Per-kernel average durations from the library's HIP-event timing (events
+    recorded on the stream each kernel is launched on), over `reps` steps."""
+    from o3dml_amd import _lib
     lib = _lib.load()
-    n = pts.shape[0]
-    ht = ops.build_spatial_hash_table(pts, RADIUS, rs)
-    prs_d = rs.to(dev)
-    hts_d = ht.hash_table_splits.to(dev)
-    B = rs.numel() - 1
-    st = stream_handle(dev)
-    out_rs = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    ws = workspace(lib.o3dml_fixed_radius_search_workspace_size(n, n), dev)
-    common = (ptr(pts), n, ptr(pts), n, RADIUS, B, ptr(prs_d), ptr(prs_d), ptr(hts_d), ptr(ht.hash_table_index),
-              ptr(ht.hash_table_cell_splits), ptr(ht.hash_table_index), 1, 0)
-    _lib.call("o3dml_fixed_radius_search_count", *common, ptr(out_rs), ptr(ws), ws.numel(), st)
-    total = int(out_rs[-1].item())
-    idx = torch.empty(total, dtype=torch.int32, device=dev)
-    fill = lambda: _lib.call("o3dml_fixed_radius_search_fill", *common, ptr(out_rs), 32, ptr(idx), None,  # noqa
-                             ptr(ws), ws.numel(), st)
-    fill()
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
+    lib.o3dml_timing_reset()
+    lib.o3dml_timing_enable(1)
     for _ in range(reps):
-        fill()
-    e1.record()
-    torch.cuda.synchronize(dev)
-    ms = e0.elapsed_time(e1) / reps
-    mean_nbrs = total / n
-    alg_bytes = n * (12 + 12 + 4 + 8 + 4 * mean_nbrs)
-    return ms, alg_bytes, mean_nbrs
+        step()
+    torch.cuda.synchronize()
+    times = _lib.kernel_times(KERNELS)
+    lib.o3dml_timing_enable(0)
+    avg = {k: (ms / c if c else 0.0) for k, (ms, c) in times.items()}
+    dominant = max(avg, key=avg.get)
+    mean_nbrs = pairs / n_queries
+    alg_bytes = n_queries * (12 + 12 + 4 + 8 + 4 * mean_nbrs)
+    return dominant, avg, alg_bytes, mean_nbrs
 
 
 def load_traffic():
@@ -158,7 +145,8 @@ def main():
     if rank == 0:
         queries_total = world * args.scenes * N_POINTS * args.steps
         value = queries_total / elapsed / 1e6
-        ms, alg_bytes, mean_nbrs = time_fill_kernel(pts, rs, args.kernel_reps)
+        dominant, avg, alg_bytes, mean_nbrs = kernel_profile(step, args.scenes * N_POINTS, pairs, args.kernel_reps)
+        ms = avg[dominant]
         achieved = alg_bytes / (ms * 1e-3) / 1e9
         out = {
             "metric": "Mpoints/s neighbor-search + sparse-conv fwd; RandLA-Net frames/s",
@@ -178,9 +166,10 @@ def main():
                             f"over {args.scenes} scenes/GPU x 65,536 U[0,1)^3 pts, r=0.05, L2, int32 idx",
                 "scenes_per_gpu": args.scenes, "points_per_scene": N_POINTS, "radius": RADIUS,
                 "pairs_per_step_rank0": pairs, "parallelism": f"scene-dp{world}"},
-            "roofline": {"bound": "hbm", "kernel": "frs_kernel<L2,fill>", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic(), "kernel_ms": round(ms, 5),
+                         "kernel_ms_all": {k: round(v, 5) for k, v in avg.items()},
                          "alg_bytes_per_launch": int(alg_bytes), "mean_neighbors": round(mean_nbrs, 3)},
             "cpu_baseline": None,
         }

@@ -31,6 +31,12 @@ extern "C" {
 const char* o3dml_last_error(void);
 int o3dml_version(void);
 int o3dml_device_info(int device, int* cu_count, int* arch_major, int* arch_minor);
+/* Optional kernel timing: HIP events on the launch stream around the main
+ * kernels (names e.g. "frs_fine_count", "frs_fine_fill", "frs_row_sort");
+ * o3dml_timing_get synchronises on the recorded events. */
+void o3dml_timing_enable(int on);
+void o3dml_timing_reset(void);
+int o3dml_timing_get(const char* name, double* total_ms, int64_t* count);
 
 /* ---- spatial hash table: replaces open3d.ml.torch.ops.build_spatial_hash_table
  * (bound by layers.FixedRadiusSearch; ml3d/torch/models/kpconv.py:2021-2023,
@@ -52,26 +58,31 @@ int o3dml_build_spatial_hash_table(const float* points, int64_t n_points, float 
 
 /* ---- fixed radius search: replaces open3d.ml.torch.ops.fixed_radius_search
  * (layers.FixedRadiusSearch; kpconv.py:2016-2034 batch_neighbors, called from
- * ml3d/torch/dataloaders/concat_batcher.py:228,257,261).
- * metric: 0 = L1, 1 = L2, 2 = Linf.  query_order (nullable): thread t handles
- * query query_order[t] (pass hash_table_index for a self search). ------------ */
-size_t o3dml_fixed_radius_search_workspace_size(int64_t n_points, int64_t n_queries);
+ * ml3d/torch/dataloaders/concat_batcher.py:228,257,261; layers.SparseConv's
+ * Linf search, sparseconvnet.py:362-367).  metric: 0 = L1, 1 = L2, 2 = Linf.
+ * Neighbour order per query: Open3D hash bins ascending, point ids ascending
+ * inside a bin (the canonical order).  points_row_splits_host: host copy of
+ * the point row splits; self_search = 1 when queries are the points (same
+ * splits) so the spatial order of the points is reused for the queries;
+ * with_distances must be the same for _count and _fill. ------------------- */
+size_t o3dml_fixed_radius_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t n_batch);
 int o3dml_fixed_radius_search_count(const float* points, int64_t n_points, const float* queries,
                                     int64_t n_queries, float radius, int64_t n_batch,
                                     const int64_t* points_row_splits, const int64_t* queries_row_splits,
-                                    const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
-                                    const uint32_t* hash_table_cell_splits, const uint32_t* query_order,
-                                    int metric, int ignore_query_point, int64_t* neighbors_row_splits,
-                                    void* workspace, size_t workspace_bytes, void* stream);
+                                    const int64_t* points_row_splits_host, const uint32_t* hash_table_splits,
+                                    const uint32_t* hash_table_index, const uint32_t* hash_table_cell_splits,
+                                    int metric, int ignore_query_point, int self_search, int with_distances,
+                                    int64_t* neighbors_row_splits, void* workspace, size_t workspace_bytes,
+                                    void* stream);
 /* index_bits 32 or 64 (index_dtype); neighbors_distance nullable (squared for L2). */
 int o3dml_fixed_radius_search_fill(const float* points, int64_t n_points, const float* queries,
                                    int64_t n_queries, float radius, int64_t n_batch,
                                    const int64_t* points_row_splits, const int64_t* queries_row_splits,
-                                   const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
-                                   const uint32_t* hash_table_cell_splits, const uint32_t* query_order,
-                                   int metric, int ignore_query_point, const int64_t* neighbors_row_splits,
-                                   int index_bits, void* neighbors_index, float* neighbors_distance,
-                                   void* workspace, size_t workspace_bytes, void* stream);
+                                   const int64_t* points_row_splits_host, const uint32_t* hash_table_splits,
+                                   const uint32_t* hash_table_index, const uint32_t* hash_table_cell_splits,
+                                   int metric, int ignore_query_point, int self_search, int with_distances,
+                                   const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
+                                   float* neighbors_distance, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- kNN: replaces open3d.ml.torch.ops.knn_search / layers.KNNSearch
  * (ml3d/torch/models/point_transformer.py:724-729) and

@@ -58,6 +58,30 @@ struct Error {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Optional per-kernel timing (o3dml_timing_enable): HIP events recorded on the
+// launch stream around a region; resolved by o3dml_timing_get.  Off by
+// default (zero cost beyond a flag test).
+bool timing_enabled();
+void timing_record(const char* name, hipEvent_t a, hipEvent_t b);
+
+struct TimedRegion {
+    const char* name;
+    hipStream_t st;
+    hipEvent_t a = nullptr, b = nullptr;
+    TimedRegion(const char* n, hipStream_t s) : name(n), st(s) {
+        if (timing_enabled() && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+            (void)hipEventRecord(a, st);
+        else
+            a = b = nullptr;
+    }
+    ~TimedRegion() {
+        if (a) {
+            (void)hipEventRecord(b, st);
+            timing_record(name, a, b);
+        }
+    }
+};
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Grid size for grid-stride streaming kernels: enough workgroups to fill the

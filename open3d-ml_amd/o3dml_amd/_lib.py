@@ -27,16 +27,19 @@ SIGNATURES = {
     "o3dml_last_error": (ctypes.c_char_p, []),
     "o3dml_version": (c_i32, []),
     "o3dml_device_info": (c_i32, [c_i32, c_p, c_p, c_p]),
+    "o3dml_timing_enable": (None, [c_i32]),
+    "o3dml_timing_reset": (None, []),
+    "o3dml_timing_get": (c_i32, [ctypes.c_char_p, c_p, c_p]),
     # nns_hash.hip
     "o3dml_hash_table_splits": (c_i64, [c_i64, c_p, c_f64, c_i64, c_p]),
     "o3dml_build_spatial_hash_table_workspace_size": (c_sz, [c_i64, c_i64]),
     "o3dml_build_spatial_hash_table": (c_i32, [c_p, c_i64, c_f32, c_i64, c_p, c_p, c_i64, c_p, c_p,
                                                c_p, c_sz, c_p]),
-    "o3dml_fixed_radius_search_workspace_size": (c_sz, [c_i64, c_i64]),
-    "o3dml_fixed_radius_search_count": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p,
-                                                c_p, c_p, c_p, c_i32, c_i32, c_p, c_p, c_sz, c_p]),
-    "o3dml_fixed_radius_search_fill": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p,
-                                               c_p, c_p, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p,
+    "o3dml_fixed_radius_search_workspace_size": (c_sz, [c_i64, c_i64, c_i64]),
+    "o3dml_fixed_radius_search_count": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p, c_p,
+                                                c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_sz, c_p]),
+    "o3dml_fixed_radius_search_fill": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p, c_p,
+                                               c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_p,
                                                c_p, c_sz, c_p]),
     # nns_knn.hip
     "o3dml_knn_search_workspace_size": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
@@ -92,6 +95,19 @@ def load():
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def kernel_times(names):
+    """{name: (total_ms, launches)} recorded since the last o3dml_timing_reset."""
+    import numpy as np
+    lib = load()
+    out = {}
+    for n in names:
+        ms = np.zeros(1, np.float64)
+        cnt = np.zeros(1, np.int64)
+        lib.o3dml_timing_get(n.encode(), ms.ctypes.data, cnt.ctypes.data)
+        out[n] = (float(ms[0]), int(cnt[0]))
+    return out
 
 
 def exported_symbols():

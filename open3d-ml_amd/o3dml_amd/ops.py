@@ -102,13 +102,12 @@ def fixed_radius_search(points, queries, radius, points_row_splits=None, queries
     hts_d = to_dev(hash_table_splits, dev, torch.int32)
     hti_d = to_dev(hash_table_index, dev, torch.int32)
     hcs_d = to_dev(hash_table_cell_splits, dev, torch.int32)
-    order = hti_d if same else None
     B = len(prs) - 1
     st = stream_handle(dev)
     rs = torch.empty(m + 1, dtype=torch.int64, device=dev)
-    ws = workspace(lib.o3dml_fixed_radius_search_workspace_size(n, m), dev)
-    common = (ptr(pts), n, ptr(qry), m, r, B, ptr(prs_d), ptr(qrs_d), ptr(hts_d), ptr(hti_d), ptr(hcs_d),
-              ptr(order), mcode, int(bool(ignore_query_point)))
+    ws = workspace(lib.o3dml_fixed_radius_search_workspace_size(n, m, B), dev)
+    common = (ptr(pts), n, ptr(qry), m, r, B, ptr(prs_d), ptr(qrs_d), prs.ctypes.data, ptr(hts_d), ptr(hti_d),
+              ptr(hcs_d), mcode, int(bool(ignore_query_point)), int(same), int(bool(return_distances)))
     _lib.call("o3dml_fixed_radius_search_count", *common, ptr(rs), ptr(ws), ws.numel(), st)
     total = int(rs[-1].item())
     idx = torch.empty(total, dtype=torch.int32 if bits == 32 else torch.int64, device=dev)

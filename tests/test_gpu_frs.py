@@ -104,3 +104,45 @@ def test_ragged_to_dense_and_reduce(cuda):
     f = rng.standard_normal(rs[-1]).astype(np.float32)
     s = ops.reduce_subarrays_sum(torch.from_numpy(f).to(cuda), torch.from_numpy(rs).to(cuda))
     assert np.array_equal(s.cpu().numpy(), O.reduce_subarrays_sum(f, rs))
+
+
+def test_frs_sparse_scene_hashed_grid(cuda):
+    """Clusters far apart relative to r: the dense grid would be too large, the
+    hashed fine grid path runs (and must still match the oracle bit for bit)."""
+    from o3dml_amd import layers
+    rng = np.random.default_rng(9)
+    c = [rng.random((3000, 3), dtype=np.float32) * 0.5 + off for off in (0.0, 500.0, -800.0)]
+    pts = np.concatenate(c).astype(np.float32)
+    res = layers.FixedRadiusSearch(return_distances=True)(torch.from_numpy(pts).to(cuda),
+                                                          torch.from_numpy(pts).to(cuda), 0.03)
+    oi, ors, od = O.fixed_radius_search(pts, pts, 0.03, return_distances=True)
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+    assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
+
+
+def test_frs_extreme_coordinates_segment_path(cuda):
+    """|coord| / r beyond the fine-grid range: the Open3D-cell segment path runs."""
+    from o3dml_amd import layers
+    rng = np.random.default_rng(10)
+    pts = (rng.random((2000, 3)) * 1e-3 + 3e4).astype(np.float32)
+    pts[1] = pts[0]
+    res = layers.FixedRadiusSearch()(torch.from_numpy(pts).to(cuda), torch.from_numpy(pts).to(cuda), 1e-5)
+    oi, ors, _ = O.fixed_radius_search(pts, pts, 1e-5)
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+
+
+def test_frs_dense_cluster_overflow_rows(cuda):
+    """Rows longer than the 64-entry temp rows take the overflow re-run + long sort."""
+    from o3dml_amd import layers
+    rng = np.random.default_rng(11)
+    pts = np.concatenate([rng.random((3000, 3), dtype=np.float32) * 0.02,
+                          rng.random((5000, 3), dtype=np.float32)]).astype(np.float32)
+    t = torch.from_numpy(pts).to(cuda)
+    res = layers.FixedRadiusSearch(return_distances=True)(t, t, 0.05)
+    oi, ors, od = O.fixed_radius_search(pts, pts, 0.05, return_distances=True)
+    assert np.diff(ors).max() > 2000
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+    assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)

@@ -1,0 +1,136 @@
+"""Import the reference's Python (ml3d) in THIS container for golden-fixture
+generation only (never shipped, never run on the GPU box).
+
+Open3D and a few third-party modules are absent, so
+in-memory stand-ins are registered before ``ml3d`` is imported:
+  * ``open3d.ml.torch.ops`` / ``.layers`` / ``open3d.ml.contrib`` /
+    ``open3d.core.nns`` backed by the CPU oracle (oracle/oracle.py);
+  * ``addict.Dict`` and ``torch.utils.tensorboard`` minimal stubs.
+The models bind these names at import time (kpconv.py:11-13,
+sparseconvnet.py:9-10, point_pillars.py:30, dataprocessing.py:3,6).
+"""
+import os
+import sys
+import types
+from collections import namedtuple
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REFERENCE = "/root/reference"
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle as O  # noqa: E402
+
+
+class _Dict(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError:
+            raise AttributeError(k)
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        for k, v in list(self.items()):
+            if isinstance(v, dict) and not isinstance(v, _Dict):
+                self[k] = _Dict(v)
+
+
+def _mod(name, **attrs):
+    m = types.ModuleType(name)
+    m.__dict__.update(attrs)
+    sys.modules[name] = m
+    return m
+
+
+def _np(t):
+    return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+
+
+# ---- oracle-backed ops with the Open3D signatures -------------------------
+_FRS = namedtuple("fixed_radius_search", ["neighbors_index", "neighbors_row_splits", "neighbors_distance"])
+_VOX = namedtuple("voxelize", ["voxel_coords", "voxel_point_indices", "voxel_point_row_splits",
+                               "voxel_batch_splits"])
+
+
+class FixedRadiusSearch:
+    def __init__(self, metric="L2", ignore_query_point=False, return_distances=False, **kw):
+        self.metric, self.ignore, self.ret = metric, ignore_query_point, return_distances
+
+    def __call__(self, points, queries, radius, points_row_splits=None, queries_row_splits=None,
+                 hash_table_size_factor=1 / 64, hash_table=None):
+        i, rs, d = O.fixed_radius_search(_np(points), _np(queries), float(radius),
+                                         None if points_row_splits is None else _np(points_row_splits),
+                                         None if queries_row_splits is None else _np(queries_row_splits),
+                                         metric=self.metric, ignore_query_point=self.ignore,
+                                         return_distances=self.ret)
+        return _FRS(torch.from_numpy(i), torch.from_numpy(rs), torch.from_numpy(d))
+
+
+def ragged_to_dense(values, row_splits, out_col_size, default_value):
+    v = _np(values)
+    return torch.from_numpy(O.ragged_to_dense(v, _np(row_splits), int(out_col_size),
+                                              _np(default_value).astype(v.dtype)))
+
+
+def voxelize(points, row_splits, voxel_size, points_range_min, points_range_max,
+             max_points_per_voxel=2**63 - 1, max_voxels=2**63 - 1):
+    r = O.voxelize(_np(points), _np(row_splits), _np(voxel_size), _np(points_range_min),
+                   _np(points_range_max), int(max_points_per_voxel), int(max_voxels))
+    return _VOX(*[torch.from_numpy(x) for x in r])
+
+
+def reduce_subarrays_sum(values, row_splits):
+    return torch.from_numpy(O.reduce_subarrays_sum(_np(values), _np(row_splits)))
+
+
+class _NNS:
+    def __init__(self, t):
+        self.pts = t.numpy() if hasattr(t, "numpy") else np.asarray(t)
+
+    def knn_index(self):
+        return True
+
+    def knn_search(self, q, k):
+        q = q.numpy() if hasattr(q, "numpy") else np.asarray(q)
+        i, _, d = O.knn_search(self.pts, q, int(k), return_distances=True, index_dtype=np.int64)
+        T = types.SimpleNamespace
+        return T(numpy=lambda: i.reshape(len(q), k)), T(numpy=lambda: d.reshape(len(q), k))
+
+
+def install():
+    if "ml3d" in sys.modules:
+        return
+    _mod("addict", Dict=_Dict)
+    o3d = _mod("open3d")
+    o3d._build_config = {"BUILD_GUI": False, "BUILD_PYTORCH_OPS": True, "BUILD_TENSORFLOW_OPS": False}
+    o3d.geometry = types.SimpleNamespace()
+    core = _mod("open3d.core")
+    core.cuda = types.SimpleNamespace(device_count=lambda: 0)
+    core.nns = types.SimpleNamespace(NearestNeighborSearch=_NNS)
+    core.Tensor = types.SimpleNamespace(from_numpy=lambda a: types.SimpleNamespace(numpy=lambda: a))
+    o3d.core = core
+    ml = _mod("open3d.ml")
+    o3d.ml = ml
+    contrib = _mod("open3d.ml.contrib", subsample=O.subsample, subsample_batch=O.subsample_batch)
+    contrib.iou_bev_cpu = contrib.iou_3d_cpu = None
+    ml.contrib = contrib
+    mt = _mod("open3d.ml.torch")
+    ops = _mod("open3d.ml.torch.ops", voxelize=voxelize, ragged_to_dense=ragged_to_dense,
+               reduce_subarrays_sum=reduce_subarrays_sum)
+    for n in ["knn_search", "nms", "roi_pool", "trilinear_devoxelize_forward", "trilinear_devoxelize_backward",
+              "furthest_point_sampling", "three_nn", "three_interpolate", "three_interpolate_grad", "ball_query"]:
+        setattr(ops, n, None)
+    lay = _mod("open3d.ml.torch.layers", FixedRadiusSearch=FixedRadiusSearch, SparseConv=None,
+               SparseConvTranspose=None)
+    mt.ops, mt.layers = ops, lay
+    ml.torch = mt
+    _mod("open3d.visualization")
+    _mod("open3d.visualization.tensorboard_plugin", summary=None)
+    _mod("torch.utils.tensorboard", SummaryWriter=None)
+    if REFERENCE not in sys.path:
+        sys.path.insert(0, REFERENCE)
