@@ -108,37 +108,47 @@ def cpu_baseline():
                       f"median of 3, {threads} OpenMP threads"}
 
 
+def timed_run(step, steps, warmup, world, sync):
+    """W untimed warmups, then EXACTLY `steps` timed steps bracketed by
+    barrier + device sync on both sides; returns (max-over-ranks elapsed s,
+    last result).  `sync` synchronises the local device (no-op on CPU)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(steps):
+        res = step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        backend = dist.get_backend()
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, res
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
     from o3dml_amd import layers
     pts, rs = make_batch(rank, args.scenes, dev)
     nns = layers.FixedRadiusSearch()
     step = lambda: nns(pts, pts, RADIUS, rs, rs)  # noqa: E731
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, res = timed_run(step, args.steps, args.warmup, world, lambda: torch.cuda.synchronize(dev))
     pairs = int(res.neighbors_row_splits[-1].item())
 
     out = None

@@ -126,6 +126,18 @@ int o3dml_voxelize_fill(int64_t n_points, int ndim, int64_t n_batch, const float
                         int32_t* voxel_coords, int64_t* voxel_point_indices, int64_t* voxel_point_row_splits,
                         int64_t* voxel_batch_splits, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- calculate_grid: replaces ml3d/torch/models/sparseconvnet.py:388-401
+ * (stride-2 output positions of Convolution, sparseconvnet.py:432).
+ * positions f32 [N,3] -> unique parents 2*floor-even(trunc(p)) + 0.5 of the
+ * inputs whose truncated coords are all >= 0, in lexicographic (x,y,z) order
+ * (torch.unique(dim=0)).  Coordinates must be < 2^21.  _count writes M to
+ * *n_out_host; _fill writes out_positions f32 [M,3]. ----------------------- */
+size_t o3dml_calculate_grid_workspace_size(int64_t n_points);
+int o3dml_calculate_grid_count(const float* positions, int64_t n_points, int64_t* n_out_host, void* workspace,
+                               size_t workspace_bytes, void* stream);
+int o3dml_calculate_grid_fill(int64_t n_points, float* out_positions, void* workspace, size_t workspace_bytes,
+                              void* stream);
+
 /* ---- grid subsampling: replaces open3d.ml.contrib.subsample / subsample_batch
  * (ml3d/datasets/utils/dataprocessing.py:33-49 <- randlanet.py:133-139;
  * kpconv.py:2099-2155 <- dataloaders/concat_batcher.py:245-247).  KPConv

@@ -492,3 +492,131 @@ O3DML_API int o3dml_grid_subsample_fill(const float* points, int64_t n_points, i
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }
+
+// ---------------------------------------------------------------------------
+// calculate_grid (ml3d/torch/models/sparseconvnet.py:388-401)
+// The reference expands each position by {-1,0}^3, keeps non-negative
+// all-even cells and takes torch.unique(dim=0).  Per axis exactly one of
+// {c-1, c} is even, so each input has a single candidate parent: c - (c & 1)
+// with c = trunc(p) (torch .long()), kept iff every c >= 0.  Parents are
+// packed as (x/2, y/2, z/2) 20-bit fields, x most significant, so one radix
+// sort + unique gives the lexicographic order torch.unique returns.
+// ---------------------------------------------------------------------------
+namespace o3dml {
+namespace {
+
+constexpr uint64_t kGridInvalid = uint64_t(1) << 60;
+constexpr int64_t kGridMax = int64_t(1) << 21;
+
+__global__ void grid_parent_kernel(const float* __restrict__ pos, int64_t n, uint64_t* __restrict__ keys,
+                                   int64_t* __restrict__ flags) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        uint64_t key = 0;
+        bool valid = true;
+        for (int d = 0; d < 3; ++d) {
+            const float p = pos[3 * i + d];
+            if (!(p > -1.0f)) {  // trunc(p) < 0 (or NaN): no non-negative parent
+                valid = false;
+                continue;
+            }
+            if (p >= static_cast<float>(kGridMax)) {
+                flags[0] = 1;  // out of the packable range -> host raises
+                valid = false;
+                continue;
+            }
+            const int64_t c = static_cast<int64_t>(p);  // trunc, as torch .long()
+            key = (key << 20) | static_cast<uint64_t>(c >> 1);
+        }
+        keys[i] = valid ? key : kGridInvalid;
+    }
+}
+
+__global__ void grid_unique_heads_kernel(const uint64_t* __restrict__ sk, int64_t n, int64_t* __restrict__ head) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+        head[i] = (sk[i] != kGridInvalid && (i == 0 || sk[i] != sk[i - 1])) ? 1 : 0;
+}
+
+__global__ void grid_unique_write_kernel(const uint64_t* __restrict__ sk, const int64_t* __restrict__ incl, int64_t n,
+                                         float* __restrict__ out) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const uint64_t k = sk[i];
+        if (k == kGridInvalid || (i > 0 && k == sk[i - 1])) continue;
+        const int64_t o = incl[i] - 1;
+        const uint64_t m = (uint64_t(1) << 20) - 1;
+        out[3 * o + 0] = static_cast<float>(static_cast<int64_t>((k >> 40) & m) * 2) + 0.5f;
+        out[3 * o + 1] = static_cast<float>(static_cast<int64_t>((k >> 20) & m) * 2) + 0.5f;
+        out[3 * o + 2] = static_cast<float>(static_cast<int64_t>(k & m) * 2) + 0.5f;
+    }
+}
+
+struct GridState {
+    uint64_t* keys;
+    uint64_t* sk;
+    uint32_t* sidx;
+    int64_t* head;
+    int64_t* incl;
+    int64_t* flags;
+};
+
+inline GridState take_grid_state(Workspace& ws, int64_t n) {
+    GridState g;
+    g.keys = ws.take<uint64_t>(n);
+    g.sk = ws.take<uint64_t>(n);
+    g.sidx = ws.take<uint32_t>(n);
+    g.head = ws.take<int64_t>(n);
+    g.incl = ws.take<int64_t>(n);
+    g.flags = ws.take<int64_t>(2);
+    return g;
+}
+
+}  // namespace
+}  // namespace o3dml
+
+O3DML_API size_t o3dml_calculate_grid_workspace_size(int64_t n_points) {
+    return 2 * ws_bytes<uint64_t>(n_points) + ws_bytes<uint32_t>(n_points) + 2 * ws_bytes<int64_t>(n_points) +
+           ws_bytes<int64_t>(2) +
+           std::max(prim::radix_sort_workspace_bytes<uint64_t>(n_points), prim::scan_workspace_bytes(n_points));
+}
+
+O3DML_API int o3dml_calculate_grid_count(const float* positions, int64_t n_points, int64_t* n_out_host,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    GridState g = take_grid_state(ws, n_points);
+    int64_t host[2] = {0, 0};
+    if (n_points > 0) {
+        O3DML_CHECK_HIP(hipMemsetAsync(g.flags, 0, 2 * sizeof(int64_t), st));
+        const unsigned gr = stream_grid(n_points, 256);
+        grid_parent_kernel<<<gr, 256, 0, st>>>(positions, n_points, g.keys, g.flags);
+        O3DML_LAUNCH_CHECK();
+        Workspace sws = ws;
+        prim::radix_sort_pairs<uint64_t>(g.keys, nullptr, g.sk, g.sidx, n_points, 61, sws, st);
+        grid_unique_heads_kernel<<<gr, 256, 0, st>>>(g.sk, n_points, g.head);
+        O3DML_LAUNCH_CHECK();
+        sws = ws;
+        prim::scan<int64_t, int64_t>(g.head, g.incl, n_points, true, sws, st);
+        O3DML_CHECK_HIP(hipMemcpyAsync(&host[0], g.flags, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        O3DML_CHECK_HIP(hipMemcpyAsync(&host[1], g.incl + n_points - 1, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    }
+    O3DML_REQUIRE(host[0] == 0, "calculate_grid: positions must be < %lld", (long long)kGridMax);
+    *n_out_host = host[1];
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_calculate_grid_fill(int64_t n_points, float* out_positions, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    GridState g = take_grid_state(ws, n_points);
+    if (n_points > 0) {
+        grid_unique_write_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(g.sk, g.incl, n_points, out_positions);
+        O3DML_LAUNCH_CHECK();
+    }
+    O3DML_GUARD_END
+}

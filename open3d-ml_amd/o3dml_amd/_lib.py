@@ -52,6 +52,9 @@ SIGNATURES = {
     "o3dml_voxelize_count": (c_i32, [c_p, c_i64, c_i32, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_sz,
                                      c_p]),
     "o3dml_voxelize_fill": (c_i32, [c_i64, c_i32, c_i64, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "o3dml_calculate_grid_workspace_size": (c_sz, [c_i64]),
+    "o3dml_calculate_grid_count": (c_i32, [c_p, c_i64, c_p, c_p, c_sz, c_p]),
+    "o3dml_calculate_grid_fill": (c_i32, [c_i64, c_p, c_p, c_sz, c_p]),
     "o3dml_grid_subsample_workspace_size": (c_sz, [c_i64, c_i64]),
     "o3dml_grid_subsample_count": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_f32, c_i64, c_p, c_p, c_sz, c_p]),
     "o3dml_grid_subsample_fill": (c_i32, [c_p, c_i64, c_i64, c_p, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_sz,

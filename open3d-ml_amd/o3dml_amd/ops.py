@@ -244,6 +244,24 @@ def voxelize(points, row_splits, voxel_size, points_range_min, points_range_max,
     return VoxelizeResult(back_to(coords, points), back_to(pidx, points), back_to(prs, points), back_to(bsp, points))
 
 
+def calculate_grid(in_positions):
+    """Stride-2 output grid of sparseconvnet ``Convolution`` (reference
+    sparseconvnet.py:388-401): unique all-even non-negative parents of
+    trunc(pos) + {-1,0}^3, lexicographically sorted, + 0.5.  f32 [M,3]."""
+    dev = gpu_device(in_positions)
+    check_points("in_positions", in_positions)
+    lib = _lib.load()
+    n = in_positions.shape[0]
+    pos = to_dev(in_positions, dev)
+    st = stream_handle(dev)
+    ws = workspace(lib.o3dml_calculate_grid_workspace_size(n), dev)
+    m = np.zeros(1, np.int64)
+    _lib.call("o3dml_calculate_grid_count", ptr(pos), n, m.ctypes.data, ptr(ws), ws.numel(), st)
+    out = torch.empty((int(m[0]), 3), dtype=torch.float32, device=dev)
+    _lib.call("o3dml_calculate_grid_fill", n, ptr(out), ptr(ws), ws.numel(), st)
+    return back_to(out, in_positions)
+
+
 # ---------------------------------------------------------------------------
 # grid subsampling (SURVEY §8a A7/A8) — backend of contrib.subsample(_batch)
 # ---------------------------------------------------------------------------
@@ -367,3 +385,9 @@ def three_interpolate_grad(grad_out, idx, weights, M):
 # sparse convolution — see sparse_conv.py
 # ---------------------------------------------------------------------------
 from .sparse_conv import sparse_conv, sparse_conv_transpose  # noqa: E402,F401
+
+
+__all__ = ["build_spatial_hash_table", "fixed_radius_search", "knn_search", "ragged_to_dense",
+           "reduce_subarrays_sum", "voxelize", "grid_subsample", "calculate_grid", "furthest_point_sampling",
+           "ball_query", "three_nn", "three_interpolate", "three_interpolate_grad", "sparse_conv",
+           "sparse_conv_transpose"]

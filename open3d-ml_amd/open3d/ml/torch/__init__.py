@@ -1,2 +1,2 @@
 """open3d.ml.torch: the hot-path ops and layers (o3dml_amd)."""
-from o3dml_amd import layers, ops  # noqa: F401
+from . import layers, ops  # noqa: F401

@@ -353,3 +353,17 @@ def kernel_index(inp_positions, query_positions, neighbors_index, neighbors_row_
                            _p(ks), ctypes.c_float(voxel_size), ctypes.c_int(int(mirror)),
                            _p(out))
     return out
+
+
+def calculate_grid(in_positions):
+    """Literal numpy restatement of sparseconvnet.py:388-401: expand each
+    trunc(pos) by the 8 offsets {-1,0}^3, keep non-negative all-even rows,
+    lexicographic unique, + 0.5."""
+    p = np.trunc(np.asarray(in_positions, np.float32)).astype(np.int64)
+    offs = np.array([[-1, -1, -1], [-1, -1, 0], [-1, 0, -1], [-1, 0, 0],
+                     [0, -1, -1], [0, -1, 0], [0, 0, -1], [0, 0, 0]], np.int64)
+    out = (p[:, None, :] + offs[None]).reshape(-1, 3)
+    out = out[out.min(1) >= 0]
+    out = out[~(out % 2).astype(bool).any(1)]
+    out = np.unique(out, axis=0)
+    return (out + 0.5).astype(np.float32)

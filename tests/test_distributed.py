@@ -1,0 +1,75 @@
+"""World-size-2 rehearsal of bench.py's multi-GPU control path on CPU (gloo):
+scene sharding by rank (no data-path collective), barrier-bracketed timing and
+the max-over-ranks elapsed time every rank agrees on."""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import time
+
+    import bench
+    pts, rs = bench.make_batch(rank, 2, "cpu")
+    calls = []
+
+    def step():
+        calls.append(1)
+        time.sleep(0.02 * (rank + 1))  # rank 1 is the straggler
+        return pts.sum()
+
+    elapsed, res = bench.timed_run(step, 5, 2, world, lambda: None)
+    q.put((rank, elapsed, len(calls), float(pts[0, 0]), int(rs[-1])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_timing_and_sharding():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, e0, c0, x0, n0), (r1, e1, c1, x1, n1) = out
+    assert c0 == c1 == 7  # 2 warmup + exactly 5 timed steps
+    assert e0 == e1  # every rank reports the max over ranks
+    assert e0 >= 5 * 0.04  # ... which is the straggler's time
+    assert x0 != x1  # ranks hold different scenes (seed = rank*100003 + scene)
+    assert n0 == n1 == 2 * bench_points()
+
+
+def bench_points():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench.N_POINTS
+
+
+def test_make_batch_is_rank_seeded():
+    sys.path.insert(0, ROOT)
+    import bench
+    a, rs = bench.make_batch(0, 2, "cpu")
+    b, _ = bench.make_batch(1, 1, "cpu")
+    ref = np.random.default_rng(100003).random((bench.N_POINTS, 3), dtype=np.float32)
+    assert torch.equal(b, torch.from_numpy(ref))
+    assert a.shape == (2 * bench.N_POINTS, 3) and rs.tolist() == [0, bench.N_POINTS, 2 * bench.N_POINTS]
