@@ -9,6 +9,7 @@
 //   A (default) fine r-cell hash grid + per-row sort      (see below)
 //   B (fallback) Open3D-cell segments through LDS windows (cells beyond +-2^30)
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "grid.hpp"
@@ -682,9 +683,290 @@ static void launch_frs(int metric, bool ignore, unsigned grid, hipStream_t st, c
     O3DML_LAUNCH_CHECK();
 }
 
+// ===========================================================================
+// Path G (default): query groups over Open3D's own buckets.
+//
+// Two queries whose 9 visited buckets (own cell + the 8 corners q +- r) are
+// identical visit exactly the same points, in the same order.  A wave takes
+// 64 consecutive queries in bucket order (self search: Open3D's own
+// hash_table_index order), splits them into such groups (typically the
+// queries of one cell octant) and, per group:
+//   1. streams the group's buckets in ascending order — Open3D's visit order —
+//      with coalesced 16-B loads, keeping only points within the metric's
+//      distance of the group's bounding box (the box test uses the same fp32
+//      operations as the exact test on smaller operands, so it can never drop
+//      a neighbour), compacted IN ORDER into an LDS list;
+//   2. tests the list against the group's queries with S = 64 / G lanes per
+//      query (G = group size rounded up to a power of two): lane (g, s)
+//      tests entries s, s + S, ... of query g; a ballot + mbcnt gives every
+//      hit its rank, so rows are written directly in canonical order.
+// No sort, no temp rows, no visit-set check: the candidate list IS Open3D's
+// visit sequence.  Count pass = the same walk with counting only.
+// ===========================================================================
+constexpr int kGroupCap = 256;  // LDS candidate list per wave (float4)
+constexpr int kStreamU = 4;     // 64-point loads in flight per lane while streaming buckets
+
+// Wave-wide float min / max: DPP within rows of 16 lanes, then the 4 row
+// results through v_readlane (uniform result, no LDS round trip).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_min_f(float v) {
+    v = fminf(v, dpp_f<0xB1>(v));   // quad_perm(1,0,3,2)
+    v = fminf(v, dpp_f<0x4E>(v));   // quad_perm(2,3,0,1)
+    v = fminf(v, dpp_f<0x141>(v));  // row_half_mirror
+    v = fminf(v, dpp_f<0x140>(v));  // row_mirror
+    const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return fminf(fminf(a, b), fminf(c, d));
+}
+__device__ __forceinline__ float wave_max_f(float v) { return -wave_min_f(-v); }
+
+// Distance of p to the box [lo, hi] with the metric's own operation order;
+// every operand is <= the corresponding one of dist_metric(p, q) for any q in
+// the box, and each step is monotone, so box_dist <= dist_metric(p, q).
+template <int METRIC>
+__device__ __forceinline__ float box_dist(const float4& p, float lx, float ly, float lz, float hx, float hy,
+                                          float hz) {
+    const float gx = fmaxf(fmaxf(lx - p.x, p.x - hx), 0.f);
+    const float gy = fmaxf(fmaxf(ly - p.y, p.y - hy), 0.f);
+    const float gz = fmaxf(fmaxf(lz - p.z, p.z - hz), 0.f);
+    if constexpr (METRIC == kL2) {
+        return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+    } else if constexpr (METRIC == kL1) {
+        return (gx + gy) + gz;
+    } else {
+        const float m = gx > gy ? gx : gy;
+        return m > gz ? m : gz;
+    }
+}
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+}
+
+template <int METRIC, bool IGNORE, bool DIST, bool FILL, class TIdx>
+__global__ void __launch_bounds__(64)
+frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs, const float4* __restrict__ qpts,
+                 int64_t m, float r, float inv, float thr, int nb, const int64_t* __restrict__ qrs,
+                 const uint32_t* __restrict__ hts, int64_t* __restrict__ counts, const int64_t* __restrict__ rs,
+                 TIdx* __restrict__ out_idx, float* __restrict__ out_dist) {
+    __shared__ float4 cand[kGroupCap];
+    __shared__ float4 qsh[64];
+    __shared__ int64_t qrow[64];
+    const int lane = threadIdx.x;
+    const int64_t nchunks = (m + 63) >> 6;
+    for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+        const int64_t t = (chunk << 6) + lane;
+        const bool valid = t < m;
+        float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        QueryBins qb;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) qb.b[k] = 0xffffffffu;
+        int64_t row = 0;
+        if (valid) {
+            q4 = qpts[t];
+            const uint32_t qid = __float_as_uint(q4.w);
+            const int b = batch_of(qid, qrs, nb);
+            const uint32_t first = hts[b], tsize = hts[b + 1] - first;
+            qb = query_bins(q4.x, q4.y, q4.z, r, inv, first, tsize);
+            if constexpr (FILL) row = rs[qid];
+        }
+        uint64_t todo = __ballot(valid);
+        while (todo) {
+            const int leader = __builtin_ctzll(todo);
+            uint32_t lb[9];
+            bool same = valid;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                lb[k] = __builtin_amdgcn_readlane(qb.b[k], leader);
+                same = same && qb.b[k] == lb[k];
+            }
+            const uint64_t gm = __ballot(same);
+            todo &= ~gm;
+            const int ng = __popcll(gm);
+            __syncthreads();  // previous group done with qsh / cand
+            if (same) {
+                const uint32_t slot = mbcnt64(gm);
+                qsh[slot] = q4;
+                qrow[slot] = row;
+            }
+            // group bounding box
+            const float inf = __builtin_huge_valf();
+            const float lx = wave_min_f(same ? q4.x : inf), ly = wave_min_f(same ? q4.y : inf),
+                        lz = wave_min_f(same ? q4.z : inf);
+            const float hx = wave_max_f(same ? q4.x : -inf), hy = wave_max_f(same ? q4.y : -inf),
+                        hz = wave_max_f(same ? q4.z : -inf);
+            // lane -> (query g, slice s)
+            const int lg = ng <= 1 ? 0 : 32 - __builtin_clz(static_cast<uint32_t>(ng - 1));  // log2 G
+            const int ls = 6 - lg;                                                         // log2 S
+            const int S = 1 << ls;
+            const int g = lane >> ls, sl = lane & (S - 1);
+            const bool active = g < ng;
+            const uint64_t gmask = ls == 6 ? ~0ull : (((1ull << S) - 1ull) << (g << ls));
+            __syncthreads();
+            float4 mq = make_float4(0.f, 0.f, 0.f, 0.f);
+            int64_t mrow = 0;
+            if (active) {
+                mq = qsh[g];
+                mrow = qrow[g];
+            }
+            int64_t cnt = 0;
+            int nc = 0;
+            // test the LDS list against the group's queries, in order
+            auto consume = [&]() {
+                __syncthreads();
+                for (int e0 = 0; e0 < nc; e0 += S) {
+                    const int e = e0 + sl;
+                    bool hit = false;
+                    float d = 0.f;
+                    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (active && e < nc) {
+                        p = cand[e];
+                        d = dist_metric<METRIC>(p.x, p.y, p.z, mq.x, mq.y, mq.z);
+                        hit = d <= thr && !(IGNORE && p.x == mq.x && p.y == mq.y && p.z == mq.z);
+                    }
+                    if constexpr (FILL) {
+                        const uint64_t mine = __ballot(hit) & gmask;
+                        if (hit) {
+                            const int64_t o = mrow + cnt + mbcnt64(mine);
+                            out_idx[o] = static_cast<TIdx>(__float_as_uint(p.w));
+                            if constexpr (DIST) out_dist[o] = d;
+                        }
+                        cnt += __popcll(mine);
+                    } else {
+                        cnt += hit ? 1 : 0;
+                    }
+                }
+                __syncthreads();
+                nc = 0;
+            };
+            // stream the group's buckets (ascending, deduplicated)
+            uint32_t start[9], pre[10];
+            pre[0] = 0;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                start[k] = cs[lb[k]];
+                const uint32_t len = (k == 0 || lb[k] != lb[k - 1]) ? cs[lb[k] + 1] - start[k] : 0u;
+                pre[k + 1] = pre[k] + len;
+            }
+            const uint32_t total = pre[9];
+            for (uint32_t f0 = 0; f0 < total; f0 += 64 * kStreamU) {
+                float4 c[kStreamU];
+                bool in[kStreamU];
+#pragma unroll
+                for (int u = 0; u < kStreamU; ++u) {  // all loads of the round in flight
+                    const uint32_t f = f0 + u * 64 + lane;
+                    in[u] = f < total;
+                    uint32_t src = 0;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k)
+                        if (f >= pre[k]) src = start[k] + (f - pre[k]);
+                    c[u] = in[u] ? pts[src] : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+#pragma unroll
+                for (int u = 0; u < kStreamU; ++u) {
+                    const bool keep = in[u] && box_dist<METRIC>(c[u], lx, ly, lz, hx, hy, hz) <= thr;
+                    const uint64_t km = __ballot(keep);
+                    if (nc + 64 > kGroupCap) consume();
+                    if (keep) cand[nc + mbcnt64(km)] = c[u];
+                    nc += __popcll(km);
+                }
+            }
+            if (nc > 0) consume();
+            if constexpr (!FILL) {
+                for (int o = S >> 1; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                if (active && sl == 0) counts[__float_as_uint(mq.w)] = cnt;
+            }
+        }
+    }
+}
+
+__global__ void set_scalars_kernel(int64_t* s, int64_t a, int64_t b, int64_t c, int64_t d) {
+    s[0] = a;
+    s[1] = b;
+    s[2] = c;
+    s[3] = d;
+}
+
+// Query order for path G: (bucket of the query's own cell, 8-bit hash of its
+// sorted 9-bucket visit list).  Queries with identical visit lists (one group)
+// become adjacent, so a 64-query chunk holds few, large groups.  Any order is
+// correct — grouping inside the kernel compares the full lists.
+__global__ void group_query_keys_kernel(const float* __restrict__ queries, int64_t m, float r, float inv,
+                                        int n_batch, const int64_t* __restrict__ qrs,
+                                        const uint32_t* __restrict__ hts, int hash_bits,
+                                        uint32_t* __restrict__ keys) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < m;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int b = batch_of(i, qrs, n_batch);
+        const uint32_t first = hts[b], tsize = hts[b + 1] - first;
+        const float qx = queries[3 * i], qy = queries[3 * i + 1], qz = queries[3 * i + 2];
+        const QueryBins qb = query_bins(qx, qy, qz, r, inv, first, tsize);
+        uint32_t h = 0x9E3779B9u;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) h = (h ^ qb.b[k]) * 0x01000193u;
+        h ^= h >> 15;
+        h *= 0x2C1B3C6Du;
+        h ^= h >> 13;
+        const uint32_t own = first + point_bin(qx, qy, qz, inv, tsize);
+        keys[i] = hash_bits > 0 ? (own << hash_bits) | (h >> (32 - hash_bits)) : own;
+    }
+}
+
+// Queries not identical to the points: key = bucket of the query's own cell.
+__global__ void query_bin_keys_kernel(const float* __restrict__ queries, int64_t m, float inv, int n_batch,
+                                      const int64_t* __restrict__ qrs, const uint32_t* __restrict__ hts,
+                                      uint32_t* __restrict__ keys) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < m;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int b = batch_of(i, qrs, n_batch);
+        const uint32_t first = hts[b], tsize = hts[b + 1] - first;
+        keys[i] = first + point_bin(queries[3 * i], queries[3 * i + 1], queries[3 * i + 2], inv, tsize);
+    }
+}
+
+template <bool FILL, class TIdx>
+static void launch_group(int metric, bool ignore, bool with_dist, hipStream_t st, const float4* pts,
+                         const uint32_t* cs, const float4* qpts, int64_t m, float r, float inv, float thr, int nb,
+                         const int64_t* qrs, const uint32_t* hts, int64_t* counts, const int64_t* rs, TIdx* idx,
+                         float* dist) {
+    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((m + 63) / 64, 1 << 20)));
+#define O3DML_GRP(M, I, D)                                                                                     \
+    frs_group_kernel<M, I, D, FILL, TIdx><<<grid, 64, 0, st>>>(pts, cs, qpts, m, r, inv, thr, nb, qrs, hts,     \
+                                                                counts, rs, idx, dist)
+#define O3DML_GRP_D(M, I)              \
+    do {                               \
+        if (with_dist)                 \
+            O3DML_GRP(M, I, true);     \
+        else                           \
+            O3DML_GRP(M, I, false);    \
+    } while (0)
+    if (metric == kL2) {
+        if (ignore) O3DML_GRP_D(kL2, true); else O3DML_GRP_D(kL2, false);
+    } else if (metric == kL1) {
+        if (ignore) O3DML_GRP_D(kL1, true); else O3DML_GRP_D(kL1, false);
+    } else {
+        if (ignore) O3DML_GRP_D(kLinf, true); else O3DML_GRP_D(kLinf, false);
+    }
+#undef O3DML_GRP_D
+#undef O3DML_GRP
+    O3DML_LAUNCH_CHECK();
+}
+
+static bool frs_legacy() {
+    const char* e = std::getenv("O3DML_FRS_PATH");
+    return e && e[0] == 'l';  // "legacy": fine r-cell grid + row sort (comparison only)
+}
+
 // Search plan kept in the workspace between _count and _fill.
 struct FrsPlan {
     float4* pts;
+    float4* qpts;
     uint64_t* keys;
     uint64_t* skeys;
     uint32_t* qord;
@@ -697,6 +979,7 @@ struct FrsPlan {
 static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m) {
     FrsPlan p;
     p.pts = ws.take<float4>(n);
+    p.qpts = ws.take<float4>(m);
     p.keys = ws.take<uint64_t>(m);
     p.skeys = ws.take<uint64_t>(m);
     p.qord = ws.take<uint32_t>(m);
@@ -708,7 +991,7 @@ static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m) {
 }
 
 static size_t plan_bytes(int64_t n, int64_t m) {
-    return ws_bytes<float4>(n) + 2 * ws_bytes<uint64_t>(m) + ws_bytes<uint32_t>(m) + 2 * ws_bytes<int64_t>(m) +
+    return ws_bytes<float4>(n) + ws_bytes<float4>(m) + 2 * ws_bytes<uint64_t>(m) + ws_bytes<uint32_t>(m) + 2 * ws_bytes<int64_t>(m) +
            ws_bytes<int32_t>(m) + ws_bytes<int64_t>(2);
 }
 
@@ -851,6 +1134,42 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     }
     const float thr = metric == kL2 ? radius * radius : radius;
     const float inv = 1.0f / (2.0f * radius);
+    if (!frs_legacy()) {
+        // ---- path G: query groups over Open3D's buckets (no host sync)
+        set_scalars_kernel<<<1, 1, 0, st>>>(fp.scalars, 3, 0, 0, 0);
+        O3DML_LAUNCH_CHECK();
+        gather_sorted_points_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points,
+                                                                               pl.pts);
+        O3DML_LAUNCH_CHECK();
+        uint32_t tb = 0;
+        O3DML_CHECK_HIP(hipMemcpyAsync(&tb, hash_table_splits + n_batch, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                       st));
+        O3DML_CHECK_HIP(hipStreamSynchronize(st));
+        const int bin_bits = prim::bits_needed(tb > 0 ? tb - 1 : 0);
+        const int hash_bits = std::max(0, std::min(8, 32 - bin_bits));
+        group_query_keys_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(
+                queries, n_queries, radius, inv, (int)n_batch, queries_row_splits, hash_table_splits, hash_bits,
+                fp.keys);
+        O3DML_LAUNCH_CHECK();
+        {
+            Workspace sws = ws;
+            prim::radix_sort_pairs<uint32_t>(fp.keys, nullptr, fp.skeys, fp.qorder, n_queries, bin_bits + hash_bits,
+                                             sws, st);
+        }
+        gather_sorted_points_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(queries, fp.qorder, n_queries,
+                                                                                pl.qpts);
+        O3DML_LAUNCH_CHECK();
+        const float4* qp = pl.qpts;
+        {
+            TimedRegion tr("frs_group_count", st);
+            launch_group<false, int32_t>(metric, ignore_query_point != 0, false, st, pl.pts, hash_table_cell_splits,
+                                         qp, n_queries, radius, inv, thr, (int)n_batch, queries_row_splits,
+                                         hash_table_splits, fp.counts, nullptr, nullptr, nullptr);
+        }
+        Workspace sws = ws;
+        prim::scan<int64_t, int64_t>(fp.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
+        return 0;
+    }
     // ---- plan: bounding boxes -> dense grid / hashed fine grid / segments
     bbox_kernel<<<static_cast<unsigned>(n_batch), 256, 0, st>>>(points, points_row_splits, fp.bbox);
     O3DML_LAUNCH_CHECK();
@@ -1013,6 +1332,21 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
     const float inv = 1.0f / (2.0f * radius);
     int64_t* rs = const_cast<int64_t*>(neighbors_row_splits);
     float* dist = with_distances ? neighbors_distance : nullptr;
+    if (sc[0] == 3) {
+        const float4* qp = pl.qpts;
+        TimedRegion tr("frs_group_fill", st);
+        if (index_bits == 32)
+            launch_group<true, int32_t>(metric, ignore_query_point != 0, dist != nullptr, st, pl.pts,
+                                        hash_table_cell_splits, qp, n_queries, radius, inv, thr, (int)n_batch,
+                                        queries_row_splits, hash_table_splits, nullptr, rs,
+                                        static_cast<int32_t*>(neighbors_index), dist);
+        else
+            launch_group<true, int64_t>(metric, ignore_query_point != 0, dist != nullptr, st, pl.pts,
+                                        hash_table_cell_splits, qp, n_queries, radius, inv, thr, (int)n_batch,
+                                        queries_row_splits, hash_table_splits, nullptr, rs,
+                                        static_cast<int64_t*>(neighbors_index), dist);
+        return 0;
+    }
     if (sc[0] == 0 || sc[0] == 2) {
         const bool dense = sc[0] == 0;
         const double inv_h = 1.0 / static_cast<double>(radius);
