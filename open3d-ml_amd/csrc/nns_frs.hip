@@ -749,16 +749,25 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
 }
 
-template <int METRIC, bool IGNORE, bool DIST, bool FILL, class TIdx>
+// MODE 0: every query of the (sorted) query array; its first kRowCap
+//         neighbours go to temp row qid, the full count to counts[qid]; ids of
+//         queries with more than kRowCap neighbours are listed in `over` for
+//         a MODE 1 re-run.
+// MODE 1: the queries of qpts[0 .. *m_dev) written straight into the final
+//         rows at rs[qid].
+template <int METRIC, bool IGNORE, bool DIST, int MODE, class TIdx>
 __global__ void __launch_bounds__(64)
 frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs, const float4* __restrict__ qpts,
-                 int64_t m, float r, float inv, float thr, int nb, const int64_t* __restrict__ qrs,
-                 const uint32_t* __restrict__ hts, int64_t* __restrict__ counts, const int64_t* __restrict__ rs,
-                 TIdx* __restrict__ out_idx, float* __restrict__ out_dist) {
+                 int64_t m_host, const int64_t* __restrict__ m_dev, float r, float inv, float thr, int nb,
+                 const int64_t* __restrict__ qrs, const uint32_t* __restrict__ hts, int64_t* __restrict__ counts,
+                 uint32_t* __restrict__ tidx, float* __restrict__ tdist, uint32_t* __restrict__ over,
+                 int64_t* __restrict__ n_over, const int64_t* __restrict__ rs, TIdx* __restrict__ out_idx,
+                 float* __restrict__ out_dist) {
     __shared__ float4 cand[kGroupCap];
     __shared__ float4 qsh[64];
     __shared__ int64_t qrow[64];
     const int lane = threadIdx.x;
+    const int64_t m = m_dev ? *m_dev : m_host;
     const int64_t nchunks = (m + 63) >> 6;
     for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
         const int64_t t = (chunk << 6) + lane;
@@ -774,7 +783,7 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
             const int b = batch_of(qid, qrs, nb);
             const uint32_t first = hts[b], tsize = hts[b + 1] - first;
             qb = query_bins(q4.x, q4.y, q4.z, r, inv, first, tsize);
-            if constexpr (FILL) row = rs[qid];
+            row = MODE == 0 ? static_cast<int64_t>(qid) : rs[qid];
         }
         uint64_t todo = __ballot(valid);
         while (todo) {
@@ -817,7 +826,8 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
             }
             int64_t cnt = 0;
             int nc = 0;
-            // test the LDS list against the group's queries, in order
+            // test the LDS list against the group's queries, in order; hits are
+            // ranked by ballot so every row is written in canonical order
             auto consume = [&]() {
                 __syncthreads();
                 for (int e0 = 0; e0 < nc; e0 += S) {
@@ -830,22 +840,25 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
                         d = dist_metric<METRIC>(p.x, p.y, p.z, mq.x, mq.y, mq.z);
                         hit = d <= thr && !(IGNORE && p.x == mq.x && p.y == mq.y && p.z == mq.z);
                     }
-                    if constexpr (FILL) {
-                        const uint64_t mine = __ballot(hit) & gmask;
-                        if (hit) {
-                            const int64_t o = mrow + cnt + mbcnt64(mine);
-                            out_idx[o] = static_cast<TIdx>(__float_as_uint(p.w));
-                            if constexpr (DIST) out_dist[o] = d;
+                    const uint64_t mine = __ballot(hit) & gmask;
+                    if (hit) {
+                        const int64_t pos = cnt + mbcnt64(mine);
+                        if constexpr (MODE == 0) {
+                            if (pos < kRowCap) {
+                                tidx[mrow * kRowCap + pos] = __float_as_uint(p.w);
+                                if constexpr (DIST) tdist[mrow * kRowCap + pos] = d;
+                            }
+                        } else {
+                            out_idx[mrow + pos] = static_cast<TIdx>(__float_as_uint(p.w));
+                            if constexpr (DIST) out_dist[mrow + pos] = d;
                         }
-                        cnt += __popcll(mine);
-                    } else {
-                        cnt += hit ? 1 : 0;
                     }
+                    cnt += __popcll(mine);
                 }
                 __syncthreads();
                 nc = 0;
             };
-            // stream the group's buckets (ascending, deduplicated)
+            // stream the group's buckets (ascending, deduplicated): Open3D's visit order
             uint32_t start[9], pre[10];
             pre[0] = 0;
 #pragma unroll
@@ -878,11 +891,72 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
                 }
             }
             if (nc > 0) consume();
-            if constexpr (!FILL) {
-                for (int o = S >> 1; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-                if (active && sl == 0) counts[__float_as_uint(mq.w)] = cnt;
+            if constexpr (MODE == 0) {
+                if (active && sl == 0) {
+                    counts[__float_as_uint(mq.w)] = cnt;
+                    if (cnt > kRowCap)
+                        over[atomicAdd(reinterpret_cast<unsigned long long*>(n_over), 1ull)] =
+                                static_cast<uint32_t>(mrow);
+                }
             }
         }
+    }
+}
+
+// Final rows from the temp rows of path G (already in canonical order, temp
+// row = query id, so both sides stream in order).  A wave owns 64
+// consecutive rows: every lane fetches one row's (count, row start), then the
+// wave copies the rows 8 at a time with all 8 loads in flight, lanes =
+// entries.  Rows longer than kRowCap are written by the MODE 1 re-run.
+template <bool DIST, class TIdx>
+__global__ void __launch_bounds__(256) group_rows_copy_kernel(int64_t m, const int64_t* __restrict__ counts,
+                                                              const int64_t* __restrict__ rs,
+                                                              const uint32_t* __restrict__ tidx,
+                                                              const float* __restrict__ tdist,
+                                                              TIdx* __restrict__ idx, float* __restrict__ dist) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    for (int64_t base = wave * 64; base < m; base += nwaves * 64) {
+        const int64_t t = base + lane;
+        int n = 0;
+        if (t < m) {
+            const int64_t c = counts[t];
+            n = c <= kRowCap ? static_cast<int>(c) : 0;
+        }
+        const int rows = static_cast<int>(m - base < 64 ? m - base : 64);
+        for (int k = 0; k < rows; k += 8) {
+            uint32_t v[8];
+            float dv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int nn = __builtin_amdgcn_readlane(n, k + u);
+                const bool ok = k + u < rows && lane < nn;
+                const int64_t src = (base + k + u) * kRowCap + lane;
+                v[u] = ok ? tidx[src] : 0u;
+                if constexpr (DIST) dv[u] = ok ? tdist[src] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int nn = __builtin_amdgcn_readlane(n, k + u);
+                if (k + u < rows && lane < nn) {
+                    const int64_t oo = rs[base + k + u] + lane;
+                    idx[oo] = static_cast<TIdx>(v[u]);
+                    if constexpr (DIST) dist[oo] = dv[u];
+                }
+            }
+        }
+    }
+}
+
+// Overflow re-run input: the listed queries (ids) as (x, y, z, id).
+__global__ void gather_over_kernel(const float* __restrict__ queries, const uint32_t* __restrict__ over,
+                                   const int64_t* __restrict__ n_over, float4* __restrict__ out) {
+    const int64_t n = *n_over;
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t q = over[i];
+        out[i] = make_float4(queries[3 * q], queries[3 * q + 1], queries[3 * q + 2], __uint_as_float(over[i]));
     }
 }
 
@@ -930,15 +1004,14 @@ __global__ void query_bin_keys_kernel(const float* __restrict__ queries, int64_t
     }
 }
 
-template <bool FILL, class TIdx>
-static void launch_group(int metric, bool ignore, bool with_dist, hipStream_t st, const float4* pts,
-                         const uint32_t* cs, const float4* qpts, int64_t m, float r, float inv, float thr, int nb,
-                         const int64_t* qrs, const uint32_t* hts, int64_t* counts, const int64_t* rs, TIdx* idx,
-                         float* dist) {
-    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((m + 63) / 64, 1 << 20)));
-#define O3DML_GRP(M, I, D)                                                                                     \
-    frs_group_kernel<M, I, D, FILL, TIdx><<<grid, 64, 0, st>>>(pts, cs, qpts, m, r, inv, thr, nb, qrs, hts,     \
-                                                                counts, rs, idx, dist)
+template <int MODE, class TIdx>
+static void launch_group(int metric, bool ignore, bool with_dist, hipStream_t st, unsigned grid, const float4* pts,
+                         const uint32_t* cs, const float4* qpts, int64_t m, const int64_t* m_dev, float r, float inv,
+                         float thr, int nb, const int64_t* qrs, const uint32_t* hts, int64_t* counts, uint32_t* tidx,
+                         float* tdist, uint32_t* over, int64_t* n_over, const int64_t* rs, TIdx* idx, float* dist) {
+#define O3DML_GRP(M, I, D)                                                                                      \
+    frs_group_kernel<M, I, D, MODE, TIdx><<<grid, 64, 0, st>>>(pts, cs, qpts, m, m_dev, r, inv, thr, nb, qrs, hts, \
+                                                                counts, tidx, tdist, over, n_over, rs, idx, dist)
 #define O3DML_GRP_D(M, I)              \
     do {                               \
         if (with_dist)                 \
@@ -967,6 +1040,7 @@ static bool frs_legacy() {
 struct FrsPlan {
     float4* pts;
     float4* qpts;
+    float4* pts_over;
     uint64_t* keys;
     uint64_t* skeys;
     uint32_t* qord;
@@ -980,6 +1054,7 @@ static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m) {
     FrsPlan p;
     p.pts = ws.take<float4>(n);
     p.qpts = ws.take<float4>(m);
+    p.pts_over = ws.take<float4>(m);
     p.keys = ws.take<uint64_t>(m);
     p.skeys = ws.take<uint64_t>(m);
     p.qord = ws.take<uint32_t>(m);
@@ -991,7 +1066,7 @@ static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m) {
 }
 
 static size_t plan_bytes(int64_t n, int64_t m) {
-    return ws_bytes<float4>(n) + ws_bytes<float4>(m) + 2 * ws_bytes<uint64_t>(m) + ws_bytes<uint32_t>(m) + 2 * ws_bytes<int64_t>(m) +
+    return ws_bytes<float4>(n) + 2 * ws_bytes<float4>(m) + 2 * ws_bytes<uint64_t>(m) + ws_bytes<uint32_t>(m) + 2 * ws_bytes<int64_t>(m) +
            ws_bytes<int32_t>(m) + ws_bytes<int64_t>(2);
 }
 
@@ -1161,10 +1236,12 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
         O3DML_LAUNCH_CHECK();
         const float4* qp = pl.qpts;
         {
-            TimedRegion tr("frs_group_count", st);
-            launch_group<false, int32_t>(metric, ignore_query_point != 0, false, st, pl.pts, hash_table_cell_splits,
-                                         qp, n_queries, radius, inv, thr, (int)n_batch, queries_row_splits,
-                                         hash_table_splits, fp.counts, nullptr, nullptr, nullptr);
+            TimedRegion tr("frs_group_search", st);
+            launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0, st,
+                                     static_cast<unsigned>(std::min<int64_t>((n_queries + 63) / 64, 1 << 20)), pl.pts,
+                                     hash_table_cell_splits, qp, n_queries, nullptr, radius, inv, thr, (int)n_batch,
+                                     queries_row_splits, hash_table_splits, fp.counts, fp.tpos, fp.tdist, fp.over,
+                                     fp.scalars + 2, nullptr, nullptr, nullptr);
         }
         Workspace sws = ws;
         prim::scan<int64_t, int64_t>(fp.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
@@ -1333,18 +1410,38 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
     int64_t* rs = const_cast<int64_t*>(neighbors_row_splits);
     float* dist = with_distances ? neighbors_distance : nullptr;
     if (sc[0] == 3) {
-        const float4* qp = pl.qpts;
-        TimedRegion tr("frs_group_fill", st);
-        if (index_bits == 32)
-            launch_group<true, int32_t>(metric, ignore_query_point != 0, dist != nullptr, st, pl.pts,
-                                        hash_table_cell_splits, qp, n_queries, radius, inv, thr, (int)n_batch,
-                                        queries_row_splits, hash_table_splits, nullptr, rs,
-                                        static_cast<int32_t*>(neighbors_index), dist);
-        else
-            launch_group<true, int64_t>(metric, ignore_query_point != 0, dist != nullptr, st, pl.pts,
-                                        hash_table_cell_splits, qp, n_queries, radius, inv, thr, (int)n_batch,
-                                        queries_row_splits, hash_table_splits, nullptr, rs,
-                                        static_cast<int64_t*>(neighbors_index), dist);
+        {
+            TimedRegion tr("frs_group_rows", st);
+            const unsigned gc = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_queries, 256), 1 << 16)));
+#define O3DML_GCOPY(T)                                                                                            \
+    do {                                                                                                          \
+        if (dist)                                                                                                 \
+            group_rows_copy_kernel<true, T><<<gc, 256, 0, st>>>(n_queries, fp.counts, rs, fp.tpos,      \
+                                                                fp.tdist, static_cast<T*>(neighbors_index), dist); \
+        else                                                                                                      \
+            group_rows_copy_kernel<false, T><<<gc, 256, 0, st>>>(n_queries, fp.counts, rs, fp.tpos,     \
+                                                                 nullptr, static_cast<T*>(neighbors_index), nullptr); \
+    } while (0)
+            if (index_bits == 32) O3DML_GCOPY(int32_t); else O3DML_GCOPY(int64_t);
+#undef O3DML_GCOPY
+            O3DML_LAUNCH_CHECK();
+        }
+        if (sc[2] > 0) {  // rows longer than kRowCap: re-run those queries into the final rows
+            const int64_t n_over = sc[2];
+            gather_over_kernel<<<stream_grid(n_over, 256), 256, 0, st>>>(queries, fp.over, fp.scalars + 2, pl.pts_over);
+            O3DML_LAUNCH_CHECK();
+            const unsigned go = static_cast<unsigned>(std::min<int64_t>((n_over + 63) / 64, 1 << 20));
+            if (index_bits == 32)
+                launch_group<1, int32_t>(metric, ignore_query_point != 0, dist != nullptr, st, go, pl.pts,
+                                         hash_table_cell_splits, pl.pts_over, n_over, nullptr, radius, inv, thr,
+                                         (int)n_batch, queries_row_splits, hash_table_splits, nullptr, nullptr,
+                                         nullptr, nullptr, nullptr, rs, static_cast<int32_t*>(neighbors_index), dist);
+            else
+                launch_group<1, int64_t>(metric, ignore_query_point != 0, dist != nullptr, st, go, pl.pts,
+                                         hash_table_cell_splits, pl.pts_over, n_over, nullptr, radius, inv, thr,
+                                         (int)n_batch, queries_row_splits, hash_table_splits, nullptr, nullptr,
+                                         nullptr, nullptr, nullptr, rs, static_cast<int64_t*>(neighbors_index), dist);
+        }
         return 0;
     }
     if (sc[0] == 0 || sc[0] == 2) {
