@@ -703,8 +703,11 @@ static void launch_frs(int metric, bool ignore, unsigned grid, hipStream_t st, c
 // No sort, no temp rows, no visit-set check: the candidate list IS Open3D's
 // visit sequence.  Count pass = the same walk with counting only.
 // ===========================================================================
+#ifndef O3DML_DIAG
+#define O3DML_DIAG 0
+#endif
 constexpr int kGroupCap = 256;  // LDS candidate list per wave (float4)
-constexpr int kStreamU = 4;     // 64-point loads in flight per lane while streaming buckets
+constexpr int kStreamU = 2;     // 64-point loads in flight per lane while streaming buckets
 
 // Wave-wide float min / max: DPP within rows of 16 lanes, then the 4 row
 // results through v_readlane (uniform result, no LDS round trip).
@@ -769,7 +772,13 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
     const int lane = threadIdx.x;
     const int64_t m = m_dev ? *m_dev : m_host;
     const int64_t nchunks = (m + 63) >> 6;
-    for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    // XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so block b
+    // takes chunk (b % 8) * per + b / 8 — every XCD sweeps one contiguous,
+    // spatially coherent range and its L2 keeps the shared buckets.
+    const int64_t per = (nchunks + 7) >> 3;
+    const bool xcd_map = gridDim.x >= 8 * per;  // host launches 8 * per blocks when it can
+    int64_t chunk = xcd_map ? static_cast<int64_t>(blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
+    for (; chunk < nchunks; chunk = xcd_map ? nchunks : chunk + gridDim.x) {
         const int64_t t = (chunk << 6) + lane;
         const bool valid = t < m;
         float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -816,7 +825,6 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
             const int S = 1 << ls;
             const int g = lane >> ls, sl = lane & (S - 1);
             const bool active = g < ng;
-            const uint64_t gmask = ls == 6 ? ~0ull : (((1ull << S) - 1ull) << (g << ls));
             __syncthreads();
             float4 mq = make_float4(0.f, 0.f, 0.f, 0.f);
             int64_t mrow = 0;
@@ -824,73 +832,84 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
                 mq = qsh[g];
                 mrow = qrow[g];
             }
-            int64_t cnt = 0;
+            int cnt = 0;  // neighbours of query g so far (uniform over its S lanes)
             int nc = 0;
-            // test the LDS list against the group's queries, in order; hits are
-            // ranked by ballot so every row is written in canonical order
-            auto consume = [&]() {
-                __syncthreads();
-                for (int e0 = 0; e0 < nc; e0 += S) {
-                    const int e = e0 + sl;
-                    bool hit = false;
-                    float d = 0.f;
-                    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (active && e < nc) {
-                        p = cand[e];
-                        d = dist_metric<METRIC>(p.x, p.y, p.z, mq.x, mq.y, mq.z);
-                        hit = d <= thr && !(IGNORE && p.x == mq.x && p.y == mq.y && p.z == mq.z);
-                    }
-                    const uint64_t mine = __ballot(hit) & gmask;
-                    if (hit) {
-                        const int64_t pos = cnt + mbcnt64(mine);
-                        if constexpr (MODE == 0) {
-                            if (pos < kRowCap) {
-                                tidx[mrow * kRowCap + pos] = __float_as_uint(p.w);
-                                if constexpr (DIST) tdist[mrow * kRowCap + pos] = d;
-                            }
-                        } else {
-                            out_idx[mrow + pos] = static_cast<TIdx>(__float_as_uint(p.w));
-                            if constexpr (DIST) out_dist[mrow + pos] = d;
-                        }
-                    }
-                    cnt += __popcll(mine);
-                }
-                __syncthreads();
-                nc = 0;
-            };
+            uint32_t* const trow = MODE == 0 ? tidx + mrow * kRowCap : nullptr;
+            float* const tdrow = (MODE == 0 && DIST) ? tdist + mrow * kRowCap : nullptr;
+            const uint64_t gmask = ls == 6 ? ~0ull : (((1ull << S) - 1ull) << (g << ls));
+            const uint32_t gm_lo = static_cast<uint32_t>(gmask), gm_hi = static_cast<uint32_t>(gmask >> 32);
             // stream the group's buckets (ascending, deduplicated): Open3D's visit order
-            uint32_t start[9], pre[10];
+            uint32_t pre[10];
+            int32_t delta[9];  // bucket start - flat offset
             pre[0] = 0;
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
-                start[k] = cs[lb[k]];
-                const uint32_t len = (k == 0 || lb[k] != lb[k - 1]) ? cs[lb[k] + 1] - start[k] : 0u;
+                const uint32_t s0 = cs[lb[k]];
+                const uint32_t len = (k == 0 || lb[k] != lb[k - 1]) ? cs[lb[k] + 1] - s0 : 0u;
+                delta[k] = static_cast<int32_t>(s0 - pre[k]);
                 pre[k + 1] = pre[k] + len;
             }
             const uint32_t total = pre[9];
-            for (uint32_t f0 = 0; f0 < total; f0 += 64 * kStreamU) {
-                float4 c[kStreamU];
-                bool in[kStreamU];
+            uint32_t f0 = 0;
+            while (true) {
+                // 1. fill the LDS list: rounds of kStreamU x 64 loads, all in flight
+                while (f0 < total && nc + 64 * kStreamU <= kGroupCap) {
+                    float4 c[kStreamU];
 #pragma unroll
-                for (int u = 0; u < kStreamU; ++u) {  // all loads of the round in flight
-                    const uint32_t f = f0 + u * 64 + lane;
-                    in[u] = f < total;
-                    uint32_t src = 0;
+                    for (int u = 0; u < kStreamU; ++u) {
+                        const uint32_t f = f0 + u * 64 + lane;
+                        int32_t dl = delta[0];
 #pragma unroll
-                    for (int k = 0; k < 9; ++k)
-                        if (f >= pre[k]) src = start[k] + (f - pre[k]);
-                    c[u] = in[u] ? pts[src] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        for (int k = 1; k < 9; ++k) dl = f >= pre[k] ? delta[k] : dl;
+                        c[u] = pts[f < total ? static_cast<uint32_t>(static_cast<int32_t>(f) + dl) : 0u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kStreamU; ++u) {
+                        const bool keep = f0 + u * 64 + lane < total &&
+                                          box_dist<METRIC>(c[u], lx, ly, lz, hx, hy, hz) <= thr;
+                        const uint64_t km = __ballot(keep);
+                        if (keep) cand[nc + mbcnt64(km)] = c[u];
+                        nc += __popcll(km);
+                    }
+                    f0 += 64 * kStreamU;
                 }
+                // 2. test the list against the group's queries, in order; hits are
+                //    ranked by ballot so every row is written in canonical order
+                __syncthreads();
+#if O3DML_DIAG != 1
+                for (int e0 = 0; e0 < nc; e0 += 4 * S) {
+                    float4 p[4];
 #pragma unroll
-                for (int u = 0; u < kStreamU; ++u) {
-                    const bool keep = in[u] && box_dist<METRIC>(c[u], lx, ly, lz, hx, hy, hz) <= thr;
-                    const uint64_t km = __ballot(keep);
-                    if (nc + 64 > kGroupCap) consume();
-                    if (keep) cand[nc + mbcnt64(km)] = c[u];
-                    nc += __popcll(km);
+                    for (int u = 0; u < 4; ++u) p[u] = cand[(e0 + u * S + sl) & (kGroupCap - 1)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float d = dist_metric<METRIC>(p[u].x, p[u].y, p[u].z, mq.x, mq.y, mq.z);
+                        const bool hit = active && e0 + u * S + sl < nc && d <= thr &&
+                                         !(IGNORE && p[u].x == mq.x && p[u].y == mq.y && p[u].z == mq.z);
+                        const uint64_t bal = __ballot(hit);
+                        const uint32_t mlo = static_cast<uint32_t>(bal) & gm_lo;
+                        const uint32_t mhi = static_cast<uint32_t>(bal >> 32) & gm_hi;
+                        if (hit) {
+                            const int pos = cnt + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                                                      mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u)));
+                            if constexpr (MODE == 0) {
+                                if (pos < kRowCap) {
+                                    trow[pos] = __float_as_uint(p[u].w);
+                                    if constexpr (DIST) tdrow[pos] = d;
+                                }
+                            } else {
+                                out_idx[mrow + pos] = static_cast<TIdx>(__float_as_uint(p[u].w));
+                                if constexpr (DIST) out_dist[mrow + pos] = d;
+                            }
+                        }
+                        cnt += __popc(mlo) + __popc(mhi);
+                    }
                 }
+#endif
+                __syncthreads();
+                nc = 0;
+                if (f0 >= total) break;
             }
-            if (nc > 0) consume();
             if constexpr (MODE == 0) {
                 if (active && sl == 0) {
                     counts[__float_as_uint(mq.w)] = cnt;
@@ -967,28 +986,32 @@ __global__ void set_scalars_kernel(int64_t* s, int64_t a, int64_t b, int64_t c, 
     s[3] = d;
 }
 
-// Query order for path G: (bucket of the query's own cell, 8-bit hash of its
-// sorted 9-bucket visit list).  Queries with identical visit lists (one group)
-// become adjacent, so a 64-query chunk holds few, large groups.  Any order is
-// correct — grouping inside the kernel compares the full lists.
-__global__ void group_query_keys_kernel(const float* __restrict__ queries, int64_t m, float r, float inv,
-                                        int n_batch, const int64_t* __restrict__ qrs,
-                                        const uint32_t* __restrict__ hts, int hash_bits,
-                                        uint32_t* __restrict__ keys) {
+// Query order for path G: (batch, Morton code of the query's r-cell) — the
+// lowest Morton level is the octant of the Open3D 2r-cell, so queries with
+// identical visit lists (one group) are adjacent, and consecutive chunks are
+// spatial neighbours that share buckets in L2.  Cell coordinates wrap modulo
+// 2^bits (locality only; any order is correct — grouping inside the kernel
+// compares the full bucket lists).
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 10 bits -> every third bit
+    v &= 0x3ffu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__global__ void group_query_keys_kernel(const float* __restrict__ queries, int64_t m, float inv2, int n_batch,
+                                        const int64_t* __restrict__ qrs, int cell_bits, uint32_t* __restrict__ keys) {
+    const uint32_t mask = (1u << cell_bits) - 1u;
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < m;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int b = batch_of(i, qrs, n_batch);
-        const uint32_t first = hts[b], tsize = hts[b + 1] - first;
-        const float qx = queries[3 * i], qy = queries[3 * i + 1], qz = queries[3 * i + 2];
-        const QueryBins qb = query_bins(qx, qy, qz, r, inv, first, tsize);
-        uint32_t h = 0x9E3779B9u;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) h = (h ^ qb.b[k]) * 0x01000193u;
-        h ^= h >> 15;
-        h *= 0x2C1B3C6Du;
-        h ^= h >> 13;
-        const uint32_t own = first + point_bin(qx, qy, qz, inv, tsize);
-        keys[i] = hash_bits > 0 ? (own << hash_bits) | (h >> (32 - hash_bits)) : own;
+        const uint32_t cx = static_cast<uint32_t>(static_cast<int32_t>(floorf(queries[3 * i] * inv2))) & mask;
+        const uint32_t cy = static_cast<uint32_t>(static_cast<int32_t>(floorf(queries[3 * i + 1] * inv2))) & mask;
+        const uint32_t cz = static_cast<uint32_t>(static_cast<int32_t>(floorf(queries[3 * i + 2] * inv2))) & mask;
+        const uint32_t mort = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
+        keys[i] = (static_cast<uint32_t>(b) << (3 * cell_bits)) | mort;
     }
 }
 
@@ -1002,6 +1025,11 @@ __global__ void query_bin_keys_kernel(const float* __restrict__ queries, int64_t
         const uint32_t first = hts[b], tsize = hts[b + 1] - first;
         keys[i] = first + point_bin(queries[3 * i], queries[3 * i + 1], queries[3 * i + 2], inv, tsize);
     }
+}
+
+static unsigned group_grid(int64_t m) {
+    const int64_t per = ((m + 63) / 64 + 7) / 8;
+    return static_cast<unsigned>(std::max<int64_t>(8, std::min<int64_t>(8 * per, 1 << 20)));
 }
 
 template <int MODE, class TIdx>
@@ -1216,20 +1244,15 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
         gather_sorted_points_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points,
                                                                                pl.pts);
         O3DML_LAUNCH_CHECK();
-        uint32_t tb = 0;
-        O3DML_CHECK_HIP(hipMemcpyAsync(&tb, hash_table_splits + n_batch, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                       st));
-        O3DML_CHECK_HIP(hipStreamSynchronize(st));
-        const int bin_bits = prim::bits_needed(tb > 0 ? tb - 1 : 0);
-        const int hash_bits = std::max(0, std::min(8, 32 - bin_bits));
+        const int batch_bits = prim::bits_needed(static_cast<uint64_t>(n_batch - 1));
+        const int cell_bits = std::max(1, std::min(10, (32 - batch_bits) / 3));
         group_query_keys_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(
-                queries, n_queries, radius, inv, (int)n_batch, queries_row_splits, hash_table_splits, hash_bits,
-                fp.keys);
+                queries, n_queries, 2.0f * inv, (int)n_batch, queries_row_splits, cell_bits, fp.keys);
         O3DML_LAUNCH_CHECK();
         {
             Workspace sws = ws;
-            prim::radix_sort_pairs<uint32_t>(fp.keys, nullptr, fp.skeys, fp.qorder, n_queries, bin_bits + hash_bits,
-                                             sws, st);
+            prim::radix_sort_pairs<uint32_t>(fp.keys, nullptr, fp.skeys, fp.qorder, n_queries,
+                                             batch_bits + 3 * cell_bits, sws, st);
         }
         gather_sorted_points_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(queries, fp.qorder, n_queries,
                                                                                 pl.qpts);
@@ -1238,7 +1261,7 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
         {
             TimedRegion tr("frs_group_search", st);
             launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0, st,
-                                     static_cast<unsigned>(std::min<int64_t>((n_queries + 63) / 64, 1 << 20)), pl.pts,
+                                     group_grid(n_queries), pl.pts,
                                      hash_table_cell_splits, qp, n_queries, nullptr, radius, inv, thr, (int)n_batch,
                                      queries_row_splits, hash_table_splits, fp.counts, fp.tpos, fp.tdist, fp.over,
                                      fp.scalars + 2, nullptr, nullptr, nullptr);
@@ -1430,7 +1453,7 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
             const int64_t n_over = sc[2];
             gather_over_kernel<<<stream_grid(n_over, 256), 256, 0, st>>>(queries, fp.over, fp.scalars + 2, pl.pts_over);
             O3DML_LAUNCH_CHECK();
-            const unsigned go = static_cast<unsigned>(std::min<int64_t>((n_over + 63) / 64, 1 << 20));
+            const unsigned go = group_grid(n_over);
             if (index_bits == 32)
                 launch_group<1, int32_t>(metric, ignore_query_point != 0, dist != nullptr, st, go, pl.pts,
                                          hash_table_cell_splits, pl.pts_over, n_over, nullptr, radius, inv, thr,
