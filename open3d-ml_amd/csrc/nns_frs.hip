@@ -706,8 +706,14 @@ static void launch_frs(int metric, bool ignore, unsigned grid, hipStream_t st, c
 #ifndef O3DML_DIAG
 #define O3DML_DIAG 0
 #endif
-constexpr int kGroupCap = 256;  // LDS candidate list per wave (float4)
-constexpr int kStreamU = 2;     // 64-point loads in flight per lane while streaming buckets
+#ifndef O3DML_GROUP_CAP
+#define O3DML_GROUP_CAP 256
+#endif
+#ifndef O3DML_STREAM_U
+#define O3DML_STREAM_U 2
+#endif
+constexpr int kGroupCap = O3DML_GROUP_CAP;  // LDS candidate list per wave (float4)
+constexpr int kStreamU = O3DML_STREAM_U;    // 64-point loads in flight per lane while streaming buckets
 
 // Wave-wide float min / max: DPP within rows of 16 lanes, then the 4 row
 // results through v_readlane (uniform result, no LDS round trip).

@@ -141,24 +141,42 @@ __global__ void __launch_bounds__(kRsBlock) radix_hist(const K* __restrict__ key
 
 // Stable scatter: rows of 256 keys are ranked in order; inside a row the
 // rank is (earlier waves) + (earlier lanes with the same digit), found with
-// eight 64-bit ballots per key.
+// eight 64-bit ballots per key.  Keys are first placed in LDS in tile-local
+// digit order (tile digit offsets = exclusive scan of this tile's histogram),
+// then written out in LDS order: consecutive threads write consecutive
+// addresses of each digit run, so the global writes coalesce.
 template <class K>
 __global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                           K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                           int64_t n, int shift,
                                                           const int64_t* __restrict__ offsets,
-                                                          int64_t tiles) {
+                                                          const uint32_t* __restrict__ hist, int64_t tiles) {
     __shared__ uint32_t wcnt[kRsWaves][256];
     __shared__ uint32_t running[256];
+    __shared__ uint32_t toff[256];
     __shared__ int64_t goff[256];
+    __shared__ K lkey[kRsTile];
+    __shared__ uint32_t lval[kRsTile];
     const int t = threadIdx.x;
     const int w = wave_id();
-    running[t] = 0;
-    goff[t] = offsets[static_cast<int64_t>(t) * tiles + blockIdx.x];
-#pragma unroll
-    for (int ww = 0; ww < kRsWaves; ++ww) wcnt[ww][t] = 0;
-    __syncthreads();
     const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile;
+    const int tile_n = static_cast<int>(n - base < kRsTile ? n - base : kRsTile);
+    {
+        // tile digit offsets: exclusive scan of this tile's histogram
+        const uint32_t c = hist[static_cast<int64_t>(t) * tiles + blockIdx.x];
+        const uint32_t inc = wave_inclusive_scan(c);
+        if (lane_id() == 63) wcnt[0][w] = inc;
+        __syncthreads();
+        uint32_t before = 0;
+        for (int ww = 0; ww < w; ++ww) before += wcnt[0][ww];
+        toff[t] = before + inc - c;
+        goff[t] = offsets[static_cast<int64_t>(t) * tiles + blockIdx.x];
+        running[t] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int ww = 0; ww < kRsWaves; ++ww) wcnt[ww][t] = 0;
+        __syncthreads();
+    }
     const uint64_t lt = lanemask_lt();
     for (int r = 0; r < kRsItems; ++r) {
         const int64_t i = base + r * kRsBlock + t;
@@ -188,14 +206,21 @@ __global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* __restrict__ 
         }
         __syncthreads();
         if (valid) {
-            const int64_t pos = goff[d] + wcnt[w][d] + rank;
-            kout[pos] = key;
-            vout[pos] = val;
+            const uint32_t lp = toff[d] + wcnt[w][d] + rank;
+            lkey[lp] = key;
+            lval[lp] = val;
         }
         __syncthreads();
 #pragma unroll
         for (int ww = 0; ww < kRsWaves; ++ww) wcnt[ww][t] = 0;
         __syncthreads();
+    }
+    for (int j = t; j < tile_n; j += kRsBlock) {
+        const K key = lkey[j];
+        const uint32_t d = static_cast<uint32_t>(key >> shift) & 255u;
+        const int64_t pos = goff[d] + (j - static_cast<int64_t>(toff[d]));
+        kout[pos] = key;
+        vout[pos] = lval[j];
     }
 }
 
@@ -252,7 +277,7 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
         Workspace sws = ws;  // scan scratch is transient per pass
         scan<uint32_t, int64_t>(hist, offs, 256 * tiles, false, sws, st);
         radix_scatter<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift,
-                                                                          offs, tiles);
+                                                                          offs, hist, tiles);
         O3DML_LAUNCH_CHECK();
         ksrc = kdst;
         vsrc = vdst;
