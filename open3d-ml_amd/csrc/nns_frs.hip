@@ -777,7 +777,8 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
     __shared__ int64_t qrow[64];
     const int lane = threadIdx.x;
     const int64_t m = m_dev ? *m_dev : m_host;
-    const int64_t nchunks = (m + 63) >> 6;
+    // MODE 1 (few, long rows): one query per wave, so the re-runs proceed in parallel
+    const int64_t nchunks = MODE == 0 ? (m + 63) >> 6 : m;
     // XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so block b
     // takes chunk (b % 8) * per + b / 8 — every XCD sweeps one contiguous,
     // spatially coherent range and its L2 keeps the shared buckets.
@@ -785,8 +786,8 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
     const bool xcd_map = gridDim.x >= 8 * per;  // host launches 8 * per blocks when it can
     int64_t chunk = xcd_map ? static_cast<int64_t>(blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
     for (; chunk < nchunks; chunk = xcd_map ? nchunks : chunk + gridDim.x) {
-        const int64_t t = (chunk << 6) + lane;
-        const bool valid = t < m;
+        const int64_t t = MODE == 0 ? (chunk << 6) + lane : chunk;
+        const bool valid = t < m && (MODE == 0 || lane == 0);
         float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f);
         QueryBins qb;
 #pragma unroll
@@ -939,35 +940,52 @@ __global__ void __launch_bounds__(256) group_rows_copy_kernel(int64_t m, const i
                                                               const uint32_t* __restrict__ tidx,
                                                               const float* __restrict__ tdist,
                                                               TIdx* __restrict__ idx, float* __restrict__ dist) {
+    // lane = (row r of 4, quarter-row qq of 16): 16-B loads of 4 entries from the
+    // 256-B temp row, 4 consecutive stores; 8 rows in flight per wave
     const int lane = threadIdx.x & 63;
+    const int sub = lane >> 4, qq = lane & 15;
     const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    const uint4* __restrict__ t4 = reinterpret_cast<const uint4*>(tidx);
+    const float4* __restrict__ d4 = reinterpret_cast<const float4*>(tdist);
     for (int64_t base = wave * 64; base < m; base += nwaves * 64) {
         const int64_t t = base + lane;
         int n = 0;
+        int64_t o = 0;
         if (t < m) {
             const int64_t c = counts[t];
             n = c <= kRowCap ? static_cast<int>(c) : 0;
+            o = rs[t];
         }
-        const int rows = static_cast<int>(m - base < 64 ? m - base : 64);
-        for (int k = 0; k < rows; k += 8) {
-            uint32_t v[8];
-            float dv[8];
+        for (int k = 0; k < 64; k += 8) {
+            uint4 v[2];
+            float4 dv[2];
+            int nn[2];
+            int64_t oo[2];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int nn = __builtin_amdgcn_readlane(n, k + u);
-                const bool ok = k + u < rows && lane < nn;
-                const int64_t src = (base + k + u) * kRowCap + lane;
-                v[u] = ok ? tidx[src] : 0u;
-                if constexpr (DIST) dv[u] = ok ? tdist[src] : 0.f;
+            for (int u = 0; u < 2; ++u) {
+                const int rr = k + u * 4 + sub;
+                nn[u] = __shfl(n, rr, 64);
+                oo[u] = __shfl(o, rr, 64);
+                const bool ok = base + rr < m && qq * 4 < nn[u];
+                const int64_t src = (base + rr) * (kRowCap / 4) + qq;
+                v[u] = ok ? t4[src] : make_uint4(0u, 0u, 0u, 0u);
+                if constexpr (DIST) dv[u] = ok ? d4[src] : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int nn = __builtin_amdgcn_readlane(n, k + u);
-                if (k + u < rows && lane < nn) {
-                    const int64_t oo = rs[base + k + u] + lane;
-                    idx[oo] = static_cast<TIdx>(v[u]);
-                    if constexpr (DIST) dist[oo] = dv[u];
+            for (int u = 0; u < 2; ++u) {
+                const int rr = k + u * 4 + sub;
+                if (base + rr < m) {
+                    const int j0 = qq * 4;
+                    const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                    const float dd[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        if (j0 + e < nn[u]) {
+                            idx[oo[u] + j0 + e] = static_cast<TIdx>(vv[e]);
+                            if constexpr (DIST) dist[oo[u] + j0 + e] = dd[e];
+                        }
+                    }
                 }
             }
         }
@@ -1033,8 +1051,8 @@ __global__ void query_bin_keys_kernel(const float* __restrict__ queries, int64_t
     }
 }
 
-static unsigned group_grid(int64_t m) {
-    const int64_t per = ((m + 63) / 64 + 7) / 8;
+static unsigned group_grid(int64_t m, int queries_per_wave = 64) {
+    const int64_t per = ((m + queries_per_wave - 1) / queries_per_wave + 7) / 8;
     return static_cast<unsigned>(std::max<int64_t>(8, std::min<int64_t>(8 * per, 1 << 20)));
 }
 
@@ -1459,7 +1477,7 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
             const int64_t n_over = sc[2];
             gather_over_kernel<<<stream_grid(n_over, 256), 256, 0, st>>>(queries, fp.over, fp.scalars + 2, pl.pts_over);
             O3DML_LAUNCH_CHECK();
-            const unsigned go = group_grid(n_over);
+            const unsigned go = group_grid(n_over, 1);
             if (index_bits == 32)
                 launch_group<1, int32_t>(metric, ignore_query_point != 0, dist != nullptr, st, go, pl.pts,
                                          hash_table_cell_splits, pl.pts_over, n_over, nullptr, radius, inv, thr,
