@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--scenes", type=int, default=64, help="C1-shaped scenes per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
+    ap.add_argument("--randla-frames", type=int, default=3, help="RandLA-Net frames timed (0: skip)")
     return ap.parse_args()
 
 
@@ -106,6 +107,50 @@ def cpu_baseline():
             "kind": "port",
             "sample": f"oracle fixed_radius_search (hash build + count + fill), one 65,536-pt C1 scene, "
                       f"median of 3, {threads} OpenMP threads"}
+
+
+def make_scan(seed):
+    """C2 synthetic 64-beam scan: elevations -24.8..+2 deg x 1,875
+    azimuths = 120,000 rays; ground at z = -1.73 m, one wall per azimuth at
+    U(8, 60) m, 2 cm noise, shuffled; labels U{0..19}."""
+    rng = np.random.default_rng(seed)
+    el = np.deg2rad(np.linspace(-24.8, 2.0, 64))
+    az = np.linspace(0, 2 * np.pi, 1875, endpoint=False)
+    wall = rng.uniform(8, 60, az.shape[0])
+    E, A = np.meshgrid(el, az, indexing="ij")
+    W = np.broadcast_to(wall, E.shape)
+    r_wall = W / np.cos(E)
+    with np.errstate(divide="ignore"):
+        r_ground = np.where(E < 0, 1.73 / np.tan(-E), np.inf)
+    rr = np.minimum(r_wall, r_ground)
+    pts = np.stack([rr * np.cos(E) * np.cos(A), rr * np.cos(E) * np.sin(A), rr * np.sin(E)], -1).reshape(-1, 3)
+    pts = pts + rng.normal(0, 0.02, pts.shape)
+    pts = pts[rng.permutation(pts.shape[0])].astype(np.float32)
+    return pts, rng.integers(0, 20, pts.shape[0]).astype(np.int32)
+
+
+def randla_frames(dev, frames):
+    """RandLA-Net GPU inference (SemSegInference, randlanet_semantickitti.yml:
+    45,056-pt patches, k=16, 4 layers, grid 0.06, random-init weights) on C2
+    scans: one frame = the full possibility loop until every sub-point > 0.5."""
+    from o3dml_amd.randlanet import RandLANet, SemSegInference
+    torch.manual_seed(0)
+    model = RandLANet(num_points=45056, num_classes=19).to(dev).eval()
+    scans = [torch.from_numpy(make_scan(s)[0]).to(dev) for s in range(frames + 1)]
+    SemSegInference(model, seed=100).run(scans[-1])  # warm-up frame
+    torch.cuda.synchronize(dev)
+    patches = 0
+    t = time.perf_counter()
+    for f in range(frames):
+        inf = SemSegInference(model, seed=f)
+        inf.run(scans[f])
+        patches += inf.stats["patches"]
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t
+    return {"frames_per_s": round(frames / dt, 3), "ms_per_frame": round(dt / frames * 1e3, 2),
+            "patches_per_frame": round(patches / frames, 2), "frames": frames,
+            "config": "C2: 120,000-pt synthetic 64-beam scan, RandLANet semantickitti cfg, fp32, random init",
+            "cpu_reference_s_per_frame_8cores_survey": 10.6}
 
 
 def timed_run(step, steps, warmup, world, sync):
@@ -185,6 +230,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
+        if world == 1 and args.randla_frames > 0:
+            out["randlanet"] = randla_frames(dev, args.randla_frames)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -202,6 +202,22 @@ int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* quer
                                    int64_t n_query, const int32_t* ksize_host, float voxel_size, int mirror,
                                    int32_t* kernel_index, void* stream);
 
+/* ---- RandLA-Net neighbour gathers (ml3d/torch/models/
+ * randlanet.py).  Channels-last: coords f32 [N,3], neighbour indices int32
+ * [N,K], per-pair tensors [N,K,C], per-point [N,C].
+ * relative_encoding: LocalSpatialEncoding's geometric input (randlanet.py:
+ *   593-606) [|c-p|, c-p, c, p] -> out [N,K,10];
+ * attentive_pool: AttentivePooling's softmax over K + weighted sum
+ *   (randlanet.py:632-650): x, logits [N,K,C] -> out [N,C];
+ * gather_max: random_sample (randlanet.py:306-331): out[m,c] = max_k
+ *   feat[idx[m,k], c] -> [M,C]. ------------------------------------------- */
+int o3dml_randla_relative_encoding(const float* coords, int64_t n, const int32_t* neighbors, int k, float* out,
+                                   void* stream);
+int o3dml_randla_attentive_pool(const float* x, const float* logits, int64_t n, int k, int c, float* out,
+                                void* stream);
+int o3dml_randla_gather_max(const float* feat, int c, const int32_t* idx, int64_t m, int k, float* out,
+                            void* stream);
+
 /* ---- ragged helpers ------------------------------------------------------
  * o3dml_ragged_to_dense replaces open3d.ml.torch.ops.ragged_to_dense
  * (kpconv.py:2030-2032, point_pillars.py:364-366): values [P, inner] of

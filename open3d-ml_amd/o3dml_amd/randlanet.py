@@ -1,0 +1,362 @@
+"""RandLA-Net on MI355X (reference
+ml3d/torch/models/randlanet.py).
+
+``RandLANet`` keeps the reference module tree — the same submodule names,
+classes and parameter shapes, so a reference ``state_dict`` (270 entries,
+1,242,307 trainable parameters) loads unchanged — but runs channels-last:
+per-point tensors [N, C], per-neighbour tensors [N, K, C], the 1x1
+convolutions as GEMMs, BatchNorm folded into them at inference, and the
+index work (neighbour relative encoding, attentive-pooling softmax/sum,
+random-sample max pooling) in HIP kernels (csrc/randla.hip).  The
+differentiable path (training / autograd) uses the same layout with torch
+ops.
+
+``SemSegInference`` is the GPU counterpart of
+``SemanticSegmentation.run_inference`` with the
+``SemSegSpatiallyRegularSampler`` patch loop (semantic_segmentation.py:122-180,
+semseg_spatially_regular.py:62-111, randlanet.py:115-239, 441-465): the cloud
+is grid-subsampled and projected ONCE, then patches are cropped, recentred,
+searched (kNN k=16 / k=1 per layer), inferred and accumulated on the GPU
+until every sub-point's possibility exceeds 0.5.
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib, ops
+from ._util import ptr, stream_handle
+
+_BN_EPS = 1e-6
+
+
+# ---------------------------------------------------------------------------
+# HIP kernels (csrc/randla.hip)
+# ---------------------------------------------------------------------------
+def relative_encoding(coords, nbr):
+    """[N,3] f32, [N,K] int32 -> [N,K,10]: (|c-p|, c-p, c, p) (randlanet.py:593-606)."""
+    n, k = nbr.shape
+    out = torch.empty((n, k, 10), dtype=torch.float32, device=coords.device)
+    _lib.call("o3dml_randla_relative_encoding", ptr(coords), n, ptr(nbr), k, ptr(out), stream_handle(coords.device))
+    return out
+
+
+def attentive_pool(x, logits):
+    """softmax over K of logits, weighted sum of x: [N,K,C] x2 -> [N,C] (randlanet.py:632-650)."""
+    n, k, c = x.shape
+    out = torch.empty((n, c), dtype=torch.float32, device=x.device)
+    _lib.call("o3dml_randla_attentive_pool", ptr(x), ptr(logits), n, k, c, ptr(out), stream_handle(x.device))
+    return out
+
+
+def gather_max(feat, idx):
+    """out[m] = max_k feat[idx[m, k]]: [N,C], [M,K] int32 -> [M,C] (randlanet.py:306-331)."""
+    m, k = idx.shape
+    c = feat.shape[1]
+    out = torch.empty((m, c), dtype=torch.float32, device=feat.device)
+    _lib.call("o3dml_randla_gather_max", ptr(feat), c, ptr(idx), m, k, ptr(out), stream_handle(feat.device))
+    return out
+
+
+def _fused():
+    return not torch.is_grad_enabled()
+
+
+# ---------------------------------------------------------------------------
+# modules (same names / parameters as the reference)
+# ---------------------------------------------------------------------------
+class SharedMLP(nn.Module):
+    """1x1 Conv2d / ConvTranspose2d + BatchNorm2d + activation (randlanet.py:469-512),
+    applied to channels-last rows."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=1, stride=1, transpose=False, bn=True,
+                 activation_fn=None):
+        super().__init__()
+        conv = nn.ConvTranspose2d if transpose else nn.Conv2d
+        self.conv = conv(in_channels, out_channels, kernel_size=kernel_size, stride=stride,
+                         padding=(kernel_size - 1) // 2)
+        self.transpose = transpose
+        self.batch_norm = nn.BatchNorm2d(out_channels, eps=_BN_EPS, momentum=0.01) if bn else None
+        self.activation_fn = activation_fn
+        self._folded = None
+
+    def _weight(self):
+        w = self.conv.weight[:, :, 0, 0]
+        return w.t() if self.transpose else w  # [out, in]
+
+    def folded(self):
+        """(W [out,in], b [out]) with eval-mode BatchNorm folded in."""
+        if self._folded is None:
+            with torch.no_grad():
+                w, b = self._weight().float(), self.conv.bias.float()
+                if self.batch_norm is not None:
+                    bn = self.batch_norm
+                    scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+                    w = w * scale[:, None]
+                    b = (b - bn.running_mean) * scale + bn.bias
+                self._folded = (w.contiguous(), b.contiguous())
+        return self._folded
+
+    def forward(self, x):
+        """x [..., in] -> [..., out]."""
+        if _fused() and not self.training:
+            w, b = self.folded()
+            y = torch.addmm(b, x.reshape(-1, x.shape[-1]), w.t()).reshape(*x.shape[:-1], w.shape[0])
+        else:
+            y = F.linear(x, self._weight(), self.conv.bias)
+            if self.batch_norm is not None:
+                bn = self.batch_norm
+                y = F.batch_norm(y.reshape(-1, y.shape[-1]), bn.running_mean, bn.running_var, bn.weight, bn.bias,
+                                 self.training, bn.momentum, bn.eps).reshape(y.shape)
+        if self.activation_fn is not None:
+            y = self.activation_fn(y)
+        return y
+
+
+class LocalSpatialEncoding(nn.Module):
+    """randlanet.py:540-606."""
+
+    def __init__(self, dim_in, dim_out, num_neighbors, encode_pos=False):
+        super().__init__()
+        self.num_neighbors = num_neighbors
+        self.mlp = SharedMLP(dim_in, dim_out, activation_fn=nn.LeakyReLU(0.2))
+        self.encode_pos = encode_pos
+
+    def forward(self, coords, features, nbr, relative_features=None):
+        """coords [N,3], features [N,d], nbr [N,K] int32 -> ([N,K,d+dout], relative [N,K,dout])."""
+        n, k = nbr.shape
+        if self.encode_pos:
+            if _fused():
+                rel = relative_encoding(coords, nbr)
+            else:
+                nc = coords[nbr.long()]
+                ext = coords[:, None, :].expand(n, k, 3)
+                rp = ext - nc
+                rel = torch.cat([torch.sqrt((rp * rp).sum(-1, keepdim=True)), rp, ext, nc], -1)
+            relative_features = rel
+        elif relative_features is None:
+            raise ValueError("LocalSpatialEncoding: Require relative_features for second pass.")
+        relative_features = self.mlp(relative_features)
+        neighbor_features = features[nbr.long()]
+        return torch.cat([neighbor_features, relative_features], -1), relative_features
+
+
+class AttentivePooling(nn.Module):
+    """randlanet.py:609-650."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.score_fn = nn.Sequential(nn.Linear(in_channels, in_channels), nn.Softmax(dim=-2))
+        self.mlp = SharedMLP(in_channels, out_channels, activation_fn=nn.LeakyReLU(0.2))
+
+    def forward(self, x):
+        """x [N,K,C] -> [N,Cout]."""
+        lin = self.score_fn[0]
+        logits = F.linear(x, lin.weight, lin.bias)
+        if _fused():
+            pooled = attentive_pool(x.contiguous(), logits.contiguous())
+        else:
+            pooled = (torch.softmax(logits, dim=-2) * x).sum(-2)
+        return self.mlp(pooled)
+
+
+class LocalFeatureAggregation(nn.Module):
+    """randlanet.py:653-692."""
+
+    def __init__(self, d_in, d_out, num_neighbors):
+        super().__init__()
+        self.num_neighbors = num_neighbors
+        self.mlp1 = SharedMLP(d_in, d_out // 2, activation_fn=nn.LeakyReLU(0.2))
+        self.lse1 = LocalSpatialEncoding(10, d_out // 2, num_neighbors, encode_pos=True)
+        self.pool1 = AttentivePooling(d_out, d_out // 2)
+        self.lse2 = LocalSpatialEncoding(d_out // 2, d_out // 2, num_neighbors)
+        self.pool2 = AttentivePooling(d_out, d_out)
+        self.mlp2 = SharedMLP(d_out, 2 * d_out)
+        self.shortcut = SharedMLP(d_in, 2 * d_out)
+        self.lrelu = nn.LeakyReLU()
+
+    def forward(self, coords, feat, nbr):
+        x = self.mlp1(feat)
+        x, rel = self.lse1(coords, x, nbr)
+        x = self.pool1(x)
+        x, _ = self.lse2(coords, x, nbr, relative_features=rel)
+        x = self.pool2(x)
+        return self.lrelu(self.mlp2(x) + self.shortcut(feat))
+
+
+class RandLANet(nn.Module):
+    """Module tree and state_dict of ml3d RandLANet (randlanet.py:16-113);
+    forward takes the reference ``inputs`` dict ([B, N, ...] lists) and returns
+    [B, N, num_classes] scores."""
+
+    def __init__(self, name="RandLANet", num_neighbors=16, num_layers=4, num_points=4096 * 11, num_classes=19,
+                 ignored_label_inds=(0,), sub_sampling_ratio=(4, 4, 4, 4), in_channels=3, dim_features=8,
+                 dim_output=(16, 64, 128, 256), grid_size=0.06, **kwargs):
+        super().__init__()
+        self.cfg = dict(name=name, num_neighbors=num_neighbors, num_layers=num_layers, num_points=num_points,
+                        num_classes=num_classes, ignored_label_inds=list(ignored_label_inds),
+                        sub_sampling_ratio=list(sub_sampling_ratio), in_channels=in_channels,
+                        dim_features=dim_features, dim_output=list(dim_output), grid_size=grid_size, **kwargs)
+        self.fc0 = nn.Linear(in_channels, dim_features)
+        self.bn0 = nn.BatchNorm2d(dim_features, eps=_BN_EPS, momentum=0.01)
+        encoder, enc_dims = [], []
+        d = dim_features
+        for i in range(num_layers):
+            encoder.append(LocalFeatureAggregation(d, dim_output[i], num_neighbors))
+            d = 2 * dim_output[i]
+            if i == 0:
+                enc_dims.append(d)
+            enc_dims.append(d)
+        self.encoder = nn.ModuleList(encoder)
+        self.mlp = SharedMLP(d, d, activation_fn=nn.LeakyReLU(0.2))
+        decoder = []
+        for i in range(num_layers):
+            decoder.append(SharedMLP(enc_dims[-i - 2] + d, enc_dims[-i - 2], transpose=True,
+                                     activation_fn=nn.LeakyReLU(0.2)))
+            d = enc_dims[-i - 2]
+        self.decoder = nn.ModuleList(decoder)
+        self.fc1 = nn.Sequential(SharedMLP(d, 64, activation_fn=nn.LeakyReLU(0.2)),
+                                 SharedMLP(64, 32, activation_fn=nn.LeakyReLU(0.2)), nn.Dropout(0.5),
+                                 SharedMLP(32, num_classes, bn=False))
+
+    # folded eval weights are invalidated whenever parameters may change
+    def _invalidate(self):
+        for m in self.modules():
+            if isinstance(m, SharedMLP):
+                m._folded = None
+
+    def train(self, mode=True):
+        self._invalidate()
+        return super().train(mode)
+
+    def load_state_dict(self, *a, **kw):
+        self._invalidate()
+        return super().load_state_dict(*a, **kw)
+
+    def forward_points(self, feat, coords, nbrs, subs, ups):
+        """One or more concatenated patches, channels-last.
+        feat [N0,Cin]; coords[i] [Ni,3]; nbrs[i] [Ni,K] int32; subs[i] [N(i+1),K] int32
+        (indices into level i); ups[i] [Ni] int64 (indices into level i+1).
+        Returns logits [N0, num_classes]."""
+        bn = self.bn0
+        x = F.linear(feat, self.fc0.weight, self.fc0.bias)
+        x = F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias, self.training, bn.momentum, bn.eps)
+        x = F.leaky_relu(x, 0.2)
+        enc = []
+        for i, layer in enumerate(self.encoder):
+            y = layer(coords[i], x, nbrs[i])
+            if _fused():
+                ys = gather_max(y.contiguous(), subs[i])
+            else:
+                ys = y[subs[i].long()].max(1).values
+            if i == 0:
+                enc.append(y)
+            enc.append(ys)
+            x = ys
+        x = self.mlp(x)
+        for i, layer in enumerate(self.decoder):
+            interp = x[ups[-i - 1]]
+            x = layer(torch.cat([enc[-i - 2], interp], -1))
+        for m in self.fc1:
+            x = m(x)
+        return x
+
+    def forward(self, inputs):
+        """Reference signature (randlanet.py:241-298): inputs['features'] [B,N,Cin],
+        'coords'/'neighbor_indices'/'sub_idx'/'interp_idx' lists of [B,...]."""
+        dev = next(self.parameters()).device
+        feats = inputs["features"].to(dev).float()
+        B, N, _ = feats.shape
+        L = len(self.encoder)
+        coords, nbrs, subs, ups = [], [], [], []
+        for i in range(L):
+            c = inputs["coords"][i].to(dev).float()
+            ni = c.shape[1]
+            off = (torch.arange(B, device=dev) * ni).view(B, 1, 1)
+            nb = inputs["neighbor_indices"][i].to(dev).long()
+            coords.append(c.reshape(-1, 3).contiguous())
+            nbrs.append((nb + off).reshape(-1, nb.shape[-1]).int().contiguous())
+            sb = inputs["sub_idx"][i].to(dev).long()
+            subs.append((sb + off).reshape(-1, sb.shape[-1]).int().contiguous())
+            up = inputs["interp_idx"][i].to(dev).long().reshape(B, -1)
+            n_next = inputs["coords"][i + 1].shape[1] if i + 1 < L else sb.shape[1]
+            ups.append((up + (torch.arange(B, device=dev) * n_next).view(B, 1)).reshape(-1))
+        out = self.forward_points(feats.reshape(B * N, -1).contiguous(), coords, nbrs, subs, ups)
+        return out.reshape(B, N, -1)
+
+
+# ---------------------------------------------------------------------------
+# inference pipeline (GPU)
+# ---------------------------------------------------------------------------
+class SemSegInference:
+    """GPU ``run_inference`` for RandLA-Net with the spatially-regular patch
+    sampler.  ``run(points)`` -> (predicted labels [N] int64, probabilities
+    [N, C] float32), both on the GPU; ``stats`` records patches per frame."""
+
+    def __init__(self, model, device=None, seed=0, test_smooth=0.95):
+        self.model = model
+        self.device = device or next(model.parameters()).device
+        self.test_smooth = test_smooth
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        self.stats = {}
+
+    def preprocess(self, points):
+        """Grid subsampling + 1-NN projection of every raw point (randlanet.py:115-152), once."""
+        cfg = self.model.cfg
+        sub, _, _, _ = ops.grid_subsample(points, [points.shape[0]], cfg["grid_size"])
+        proj = ops.knn_search(sub, points, 1).neighbors_index.long()
+        return sub, proj
+
+    def transform(self, sub, possibility):
+        """Patch crop + possibility update + per-layer kNN (randlanet.py:156-239,
+        semseg_spatially_regular.py:82-109)."""
+        cfg = self.model.cfg
+        n_pts = cfg["num_points"]
+        center_id = int(torch.argmin(possibility))
+        center = sub[center_id:center_id + 1]
+        if sub.shape[0] < n_pts:
+            extra = torch.randint(0, sub.shape[0], (n_pts - sub.shape[0],), generator=self.gen, device=self.device)
+            idxs = torch.cat([torch.arange(sub.shape[0], device=self.device), extra])
+        else:
+            idxs = ops.knn_search(sub, center, n_pts).neighbors_index.long()
+        idxs = idxs[torch.randperm(idxs.shape[0], generator=self.gen, device=self.device)]
+        pc = sub[idxs]
+        d = ((pc - center) ** 2).sum(1)
+        delta = (1 - d / d.max()) ** 2
+        possibility.index_add_(0, idxs, delta)
+        pc = pc.clone()
+        pc[:, :2] -= pc[:, :2].mean(0)  # augment recenter dim [0, 1]
+        coords, nbrs, subs, ups = [], [], [], []
+        cur = pc
+        for i in range(cfg["num_layers"]):
+            nb = ops.knn_search(cur, cur, cfg["num_neighbors"]).neighbors_index.view(-1, cfg["num_neighbors"])
+            m = cur.shape[0] // cfg["sub_sampling_ratio"][i]
+            nxt = cur[:m].contiguous()
+            up = ops.knn_search(nxt, cur, 1).neighbors_index.long()
+            coords.append(cur)
+            nbrs.append(nb)
+            subs.append(nb[:m].contiguous())
+            ups.append(up)
+            cur = nxt
+        return pc, idxs, coords, nbrs, subs, ups
+
+    @torch.no_grad()
+    def run(self, points):
+        self.model.eval()
+        points = points.to(self.device).float().contiguous()
+        C = self.model.cfg["num_classes"]
+        sub, proj = self.preprocess(points)
+        n_sub = sub.shape[0]
+        possibility = torch.rand(n_sub, generator=self.gen, device=self.device) * 1e-3
+        test_probs = torch.zeros((n_sub, C), dtype=torch.float32, device=self.device)
+        patches = 0
+        while float(possibility.min()) <= 0.5:
+            pc, idxs, coords, nbrs, subs, ups = self.transform(sub, possibility)
+            logits = self.model.forward_points(pc, coords, nbrs, subs, ups)
+            probs = torch.softmax(logits, -1)
+            test_probs[idxs] = self.test_smooth * test_probs[idxs] + (1 - self.test_smooth) * probs
+            patches += 1
+        self.stats = {"patches": patches, "sub_points": n_sub}
+        probs = test_probs[proj]
+        return probs.argmax(1), probs
