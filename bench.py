@@ -82,15 +82,17 @@ def kernel_profile(step, n_queries, pairs, reps):
     return dominant, avg, alg_bytes, mean_nbrs
 
 
-def load_traffic():
-    path = os.path.join(ROOT, "profiles", "pmc_frs_fill.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/*/pmc_<kernel>.json written by tools/pmc_traffic.py), newest round first."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_{kernel}.json")), reverse=True):
+        try:
+            with open(path) as f:
+                return json.load(f).get("hbm_bytes_per_launch")
+        except Exception:
+            continue
+    return None
 
 
 def cpu_baseline():
@@ -223,7 +225,7 @@ def main():
                 "pairs_per_step_rank0": pairs, "parallelism": f"scene-dp{world}"},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(), "kernel_ms": round(ms, 5),
+                         "traffic": load_traffic(dominant), "kernel_ms": round(ms, 5),
                          "kernel_ms_all": {k: round(v, 5) for k, v in avg.items()},
                          "alg_bytes_per_launch": int(alg_bytes), "mean_neighbors": round(mean_nbrs, 3)},
             "cpu_baseline": None,
