@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--randla-frames", type=int, default=3, help="RandLA-Net frames timed (0: skip)")
+    ap.add_argument("--sparse-conv-reps", type=int, default=10, help="C4 sparse-conv forwards timed (0: skip)")
     return ap.parse_args()
 
 
@@ -155,6 +156,71 @@ def randla_frames(dev, frames):
             "cpu_reference_s_per_frame_8cores_survey": 10.6}
 
 
+def make_room(seed=0):
+    """C4-shaped voxel set: ~80k active 2 cm voxels on room surfaces
+    (4 m x 3 m floor, 1.2 m walls, four boxes), half-integer positions in voxel
+    units, 3 colour features U[0,1)."""
+    rng = np.random.default_rng(seed)
+    vox = set()
+    X, Y, H = 200, 150, 60
+    for x in range(X):
+        for y in range(Y):
+            vox.add((x, y, 0))
+    for z in range(H):
+        for x in range(X):
+            vox.add((x, 0, z)); vox.add((x, Y - 1, z))
+        for y in range(Y):
+            vox.add((0, y, z)); vox.add((X - 1, y, z))
+    for _ in range(4):
+        bx, by = rng.integers(20, X - 60), rng.integers(20, Y - 60)
+        sx, sy, sz = rng.integers(20, 40, 3)
+        for z in range(sz):
+            for x in range(bx, bx + sx):
+                vox.add((x, by, z)); vox.add((x, by + sy - 1, z))
+            for y in range(by, by + sy):
+                vox.add((bx, y, z)); vox.add((bx + sx - 1, y, z))
+        for x in range(bx, bx + sx):
+            for y in range(by, by + sy):
+                vox.add((x, y, sz))
+    pos = np.array(sorted(vox), np.float32) + 0.5
+    pos = pos[rng.permutation(len(pos))]
+    return pos, rng.random((len(pos), 3), dtype=np.float32)
+
+
+def sparse_conv_bench(dev, reps):
+    """C4 submanifold 3^3 sparse convolution, 32 -> 32 channels, fp32 (the
+    SparseConvUnet m=32 level-0 conv): full layers.SparseConv forward (rulebook
+    via Linf fixed-radius search + kernel index + MFMA gather-GEMM) and the
+    GEMM alone (ops.sparse_conv on the prebuilt rulebook)."""
+    from o3dml_amd import layers, sparse_conv as sc
+    pos_np, _ = make_room(0)
+    pos = torch.from_numpy(pos_np).to(dev)
+    torch.manual_seed(0)
+    conv = layers.SparseConv(32, 32, [3, 3, 3], use_bias=False).to(dev)
+    feat = torch.rand((pos.shape[0], 32), device=dev)
+    with torch.no_grad():
+        out = conv(feat, pos, pos, 1.0)
+        nb, kidx = conv._rulebook(pos, pos, 1.0, None, False, 1.0)
+        pairs = int(nb.neighbors_index.shape[0])
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(reps):
+            out = conv(feat, pos, pos, 1.0)
+        torch.cuda.synchronize(dev)
+        t_layer = (time.perf_counter() - t) / reps
+        t = time.perf_counter()
+        for _ in range(reps):
+            out = sc.sparse_conv(conv.kernel, feat, None, nb.neighbors_index, kidx, None, nb.neighbors_row_splits)
+        torch.cuda.synchronize(dev)
+        t_gemm = (time.perf_counter() - t) / reps
+    flops = 2.0 * pairs * 32 * 32
+    n = pos.shape[0]
+    return {"voxels": int(n), "pairs": pairs, "mvoxels_per_s_layer": round(n / t_layer / 1e6, 2),
+            "ms_layer": round(t_layer * 1e3, 4), "ms_gemm": round(t_gemm * 1e3, 4),
+            "tflops_gemm": round(flops / t_gemm / 1e12, 3),
+            "config": "C4: ~80k 2 cm room voxels, SparseConv 3^3 32->32 fp32, rulebook rebuilt per call"}
+
+
 def timed_run(step, steps, warmup, world, sync):
     """W untimed warmups, then EXACTLY `steps` timed steps bracketed by
     barrier + device sync on both sides; returns (max-over-ranks elapsed s,
@@ -232,6 +298,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
+        if world == 1 and args.sparse_conv_reps > 0:
+            out["sparse_conv"] = sparse_conv_bench(dev, args.sparse_conv_reps)
         if world == 1 and args.randla_frames > 0:
             out["randlanet"] = randla_frames(dev, args.randla_frames)
         print(json.dumps(out), flush=True)

@@ -99,97 +99,100 @@ __global__ void transpose_filters_kernel(const float* __restrict__ w, int K, int
 }
 
 // --------------------------------------------------------------------------
-// implicit GEMM (forward / dIn)
+// implicit GEMM (forward / dIn): one wave owns 32 output rows x 32 output
+// channels and walks the (offset, Cin-chunk) stages its rows use.  Operands go
+// straight from global memory into registers in the MFMA layout — lane (i, h)
+// gathers 16 consecutive channels [c0 + 16h, +16) of row i's input (4 x 16-B
+// loads) and the matching 16 weights of column i — so no LDS and no barriers;
+// the next stage's loads are issued before the current stage's 16
+// v_mfma_f32_32x32x2_f32 (reduction index permuted consistently on A and B:
+// step s pairs channels c0+s and c0+16+s), hiding the gather latency.
 // --------------------------------------------------------------------------
-template <int TN, bool VEC4>
+struct GemmStage {
+    float a[16], b[16];
+};
+
+template <bool VEC4>
+__device__ __forceinline__ void gemm_load(GemmStage& st, const int32_t* __restrict__ map, int K, int64_t o, bool orow,
+                                          int k, int c0, int h, int col, const float* __restrict__ src,
+                                          const float* __restrict__ sscale, const float* __restrict__ pscale,
+                                          const float* __restrict__ W, int cin, int cout) {
+    const int32_t m = orow ? map[o * K + k] : -1;
+    const int cb = c0 + 16 * h;
+    float sc = 0.f;
+    if (m >= 0) sc = (sscale ? sscale[m] : 1.f) * (pscale ? pscale[o * K + k] : 1.f);
+    if (VEC4 && cb + 16 <= cin) {
+        const float4* row = reinterpret_cast<const float4*>(src + static_cast<int64_t>(m >= 0 ? m : 0) * cin + cb);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 v = m >= 0 ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            st.a[4 * q] = v.x * sc;
+            st.a[4 * q + 1] = v.y * sc;
+            st.a[4 * q + 2] = v.z * sc;
+            st.a[4 * q + 3] = v.w * sc;
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+            st.a[s] = (m >= 0 && cb + s < cin) ? src[static_cast<int64_t>(m) * cin + cb + s] * sc : 0.f;
+    }
+    const float* wk = W + static_cast<int64_t>(k) * cin * cout;
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+        st.b[s] = (cb + s < cin && col < cout) ? wk[static_cast<int64_t>(cb + s) * cout + col] : 0.f;
+}
+
+template <bool VEC4>
 __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, const float* __restrict__ src,
                      const float* __restrict__ sscale, const float* __restrict__ pscale,
                      const float* __restrict__ W /*[K][cin][cout]*/, int cin, int cout,
                      const float* __restrict__ oscale, const float* __restrict__ bias, float* __restrict__ out) {
-    constexpr int WN = TN / 32;           // waves along N
-    constexpr int WM = 4 / WN;            // waves along M
-    constexpr int TM = 32 * WM;           // rows per workgroup
-    constexpr int KMAX = 32;
-    __shared__ float As[TM][kKC + 1];
-    __shared__ float Bs[kKC][TN];
-    __shared__ int32_t Ms[TM][KMAX];
-    __shared__ float Ps[TM][KMAX];
-    __shared__ unsigned used_mask;
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int w = t >> 6;
-    const int wr = w / WN, wc = w % WN;
-    const int64_t o0 = static_cast<int64_t>(blockIdx.x) * TM;
-    const int n0 = blockIdx.y * TN;
-    if (t == 0) used_mask = 0u;
-    __syncthreads();
-    for (int e = t; e < TM * K; e += kGemmThreads) {
-        const int r = e / K, k = e - r * K;
-        const int64_t o = o0 + r;
-        const int32_t i = o < n_out ? map[o * K + k] : -1;
-        Ms[r][k] = i;
-        Ps[r][k] = (i >= 0 && pscale) ? pscale[o * K + k] : 1.f;
-        if (i >= 0) atomicOr(&used_mask, 1u << k);
+    const int lane = threadIdx.x & 63;
+    const int64_t o0 = (static_cast<int64_t>(blockIdx.x) * (kGemmThreads / 64) + (threadIdx.x >> 6)) * 32;
+    if (o0 >= n_out) return;  // whole wave; the kernel has no barriers
+    const int i = lane & 31, h = lane >> 5;
+    const int col = blockIdx.y * 32 + i;
+    const int64_t o = o0 + i;
+    const bool orow = o < n_out;
+    unsigned used = 0u;  // offsets any of the wave's 32 rows uses
+    for (int k = 0; k < K; ++k) {
+        const int32_t m = orow ? map[o * K + k] : -1;
+        if (__ballot(m >= 0) != 0ull) used |= 1u << k;
     }
-    __syncthreads();
-    const unsigned mask = used_mask;
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    for (int k = 0; k < K; ++k) {
-        if (!((mask >> k) & 1u)) continue;  // no row of this tile uses offset k
-        const float* Wk = W + static_cast<int64_t>(k) * cin * cout;
-        for (int c0 = 0; c0 < cin; c0 += kKC) {
-            // gather A: TM rows x KC channels (scaled), zero for missing pairs
-            if constexpr (VEC4) {
-                for (int e = t; e < TM * (kKC / 4); e += kGemmThreads) {
-                    const int r = e / (kKC / 4), c4 = (e - r * (kKC / 4)) * 4;
-                    const int32_t i = Ms[r][k];
-                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (i >= 0 && c0 + c4 < cin) {
-                        v = *reinterpret_cast<const float4*>(src + static_cast<int64_t>(i) * cin + c0 + c4);
-                        const float s = (sscale ? sscale[i] : 1.f) * Ps[r][k];
-                        v.x *= s; v.y *= s; v.z *= s; v.w *= s;
-                    }
-                    As[r][c4] = v.x; As[r][c4 + 1] = v.y; As[r][c4 + 2] = v.z; As[r][c4 + 3] = v.w;
-                }
-            } else {
-                for (int e = t; e < TM * kKC; e += kGemmThreads) {
-                    const int r = e / kKC, c = e - r * kKC;
-                    const int32_t i = Ms[r][k];
-                    float v = 0.f;
-                    if (i >= 0 && c0 + c < cin)
-                        v = src[static_cast<int64_t>(i) * cin + c0 + c] * ((sscale ? sscale[i] : 1.f) * Ps[r][k]);
-                    As[r][c] = v;
-                }
+    if (used) {
+        GemmStage cur, nxt;
+        int k = __builtin_ctz(used), c0 = 0;
+        gemm_load<VEC4>(cur, map, K, o, orow, k, c0, h, col, src, sscale, pscale, W, cin, cout);
+        while (true) {
+            int nk = k, nc = c0 + 32;
+            if (nc >= cin) {
+                nc = 0;
+                const unsigned rest = k + 1 < 32 ? used & ~((2u << k) - 1u) : 0u;
+                nk = rest ? __builtin_ctz(rest) : -1;
             }
-            // B: W[k][c0 .. c0+KC)[n0 .. n0+TN)
-            for (int e = t; e < kKC * TN; e += kGemmThreads) {
-                const int r = e / TN, c = e - r * TN;
-                Bs[r][c] = (c0 + r < cin && n0 + c < cout) ? Wk[static_cast<int64_t>(c0 + r) * cout + n0 + c] : 0.f;
-            }
-            __syncthreads();
-            const int ar = wr * 32 + (lane & 31);
-            const int bc = wc * 32 + (lane & 31);
-            const int kh = lane >> 5;
+            if (nk >= 0) gemm_load<VEC4>(nxt, map, K, o, orow, nk, nc, h, col, src, sscale, pscale, W, cin, cout);
 #pragma unroll
-            for (int s = 0; s < kKC / 2; ++s)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[ar][2 * s + kh], Bs[2 * s + kh][bc], acc, 0, 0, 0);
-            __syncthreads();
+            for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[s], cur.b[s], acc, 0, 0, 0);
+            if (nk < 0) break;
+            k = nk;
+            c0 = nc;
+            cur = nxt;
         }
     }
     // epilogue: C/D map row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31
-    const int col = n0 + wc * 32 + (lane & 31);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int64_t o = o0 + wr * 32 + row;
-        if (o < n_out && col < cout) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t orr = o0 + row;
+        if (orr < n_out && col < cout) {
             float v = acc[r];
-            if (oscale) v *= oscale[o];
+            if (oscale) v *= oscale[orr];
             if (bias) v += bias[col];
-            out[o * cout + col] = v;
+            out[orr * cout + col] = v;
         }
     }
 }
@@ -317,31 +320,20 @@ __global__ void kernel_index_kernel(const float* __restrict__ inp_pos, const flo
     }
 }
 
-template <int TN>
-static void launch_gemm(bool vec4, dim3 g, hipStream_t st, const int32_t* map, int K, int64_t n_out, const float* src,
-                        const float* sscale, const float* pscale, const float* W, int cin, int cout,
-                        const float* oscale, const float* bias, float* out) {
-    if (vec4)
-        implicit_gemm_kernel<TN, true><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
-                                                                   oscale, bias, out);
-    else
-        implicit_gemm_kernel<TN, false><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
-                                                                    oscale, bias, out);
-    O3DML_LAUNCH_CHECK();
-}
-
 static void run_gemm(hipStream_t st, const int32_t* map, int K, int64_t n_out, const float* src, const float* sscale,
                      const float* pscale, const float* W, int cin, int cout, const float* oscale, const float* bias,
                      float* out) {
     if (n_out == 0 || cout == 0) return;
     const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0;
-    if (cout <= 32) {
-        dim3 g(static_cast<unsigned>(ceil_div(n_out, 128)), 1);
-        launch_gemm<32>(vec4, g, st, map, K, n_out, src, sscale, pscale, W, cin, cout, oscale, bias, out);
-    } else {
-        dim3 g(static_cast<unsigned>(ceil_div(n_out, 64)), static_cast<unsigned>(ceil_div(cout, 64)));
-        launch_gemm<64>(vec4, g, st, map, K, n_out, src, sscale, pscale, W, cin, cout, oscale, bias, out);
-    }
+    const dim3 g(static_cast<unsigned>(ceil_div(n_out, 32 * (kGemmThreads / 64))),
+                 static_cast<unsigned>(ceil_div(cout, 32)));
+    if (vec4)
+        implicit_gemm_kernel<true><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
+                                                               oscale, bias, out);
+    else
+        implicit_gemm_kernel<false><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
+                                                                oscale, bias, out);
+    O3DML_LAUNCH_CHECK();
 }
 
 }  // namespace o3dml

@@ -22,7 +22,8 @@ class _ConvFn(torch.autograd.Function):
     """out = oscale * sum_k gather(x * sscale * pscale) @ W[k] (+ bias)."""
 
     @staticmethod
-    def forward(ctx, filters, inp_features, bias, nidx, kidx, nimp, rs, sscale, normalize, out_importance):
+    def forward(ctx, filters, inp_features, bias, nidx, kidx, nimp, rs, sscale, normalize, out_importance,
+                want_grad):
         dev = inp_features.device
         lib = _lib.load()
         K = int(np.prod(filters.shape[:-2]))
@@ -34,7 +35,7 @@ class _ConvFn(torch.autograd.Function):
         st = stream_handle(dev)
         mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
         status = np.zeros(1, np.int32)
-        want_inv = int(inp_features.requires_grad or filters.requires_grad)
+        want_inv = int(bool(want_grad))  # the inverse map serves dIn / dW only
         _lib.call("o3dml_sparse_conv_build_map", ptr(nidx), ptr(kidx), ptr(nimp), ptr(rs), n_out, n_in, K,
                   int(bool(normalize)), ptr(out_importance), want_inv, status.ctypes.data, ptr(mws), mws.numel(), st)
         if status[0] & 2:
@@ -68,7 +69,7 @@ class _ConvFn(torch.autograd.Function):
                   int(has_nimp), use_os, ptr(g), n_out, ptr(gx), ptr(gw), ptr(mws), mws.numel(), ptr(ws), ws.numel(),
                   stream_handle(dev))
         gb = g.sum(0) if (has_bias and ctx.needs_input_grad[2]) else None
-        return gw, gx, gb, None, None, None, None, None, None, None
+        return gw, gx, gb, None, None, None, None, None, None, None, None
 
 
 def _conv(filters, inp_features, bias, neighbors_index, neighbors_kernel_index, neighbors_importance,
@@ -85,7 +86,9 @@ def _conv(filters, inp_features, bias, neighbors_index, neighbors_kernel_index, 
     nimp = _opt(neighbors_importance, dev)
     oimp = _opt(out_importance, dev)
     b = None if bias is None else (bias.to(dev) if not bias.is_cuda else bias)
-    out = _ConvFn.apply(f, x, b, nidx, kidx, nimp, rs, sscale, bool(normalize), oimp)
+    want_grad = torch.is_grad_enabled() and (f.requires_grad or x.requires_grad or
+                                             (b is not None and b.requires_grad))
+    out = _ConvFn.apply(f, x, b, nidx, kidx, nimp, rs, sscale, bool(normalize), oimp, want_grad)
     return out.cpu() if back_cpu else out
 
 
