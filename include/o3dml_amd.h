@@ -202,6 +202,19 @@ int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* quer
                                    int64_t n_query, const int32_t* ksize_host, float voxel_size, int mirror,
                                    int32_t* kernel_index, void* stream);
 
+/* Lattice rulebook for cubic ks^3 (ks <= 3) layers.SparseConv /
+ * SparseConvTranspose (sparseconvnet.py:344-482): when every input position
+ * and every query (out_pos -/+ offset*vs) lies on one voxel lattice, the Linf
+ * neighbourhood of radius ks*vs/2 is exactly the ks^3 lattice offsets, so the
+ * dense kernel map (same workspace layout as _build_map) comes from a voxel
+ * hash with K lookups per output.  status_host[0] bit 2 (value 4): not a
+ * lattice set — use the fixed-radius-search rulebook instead. */
+size_t o3dml_sparse_conv_lattice_workspace_size(int64_t n_in);
+int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, const float* query_pos, int64_t n_out,
+                                  float voxel_size, int ksize, int mirror, int normalize, const float* out_importance,
+                                  int want_inverse, int* status_host, void* workspace, size_t workspace_bytes,
+                                  void* lattice_workspace, size_t lattice_workspace_bytes, void* stream);
+
 /* ---- RandLA-Net neighbour gathers (ml3d/torch/models/
  * randlanet.py).  Channels-last: coords f32 [N,3], neighbour indices int32
  * [N,K], per-pair tensors [N,K,C], per-point [N,C].

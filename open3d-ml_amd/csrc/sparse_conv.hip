@@ -19,6 +19,8 @@
 //            slabs, reduced in a fixed order (deterministic).
 // Roofline: MFMA fp32 (157 TF/s dense) for Cin*Cout >= ~64^2, gather/HBM bound
 // below that.
+#include <cmath>
+#include <cstring>
 #include <vector>
 
 #include "primitives.hpp"
@@ -336,6 +338,118 @@ static void run_gemm(hipStream_t st, const int32_t* map, int K, int64_t n_out, c
     O3DML_LAUNCH_CHECK();
 }
 
+// --------------------------------------------------------------------------
+// lattice rulebook: when every input and query position sits exactly on one
+// voxel lattice (SparseConvUnet: half-integer positions, vs = 1), the
+// Linf-ball neighbours of a query are exactly the K lattice offsets, so the
+// dense kernel map is built with a hash table of input voxel keys and K
+// lookups per output — identical to the map the fixed-radius-search rulebook
+// produces, without the search.
+// --------------------------------------------------------------------------
+constexpr uint64_t kLatEmpty = ~0ull;
+
+__device__ __forceinline__ uint64_t lat_key(int x, int y, int z) {
+    return (static_cast<uint64_t>(static_cast<uint32_t>(x + (1 << 20)) & 0x1fffffu) << 42) |
+           (static_cast<uint64_t>(static_cast<uint32_t>(y + (1 << 20)) & 0x1fffffu) << 21) |
+           static_cast<uint64_t>(static_cast<uint32_t>(z + (1 << 20)) & 0x1fffffu);
+}
+
+__device__ __forceinline__ uint32_t lat_hash(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return static_cast<uint32_t>(k);
+}
+
+// per-axis [min frac, max frac, min key, max key] of p / vs (frac as float bits,
+// keys as ints) for one point set -> stats[0..11]
+__global__ void lattice_stats_kernel(const float* __restrict__ pos, int64_t n, float inv_vs, int* __restrict__ stats) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const float u = pos[3 * i + d] * inv_vs;
+            const float fl = floorf(u);
+            const float fr = u - fl;  // >= 0, so int ordering of the bits is float ordering
+            const int key = fabsf(fl) < 1.0e6f ? static_cast<int>(fl) : 0x7fffffff;
+            atomicMin(&stats[4 * d + 0], __float_as_int(fr));
+            atomicMax(&stats[4 * d + 1], __float_as_int(fr));
+            atomicMin(&stats[4 * d + 2], key);
+            atomicMax(&stats[4 * d + 3], key);
+        }
+    }
+}
+
+__global__ void lattice_insert_kernel(const float* __restrict__ pos, int64_t n, float inv_vs, uint64_t* __restrict__ keys,
+                                      int32_t* __restrict__ vals, uint32_t mask, int* __restrict__ status) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const uint64_t k = lat_key(static_cast<int>(floorf(pos[3 * i] * inv_vs)),
+                                   static_cast<int>(floorf(pos[3 * i + 1] * inv_vs)),
+                                   static_cast<int>(floorf(pos[3 * i + 2] * inv_vs)));
+        uint32_t h = lat_hash(k) & mask;
+        while (true) {
+            const unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(&keys[h]),
+                                                      static_cast<unsigned long long>(kLatEmpty),
+                                                      static_cast<unsigned long long>(k));
+            if (prev == kLatEmpty) {
+                vals[h] = static_cast<int32_t>(i);
+                break;
+            }
+            if (prev == k) {  // two inputs on one voxel: not a plain lattice set
+                atomicOr(status, 4);
+                break;
+            }
+            h = (h + 1) & mask;
+        }
+    }
+}
+
+struct LatticeOffsets {
+    int off[3][8];  // key_p - key_q for kernel index j along axis d (x, y, z)
+};
+
+// map[o*K + k] for k = (kz*ks + ky)*ks + kx; norm[o] = neighbour count
+__global__ void lattice_map_kernel(const float* __restrict__ inp_pos, const float* __restrict__ qpos, int64_t n_out,
+                                   float inv_vs, float radius, int ks, LatticeOffsets lo,
+                                   const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, uint32_t mask,
+                                   int32_t* __restrict__ map, float* __restrict__ norm) {
+    const int K = ks * ks * ks;
+    for (int64_t o = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; o < n_out;
+         o += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const float qx = qpos[3 * o], qy = qpos[3 * o + 1], qz = qpos[3 * o + 2];
+        const int kx0 = static_cast<int>(floorf(qx * inv_vs)), ky0 = static_cast<int>(floorf(qy * inv_vs)),
+                  kz0 = static_cast<int>(floorf(qz * inv_vs));
+        int cnt = 0;
+        for (int k = 0; k < K; ++k) {
+            const int ix = k % ks, iy = (k / ks) % ks, iz = k / (ks * ks);
+            const uint64_t key = lat_key(kx0 + lo.off[0][ix], ky0 + lo.off[1][iy], kz0 + lo.off[2][iz]);
+            uint32_t h = lat_hash(key) & mask;
+            int32_t found = -1;
+            while (true) {
+                const uint64_t kk = keys[h];
+                if (kk == key) {
+                    found = vals[h];
+                    break;
+                }
+                if (kk == kLatEmpty) break;
+                h = (h + 1) & mask;
+            }
+            if (found >= 0) {  // the fixed-radius (Linf) test the search would apply
+                const float dx = fabsf(inp_pos[3 * found] - qx), dy = fabsf(inp_pos[3 * found + 1] - qy),
+                            dz = fabsf(inp_pos[3 * found + 2] - qz);
+                const float m = dx > dy ? dx : dy;
+                if ((m > dz ? m : dz) > radius) found = -1;
+            }
+            map[o * K + k] = found;
+            cnt += found >= 0 ? 1 : 0;
+        }
+        norm[o] = static_cast<float>(cnt);
+    }
+}
+
 }  // namespace o3dml
 
 using namespace o3dml;
@@ -390,6 +504,126 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
                     neighbors_importance ? ipscale : nullptr, status);
             O3DML_LAUNCH_CHECK();
         }
+    }
+    O3DML_CHECK_HIP(hipMemcpyAsync(status_host, status, sizeof(int), hipMemcpyDeviceToHost, st));
+    O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    O3DML_GUARD_END
+}
+
+O3DML_API size_t o3dml_sparse_conv_lattice_workspace_size(int64_t n_in) {
+    int64_t cap = 64;
+    while (cap < 2 * n_in) cap <<= 1;
+    return ws_bytes<uint64_t>(cap) + ws_bytes<int32_t>(cap) + ws_bytes<int>(16);
+}
+
+// Dense kernel map (same workspace layout as o3dml_sparse_conv_build_map) for
+// a cubic ks^3 SparseConv / SparseConvTranspose whose queries are `query_pos`
+// (= out_pos -/+ offset * vs) and whose neighbourhood is the Linf ball of
+// radius ks*vs/2, built directly when all positions lie on one voxel lattice.
+// status_host[0]: 4 = not a lattice set (caller uses the search rulebook).
+O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, const float* query_pos, int64_t n_out,
+                                            float voxel_size, int ksize, int mirror, int normalize,
+                                            const float* out_importance, int want_inverse, int* status_host,
+                                            void* workspace, size_t workspace_bytes, void* lattice_workspace,
+                                            size_t lattice_workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(ksize >= 1 && ksize <= 3, "lattice rulebook: kernel size must be 1..3");
+    const int K = ksize * ksize * ksize;
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    int32_t* map = ws.take<int32_t>(n_out * K);
+    float* pscale = ws.take<float>(n_out * K);
+    float* norm = ws.take<float>(n_out);
+    float* oscale = ws.take<float>(n_out);
+    int32_t* inv = ws.take<int32_t>(n_in * K);
+    float* ipscale = ws.take<float>(n_in * K);
+    int* status = ws.take<int>(4);
+    (void)pscale;
+    (void)ipscale;
+    *status_host = 0;
+    if (n_in == 0 || n_out == 0) {
+        *status_host = 4;
+        return 0;
+    }
+    Workspace lws(lattice_workspace, lattice_workspace_bytes);
+    int64_t cap = 64;
+    while (cap < 2 * n_in) cap <<= 1;
+    uint64_t* keys = lws.take<uint64_t>(cap);
+    int32_t* vals = lws.take<int32_t>(cap);
+    int* stats = lws.take<int>(16);
+    const float inv_vs = 1.0f / voxel_size;
+    // ---- 1. lattice check (fractions constant per axis, keys in range)
+    int init[16];
+    for (int d = 0; d < 3; ++d) {
+        init[4 * d + 0] = 0x7fffffff;
+        init[4 * d + 1] = 0;
+        init[4 * d + 2] = 0x7fffffff;
+        init[4 * d + 3] = static_cast<int>(0x80000000u);
+    }
+    int h_in[12], h_q[12];
+    O3DML_CHECK_HIP(hipMemcpyAsync(stats, init, sizeof(int) * 12, hipMemcpyHostToDevice, st));
+    lattice_stats_kernel<<<stream_grid(n_in, 256), 256, 0, st>>>(inp_pos, n_in, inv_vs, stats);
+    O3DML_LAUNCH_CHECK();
+    O3DML_CHECK_HIP(hipMemcpyAsync(h_in, stats, sizeof(int) * 12, hipMemcpyDeviceToHost, st));
+    O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    O3DML_CHECK_HIP(hipMemcpyAsync(stats, init, sizeof(int) * 12, hipMemcpyHostToDevice, st));
+    lattice_stats_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(query_pos, n_out, inv_vs, stats);
+    O3DML_LAUNCH_CHECK();
+    O3DML_CHECK_HIP(hipMemcpyAsync(h_q, stats, sizeof(int) * 12, hipMemcpyDeviceToHost, st));
+    O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    LatticeOffsets lo{};
+    const double h = 0.5 * ksize;
+    for (int d = 0; d < 3; ++d) {
+        float fi_lo, fi_hi, fq_lo, fq_hi;
+        std::memcpy(&fi_lo, &h_in[4 * d], 4);
+        std::memcpy(&fi_hi, &h_in[4 * d + 1], 4);
+        std::memcpy(&fq_lo, &h_q[4 * d], 4);
+        std::memcpy(&fq_hi, &h_q[4 * d + 1], 4);
+        const bool keys_ok = h_in[4 * d + 2] > -(1 << 19) && h_in[4 * d + 3] < (1 << 19) &&
+                             h_q[4 * d + 2] > -(1 << 19) && h_q[4 * d + 3] < (1 << 19);
+        if (fi_lo != fi_hi || fq_lo != fq_hi || !keys_ok) {
+            *status_host = 4;
+            return 0;
+        }
+        // lattice offsets d = j + dc within [-h, h]: exactly ksize of them, each
+        // with a distinct in-range kernel index
+        const double dc = static_cast<double>(fi_lo) - static_cast<double>(fq_lo);
+        int n_within = 0;
+        for (int j = -8; j <= 8; ++j) {
+            const double dd = j + dc;
+            if (dd < -h || dd > h) continue;
+            const int kid = mirror ? static_cast<int>(std::floor(h - dd)) : static_cast<int>(std::floor(dd + h));
+            if (kid < 0 || kid >= ksize || n_within >= ksize) {
+                *status_host = 4;
+                return 0;
+            }
+            lo.off[d][kid] = j;
+            ++n_within;
+        }
+        if (n_within != ksize) {
+            *status_host = 4;
+            return 0;
+        }
+    }
+    // ---- 2. hash the input voxels, 3. K lookups per output
+    O3DML_CHECK_HIP(hipMemsetAsync(keys, 0xff, sizeof(uint64_t) * cap, st));
+    O3DML_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, st));
+    lattice_insert_kernel<<<stream_grid(n_in, 256), 256, 0, st>>>(inp_pos, n_in, inv_vs, keys, vals,
+                                                                 static_cast<uint32_t>(cap - 1), status);
+    O3DML_LAUNCH_CHECK();
+    lattice_map_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(inp_pos, query_pos, n_out, inv_vs,
+                                                               0.5f * voxel_size * static_cast<float>(ksize), ksize,
+                                                               lo, keys, vals, static_cast<uint32_t>(cap - 1), map,
+                                                               norm);
+    O3DML_LAUNCH_CHECK();
+    recip_norm_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(normalize ? norm : nullptr, out_importance, n_out,
+                                                              oscale);
+    O3DML_LAUNCH_CHECK();
+    if (want_inverse) {
+        O3DML_CHECK_HIP(hipMemsetAsync(inv, 0xff, sizeof(int32_t) * n_in * K, st));
+        build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, nullptr, n_out, K, inv, nullptr,
+                                                                            status);
+        O3DML_LAUNCH_CHECK();
     }
     O3DML_CHECK_HIP(hipMemcpyAsync(status_host, status, sizeof(int), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));

@@ -104,6 +104,7 @@ class SparseConv(torch.nn.Module):
         else:
             self.bias = None
         self.nns = FixedRadiusSearch(metric="Linf", ignore_query_point=False, return_distances=False)
+        self.lattice_rulebook = True  # False forces the fixed-radius-search rulebook
 
     def _rulebook(self, inp_positions, out_positions, voxel_size, hash_table, mirror, sign):
         vs = _voxel_size_scalar(voxel_size, inp_positions)
@@ -115,8 +116,22 @@ class SparseConv(torch.nn.Module):
         self._avg_neighbors = nb.neighbors_index.shape[0] / max(1, out_positions.shape[0])
         return nb, kidx
 
+    def _lattice(self, inp_features, inp_positions, out_positions, voxel_size, hash_table, mirror, sign, **kw):
+        """Lattice rulebook (same dense map as the Linf search, see
+        sparse_conv.conv_lattice) unless a prebuilt search hash table is given."""
+        if hash_table is not None or not self.lattice_rulebook:
+            return None
+        vs = _voxel_size_scalar(voxel_size, inp_positions)
+        queries = (out_positions - sign * self.offset.to(out_positions.device) * vs).contiguous()
+        return sc.conv_lattice(self.kernel, kw.pop("bias", self.bias), inp_features, inp_positions, queries, vs,
+                               mirror=mirror, **kw)
+
     def forward(self, inp_features, inp_positions, out_positions, voxel_size, inp_importance=None,
                 fixed_radius_search_hash_table=None):
+        out = self._lattice(inp_features, inp_positions, out_positions, voxel_size, fixed_radius_search_hash_table,
+                            False, 1.0, inp_importance=inp_importance, normalize=self.normalize)
+        if out is not None:
+            return self.activation(out) if self.activation else out
         nb, kidx = self._rulebook(inp_positions, out_positions, voxel_size, fixed_radius_search_hash_table,
                                   False, 1.0)
         out = sc.conv_with_bias(self.kernel, self.bias, inp_features, nb.neighbors_index, kidx,
@@ -137,6 +152,12 @@ class SparseConvTranspose(SparseConv):
                 fixed_radius_search_hash_table=None):
         if self.normalize:
             raise NotImplementedError("SparseConvTranspose(normalize=True) is not supported")
+        out = self._lattice(inp_features, inp_positions, out_positions, voxel_size, fixed_radius_search_hash_table,
+                            True, -1.0, bias=None, out_importance=out_importance)
+        if out is not None:
+            if self.bias is not None:
+                out = out + self.bias
+            return self.activation(out) if self.activation else out
         nb, kidx = self._rulebook(inp_positions, out_positions, voxel_size, fixed_radius_search_hash_table,
                                   True, -1.0)
         out = sc.sparse_conv_transpose(self.kernel, out_importance, inp_features, None, None, None,

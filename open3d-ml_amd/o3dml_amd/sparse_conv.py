@@ -23,7 +23,7 @@ class _ConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, filters, inp_features, bias, nidx, kidx, nimp, rs, sscale, normalize, out_importance,
-                want_grad):
+                want_grad, prebuilt=None):
         dev = inp_features.device
         lib = _lib.load()
         K = int(np.prod(filters.shape[:-2]))
@@ -31,18 +31,22 @@ class _ConvFn(torch.autograd.Function):
         if inp_features.dim() != 2 or inp_features.shape[1] != cin:
             raise RuntimeError(f"sparse_conv: inp_features must be [N, {cin}], got {list(inp_features.shape)}")
         n_in = inp_features.shape[0]
-        n_out = rs.shape[0] - 1
         st = stream_handle(dev)
-        mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
-        status = np.zeros(1, np.int32)
-        want_inv = int(bool(want_grad))  # the inverse map serves dIn / dW only
-        _lib.call("o3dml_sparse_conv_build_map", ptr(nidx), ptr(kidx), ptr(nimp), ptr(rs), n_out, n_in, K,
-                  int(bool(normalize)), ptr(out_importance), want_inv, status.ctypes.data, ptr(mws), mws.numel(), st)
-        if status[0] & 2:
-            raise RuntimeError("sparse_conv: neighbors_kernel_index out of range for the filter")
-        if status[0] & 1:
-            raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index "
-                               "(non-lattice neighbourhood); not representable by the dense kernel map")
+        if prebuilt is not None:  # dense map already built (lattice rulebook)
+            mws, n_out = prebuilt
+        else:
+            n_out = rs.shape[0] - 1
+            mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
+            status = np.zeros(1, np.int32)
+            want_inv = int(bool(want_grad))  # the inverse map serves dIn / dW only
+            _lib.call("o3dml_sparse_conv_build_map", ptr(nidx), ptr(kidx), ptr(nimp), ptr(rs), n_out, n_in, K,
+                      int(bool(normalize)), ptr(out_importance), want_inv, status.ctypes.data, ptr(mws), mws.numel(),
+                      st)
+            if status[0] & 2:
+                raise RuntimeError("sparse_conv: neighbors_kernel_index out of range for the filter")
+            if status[0] & 1:
+                raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index "
+                                   "(non-lattice neighbourhood); not representable by the dense kernel map")
         W = filters.detach().contiguous()
         x = inp_features.detach().contiguous()
         out = torch.empty((n_out, cout), dtype=torch.float32, device=dev)
@@ -69,7 +73,7 @@ class _ConvFn(torch.autograd.Function):
                   int(has_nimp), use_os, ptr(g), n_out, ptr(gx), ptr(gw), ptr(mws), mws.numel(), ptr(ws), ws.numel(),
                   stream_handle(dev))
         gb = g.sum(0) if (has_bias and ctx.needs_input_grad[2]) else None
-        return gw, gx, gb, None, None, None, None, None, None, None, None
+        return gw, gx, gb, None, None, None, None, None, None, None, None, None
 
 
 def _conv(filters, inp_features, bias, neighbors_index, neighbors_kernel_index, neighbors_importance,
@@ -134,6 +138,43 @@ def conv_with_bias(filters, bias, inp_features, neighbors_index, neighbors_kerne
     dev = gpu_device(inp_features, filters)
     return _conv(filters, inp_features, bias, neighbors_index, neighbors_kernel_index, None, neighbors_row_splits,
                  _opt(inp_importance, dev), normalize, None)
+
+
+def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, voxel_size, mirror=False,
+                 inp_importance=None, normalize=False, out_importance=None):
+    """Layer forward with the lattice rulebook (dense kernel map straight from a
+    voxel hash; csrc/sparse_conv.hip o3dml_sparse_conv_lattice_map).  Returns
+    None when the positions are not on one voxel lattice — the caller then
+    builds the rulebook with the Linf fixed-radius search (same map)."""
+    dev = gpu_device(inp_features, filters)
+    ks = int(filters.shape[0])
+    if tuple(filters.shape[:3]) != (ks, ks, ks) or ks > 3:
+        return None
+    x = to_dev(inp_features, dev)
+    ip = to_dev(inp_positions, dev, torch.float32)
+    qp = to_dev(query_positions, dev, torch.float32)
+    lib = _lib.load()
+    K = ks ** 3
+    n_in, n_out = ip.shape[0], qp.shape[0]
+    b = None if bias is None else bias.to(dev)
+    want_grad = torch.is_grad_enabled() and (filters.requires_grad or x.requires_grad or
+                                             (b is not None and b.requires_grad))
+    mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
+    lws = workspace(lib.o3dml_sparse_conv_lattice_workspace_size(n_in), dev)
+    oimp = _opt(out_importance, dev)
+    status = np.zeros(1, np.int32)
+    _lib.call("o3dml_sparse_conv_lattice_map", ptr(ip), n_in, ptr(qp), n_out, float(voxel_size), ks,
+              int(bool(mirror)), int(bool(normalize)), ptr(oimp), int(bool(want_grad)), status.ctypes.data, ptr(mws),
+              mws.numel(), ptr(lws), lws.numel(), stream_handle(dev))
+    if status[0] & 4:
+        return None
+    if status[0] & 1:
+        raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index")
+    f = filters.to(dev)
+    empty = torch.empty(0, dtype=torch.int64, device=dev)
+    out = _ConvFn.apply(f, x, b, empty, empty, None, empty, _opt(inp_importance, dev), bool(normalize), oimp,
+                        want_grad, (mws, n_out))
+    return out if inp_features.is_cuda else out.cpu()
 
 
 def kernel_index(inp_positions, query_positions, neighbors_index, neighbors_row_splits, kernel_size, voxel_size,

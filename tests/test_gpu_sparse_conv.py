@@ -136,3 +136,51 @@ def test_sparse_conv_importance_normalize(cuda):
                           normalize=True)
     ref = O.sparse_conv(W, x, oi, ok, ors, inp_importance=ii, neighbors_importance=ni, normalize=True)
     _close(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("case", ["submanifold", "strided", "transposed"])
+def test_lattice_rulebook_equals_search_rulebook(cuda, case):
+    """The lattice rulebook (voxel hash) and the Linf fixed-radius-search
+    rulebook give the same dense kernel map, so outputs and gradients agree
+    bit for bit."""
+    from o3dml_amd import layers
+    from o3dml_amd.ops import calculate_grid
+    pos = torch.from_numpy(_voxels(5000, 30, 11)).to(cuda)
+    torch.manual_seed(1)
+    if case == "submanifold":
+        conv = layers.SparseConv(16, 24, [3, 3, 3]).to(cuda)
+        inp, outp = pos, pos
+    elif case == "strided":
+        conv = layers.SparseConv(16, 24, [2, 2, 2], offset=torch.full((3,), -0.5)).to(cuda)
+        inp, outp = pos, calculate_grid(pos)
+    else:
+        conv = layers.SparseConvTranspose(16, 24, [2, 2, 2], offset=torch.full((3,), -0.5)).to(cuda)
+        inp, outp = calculate_grid(pos), pos
+    feat = torch.randn(inp.shape[0], 16, device=cuda, requires_grad=True)
+    outs, grads = [], []
+    for lattice in (True, False):
+        conv.lattice_rulebook = lattice
+        conv.kernel.grad = None
+        feat.grad = None
+        out = conv(feat, inp, outp, 1.0)
+        out.square().sum().backward()
+        outs.append(out.detach())
+        grads.append((feat.grad.clone(), conv.kernel.grad.clone()))
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+
+
+def test_lattice_rulebook_falls_back_off_lattice(cuda):
+    from o3dml_amd import layers, sparse_conv as sc
+    pos = _voxels(3000, 20, 5)
+    jitter = pos + np.random.default_rng(0).uniform(-0.2, 0.2, pos.shape).astype(np.float32)
+    p = torch.from_numpy(jitter).to(cuda)
+    conv = layers.SparseConv(8, 8, [3, 3, 3]).to(cuda)
+    feat = torch.randn(len(pos), 8, device=cuda)
+    with torch.no_grad():
+        assert sc.conv_lattice(conv.kernel, conv.bias, feat, p, p, 1.0) is None  # not a lattice
+        out = conv(feat, p, p, 1.0)
+    oi, ors, _ = O.fixed_radius_search(jitter, jitter, 1.5, metric="Linf")
+    ok = O.kernel_index(jitter, jitter, oi, ors, [3, 3, 3], 1.0)
+    ref = O.sparse_conv(conv.kernel.detach().cpu().numpy(), feat.cpu().numpy(), oi, ok, ors)
+    _close(out.cpu().numpy(), ref + conv.bias.detach().cpu().numpy())
