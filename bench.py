@@ -159,7 +159,8 @@ def randla_frames(dev, frames):
 def make_room(seed=0):
     """C4-shaped voxel set: ~80k active 2 cm voxels on room surfaces
     (4 m x 3 m floor, 1.2 m walls, four boxes), half-integer positions in voxel
-    units, 3 colour features U[0,1)."""
+    units in ops.voxelize output order (x-fastest linear id, as InputLayer feeds
+    the convolutions), 3 colour features U[0,1)."""
     rng = np.random.default_rng(seed)
     vox = set()
     X, Y, H = 200, 150, 60
@@ -182,8 +183,9 @@ def make_room(seed=0):
         for x in range(bx, bx + sx):
             for y in range(by, by + sy):
                 vox.add((x, y, sz))
-    pos = np.array(sorted(vox), np.float32) + 0.5
-    pos = pos[rng.permutation(len(pos))]
+    v = np.array(list(vox), np.int64)
+    v = v[np.lexsort((v[:, 0], v[:, 1], v[:, 2]))]  # voxelize order: linear id, x fastest
+    pos = v.astype(np.float32) + 0.5
     return pos, rng.random((len(pos), 3), dtype=np.float32)
 
 

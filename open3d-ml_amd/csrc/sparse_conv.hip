@@ -364,8 +364,19 @@ __device__ __forceinline__ uint32_t lat_hash(uint64_t k) {
 }
 
 // per-axis [min frac, max frac, min key, max key] of p / vs (frac as float bits,
-// keys as ints) for one point set -> stats[0..11]
-__global__ void lattice_stats_kernel(const float* __restrict__ pos, int64_t n, float inv_vs, int* __restrict__ stats) {
+// keys as ints) for one point set -> stats[0..11]; block-reduced in LDS, one
+// atomic per block and statistic
+__global__ void __launch_bounds__(256) lattice_stats_kernel(const float* __restrict__ pos, int64_t n, float inv_vs,
+                                                            int* __restrict__ stats) {
+    __shared__ int red[12][256];
+    int v[12];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        v[4 * d + 0] = 0x7fffffff;
+        v[4 * d + 1] = 0;
+        v[4 * d + 2] = 0x7fffffff;
+        v[4 * d + 3] = static_cast<int>(0x80000000u);
+    }
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
 #pragma unroll
@@ -374,11 +385,28 @@ __global__ void lattice_stats_kernel(const float* __restrict__ pos, int64_t n, f
             const float fl = floorf(u);
             const float fr = u - fl;  // >= 0, so int ordering of the bits is float ordering
             const int key = fabsf(fl) < 1.0e6f ? static_cast<int>(fl) : 0x7fffffff;
-            atomicMin(&stats[4 * d + 0], __float_as_int(fr));
-            atomicMax(&stats[4 * d + 1], __float_as_int(fr));
-            atomicMin(&stats[4 * d + 2], key);
-            atomicMax(&stats[4 * d + 3], key);
+            v[4 * d + 0] = min(v[4 * d + 0], __float_as_int(fr));
+            v[4 * d + 1] = max(v[4 * d + 1], __float_as_int(fr));
+            v[4 * d + 2] = min(v[4 * d + 2], key);
+            v[4 * d + 3] = max(v[4 * d + 3], key);
         }
+    }
+#pragma unroll
+    for (int j = 0; j < 12; ++j) red[j][threadIdx.x] = v[j];
+    __syncthreads();
+    for (int w = 128; w >= 1; w >>= 1) {
+        if (threadIdx.x < w) {
+#pragma unroll
+            for (int j = 0; j < 12; ++j) {
+                const int o = red[j][threadIdx.x + w];
+                red[j][threadIdx.x] = (j & 1) ? max(red[j][threadIdx.x], o) : min(red[j][threadIdx.x], o);
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 12) {
+        const int j = threadIdx.x;
+        if (j & 1) atomicMax(&stats[j], red[j][0]); else atomicMin(&stats[j], red[j][0]);
     }
 }
 
@@ -411,42 +439,49 @@ struct LatticeOffsets {
     int off[3][8];  // key_p - key_q for kernel index j along axis d (x, y, z)
 };
 
-// map[o*K + k] for k = (kz*ks + ky)*ks + kx; norm[o] = neighbour count
+// map[o*K + k] for k = (kz*ks + ky)*ks + kx: one thread per (output, offset)
 __global__ void lattice_map_kernel(const float* __restrict__ inp_pos, const float* __restrict__ qpos, int64_t n_out,
                                    float inv_vs, float radius, int ks, LatticeOffsets lo,
                                    const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, uint32_t mask,
-                                   int32_t* __restrict__ map, float* __restrict__ norm) {
+                                   int32_t* __restrict__ map) {
     const int K = ks * ks * ks;
+    const int64_t total = n_out * K;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t o = e / K;
+        const int k = static_cast<int>(e - o * K);
+        const float qx = qpos[3 * o], qy = qpos[3 * o + 1], qz = qpos[3 * o + 2];
+        const int ix = k % ks, iy = (k / ks) % ks, iz = k / (ks * ks);
+        const uint64_t key = lat_key(static_cast<int>(floorf(qx * inv_vs)) + lo.off[0][ix],
+                                     static_cast<int>(floorf(qy * inv_vs)) + lo.off[1][iy],
+                                     static_cast<int>(floorf(qz * inv_vs)) + lo.off[2][iz]);
+        uint32_t h = lat_hash(key) & mask;
+        int32_t found = -1;
+        while (true) {
+            const uint64_t kk = keys[h];
+            if (kk == key) {
+                found = vals[h];
+                break;
+            }
+            if (kk == kLatEmpty) break;
+            h = (h + 1) & mask;
+        }
+        if (found >= 0) {  // the fixed-radius (Linf) test the search would apply
+            const float dx = fabsf(inp_pos[3 * found] - qx), dy = fabsf(inp_pos[3 * found + 1] - qy),
+                        dz = fabsf(inp_pos[3 * found + 2] - qz);
+            const float m = dx > dy ? dx : dy;
+            if ((m > dz ? m : dz) > radius) found = -1;
+        }
+        map[e] = found;
+    }
+}
+
+__global__ void map_count_kernel(const int32_t* __restrict__ map, int64_t n_out, int K, float* __restrict__ norm) {
     for (int64_t o = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; o < n_out;
          o += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const float qx = qpos[3 * o], qy = qpos[3 * o + 1], qz = qpos[3 * o + 2];
-        const int kx0 = static_cast<int>(floorf(qx * inv_vs)), ky0 = static_cast<int>(floorf(qy * inv_vs)),
-                  kz0 = static_cast<int>(floorf(qz * inv_vs));
-        int cnt = 0;
-        for (int k = 0; k < K; ++k) {
-            const int ix = k % ks, iy = (k / ks) % ks, iz = k / (ks * ks);
-            const uint64_t key = lat_key(kx0 + lo.off[0][ix], ky0 + lo.off[1][iy], kz0 + lo.off[2][iz]);
-            uint32_t h = lat_hash(key) & mask;
-            int32_t found = -1;
-            while (true) {
-                const uint64_t kk = keys[h];
-                if (kk == key) {
-                    found = vals[h];
-                    break;
-                }
-                if (kk == kLatEmpty) break;
-                h = (h + 1) & mask;
-            }
-            if (found >= 0) {  // the fixed-radius (Linf) test the search would apply
-                const float dx = fabsf(inp_pos[3 * found] - qx), dy = fabsf(inp_pos[3 * found + 1] - qy),
-                            dz = fabsf(inp_pos[3 * found + 2] - qz);
-                const float m = dx > dy ? dx : dy;
-                if ((m > dz ? m : dz) > radius) found = -1;
-            }
-            map[o * K + k] = found;
-            cnt += found >= 0 ? 1 : 0;
-        }
-        norm[o] = static_cast<float>(cnt);
+        int c = 0;
+        for (int k = 0; k < K; ++k) c += map[o * K + k] >= 0 ? 1 : 0;
+        norm[o] = static_cast<float>(c);
     }
 }
 
@@ -513,7 +548,7 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
 O3DML_API size_t o3dml_sparse_conv_lattice_workspace_size(int64_t n_in) {
     int64_t cap = 64;
     while (cap < 2 * n_in) cap <<= 1;
-    return ws_bytes<uint64_t>(cap) + ws_bytes<int32_t>(cap) + ws_bytes<int>(16);
+    return ws_bytes<uint64_t>(cap) + ws_bytes<int32_t>(cap) + ws_bytes<int>(32);
 }
 
 // Dense kernel map (same workspace layout as o3dml_sparse_conv_build_map) for
@@ -550,7 +585,7 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     while (cap < 2 * n_in) cap <<= 1;
     uint64_t* keys = lws.take<uint64_t>(cap);
     int32_t* vals = lws.take<int32_t>(cap);
-    int* stats = lws.take<int>(16);
+    int* stats = lws.take<int>(32);
     const float inv_vs = 1.0f / voxel_size;
     // ---- 1. lattice check (fractions constant per axis, keys in range)
     int init[16];
@@ -562,14 +597,13 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     }
     int h_in[12], h_q[12];
     O3DML_CHECK_HIP(hipMemcpyAsync(stats, init, sizeof(int) * 12, hipMemcpyHostToDevice, st));
-    lattice_stats_kernel<<<stream_grid(n_in, 256), 256, 0, st>>>(inp_pos, n_in, inv_vs, stats);
+    O3DML_CHECK_HIP(hipMemcpyAsync(stats + 12, init, sizeof(int) * 12, hipMemcpyHostToDevice, st));
+    lattice_stats_kernel<<<stream_grid(n_in, 256, 512), 256, 0, st>>>(inp_pos, n_in, inv_vs, stats);
+    O3DML_LAUNCH_CHECK();
+    lattice_stats_kernel<<<stream_grid(n_out, 256, 512), 256, 0, st>>>(query_pos, n_out, inv_vs, stats + 12);
     O3DML_LAUNCH_CHECK();
     O3DML_CHECK_HIP(hipMemcpyAsync(h_in, stats, sizeof(int) * 12, hipMemcpyDeviceToHost, st));
-    O3DML_CHECK_HIP(hipStreamSynchronize(st));
-    O3DML_CHECK_HIP(hipMemcpyAsync(stats, init, sizeof(int) * 12, hipMemcpyHostToDevice, st));
-    lattice_stats_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(query_pos, n_out, inv_vs, stats);
-    O3DML_LAUNCH_CHECK();
-    O3DML_CHECK_HIP(hipMemcpyAsync(h_q, stats, sizeof(int) * 12, hipMemcpyDeviceToHost, st));
+    O3DML_CHECK_HIP(hipMemcpyAsync(h_q, stats + 12, sizeof(int) * 12, hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
     LatticeOffsets lo{};
     const double h = 0.5 * ksize;
@@ -611,11 +645,14 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     lattice_insert_kernel<<<stream_grid(n_in, 256), 256, 0, st>>>(inp_pos, n_in, inv_vs, keys, vals,
                                                                  static_cast<uint32_t>(cap - 1), status);
     O3DML_LAUNCH_CHECK();
-    lattice_map_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(inp_pos, query_pos, n_out, inv_vs,
-                                                               0.5f * voxel_size * static_cast<float>(ksize), ksize,
-                                                               lo, keys, vals, static_cast<uint32_t>(cap - 1), map,
-                                                               norm);
+    lattice_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(
+            inp_pos, query_pos, n_out, inv_vs, 0.5f * voxel_size * static_cast<float>(ksize), ksize, lo, keys, vals,
+            static_cast<uint32_t>(cap - 1), map);
     O3DML_LAUNCH_CHECK();
+    if (normalize) {
+        map_count_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(map, n_out, K, norm);
+        O3DML_LAUNCH_CHECK();
+    }
     recip_norm_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(normalize ? norm : nullptr, out_importance, n_out,
                                                               oscale);
     O3DML_LAUNCH_CHECK();
