@@ -115,11 +115,10 @@ struct GemmStage {
 };
 
 template <bool VEC4>
-__device__ __forceinline__ void gemm_load(GemmStage& st, const int32_t* __restrict__ map, int K, int64_t o, bool orow,
-                                          int k, int c0, int h, int col, const float* __restrict__ src,
-                                          const float* __restrict__ sscale, const float* __restrict__ pscale,
-                                          const float* __restrict__ W, int cin, int cout) {
-    const int32_t m = orow ? map[o * K + k] : -1;
+__device__ __forceinline__ void gemm_load(GemmStage& st, int32_t m, int K, int64_t o, int k, int c0, int h, int col,
+                                          const float* __restrict__ src, const float* __restrict__ sscale,
+                                          const float* __restrict__ pscale, const float* __restrict__ W, int cin,
+                                          int cout) {
     const int cb = c0 + 16 * h;
     float sc = 0.f;
     if (m >= 0) sc = (sscale ? sscale[m] : 1.f) * (pscale ? pscale[o * K + k] : 1.f);
@@ -156,19 +155,29 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
     const int i = lane & 31, h = lane >> 5;
     const int col = blockIdx.y * 32 + i;
     const int64_t o = o0 + i;
-    const bool orow = o < n_out;
-    unsigned used = 0u;  // offsets any of the wave's 32 rows uses
-    for (int k = 0; k < K; ++k) {
-        const int32_t m = orow ? map[o * K + k] : -1;
-        if (__ballot(m >= 0) != 0ull) used |= 1u << k;
+    // the wave's 32 map rows -> LDS (one coalesced sweep), offsets in use
+    __shared__ int32_t mtile_all[kGemmThreads / 64][32 * 32];
+    int32_t* mtile = mtile_all[threadIdx.x >> 6];
+    for (int e = lane; e < 32 * K; e += 64) {
+        const int64_t oo = o0 + e / K;
+        mtile[e] = oo < n_out ? map[o0 * K + e] : -1;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    unsigned used = 0u;
+    for (int k = h; k < K; k += 2) {  // lanes 0-31 test even k, lanes 32-63 odd k
+        const uint64_t b = __ballot(mtile[i * K + k] >= 0);
+        used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
+    }
+    used |= __builtin_amdgcn_readlane(used, 32) | __builtin_amdgcn_readlane(used, 0);
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     if (used) {
         GemmStage cur, nxt;
         int k = __builtin_ctz(used), c0 = 0;
-        gemm_load<VEC4>(cur, map, K, o, orow, k, c0, h, col, src, sscale, pscale, W, cin, cout);
+        gemm_load<VEC4>(cur, mtile[i * K + k], K, o, k, c0, h, col, src, sscale, pscale, W, cin, cout);
         while (true) {
             int nk = k, nc = c0 + 32;
             if (nc >= cin) {
@@ -176,7 +185,8 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
                 const unsigned rest = k + 1 < 32 ? used & ~((2u << k) - 1u) : 0u;
                 nk = rest ? __builtin_ctz(rest) : -1;
             }
-            if (nk >= 0) gemm_load<VEC4>(nxt, map, K, o, orow, nk, nc, h, col, src, sscale, pscale, W, cin, cout);
+            if (nk >= 0)
+                gemm_load<VEC4>(nxt, mtile[i * K + nk], K, o, nk, nc, h, col, src, sscale, pscale, W, cin, cout);
 #pragma unroll
             for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[s], cur.b[s], acc, 0, 0, 0);
             if (nk < 0) break;
