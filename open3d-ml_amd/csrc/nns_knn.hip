@@ -13,6 +13,8 @@
 // of the query's batch item + stable radix sort on the distance bits.
 // Result order per query: ascending (distance, index) — exact ties by index.
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "grid.hpp"
@@ -48,15 +50,12 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
         float kd = INFINITY;
         uint32_t ki = 0xffffffffu;
         int cnt = 0;
-        auto visit = [&](int x, int y, int z) {
-            const uint32_t c = g.offset + static_cast<uint32_t>(x + g.dx * (y + g.dy * z));
-            const uint32_t s = splits[c], e = splits[c + 1];
-            for (uint32_t j = s; j < e; ++j) {
-                const float4 p = sorted[j];
-                if (IGNORE && p.x == qx && p.y == qy && p.z == qz) continue;
+        auto consider = [&](const float4& p) {
+            {
+                if (IGNORE && p.x == qx && p.y == qy && p.z == qz) return;
                 const float d = dist_metric<METRIC>(p.x, p.y, p.z, qx, qy, qz);
                 const uint32_t id = __float_as_uint(p.w);
-                if (!lex_less(d, id, kd, ki)) continue;
+                if (!lex_less(d, id, kd, ki)) return;
                 ++cnt;
 #pragma unroll
                 for (int r = K - 1; r >= 0; --r) {
@@ -79,6 +78,19 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
                         }
                 }
             }
+        };
+        auto visit = [&](int x, int y, int z) {
+            const uint32_t c = g.offset + static_cast<uint32_t>(x + g.dx * (y + g.dy * z));
+            const uint32_t s = splits[c], e = splits[c + 1];
+            uint32_t j = s;
+            for (; j + 8 <= e; j += 8) {  // 8 loads in flight per lane
+                float4 p[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) p[u] = sorted[j + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) consider(p[u]);
+            }
+            for (; j < e; ++j) consider(sorted[j]);
         };
         for (int R = 0;; ++R) {
             const int x0 = cx - R, x1 = cx + R, y0 = cy - R, y1 = cy + R, z0 = cz - R, z1 = cz + R;
@@ -217,6 +229,7 @@ O3DML_API size_t o3dml_knn_search_workspace_size(int64_t n_points, int64_t n_que
            ws_bytes<int32_t>(n_queries * k) + ws_bytes<float>(n_queries * k) + ws_bytes<int64_t>(n_queries) +
            prim::scan_workspace_bytes(n_queries);
 }
+
 
 // Phase 1: search; writes neighbors_row_splits [M+1] (device) and keeps the
 // per-query results in the workspace for o3dml_knn_search_fill.

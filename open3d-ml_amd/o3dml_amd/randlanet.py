@@ -327,18 +327,27 @@ class SemSegInference:
         possibility.index_add_(0, idxs, delta)
         pc = pc.clone()
         pc[:, :2] -= pc[:, :2].mean(0)  # augment recenter dim [0, 1]
+        # all levels are prefixes of the shuffled patch: one batched self-kNN
+        # (k=16) and one batched up-sampling kNN (k=1) cover the 4 layers
+        L = cfg["num_layers"]
+        sizes = [pc.shape[0]]
+        for i in range(L):
+            sizes.append(sizes[-1] // cfg["sub_sampling_ratio"][i])
+        levels = [pc[:sizes[i]] for i in range(L + 1)]
+        k = cfg["num_neighbors"]
+        cat = torch.cat(levels[:L]).contiguous()
+        rs = np.concatenate([[0], np.cumsum(sizes[:L])]).astype(np.int64)
+        nb_all = ops.knn_search(cat, cat, k, rs, rs).neighbors_index.view(-1, k)
+        sup = torch.cat(levels[1:]).contiguous()
+        srs = np.concatenate([[0], np.cumsum(sizes[1:])]).astype(np.int64)
+        up_all = ops.knn_search(sup, cat, 1, srs, rs).neighbors_index.long()
         coords, nbrs, subs, ups = [], [], [], []
-        cur = pc
-        for i in range(cfg["num_layers"]):
-            nb = ops.knn_search(cur, cur, cfg["num_neighbors"]).neighbors_index.view(-1, cfg["num_neighbors"])
-            m = cur.shape[0] // cfg["sub_sampling_ratio"][i]
-            nxt = cur[:m].contiguous()
-            up = ops.knn_search(nxt, cur, 1).neighbors_index.long()
-            coords.append(cur)
+        for i in range(L):
+            nb = (nb_all[rs[i]:rs[i + 1]] - int(rs[i])).contiguous()
+            coords.append(levels[i].contiguous())
             nbrs.append(nb)
-            subs.append(nb[:m].contiguous())
-            ups.append(up)
-            cur = nxt
+            subs.append(nb[:sizes[i + 1]].contiguous())
+            ups.append(up_all[rs[i]:rs[i + 1]] - int(srs[i]))
         return pc, idxs, coords, nbrs, subs, ups
 
     @torch.no_grad()
