@@ -109,10 +109,7 @@ def fixed_radius_search(points, queries, radius, points_row_splits=None, queries
     common = (ptr(pts), n, ptr(qry), m, r, B, ptr(prs_d), ptr(qrs_d), prs.ctypes.data, ptr(hts_d), ptr(hti_d),
               ptr(hcs_d), mcode, int(bool(ignore_query_point)), int(same), int(bool(return_distances)))
     _lib.call("o3dml_fixed_radius_search_count", *common, ptr(rs), ptr(ws), ws.numel(), st)
-    if ignore_query_point:
-        total = int(rs[-1].item())
-    else:  # min(k, N_b) per query: known on the host, no device read
-        total = int(sum((qrs[b + 1] - qrs[b]) * min(k, prs[b + 1] - prs[b]) for b in range(B)))
+    total = int(rs[-1].item())
     idx = torch.empty(total, dtype=torch.int32 if bits == 32 else torch.int64, device=dev)
     dist = torch.empty(total if return_distances else 0, dtype=torch.float32, device=dev)
     _lib.call("o3dml_fixed_radius_search_fill", *common, ptr(rs), bits, ptr(idx),
