@@ -82,22 +82,18 @@ __global__ void grid_key_kernel(const float* __restrict__ pts, int64_t n, const 
     }
 }
 
-// CSR splits from sorted keys: splits[c] = first position with key >= c.
+// CSR splits from sorted keys: splits[c] = first position with key >= c —
+// one thread per cell, binary search (balanced however many cells are empty).
 __global__ void key_boundaries_kernel(const uint32_t* __restrict__ skeys, int64_t n, int64_t n_cells,
                                       uint32_t* __restrict__ splits) {
-    if (n == 0) {
-        for (int64_t c = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; c <= n_cells;
-             c += static_cast<int64_t>(gridDim.x) * blockDim.x)
-            splits[c] = 0;
-        return;
-    }
-    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
-         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t k = skeys[j];
-        const int64_t kp = j == 0 ? -1 : static_cast<int64_t>(skeys[j - 1]);
-        for (int64_t c = kp + 1; c <= k; ++c) splits[c] = static_cast<uint32_t>(j);
-        if (j == n - 1)
-            for (int64_t c = k + 1; c <= n_cells; ++c) splits[c] = static_cast<uint32_t>(n);
+    for (int64_t c = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; c <= n_cells;
+         c += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        int64_t lo = 0, hi = n;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (static_cast<int64_t>(skeys[mid]) < c) lo = mid + 1; else hi = mid;
+        }
+        splits[c] = static_cast<uint32_t>(lo);
     }
 }
 
@@ -205,7 +201,7 @@ inline GridIndex build_grid(const float* pts, int64_t n, const int64_t* rs_dev, 
         gather_float4_kernel<<<stream_grid(n, 256), 256, 0, st>>>(pts, gi.order, n, gi.sorted);
         O3DML_LAUNCH_CHECK();
     }
-    key_boundaries_kernel<<<stream_grid(n > 0 ? n : gi.cells + 1, 256), 256, 0, st>>>(skeys, n, gi.cells, gi.splits);
+    key_boundaries_kernel<<<stream_grid(gi.cells + 1, 256, 1 << 16), 256, 0, st>>>(skeys, n, gi.cells, gi.splits);
     O3DML_LAUNCH_CHECK();
     return gi;
 }
