@@ -215,6 +215,25 @@ int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, const floa
                                   int want_inverse, int* status_host, void* workspace, size_t workspace_bytes,
                                   void* lattice_workspace, size_t lattice_workspace_bytes, void* stream);
 
+/* ---- KPConv neighbourhood aggregation (ml3d/torch/models/
+ * kpconv.py:1005-1159).  q_pts f32 [n,3], s_pts f32 [n_support,3], neighbors
+ * [n, nb] (int32/int64 per index_bits; index n_support = shadow, zero
+ * contribution), features f32 [n_support, cin], kernel_points f32 [K,3] or
+ * per query [n,K,3] (kp_per_query), influence 0 constant / 1 linear /
+ * 2 gaussian, closest = nearest-kernel-point aggregation, modulations f32
+ * [n,K] nullable -> out WF f32 [n, K, cin] with WF[q,k] = sum_j infl * x[j].
+ * The backward accumulates grad_features [n_support, cin] (must be zeroed)
+ * from grad WF with fp32 atomics. ---------------------------------------- */
+int o3dml_kpconv_weighted_features(const float* q_pts, int64_t n, const float* s_pts, int64_t n_support,
+                                   const void* neighbors, int index_bits, int nb, const float* features, int cin,
+                                   const float* kernel_points, int K, int kp_per_query, float extent, int influence,
+                                   int closest, const float* modulations, float* out, void* stream);
+int o3dml_kpconv_weighted_features_backward(const float* q_pts, int64_t n, const float* s_pts, int64_t n_support,
+                                            const void* neighbors, int index_bits, int nb, const float* grad_wf,
+                                            int cin, const float* kernel_points, int K, int kp_per_query,
+                                            float extent, int influence, int closest, float* grad_features,
+                                            void* stream);
+
 /* ---- RandLA-Net neighbour gathers (ml3d/torch/models/
  * randlanet.py).  Channels-last: coords f32 [N,3], neighbour indices int32
  * [N,K], per-pair tensors [N,K,C], per-point [N,C].

@@ -1,0 +1,215 @@
+// kpconv.hip — fused KPConv neighbourhood aggregation (SURVEY.md §8a A18;
+// ml3d/torch/models/kpconv.py:1005-1159, KPConv.forward).
+//
+// The reference materialises [n, nb, K, 3] differences, [n, K, nb] influences
+// and [n, nb, Cin] gathered features, then  WF = influences @ gathered
+// ([n, K, Cin]) and  out = sum_k WF[:, k] @ W[k].  Here one wave owns one
+// query: the K x nb influences are computed once into LDS (lane per
+// neighbour), then lanes own channels and accumulate the K weighted sums
+// while streaming the neighbours' feature rows (coalesced, each row read
+// once); WF is written once.  out = WF.view(n, K*Cin) @ W.view(K*Cin, Cout)
+// is then a plain dense GEMM (hipBLASLt through torch).
+//
+// Shadow neighbours (index == n_support, the reference's point at 1e6 with a
+// zero feature, kpconv.py:1048, 1139) contribute exactly zero and are skipped.
+// Influence: 0 constant, 1 linear max(0, 1 - d/extent), 2 gaussian
+// exp(-d^2 / (2 sigma^2)), sigma = 0.3 extent (kpconv.py radius_gaussian);
+// closest: only the nearest kernel point of each neighbour contributes.
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace o3dml {
+
+constexpr int kKpMaxK = 32;    // kernel points
+
+template <int INFL, bool CLOSEST>
+__device__ __forceinline__ void kp_influences(float dx, float dy, float dz, const float* __restrict__ kq, int K,
+                                              float extent, float* __restrict__ wrow) {
+    float best = INFINITY;
+    int bk = 0;
+#pragma unroll
+    for (int k = 0; k < kKpMaxK; ++k) {  // compile-time indices: wrow may live in registers
+        if (k >= K) continue;
+        const float ex = dx - kq[3 * k], ey = dy - kq[3 * k + 1], ez = dz - kq[3 * k + 2];
+        const float d2 = ex * ex + ey * ey + ez * ez;
+        float v;
+        if constexpr (INFL == 0) v = 1.f;
+        else if constexpr (INFL == 1) v = fmaxf(1.f - sqrtf(d2) / extent, 0.f);
+        else v = __expf(-d2 / (2.f * (0.3f * extent) * (0.3f * extent)));
+        if (CLOSEST && d2 < best) {
+            best = d2;
+            bk = k;
+        }
+        wrow[k] = v;
+    }
+    if constexpr (CLOSEST) {
+#pragma unroll
+        for (int k = 0; k < kKpMaxK; ++k)
+            if (k < K && k != bk) wrow[k] = 0.f;
+    }
+}
+
+template <int INFL, bool CLOSEST, class TI>
+__global__ void __launch_bounds__(256) kpconv_wf_kernel(const float* __restrict__ q_pts, const float* __restrict__ s_pts,
+                                                        int64_t n_support, const TI* __restrict__ nbr, int64_t n,
+                                                        int nb, const float* __restrict__ x, int cin,
+                                                        const float* __restrict__ kp, int K, int kp_per_query,
+                                                        float extent, const float* __restrict__ modulations,
+                                                        float* __restrict__ wf) {
+    __shared__ float w_all[4][64][kKpMaxK + 1];
+    __shared__ int32_t id_all[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float(*w)[kKpMaxK + 1] = w_all[wv];
+    int32_t* ids = id_all[wv];
+    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+    for (int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + wv; q < n; q += nwaves) {
+        const float qx = q_pts[3 * q], qy = q_pts[3 * q + 1], qz = q_pts[3 * q + 2];
+        const float* kq = kp + (kp_per_query ? q * K * 3 : 0);
+        for (int c0 = 0; c0 < cin; c0 += 64) {
+            const int c = c0 + lane;
+            float acc[kKpMaxK];
+#pragma unroll
+            for (int k = 0; k < kKpMaxK; ++k) acc[k] = 0.f;
+            for (int j0 = 0; j0 < nb; j0 += 64) {
+                // influences of this chunk of neighbours: lane per neighbour
+                const int j = j0 + lane;
+                int64_t idx = -1;
+                if (j < nb) {
+                    const int64_t v = static_cast<int64_t>(nbr[q * nb + j]);
+                    if (v >= 0 && v < n_support) idx = v;  // shadow neighbours contribute zero
+                }
+                ids[lane] = static_cast<int32_t>(idx);
+                if (idx >= 0)
+                    kp_influences<INFL, CLOSEST>(s_pts[3 * idx] - qx, s_pts[3 * idx + 1] - qy, s_pts[3 * idx + 2] - qz,
+                                                 kq, K, extent, w[lane]);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // lanes own channels: acc[k] += w[j][k] * x[ids[j]][c]
+                const int jn = nb - j0 < 64 ? nb - j0 : 64;
+                if (c < cin) {
+                    for (int jj = 0; jj < jn; ++jj) {
+                        const int32_t id = ids[jj];
+                        if (id < 0) continue;
+                        const float xv = x[static_cast<int64_t>(id) * cin + c];
+#pragma unroll
+                        for (int k = 0; k < kKpMaxK; ++k)
+                            if (k < K) acc[k] = __builtin_fmaf(w[jj][k], xv, acc[k]);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (c < cin) {
+                float* o = wf + q * static_cast<int64_t>(K) * cin + c;
+#pragma unroll
+                for (int k = 0; k < kKpMaxK; ++k)
+                    if (k < K) o[static_cast<int64_t>(k) * cin] = modulations ? acc[k] * modulations[q * K + k] : acc[k];
+            }
+        }
+    }
+}
+
+// Backward of the aggregation for the features: dx[ids[j]][c] += sum_k w[j][k]
+// * dWF[q][k][c] (fp32 atomics; modulations folded into dWF by the caller).
+template <int INFL, bool CLOSEST, class TI>
+__global__ void __launch_bounds__(256) kpconv_wf_backward_kernel(const float* __restrict__ q_pts,
+                                                                 const float* __restrict__ s_pts, int64_t n_support,
+                                                                 const TI* __restrict__ nbr, int64_t n, int nb,
+                                                                 const float* __restrict__ dwf, int cin,
+                                                                 const float* __restrict__ kp, int K, int kp_per_query,
+                                                                 float extent, float* __restrict__ dx) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+    for (int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + wv; q < n; q += nwaves) {
+        const float qx = q_pts[3 * q], qy = q_pts[3 * q + 1], qz = q_pts[3 * q + 2];
+        const float* kq = kp + (kp_per_query ? q * K * 3 : 0);
+        for (int j = 0; j < nb; ++j) {
+            const int64_t idx = static_cast<int64_t>(nbr[q * nb + j]);
+            if (idx < 0 || idx >= n_support) continue;
+            const float dxp = s_pts[3 * idx] - qx, dyp = s_pts[3 * idx + 1] - qy, dzp = s_pts[3 * idx + 2] - qz;
+            float wk[kKpMaxK];
+#pragma unroll
+            for (int k = 0; k < kKpMaxK; ++k) wk[k] = 0.f;
+            kp_influences<INFL, CLOSEST>(dxp, dyp, dzp, kq, K, extent, wk);
+            for (int c = lane; c < cin; c += 64) {
+                float s = 0.f;
+                const float* g = dwf + q * static_cast<int64_t>(K) * cin + c;
+#pragma unroll
+                for (int k = 0; k < kKpMaxK; ++k)
+                    if (k < K) s = __builtin_fmaf(wk[k], g[static_cast<int64_t>(k) * cin], s);
+                atomicAdd(dx + idx * cin + c, s);
+            }
+        }
+    }
+}
+
+template <bool BWD, class TI>
+static void launch_kp(int influence, int closest, unsigned g, hipStream_t st, const float* qp, const float* sp,
+                      int64_t ns, const void* nbr, int64_t n, int nb, const float* in, int cin, const float* kp, int K,
+                      int kpq, float extent, const float* mod, float* out) {
+#define O3DML_KP(I, C)                                                                                            \
+    do {                                                                                                          \
+        if constexpr (BWD)                                                                                        \
+            kpconv_wf_backward_kernel<I, C, TI><<<g, 256, 0, st>>>(qp, sp, ns, static_cast<const TI*>(nbr), n, nb, \
+                                                                   in, cin, kp, K, kpq, extent, out);             \
+        else                                                                                                      \
+            kpconv_wf_kernel<I, C, TI><<<g, 256, 0, st>>>(qp, sp, ns, static_cast<const TI*>(nbr), n, nb, in, cin, \
+                                                          kp, K, kpq, extent, mod, out);                          \
+    } while (0)
+    if (influence == 0) {
+        if (closest) O3DML_KP(0, true); else O3DML_KP(0, false);
+    } else if (influence == 1) {
+        if (closest) O3DML_KP(1, true); else O3DML_KP(1, false);
+    } else {
+        if (closest) O3DML_KP(2, true); else O3DML_KP(2, false);
+    }
+#undef O3DML_KP
+    O3DML_LAUNCH_CHECK();
+}
+
+}  // namespace o3dml
+
+using namespace o3dml;
+
+O3DML_API int o3dml_kpconv_weighted_features(const float* q_pts, int64_t n, const float* s_pts, int64_t n_support,
+                                             const void* neighbors, int index_bits, int nb, const float* features,
+                                             int cin, const float* kernel_points, int K, int kp_per_query,
+                                             float extent, int influence, int closest, const float* modulations,
+                                             float* out, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(K >= 1 && K <= kKpMaxK, "KPConv: kernel points must be in [1, %d]", kKpMaxK);
+    O3DML_REQUIRE(nb >= 0, "KPConv: negative neighbour count");
+    O3DML_REQUIRE(influence >= 0 && influence <= 2, "KPConv: influence must be constant, linear or gaussian");
+    O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
+    if (n == 0) return 0;
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n, 4), 1 << 20));
+    if (index_bits == 32)
+        launch_kp<false, int32_t>(influence, closest, g, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
+                                  features, cin, kernel_points, K, kp_per_query, extent, modulations, out);
+    else
+        launch_kp<false, int64_t>(influence, closest, g, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
+                                  features, cin, kernel_points, K, kp_per_query, extent, modulations, out);
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_kpconv_weighted_features_backward(const float* q_pts, int64_t n, const float* s_pts,
+                                                      int64_t n_support, const void* neighbors, int index_bits, int nb,
+                                                      const float* grad_wf, int cin, const float* kernel_points, int K,
+                                                      int kp_per_query, float extent, int influence, int closest,
+                                                      float* grad_features, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(K >= 1 && K <= kKpMaxK, "KPConv: kernel points must be in [1, %d]", kKpMaxK);
+    O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
+    if (n == 0) return 0;
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n, 4), 1 << 20));
+    if (index_bits == 32)
+        launch_kp<true, int32_t>(influence, closest, g, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
+                                 grad_wf, cin, kernel_points, K, kp_per_query, extent, nullptr, grad_features);
+    else
+        launch_kp<true, int64_t>(influence, closest, g, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
+                                 grad_wf, cin, kernel_points, K, kp_per_query, extent, nullptr, grad_features);
+    O3DML_GUARD_END
+}

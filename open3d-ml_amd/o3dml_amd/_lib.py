@@ -55,6 +55,10 @@ SIGNATURES = {
     "o3dml_sparse_conv_lattice_workspace_size": (c_sz, [c_i64]),
     "o3dml_sparse_conv_lattice_map": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i32, c_i32, c_i32, c_p, c_i32, c_p,
                                               c_p, c_sz, c_p, c_sz, c_p]),
+    "o3dml_kpconv_weighted_features": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_i32,
+                                               c_i32, c_f32, c_i32, c_i32, c_p, c_p, c_p]),
+    "o3dml_kpconv_weighted_features_backward": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p,
+                                                        c_i32, c_i32, c_f32, c_i32, c_i32, c_p, c_p]),
     "o3dml_randla_relative_encoding": (c_i32, [c_p, c_i64, c_p, c_i32, c_p, c_p]),
     "o3dml_randla_attentive_pool": (c_i32, [c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p]),
     "o3dml_randla_gather_max": (c_i32, [c_p, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
