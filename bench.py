@@ -220,7 +220,30 @@ def sparse_conv_bench(dev, reps):
     return {"voxels": int(n), "pairs": pairs, "mvoxels_per_s_layer": round(n / t_layer / 1e6, 2),
             "ms_layer": round(t_layer * 1e3, 4), "ms_gemm": round(t_gemm * 1e3, 4),
             "tflops_gemm": round(flops / t_gemm / 1e12, 3),
-            "config": "C4: ~80k 2 cm room voxels, SparseConv 3^3 32->32 fp32, rulebook rebuilt per call"}
+            "config": "C4: ~80k 2 cm room voxels, SparseConv 3^3 32->32 fp32, rulebook rebuilt per call",
+            "unet": scn_bench(dev, pos, reps)}
+
+
+def scn_bench(dev, pos, reps):
+    """C4 whole-network forward: SparseConvUnet with the reference scannet
+    config (multiplier 32, residual blocks, 1 rep, 20 classes; random init, eval
+    mode), InputLayer -> 7-level UNet -> per-point logits, one point per voxel."""
+    import types
+    from o3dml_amd.sparseconvnet import SparseConvUnet
+    torch.manual_seed(0)
+    m = SparseConvUnet(multiplier=32, residual_blocks=True, conv_block_reps=1, num_classes=20).to(dev).eval()
+    feat = torch.rand((pos.shape[0], 3), device=dev)
+    inp = types.SimpleNamespace(point=[pos], feat=[feat], batch_lengths=[pos.shape[0]])
+    with torch.no_grad():
+        m(inp)
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(reps):
+            m(inp)
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t) / reps
+    return {"ms_per_frame": round(dt * 1e3, 3), "mvoxels_per_s": round(pos.shape[0] / dt / 1e6, 3),
+            "config": "SparseConvUnet m=32 residual reps=1 (sparseconvunet_scannet.yml), fp32, eval"}
 
 
 def timed_run(step, steps, warmup, world, sync):

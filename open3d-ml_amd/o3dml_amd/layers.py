@@ -123,8 +123,12 @@ class SparseConv(torch.nn.Module):
             return None
         vs = _voxel_size_scalar(voxel_size, inp_positions)
         queries = (out_positions - sign * self.offset.to(out_positions.device) * vs).contiguous()
+        if getattr(self, "_off_ver", None) != (self.offset._version, self.offset.device):
+            self._off_host = tuple(float(v) for v in self.offset.detach().cpu())  # one read per load
+            self._off_ver = (self.offset._version, self.offset.device)
+        off = self._off_host
         return sc.conv_lattice(self.kernel, kw.pop("bias", self.bias), inp_features, inp_positions, queries, vs,
-                               mirror=mirror, **kw)
+                               mirror=mirror, cache_key=(inp_positions, out_positions, sign) + off, **kw)
 
     def forward(self, inp_features, inp_positions, out_positions, voxel_size, inp_importance=None,
                 fixed_radius_search_hash_table=None):

@@ -5,6 +5,8 @@ The neighbourhood arrives as CSR pairs over OUTPUT points (neighbors_index,
 neighbors_kernel_index, neighbors_row_splits); the HIP library turns it into a
 dense kernel map and runs the MFMA implicit GEMM (forward), the inverse-map
 GEMM with W^T (input gradient) and split-K slabs (filter gradient)."""
+import contextlib
+
 import numpy as np
 import torch
 
@@ -140,8 +142,25 @@ def conv_with_bias(filters, bias, inp_features, neighbors_index, neighbors_kerne
                  _opt(inp_importance, dev), normalize, None)
 
 
+_MAP_CACHE = None  # dict while a rulebook_cache() scope is active
+
+
+@contextlib.contextmanager
+def rulebook_cache():
+    """Reuse dense kernel maps inside the scope: layers with the same input /
+    output positions, kernel size and offset (every same-level submanifold
+    convolution of a SparseConvUnet) share one rulebook.
+    Entries hold the position tensors, so their identities stay unique."""
+    global _MAP_CACHE
+    prev, _MAP_CACHE = _MAP_CACHE, {}
+    try:
+        yield
+    finally:
+        _MAP_CACHE = prev
+
+
 def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, voxel_size, mirror=False,
-                 inp_importance=None, normalize=False, out_importance=None):
+                 inp_importance=None, normalize=False, out_importance=None, cache_key=None):
     """Layer forward with the lattice rulebook (dense kernel map straight from a
     voxel hash; csrc/sparse_conv.hip o3dml_sparse_conv_lattice_map).  Returns
     None when the positions are not on one voxel lattice — the caller then
@@ -159,16 +178,27 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
     b = None if bias is None else bias.to(dev)
     want_grad = torch.is_grad_enabled() and (filters.requires_grad or x.requires_grad or
                                              (b is not None and b.requires_grad))
-    mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
-    lws = workspace(lib.o3dml_sparse_conv_lattice_workspace_size(n_in), dev)
     oimp = _opt(out_importance, dev)
-    status = np.zeros(1, np.int32)
-    _lib.call("o3dml_sparse_conv_lattice_map", ptr(ip), n_in, ptr(qp), n_out, float(voxel_size), ks,
-              int(bool(mirror)), int(bool(normalize)), ptr(oimp), int(bool(want_grad)), status.ctypes.data, ptr(mws),
-              mws.numel(), ptr(lws), lws.numel(), stream_handle(dev))
-    if status[0] & 4:
+    key = None
+    if _MAP_CACHE is not None and cache_key is not None and out_importance is None:
+        key = (ks, bool(mirror), bool(normalize), bool(want_grad), float(voxel_size)) + tuple(cache_key[2:])
+        key = key + (id(cache_key[0]), cache_key[0]._version, id(cache_key[1]), cache_key[1]._version)
+    hit = _MAP_CACHE.get(key) if key is not None else None
+    if hit is not None:
+        mws, status0 = hit[0], hit[1]
+    else:
+        mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
+        lws = workspace(lib.o3dml_sparse_conv_lattice_workspace_size(n_in), dev)
+        status = np.zeros(1, np.int32)
+        _lib.call("o3dml_sparse_conv_lattice_map", ptr(ip), n_in, ptr(qp), n_out, float(voxel_size), ks,
+                  int(bool(mirror)), int(bool(normalize)), ptr(oimp), int(bool(want_grad)), status.ctypes.data,
+                  ptr(mws), mws.numel(), ptr(lws), lws.numel(), stream_handle(dev))
+        status0 = int(status[0])
+        if key is not None:
+            _MAP_CACHE[key] = (mws, status0, cache_key[0], cache_key[1])
+    if status0 & 4:
         return None
-    if status[0] & 1:
+    if status0 & 1:
         raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index")
     f = filters.to(dev)
     empty = torch.empty(0, dtype=torch.int64, device=dev)

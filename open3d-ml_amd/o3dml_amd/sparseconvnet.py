@@ -1,0 +1,266 @@
+"""SparseConvUnet on MI355X (reference
+ml3d/torch/models/sparseconvnet.py).
+
+The module tree (names, classes, parameter shapes) matches the reference, so
+its state_dicts load unchanged; the layers are this build's SparseConv /
+SparseConvTranspose (lattice rulebook + MFMA implicit GEMM, csrc/sparse_conv.hip)
+and the InputLayer / OutputLayer index work stays on the GPU (the reference
+round-trips the voxel maps through numpy, sparseconvnet.py:302-315).  One
+forward runs inside a rulebook-cache scope, so all submanifold convolutions of
+one level share one kernel map instead of rebuilding it per layer.
+"""
+import torch
+import torch.nn as nn
+
+from . import ops
+from .layers import SparseConv, SparseConvTranspose
+from .sparse_conv import rulebook_cache
+
+
+class BatchNormBlock(nn.Module):
+    """sparseconvnet.py:240-258."""
+
+    def __init__(self, m, eps=1e-4, momentum=0.01):
+        super().__init__()
+        self.bn = nn.BatchNorm1d(m, eps=eps, momentum=momentum)
+
+    def forward(self, feat_list):
+        lengths = [f.shape[0] for f in feat_list]
+        return list(torch.split(self.bn(torch.cat(feat_list, 0)), lengths))
+
+
+class ReLUBlock(nn.Module):
+    """sparseconvnet.py:261-279."""
+
+    def __init__(self):
+        super().__init__()
+        self.relu = nn.ReLU()
+
+    def forward(self, feat_list):
+        return [self.relu(f) for f in feat_list]
+
+
+class LinearBlock(nn.Module):
+    """sparseconvnet.py:282-293."""
+
+    def __init__(self, a, b):
+        super().__init__()
+        self.linear = nn.Linear(a, b)
+
+    def forward(self, feat_list):
+        return [self.linear(f) for f in feat_list]
+
+
+class InputLayer(nn.Module):
+    """Voxelize at vs = 1 in [0, 40960)^3 and average the features of each voxel
+    (sparseconvnet.py:296-331); returns (features, voxel positions, the voxel of
+    every input point)."""
+
+    def __init__(self, voxel_size=1.0):
+        super().__init__()
+        self.voxel_size = torch.Tensor([voxel_size, voxel_size, voxel_size])
+
+    def forward(self, features, in_positions):
+        dev = in_positions.device
+        v = ops.voxelize(in_positions, torch.LongTensor([0, in_positions.shape[0]]), self.voxel_size,
+                         torch.Tensor([0, 0, 0]), torch.Tensor([40960, 40960, 40960]))
+        pidx, prs = v.voxel_point_indices, v.voxel_point_row_splits
+        pos_sorted = in_positions[pidx]
+        feat_sorted = features[pidx]
+        count = prs[1:] - prs[:-1]
+        nvox = count.shape[0]
+        positions = pos_sorted[prs[:-1]]
+        avg = torch.stack([ops.reduce_subarrays_sum(feat_sorted[:, c].contiguous(), prs) for c in range(3)], 1)
+        avg = avg / count.unsqueeze(1)
+        # voxel of every input point (points outside the range map nowhere, as
+        # the reference's zero-initialised reverse map does: voxel 0)
+        index_map = torch.zeros(in_positions.shape[0], dtype=torch.int64, device=dev)
+        index_map[pidx] = torch.repeat_interleave(torch.arange(nvox, device=dev), count)
+        return avg, positions, index_map
+
+
+class OutputLayer(nn.Module):
+    """sparseconvnet.py:334-344."""
+
+    def __init__(self, voxel_size=1.0):
+        super().__init__()
+
+    def forward(self, features_list, index_map_list):
+        return torch.cat([f[m] for f, m in zip(features_list, index_map_list)], 0)
+
+
+class SubmanifoldSparseConv(nn.Module):
+    """sparseconvnet.py:347-385."""
+
+    def __init__(self, in_channels, filters, kernel_size, use_bias=False, offset=None, normalize=False):
+        super().__init__()
+        if offset is None:
+            offset = 0.0 if kernel_size[0] % 2 else 0.5
+        self.net = SparseConv(in_channels=in_channels, filters=filters, kernel_size=kernel_size, use_bias=use_bias,
+                              offset=torch.full((3,), offset, dtype=torch.float32), normalize=normalize)
+
+    def forward(self, features_list, in_positions_list, out_positions_list=None, voxel_size=1.0):
+        if out_positions_list is None:
+            out_positions_list = in_positions_list
+        return [self.net(f, i, o, voxel_size) for f, i, o in zip(features_list, in_positions_list,
+                                                                 out_positions_list)]
+
+
+class Convolution(nn.Module):
+    """Stride-2 2^3 convolution onto calculate_grid (sparseconvnet.py:404-441)."""
+
+    def __init__(self, in_channels, filters, kernel_size, use_bias=False, offset=None, normalize=False):
+        super().__init__()
+        if offset is None:
+            offset = 0.0 if kernel_size[0] % 2 else -0.5
+        self.net = SparseConv(in_channels=in_channels, filters=filters, kernel_size=kernel_size, use_bias=use_bias,
+                              offset=torch.full((3,), offset, dtype=torch.float32), normalize=normalize)
+
+    def forward(self, features_list, in_positions_list, voxel_size=1.0):
+        out_positions_list = [ops.calculate_grid(p) for p in in_positions_list]
+        out_feat = [self.net(f, i, o, voxel_size) for f, i, o in zip(features_list, in_positions_list,
+                                                                    out_positions_list)]
+        return out_feat, [o / 2 for o in out_positions_list]
+
+
+class DeConvolution(nn.Module):
+    """sparseconvnet.py:444-482."""
+
+    def __init__(self, in_channels, filters, kernel_size, use_bias=False, offset=None, normalize=False):
+        super().__init__()
+        if offset is None:
+            offset = 0.0 if kernel_size[0] % 2 else -0.5
+        self.net = SparseConvTranspose(in_channels=in_channels, filters=filters, kernel_size=kernel_size,
+                                       use_bias=use_bias, offset=torch.full((3,), offset, dtype=torch.float32),
+                                       normalize=normalize)
+
+    def forward(self, features_list, in_positions_list, out_positions_list, voxel_size=1.0):
+        return [self.net(f, i, o, voxel_size) for f, i, o in zip(features_list, in_positions_list,
+                                                                 out_positions_list)]
+
+
+class ConcatFeat(nn.Module):
+    def forward(self, feat):
+        return feat
+
+
+class JoinFeat(nn.Module):
+    def forward(self, feat_cat, feat):
+        return [torch.cat([a, b], -1) for a, b in zip(feat_cat, feat)]
+
+
+class NetworkInNetwork(nn.Module):
+    def __init__(self, nIn, nOut, bias=False):
+        super().__init__()
+        self.linear = nn.Identity() if nIn == nOut else nn.Linear(nIn, nOut, bias=bias)
+
+    def forward(self, inputs):
+        return [self.linear(x) for x in inputs]
+
+
+class ResidualBlock(nn.Module):
+    """sparseconvnet.py:532-565."""
+
+    def __init__(self, nIn, nOut):
+        super().__init__()
+        self.lin = NetworkInNetwork(nIn, nOut)
+        self.batch_norm1 = BatchNormBlock(nIn)
+        self.relu1 = ReLUBlock()
+        self.sub_sparse_conv1 = SubmanifoldSparseConv(in_channels=nIn, filters=nOut, kernel_size=[3, 3, 3])
+        self.batch_norm2 = BatchNormBlock(nOut)
+        self.relu2 = ReLUBlock()
+        self.sub_sparse_conv2 = SubmanifoldSparseConv(in_channels=nOut, filters=nOut, kernel_size=[3, 3, 3])
+
+    def forward(self, feat_list, pos_list):
+        out1 = self.lin(feat_list)
+        f = self.relu1(self.batch_norm1(feat_list))
+        f = self.sub_sparse_conv1(f, pos_list)
+        f = self.relu2(self.batch_norm2(f))
+        out2 = self.sub_sparse_conv2(f, pos_list)
+        return [a + b for a, b in zip(out1, out2)]
+
+
+def _unet_layers(planes, residual, reps):
+    """The reference's recursive layer list (sparseconvnet.py:585-618)."""
+    layers = []
+
+    def block(a, b):
+        if residual:
+            layers.append(ResidualBlock(a, b))
+        else:
+            layers.extend([BatchNormBlock(a), ReLUBlock(), SubmanifoldSparseConv(a, b, [3, 3, 3])])
+
+    for _ in range(reps):
+        block(planes[0], planes[0])
+    if len(planes) > 1:
+        layers.extend([ConcatFeat(), BatchNormBlock(planes[0]), ReLUBlock(),
+                       Convolution(planes[0], planes[1], [2, 2, 2])])
+        layers.extend(_unet_layers(planes[1:], residual, reps))
+        layers.extend([BatchNormBlock(planes[1]), ReLUBlock(), DeConvolution(planes[1], planes[0], [2, 2, 2]),
+                       JoinFeat()])
+        for i in range(reps):
+            block(planes[0] * (2 if i == 0 else 1), planes[0])
+    return layers
+
+
+class UNet(nn.Module):
+    """sparseconvnet.py:568-653."""
+
+    def __init__(self, conv_block_reps, nPlanes, residual_blocks=False, downsample=(2, 2), leakiness=0):
+        super().__init__()
+        self.net = nn.ModuleList(_unet_layers(list(nPlanes), residual_blocks, conv_block_reps))
+        self.residual_blocks = residual_blocks
+
+    def forward(self, pos_list, feat_list):
+        conv_pos, concat_feat = [], []
+        for m in self.net:
+            if isinstance(m, (BatchNormBlock, ReLUBlock)):
+                feat_list = m(feat_list)
+            elif isinstance(m, (ResidualBlock, SubmanifoldSparseConv)):
+                feat_list = m(feat_list, pos_list)
+            elif isinstance(m, Convolution):
+                conv_pos.append(pos_list)
+                feat_list, pos_list = m(feat_list, pos_list)
+            elif isinstance(m, DeConvolution):
+                feat_list = m(feat_list, [2 * p for p in pos_list], conv_pos[-1])
+                pos_list = conv_pos.pop()
+            elif isinstance(m, ConcatFeat):
+                concat_feat.append(m(feat_list))
+            elif isinstance(m, JoinFeat):
+                feat_list = m(concat_feat.pop(), feat_list)
+            else:
+                raise Exception("Unknown module {}".format(m))
+        return feat_list
+
+
+class SparseConvUnet(nn.Module):
+    """sparseconvnet.py:13-93 (model part; data preprocessing stays the caller's).
+    forward(inputs) takes an object with .point / .feat lists and .batch_lengths
+    like the reference ConcatBatcher output and returns per-point logits."""
+
+    def __init__(self, name="SparseConvUnet", device="cuda", multiplier=16, voxel_size=0.05, conv_block_reps=1,
+                 residual_blocks=False, in_channels=3, num_classes=20, grid_size=4096, **kwargs):
+        super().__init__()
+        self.multiplier = multiplier
+        self.input_layer = InputLayer()
+        self.sub_sparse_conv = SubmanifoldSparseConv(in_channels=in_channels, filters=multiplier,
+                                                     kernel_size=[3, 3, 3])
+        self.unet = UNet(conv_block_reps, [multiplier * i for i in range(1, 8)], residual_blocks)
+        self.batch_norm = BatchNormBlock(multiplier)
+        self.relu = ReLUBlock()
+        self.linear = LinearBlock(multiplier, num_classes)
+        self.output_layer = OutputLayer()
+
+    def forward(self, inputs):
+        with rulebook_cache():
+            pos_list, feat_list, index_maps = [], [], []
+            for i in range(len(inputs.batch_lengths)):
+                f, p, m = self.input_layer(inputs.feat[i], inputs.point[i])
+                pos_list.append(p)
+                feat_list.append(f)
+                index_maps.append(m)
+            feat_list = self.sub_sparse_conv(feat_list, pos_list, voxel_size=1.0)
+            feat_list = self.unet(pos_list, feat_list)
+            feat_list = self.relu(self.batch_norm(feat_list))
+            feat_list = self.linear(feat_list)
+            return self.output_layer(feat_list, index_maps)

@@ -1,0 +1,71 @@
+"""SparseConvUnet forward on the HIP layers vs the reference model's logits
+(tests/golden/scn.npz: the reference SparseConvUnet with oracle-backed
+SparseConv layers, deterministic weights from randla_weights.fill), residual
+and plain; tolerance 1e-4 of the logit range.  Also: the rulebook cache of one
+forward changes nothing, and the InputLayer voxel map matches the reference's
+(every point maps to the voxel holding its floor cell)."""
+import os
+import sys
+import types
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import randla_weights  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+G = np.load(os.path.join(HERE, "golden", "scn.npz"))
+
+
+def _model(residual, dev):
+    from o3dml_amd.sparseconvnet import SparseConvUnet
+    m = SparseConvUnet(multiplier=8, residual_blocks=residual, conv_block_reps=1, num_classes=5)
+    sd = m.state_dict()
+    m.load_state_dict(randla_weights.state_dict_for([(k, tuple(v.shape)) for k, v in sd.items()], sd))
+    return m.to(dev).eval()
+
+
+def _inputs(dev):
+    pos = torch.from_numpy(G["pos"]).to(dev)
+    feat = torch.from_numpy(G["feat"]).to(dev)
+    return types.SimpleNamespace(point=[pos], feat=[feat], batch_lengths=[pos.shape[0]])
+
+
+@pytest.mark.parametrize("tag,residual", [("res", True), ("plain", False)])
+def test_scn_logits_match_reference(cuda, tag, residual):
+    m = _model(residual, cuda)
+    with torch.no_grad():
+        out = m(_inputs(cuda)).cpu().numpy()
+    ref = G[f"{tag}_logits"]
+    assert out.shape == ref.shape
+    err = np.abs(out - ref).max() / np.abs(ref).max()
+    assert err < 1e-4, err
+
+
+def test_scn_search_rulebook_equals_lattice(cuda):
+    from o3dml_amd import layers
+    m = _model(True, cuda)
+    inp = _inputs(cuda)
+    with torch.no_grad():
+        a = m(inp)
+        for mod in m.modules():
+            if isinstance(mod, layers.SparseConv):
+                mod.lattice_rulebook = False
+        b = m(inp)
+    assert torch.equal(a, b)
+
+
+def test_input_layer_voxel_map(cuda):
+    from o3dml_amd.sparseconvnet import InputLayer
+    g = torch.Generator().manual_seed(0)
+    pos = (torch.rand((3000, 3), generator=g) * 20).to(cuda)
+    feat = torch.rand((3000, 3), generator=g).to(cuda)
+    avg, vpos, imap = InputLayer()(feat, pos)
+    cell_of_voxel = torch.floor(vpos).long()
+    assert torch.equal(cell_of_voxel[imap], torch.floor(pos).long())
+    # voxel mean
+    ref = torch.zeros_like(avg).index_add_(0, imap, feat) / torch.bincount(imap, minlength=avg.shape[0])[:, None]
+    assert torch.allclose(avg, ref, atol=1e-6)

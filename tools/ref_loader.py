@@ -88,6 +88,42 @@ def reduce_subarrays_sum(values, row_splits):
     return torch.from_numpy(O.reduce_subarrays_sum(_np(values), _np(row_splits)))
 
 
+class _SparseConvStub(torch.nn.Module):
+    """Open3D layers.SparseConv restated on the oracle (CPU, forward only):
+    Linf fixed-radius neighbours of out_pos - offset*vs (radius k*vs/2), kernel
+    index per pair, oracle sparse_conv (+ bias).  Parameters kernel / bias /
+    offset as the layer's state_dict."""
+    _mirror, _sign = False, 1.0
+
+    def __init__(self, in_channels, filters, kernel_size, activation=None, use_bias=True, normalize=False,
+                 offset=None, **kw):
+        super().__init__()
+        self.kernel_size = list(kernel_size)
+        if offset is None:
+            offset = torch.zeros(3)
+        self.offset = torch.nn.Parameter(torch.as_tensor(offset, dtype=torch.float32), requires_grad=False)
+        self.kernel = torch.nn.Parameter(torch.zeros(*self.kernel_size, in_channels, filters))
+        self.bias = torch.nn.Parameter(torch.zeros(filters)) if use_bias else None
+        self.normalize = normalize
+        self.activation = activation
+
+    def forward(self, inp_features, inp_positions, out_positions, voxel_size, *a, **kw):
+        vs = float(voxel_size)
+        ip, op = _np(inp_positions).astype(np.float32), _np(out_positions).astype(np.float32)
+        q = (op - self._sign * _np(self.offset) * vs).astype(np.float32)
+        idx, rs, _ = O.fixed_radius_search(ip, q, 0.5 * vs * self.kernel_size[0], metric="Linf")
+        kid = O.kernel_index(ip, q, idx, rs, self.kernel_size, vs, mirror=self._mirror)
+        out = O.sparse_conv(_np(self.kernel), _np(inp_features), idx, kid, rs, normalize=self.normalize)
+        out = torch.from_numpy(out)
+        if self.bias is not None:
+            out = out + self.bias.detach()
+        return self.activation(out) if self.activation else out
+
+
+class _SparseConvTransposeStub(_SparseConvStub):
+    _mirror, _sign = True, -1.0
+
+
 class _NNS:
     def __init__(self, t):
         self.pts = t.numpy() if hasattr(t, "numpy") else np.asarray(t)
@@ -125,8 +161,8 @@ def install():
     for n in ["knn_search", "nms", "roi_pool", "trilinear_devoxelize_forward", "trilinear_devoxelize_backward",
               "furthest_point_sampling", "three_nn", "three_interpolate", "three_interpolate_grad", "ball_query"]:
         setattr(ops, n, None)
-    lay = _mod("open3d.ml.torch.layers", FixedRadiusSearch=FixedRadiusSearch, SparseConv=None,
-               SparseConvTranspose=None)
+    lay = _mod("open3d.ml.torch.layers", FixedRadiusSearch=FixedRadiusSearch, SparseConv=_SparseConvStub,
+               SparseConvTranspose=_SparseConvTransposeStub)
     mt.ops, mt.layers = ops, lay
     ml.torch = mt
     _mod("open3d.visualization")
