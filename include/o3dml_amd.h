@@ -187,11 +187,14 @@ int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const int32_t* n
                                 const float* neighbors_importance, const int64_t* neighbors_row_splits, int64_t n_out,
                                 int64_t n_in, int K, int normalize, const float* out_importance, int want_inverse,
                                 int* status_host, void* workspace, size_t workspace_bytes, void* stream);
+/* split-K partial sums for the forward GEMM (deep levels with few output
+ * rows split the offset x Cin reduction across waves; 0 when unsplit) */
+size_t o3dml_sparse_conv_forward_workspace_size(int64_t n_out, int K, int cin, int cout);
 int o3dml_sparse_conv_forward(const float* filters, int K, int cin, int cout, const float* inp_features, int64_t n_in,
                               const float* inp_importance, int has_neighbors_importance, int use_out_scale,
                               const float* bias, int64_t n_out, float* out_features, void* map_workspace,
-                              size_t map_workspace_bytes, void* stream);
-size_t o3dml_sparse_conv_backward_workspace_size(int64_t n_out, int K, int cin, int cout);
+                              size_t map_workspace_bytes, void* workspace, size_t workspace_bytes, void* stream);
+size_t o3dml_sparse_conv_backward_workspace_size(int64_t n_out, int64_t n_in, int K, int cin, int cout);
 int o3dml_sparse_conv_backward(const float* filters, int K, int cin, int cout, const float* inp_features, int64_t n_in,
                                const float* inp_importance, int has_neighbors_importance, int use_out_scale,
                                const float* grad_out, int64_t n_out, float* grad_inp, float* grad_filters,

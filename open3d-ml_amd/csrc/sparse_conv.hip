@@ -19,7 +19,9 @@
 //            slabs, reduced in a fixed order (deterministic).
 // Roofline: MFMA fp32 (157 TF/s dense) for Cin*Cout >= ~64^2, gather/HBM bound
 // below that.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -148,7 +150,8 @@ __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, const float* __restrict__ src,
                      const float* __restrict__ sscale, const float* __restrict__ pscale,
                      const float* __restrict__ W /*[K][cin][cout]*/, int cin, int cout,
-                     const float* __restrict__ oscale, const float* __restrict__ bias, float* __restrict__ out) {
+                     const float* __restrict__ oscale, const float* __restrict__ bias, float* __restrict__ out,
+                     int nsplit, float* __restrict__ part) {
     const int lane = threadIdx.x & 63;
     const int64_t o0 = (static_cast<int64_t>(blockIdx.x) * (kGemmThreads / 64) + (threadIdx.x >> 6)) * 32;
     if (o0 >= n_out) return;  // whole wave; the kernel has no barriers
@@ -174,26 +177,45 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    if (used) {
+    // the wave's stage stream = (used offset, 32-channel chunk) in order; split
+    // s of nsplit takes stages [s*n/nsplit, (s+1)*n/nsplit)
+    const int nch = (cin + 31) >> 5;
+    const int nst = __builtin_popcount(used) * nch;
+    const int s = blockIdx.z;
+    const int j0 = static_cast<int>(static_cast<int64_t>(s) * nst / nsplit);
+    const int j1 = static_cast<int>(static_cast<int64_t>(s + 1) * nst / nsplit);
+    if (j0 < j1) {
+        unsigned u = used;
+        for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
         GemmStage cur, nxt;
-        int k = __builtin_ctz(used), c0 = 0;
+        int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
         gemm_load<VEC4>(cur, mtile[i * K + k], K, o, k, c0, h, col, src, sscale, pscale, W, cin, cout);
-        while (true) {
+        for (int j = j0 + 1;; ++j) {
             int nk = k, nc = c0 + 32;
             if (nc >= cin) {
                 nc = 0;
-                const unsigned rest = k + 1 < 32 ? used & ~((2u << k) - 1u) : 0u;
-                nk = rest ? __builtin_ctz(rest) : -1;
+                u &= u - 1u;
+                nk = u ? __builtin_ctz(u) : -1;
             }
-            if (nk >= 0)
+            const bool more = j < j1;
+            if (more)
                 gemm_load<VEC4>(nxt, mtile[i * K + nk], K, o, nk, nc, h, col, src, sscale, pscale, W, cin, cout);
 #pragma unroll
-            for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[s], cur.b[s], acc, 0, 0, 0);
-            if (nk < 0) break;
+            for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[r], cur.b[r], acc, 0, 0, 0);
+            if (!more) break;
             k = nk;
             c0 = nc;
             cur = nxt;
         }
+    }
+    if (nsplit > 1) {  // raw partial sums; split_reduce_kernel applies oscale / bias
+        float* P = part + static_cast<int64_t>(s) * n_out * cout;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t orr = o0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (orr < n_out && col < cout) P[orr * cout + col] = acc[r];
+        }
+        return;
     }
     // epilogue: C/D map row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31
 #pragma unroll
@@ -332,20 +354,69 @@ __global__ void kernel_index_kernel(const float* __restrict__ inp_pos, const flo
     }
 }
 
+// out[o, c] = (sum_s part[s][o, c]) * oscale[o] + bias[c], splits in order
+__global__ void split_reduce_kernel(const float* __restrict__ part, int nsplit, int64_t n_out, int cout,
+                                    const float* __restrict__ oscale, const float* __restrict__ bias,
+                                    float* __restrict__ out) {
+    const int64_t total = n_out * cout;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        float v = 0.f;
+        for (int s = 0; s < nsplit; ++s) v += part[s * total + e];
+        const int64_t o = e / cout;
+        if (oscale) v *= oscale[o];
+        if (bias) v += bias[e - o * cout];
+        out[e] = v;
+    }
+}
+
+// Split of the (offset, Cin-chunk) reduction across waves when the output
+// tiles alone cannot fill the chip (deep UNet levels: a few hundred rows, up to
+// 448 input channels): enough splits for ~kGemmTargetWaves waves, at least
+// kGemmMinStages stages each, partial sums bounded by kGemmSplitBytes.
+constexpr int64_t kGemmTargetWaves = 4096;
+constexpr int kGemmMinStages = 4;
+constexpr int64_t kGemmSplitBytes = int64_t(64) << 20;
+
+static int gemm_splits(int64_t n_out, int K, int cin, int cout) {
+    if (n_out <= 0 || cout <= 0) return 1;
+    static const int64_t target = [] {
+        const char* e = std::getenv("O3DML_GEMM_TARGET_WAVES");
+        return e ? std::max<int64_t>(1, std::atoll(e)) : kGemmTargetWaves;
+    }();
+    const int64_t tiles = ceil_div(n_out, 32) * ceil_div(cout, 32);
+    int64_t ns = ceil_div(target, tiles);
+    ns = std::min<int64_t>(ns, std::max<int64_t>(1, (static_cast<int64_t>(K) * ceil_div(cin, 32)) / kGemmMinStages));
+    ns = std::min<int64_t>(ns, kGemmSplitBytes / (n_out * cout * static_cast<int64_t>(sizeof(float))));
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ns, 64)));
+}
+
+static size_t gemm_split_bytes(int64_t n_out, int K, int cin, int cout) {
+    const int ns = gemm_splits(n_out, K, cin, cout);
+    return ns > 1 ? ws_bytes<float>(ns * n_out * cout) : 0;
+}
+
 static void run_gemm(hipStream_t st, const int32_t* map, int K, int64_t n_out, const float* src, const float* sscale,
                      const float* pscale, const float* W, int cin, int cout, const float* oscale, const float* bias,
-                     float* out) {
+                     float* out, float* part, size_t part_bytes) {
     if (n_out == 0 || cout == 0) return;
     const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0;
+    int ns = gemm_splits(n_out, K, cin, cout);
+    if (!part || part_bytes < sizeof(float) * static_cast<size_t>(ns) * n_out * cout) ns = 1;
     const dim3 g(static_cast<unsigned>(ceil_div(n_out, 32 * (kGemmThreads / 64))),
-                 static_cast<unsigned>(ceil_div(cout, 32)));
+                 static_cast<unsigned>(ceil_div(cout, 32)), static_cast<unsigned>(ns));
     if (vec4)
         implicit_gemm_kernel<true><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
-                                                               oscale, bias, out);
+                                                               oscale, bias, out, ns, part);
     else
         implicit_gemm_kernel<false><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
-                                                                oscale, bias, out);
+                                                                oscale, bias, out, ns, part);
     O3DML_LAUNCH_CHECK();
+    if (ns > 1) {
+        split_reduce_kernel<<<stream_grid(n_out * cout, 256), 256, 0, st>>>(part, ns, n_out, cout, oscale, bias,
+                                                                           out);
+        O3DML_LAUNCH_CHECK();
+    }
 }
 
 // --------------------------------------------------------------------------
@@ -688,27 +759,35 @@ static void map_views(void* workspace, size_t bytes, int64_t n_out, int64_t n_in
     *ipscale = ws.take<float>(n_in * K);
 }
 
+// split-K partial sums of o3dml_sparse_conv_forward (0 when no split is used)
+O3DML_API size_t o3dml_sparse_conv_forward_workspace_size(int64_t n_out, int K, int cin, int cout) {
+    return gemm_split_bytes(n_out, K, cin, cout);
+}
+
 // out [n_out, cout] = oscale * sum_k gather(inp) @ W[k] (+ bias).  filters:
 // [K][cin][cout].  inp_importance (nullable) scales input rows; pair
 // importance / normalisation / out_importance come from the map workspace.
 O3DML_API int o3dml_sparse_conv_forward(const float* filters, int K, int cin, int cout, const float* inp_features,
                                         int64_t n_in, const float* inp_importance, int has_neighbors_importance,
                                         int use_out_scale, const float* bias, int64_t n_out, float* out_features,
-                                        void* map_workspace, size_t map_workspace_bytes, void* stream) {
+                                        void* map_workspace, size_t map_workspace_bytes, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
     int32_t *map, *inv;
     float *pscale, *oscale, *ipscale;
     map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale);
     run_gemm(as_stream(stream), map, K, n_out, inp_features, inp_importance, has_neighbors_importance ? pscale : nullptr,
-             filters, cin, cout, use_out_scale ? oscale : nullptr, bias, out_features);
+             filters, cin, cout, use_out_scale ? oscale : nullptr, bias, out_features,
+             static_cast<float*>(workspace), workspace_bytes);
     O3DML_GUARD_END
 }
 
-O3DML_API size_t o3dml_sparse_conv_backward_workspace_size(int64_t n_out, int K, int cin, int cout) {
+O3DML_API size_t o3dml_sparse_conv_backward_workspace_size(int64_t n_out, int64_t n_in, int K, int cin, int cout) {
     const int nchunk = 16;
     return ws_bytes<float>(static_cast<int64_t>(K) * cin * cout) + ws_bytes<float>(n_out * cout) +
-           ws_bytes<int64_t>(n_out * K) * 2 + ws_bytes<int32_t>(n_out * K) + ws_bytes<int64_t>(K + 1) +
-           ws_bytes<float>(static_cast<int64_t>(K) * nchunk * cin * cout) + prim::scan_workspace_bytes(n_out * K);
+           gemm_split_bytes(n_in, K, cout, cin) + ws_bytes<int64_t>(n_out * K) * 2 + ws_bytes<int32_t>(n_out * K) +
+           ws_bytes<int64_t>(K + 1) + ws_bytes<float>(static_cast<int64_t>(K) * nchunk * cin * cout) +
+           prim::scan_workspace_bytes(n_out * K);
 }
 
 // grad_out [n_out, cout] -> grad_inp [n_in, cin] (nullable) and grad_filters
@@ -728,6 +807,8 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
     float* wt = ws.take<float>(static_cast<int64_t>(K) * cin * cout);
     float* g = ws.take<float>(n_out * cout);  // unused slot kept for layout stability
     (void)g;
+    const size_t split_bytes = gemm_split_bytes(n_in, K, cout, cin);
+    float* split = split_bytes ? ws.take<float>(static_cast<int64_t>(split_bytes / sizeof(float))) : nullptr;
     const float* os = use_out_scale ? oscale : nullptr;
     if (grad_inp && n_in > 0) {
         // dIn[i] = sscale[i] * sum_k (g[inv[i,k]] * oscale[o] * pscale) @ W[k]^T
@@ -737,7 +818,7 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
         // the per-row out-scale belongs to the gathered rows (source = grad_out):
         // fold it in as sscale; pair importance via the inverse pscale.
         run_gemm(st, inv, K, n_in, grad_out, os, has_neighbors_importance ? ipscale : nullptr, wt, cout, cin,
-                 inp_importance, nullptr, grad_inp);
+                 inp_importance, nullptr, grad_inp, split, split_bytes);
     }
     if (grad_filters) {
         const int64_t KC = static_cast<int64_t>(K) * cin * cout;

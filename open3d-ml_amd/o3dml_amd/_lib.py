@@ -80,9 +80,10 @@ SIGNATURES = {
     "o3dml_sparse_conv_map_workspace_size": (c_sz, [c_i64, c_i64, c_i32]),
     "o3dml_sparse_conv_build_map": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_i32, c_p, c_p,
                                             c_sz, c_p]),
+    "o3dml_sparse_conv_forward_workspace_size": (c_sz, [c_i64, c_i32, c_i32, c_i32]),
     "o3dml_sparse_conv_forward": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i64, c_p,
-                                          c_p, c_sz, c_p]),
-    "o3dml_sparse_conv_backward_workspace_size": (c_sz, [c_i64, c_i32, c_i32, c_i32]),
+                                          c_p, c_sz, c_p, c_sz, c_p]),
+    "o3dml_sparse_conv_backward_workspace_size": (c_sz, [c_i64, c_i64, c_i32, c_i32, c_i32]),
     "o3dml_sparse_conv_backward": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i64, c_p,
                                            c_p, c_p, c_sz, c_p, c_sz, c_p]),
     "o3dml_sparse_conv_kernel_index": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_i32, c_p, c_p]),

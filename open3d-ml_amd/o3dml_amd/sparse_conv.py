@@ -53,9 +53,10 @@ class _ConvFn(torch.autograd.Function):
         x = inp_features.detach().contiguous()
         out = torch.empty((n_out, cout), dtype=torch.float32, device=dev)
         use_os = int(bool(normalize) or out_importance is not None)
+        fws = workspace(lib.o3dml_sparse_conv_forward_workspace_size(n_out, K, cin, cout), dev)
         _lib.call("o3dml_sparse_conv_forward", ptr(W), K, cin, cout, ptr(x), n_in, ptr(sscale), int(nimp is not None),
                   use_os, ptr(bias.detach().contiguous() if bias is not None else None), n_out, ptr(out), ptr(mws),
-                  mws.numel(), st)
+                  mws.numel(), ptr(fws), fws.numel(), st)
         ctx.save_for_backward(W, x, mws, sscale if sscale is not None else torch.empty(0, device=dev))
         ctx.meta = (K, cin, cout, n_in, n_out, nimp is not None, use_os, sscale is not None, bias is not None)
         return out
@@ -70,7 +71,7 @@ class _ConvFn(torch.autograd.Function):
         need_x, need_w = ctx.needs_input_grad[1], ctx.needs_input_grad[0]
         gx = torch.empty((n_in, cin), dtype=torch.float32, device=dev) if need_x else None
         gw = torch.empty(W.shape, dtype=torch.float32, device=dev) if need_w else None
-        ws = workspace(lib.o3dml_sparse_conv_backward_workspace_size(n_out, K, cin, cout), dev)
+        ws = workspace(lib.o3dml_sparse_conv_backward_workspace_size(n_out, n_in, K, cin, cout), dev)
         _lib.call("o3dml_sparse_conv_backward", ptr(W), K, cin, cout, ptr(x), n_in, ptr(sscale) if has_ss else None,
                   int(has_nimp), use_os, ptr(g), n_out, ptr(gx), ptr(gw), ptr(mws), mws.numel(), ptr(ws), ws.numel(),
                   stream_handle(dev))
