@@ -194,6 +194,14 @@ int o3dml_sparse_conv_forward(const float* filters, int K, int cin, int cout, co
                               const float* inp_importance, int has_neighbors_importance, int use_out_scale,
                               const float* bias, int64_t n_out, float* out_features, void* map_workspace,
                               size_t map_workspace_bytes, void* workspace, size_t workspace_bytes, void* stream);
+/* forward with an input prologue relu(x * pre_scale + pre_shift) (eval-mode
+ * BatchNorm + ReLU folded per channel) and a residual added in the epilogue;
+ * pre_* [cin] and residual [n_out, cout] nullable; no importance / normalize */
+int o3dml_sparse_conv_forward_fused(const float* filters, int K, int cin, int cout, const float* inp_features,
+                                    int64_t n_in, const float* pre_scale, const float* pre_shift,
+                                    const float* residual, const float* bias, int64_t n_out, float* out_features,
+                                    void* map_workspace, size_t map_workspace_bytes, void* workspace,
+                                    size_t workspace_bytes, void* stream);
 size_t o3dml_sparse_conv_backward_workspace_size(int64_t n_out, int64_t n_in, int K, int cin, int cout);
 int o3dml_sparse_conv_backward(const float* filters, int K, int cin, int cout, const float* inp_features, int64_t n_in,
                                const float* inp_importance, int has_neighbors_importance, int use_out_scale,
@@ -211,12 +219,18 @@ int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* quer
  * neighbourhood of radius ks*vs/2 is exactly the ks^3 lattice offsets, so the
  * dense kernel map (same workspace layout as _build_map) comes from a voxel
  * hash with K lookups per output.  status_host[0] bit 2 (value 4): not a
- * lattice set — use the fixed-radius-search rulebook instead. */
+ * lattice set — use the fixed-radius-search rulebook instead.  The test runs
+ * on the device; defer_status = 1 skips the host round trip (status_host
+ * stays 0 unless a set is empty) and leaves the status word in the map
+ * workspace at o3dml_sparse_conv_map_status_offset — a failed test leaves an
+ * all-empty (safe) map. */
 size_t o3dml_sparse_conv_lattice_workspace_size(int64_t n_in);
+size_t o3dml_sparse_conv_map_status_offset(int64_t n_out, int64_t n_in, int K);
 int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, const float* query_pos, int64_t n_out,
                                   float voxel_size, int ksize, int mirror, int normalize, const float* out_importance,
-                                  int want_inverse, int* status_host, void* workspace, size_t workspace_bytes,
-                                  void* lattice_workspace, size_t lattice_workspace_bytes, void* stream);
+                                  int want_inverse, int defer_status, int* status_host, void* workspace,
+                                  size_t workspace_bytes, void* lattice_workspace, size_t lattice_workspace_bytes,
+                                  void* stream);
 
 /* ---- KPConv neighbourhood aggregation (ml3d/torch/models/
  * kpconv.py:1005-1159).  q_pts f32 [n,3], s_pts f32 [n_support,3], neighbors

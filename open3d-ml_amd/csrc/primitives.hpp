@@ -234,6 +234,53 @@ __global__ void copy_pairs(const K* __restrict__ kin, const uint32_t* __restrict
     }
 }
 
+// Small sorts (n <= kBsMax, e.g. the deep SparseConvUnet levels) in ONE
+// workgroup: bitonic network over (key & mask, input position) in LDS, so the
+// result is the stable LSD order without the 3-4 launches per radix pass.
+constexpr int kBsMax = 8192;
+constexpr int kBsThreads = 1024;
+
+template <class K>
+__global__ void __launch_bounds__(kBsThreads) block_sort_pairs(const K* __restrict__ kin,
+                                                               const uint32_t* __restrict__ vin,
+                                                               K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                               int n, K mask) {
+    __shared__ K sk[kBsMax];
+    __shared__ uint32_t sp[kBsMax];
+    const int t = threadIdx.x;
+    int N = 1;
+    while (N < n) N <<= 1;
+    for (int i = t; i < N; i += kBsThreads) {
+        sk[i] = i < n ? (kin[i] & mask) : ~K(0);
+        sp[i] = i < n ? static_cast<uint32_t>(i) : 0xffffffffu;
+    }
+    __syncthreads();
+    for (int k = 2; k <= N; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = t; i < N; i += kBsThreads) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const K a = sk[i], b = sk[ixj];
+                    const uint32_t pa = sp[i], pb = sp[ixj];
+                    const bool gt = a > b || (a == b && pa > pb);
+                    if (gt == ((i & k) == 0)) {
+                        sk[i] = b;
+                        sk[ixj] = a;
+                        sp[i] = pb;
+                        sp[ixj] = pa;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = t; i < n; i += kBsThreads) {
+        const uint32_t p = sp[i];
+        kout[i] = kin[p];
+        vout[i] = vin ? vin[p] : p;
+    }
+}
+
 inline int bits_needed(uint64_t max_key) {
     int b = 0;
     while (b < 64 && (max_key >> b) != 0) ++b;
@@ -257,6 +304,13 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
     const int passes = (end_bit + 7) / 8;
     if (passes == 0 || n == 1) {
         copy_pairs<K><<<stream_grid(n, 256), 256, 0, st>>>(keys_in, vals_in, keys_out, vals_out, n);
+        O3DML_LAUNCH_CHECK();
+        return;
+    }
+    if (n <= kBsMax) {
+        const K mask = end_bit >= static_cast<int>(8 * sizeof(K)) ? ~K(0) : ((K(1) << end_bit) - 1);
+        block_sort_pairs<K><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, static_cast<int>(n),
+                                                      mask);
         O3DML_LAUNCH_CHECK();
         return;
     }

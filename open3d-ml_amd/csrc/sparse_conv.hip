@@ -116,11 +116,22 @@ struct GemmStage {
     float a[16], b[16];
 };
 
+// Optional prologue on the gathered rows (eval-mode BatchNorm + ReLU of the
+// layer input, folded to a per-channel affine): a = relu(x * ps[c] + pb[c]).
+// Missing neighbours stay exactly 0 (sc = 0), as the zero padding of the
+// activated features.
+struct GemmPrologue {
+    const float* scale;  // [cin] or null
+    const float* shift;  // [cin]
+};
+
+__device__ __forceinline__ float pre_act(float v, float s, float b) { return fmaxf(fmaf(v, s, b), 0.f); }
+
 template <bool VEC4>
 __device__ __forceinline__ void gemm_load(GemmStage& st, int32_t m, int K, int64_t o, int k, int c0, int h, int col,
                                           const float* __restrict__ src, const float* __restrict__ sscale,
                                           const float* __restrict__ pscale, const float* __restrict__ W, int cin,
-                                          int cout) {
+                                          int cout, GemmPrologue pre) {
     const int cb = c0 + 16 * h;
     float sc = 0.f;
     if (m >= 0) sc = (sscale ? sscale[m] : 1.f) * (pscale ? pscale[o * K + k] : 1.f);
@@ -128,7 +139,13 @@ __device__ __forceinline__ void gemm_load(GemmStage& st, int32_t m, int K, int64
         const float4* row = reinterpret_cast<const float4*>(src + static_cast<int64_t>(m >= 0 ? m : 0) * cin + cb);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const float4 v = m >= 0 ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 v = m >= 0 ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            if (pre.scale) {
+                const float4 ps = reinterpret_cast<const float4*>(pre.scale + cb)[q];
+                const float4 pb = reinterpret_cast<const float4*>(pre.shift + cb)[q];
+                v = make_float4(pre_act(v.x, ps.x, pb.x), pre_act(v.y, ps.y, pb.y), pre_act(v.z, ps.z, pb.z),
+                                pre_act(v.w, ps.w, pb.w));
+            }
             st.a[4 * q] = v.x * sc;
             st.a[4 * q + 1] = v.y * sc;
             st.a[4 * q + 2] = v.z * sc;
@@ -136,8 +153,11 @@ __device__ __forceinline__ void gemm_load(GemmStage& st, int32_t m, int K, int64
         }
     } else {
 #pragma unroll
-        for (int s = 0; s < 16; ++s)
-            st.a[s] = (m >= 0 && cb + s < cin) ? src[static_cast<int64_t>(m) * cin + cb + s] * sc : 0.f;
+        for (int s = 0; s < 16; ++s) {
+            float v = (m >= 0 && cb + s < cin) ? src[static_cast<int64_t>(m) * cin + cb + s] : 0.f;
+            if (pre.scale && cb + s < cin) v = pre_act(v, pre.scale[cb + s], pre.shift[cb + s]);
+            st.a[s] = v * sc;
+        }
     }
     const float* wk = W + static_cast<int64_t>(k) * cin * cout;
 #pragma unroll
@@ -151,7 +171,7 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
                      const float* __restrict__ sscale, const float* __restrict__ pscale,
                      const float* __restrict__ W /*[K][cin][cout]*/, int cin, int cout,
                      const float* __restrict__ oscale, const float* __restrict__ bias, float* __restrict__ out,
-                     int nsplit, float* __restrict__ part) {
+                     int nsplit, float* __restrict__ part, GemmPrologue pre, const float* __restrict__ residual) {
     const int lane = threadIdx.x & 63;
     const int64_t o0 = (static_cast<int64_t>(blockIdx.x) * (kGemmThreads / 64) + (threadIdx.x >> 6)) * 32;
     if (o0 >= n_out) return;  // whole wave; the kernel has no barriers
@@ -189,7 +209,7 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
         GemmStage cur, nxt;
         int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
-        gemm_load<VEC4>(cur, mtile[i * K + k], K, o, k, c0, h, col, src, sscale, pscale, W, cin, cout);
+        gemm_load<VEC4>(cur, mtile[i * K + k], K, o, k, c0, h, col, src, sscale, pscale, W, cin, cout, pre);
         for (int j = j0 + 1;; ++j) {
             int nk = k, nc = c0 + 32;
             if (nc >= cin) {
@@ -199,7 +219,7 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
             }
             const bool more = j < j1;
             if (more)
-                gemm_load<VEC4>(nxt, mtile[i * K + nk], K, o, nk, nc, h, col, src, sscale, pscale, W, cin, cout);
+                gemm_load<VEC4>(nxt, mtile[i * K + nk], K, o, nk, nc, h, col, src, sscale, pscale, W, cin, cout, pre);
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[r], cur.b[r], acc, 0, 0, 0);
             if (!more) break;
@@ -226,6 +246,7 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
             float v = acc[r];
             if (oscale) v *= oscale[orr];
             if (bias) v += bias[col];
+            if (residual) v += residual[orr * cout + col];
             out[orr * cout + col] = v;
         }
     }
@@ -357,7 +378,7 @@ __global__ void kernel_index_kernel(const float* __restrict__ inp_pos, const flo
 // out[o, c] = (sum_s part[s][o, c]) * oscale[o] + bias[c], splits in order
 __global__ void split_reduce_kernel(const float* __restrict__ part, int nsplit, int64_t n_out, int cout,
                                     const float* __restrict__ oscale, const float* __restrict__ bias,
-                                    float* __restrict__ out) {
+                                    const float* __restrict__ residual, float* __restrict__ out) {
     const int64_t total = n_out * cout;
     for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
@@ -366,6 +387,7 @@ __global__ void split_reduce_kernel(const float* __restrict__ part, int nsplit, 
         const int64_t o = e / cout;
         if (oscale) v *= oscale[o];
         if (bias) v += bias[e - o * cout];
+        if (residual) v += residual[e];
         out[e] = v;
     }
 }
@@ -398,23 +420,25 @@ static size_t gemm_split_bytes(int64_t n_out, int K, int cin, int cout) {
 
 static void run_gemm(hipStream_t st, const int32_t* map, int K, int64_t n_out, const float* src, const float* sscale,
                      const float* pscale, const float* W, int cin, int cout, const float* oscale, const float* bias,
-                     float* out, float* part, size_t part_bytes) {
+                     float* out, float* part, size_t part_bytes, GemmPrologue pre = {nullptr, nullptr},
+                     const float* residual = nullptr) {
     if (n_out == 0 || cout == 0) return;
-    const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0;
+    const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0 &&
+                      (reinterpret_cast<uintptr_t>(pre.scale) % 16) == 0 && (reinterpret_cast<uintptr_t>(pre.shift) % 16) == 0;
     int ns = gemm_splits(n_out, K, cin, cout);
     if (!part || part_bytes < sizeof(float) * static_cast<size_t>(ns) * n_out * cout) ns = 1;
     const dim3 g(static_cast<unsigned>(ceil_div(n_out, 32 * (kGemmThreads / 64))),
                  static_cast<unsigned>(ceil_div(cout, 32)), static_cast<unsigned>(ns));
     if (vec4)
         implicit_gemm_kernel<true><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
-                                                               oscale, bias, out, ns, part);
+                                                               oscale, bias, out, ns, part, pre, residual);
     else
         implicit_gemm_kernel<false><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
-                                                                oscale, bias, out, ns, part);
+                                                                oscale, bias, out, ns, part, pre, residual);
     O3DML_LAUNCH_CHECK();
     if (ns > 1) {
         split_reduce_kernel<<<stream_grid(n_out * cout, 256), 256, 0, st>>>(part, ns, n_out, cout, oscale, bias,
-                                                                           out);
+                                                                           residual, out);
         O3DML_LAUNCH_CHECK();
     }
 }
@@ -445,12 +469,11 @@ __device__ __forceinline__ uint32_t lat_hash(uint64_t k) {
 }
 
 // per-axis [min frac, max frac, min key, max key] of p / vs (frac as float bits,
-// keys as ints) for one point set -> stats[0..11]; block-reduced in LDS, one
-// atomic per block and statistic
-__global__ void __launch_bounds__(256) lattice_stats_kernel(const float* __restrict__ pos, int64_t n, float inv_vs,
-                                                            int* __restrict__ stats) {
-    __shared__ int red[12][256];
-    int v[12];
+// keys as ints); blockIdx.y = point set (0 inputs, 1 queries); one partial per
+// block -> part[(y * gridDim.x + x) * 12 + j], reduced by lattice_finalize_kernel
+constexpr int kLatStatBlocks = 64;
+
+__device__ __forceinline__ void lat_stat_init(int* v) {
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
         v[4 * d + 0] = 0x7fffffff;
@@ -458,6 +481,18 @@ __global__ void __launch_bounds__(256) lattice_stats_kernel(const float* __restr
         v[4 * d + 2] = 0x7fffffff;
         v[4 * d + 3] = static_cast<int>(0x80000000u);
     }
+}
+
+__device__ __forceinline__ int lat_stat_merge(int j, int a, int b) { return (j & 1) ? max(a, b) : min(a, b); }
+
+__global__ void __launch_bounds__(256) lattice_stats_kernel(const float* __restrict__ inp_pos, int64_t n_in,
+                                                            const float* __restrict__ qpos, int64_t n_q,
+                                                            float inv_vs, int* __restrict__ part) {
+    __shared__ int red[12][256];
+    const float* pos = blockIdx.y ? qpos : inp_pos;
+    const int64_t n = blockIdx.y ? n_q : n_in;
+    int v[12];
+    lat_stat_init(v);
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
 #pragma unroll
@@ -478,21 +513,71 @@ __global__ void __launch_bounds__(256) lattice_stats_kernel(const float* __restr
     for (int w = 128; w >= 1; w >>= 1) {
         if (threadIdx.x < w) {
 #pragma unroll
-            for (int j = 0; j < 12; ++j) {
-                const int o = red[j][threadIdx.x + w];
-                red[j][threadIdx.x] = (j & 1) ? max(red[j][threadIdx.x], o) : min(red[j][threadIdx.x], o);
-            }
+            for (int j = 0; j < 12; ++j) red[j][threadIdx.x] = lat_stat_merge(j, red[j][threadIdx.x], red[j][threadIdx.x + w]);
         }
         __syncthreads();
     }
-    if (threadIdx.x < 12) {
-        const int j = threadIdx.x;
-        if (j & 1) atomicMax(&stats[j], red[j][0]); else atomicMin(&stats[j], red[j][0]);
+    if (threadIdx.x < 12)
+        part[(static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * 12 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+struct LatticeOffsets {
+    int off[3][8];  // key_p - key_q for kernel index j along axis d (x, y, z)
+};
+
+// Reduces the stats partials (nblk per set) and derives the per-axis lattice
+// offsets on the device: the lattice test is "every input shares one fraction
+// per axis, every query shares one, keys within +-2^19, and exactly ksize
+// lattice offsets j + (f_in - f_q) lie in [-ks/2, ks/2] with distinct kernel
+// indices".  status[0] = 4 when the test fails (then nothing else reads lo),
+// else 0; lattice_insert_kernel may still add 4 (two inputs on one voxel).
+__global__ void __launch_bounds__(64) lattice_finalize_kernel(const int* __restrict__ part, int nblk, int ksize,
+                                                              int mirror, LatticeOffsets* __restrict__ lo_out,
+                                                              int* __restrict__ status) {
+    __shared__ int st[24];
+    const int t = threadIdx.x;
+    if (t < 24) {
+        const int set = t / 12, j = t % 12;
+        int v = (j & 1) ? ((j & 2) ? static_cast<int>(0x80000000u) : 0) : 0x7fffffff;
+        for (int b = 0; b < nblk; ++b) v = lat_stat_merge(j, v, part[(set * nblk + b) * 12 + j]);
+        st[t] = v;
     }
+    __syncthreads();
+    if (t != 0) return;
+    LatticeOffsets lo{};
+    const double h = 0.5 * ksize;
+    bool ok = true;
+    for (int d = 0; d < 3 && ok; ++d) {
+        const float fi_lo = __int_as_float(st[4 * d]), fi_hi = __int_as_float(st[4 * d + 1]);
+        const float fq_lo = __int_as_float(st[12 + 4 * d]), fq_hi = __int_as_float(st[12 + 4 * d + 1]);
+        const bool keys_ok = st[4 * d + 2] > -(1 << 19) && st[4 * d + 3] < (1 << 19) &&
+                             st[12 + 4 * d + 2] > -(1 << 19) && st[12 + 4 * d + 3] < (1 << 19);
+        if (fi_lo != fi_hi || fq_lo != fq_hi || !keys_ok) {
+            ok = false;
+            break;
+        }
+        const double dc = static_cast<double>(fi_lo) - static_cast<double>(fq_lo);
+        int n_within = 0;
+        for (int j = -8; j <= 8; ++j) {
+            const double dd = j + dc;
+            if (dd < -h || dd > h) continue;
+            const int kid = mirror ? static_cast<int>(floor(h - dd)) : static_cast<int>(floor(dd + h));
+            if (kid < 0 || kid >= ksize || n_within >= ksize) {
+                ok = false;
+                break;
+            }
+            lo.off[d][kid] = j;
+            ++n_within;
+        }
+        if (n_within != ksize) ok = false;
+    }
+    *lo_out = lo;
+    status[0] = ok ? 0 : 4;
 }
 
 __global__ void lattice_insert_kernel(const float* __restrict__ pos, int64_t n, float inv_vs, uint64_t* __restrict__ keys,
                                       int32_t* __restrict__ vals, uint32_t mask, int* __restrict__ status) {
+    if (*status & 4) return;  // not a lattice set: the map is discarded
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const uint64_t k = lat_key(static_cast<int>(floorf(pos[3 * i] * inv_vs)),
@@ -516,19 +601,21 @@ __global__ void lattice_insert_kernel(const float* __restrict__ pos, int64_t n, 
     }
 }
 
-struct LatticeOffsets {
-    int off[3][8];  // key_p - key_q for kernel index j along axis d (x, y, z)
-};
-
 // map[o*K + k] for k = (kz*ks + ky)*ks + kx: one thread per (output, offset)
 __global__ void lattice_map_kernel(const float* __restrict__ inp_pos, const float* __restrict__ qpos, int64_t n_out,
-                                   float inv_vs, float radius, int ks, LatticeOffsets lo,
+                                   float inv_vs, float radius, int ks, const LatticeOffsets* __restrict__ lop,
                                    const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, uint32_t mask,
-                                   int32_t* __restrict__ map) {
+                                   const int* __restrict__ status, int32_t* __restrict__ map) {
+    const bool skip = (*status & 4) != 0;  // not a lattice set: an all-empty (safe) map
+    const LatticeOffsets lo = skip ? LatticeOffsets{} : *lop;
     const int K = ks * ks * ks;
     const int64_t total = n_out * K;
     for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        if (skip) {
+            map[e] = -1;
+            continue;
+        }
         const int64_t o = e / K;
         const int k = static_cast<int>(e - o * K);
         const float qx = qpos[3 * o], qy = qpos[3 * o + 1], qz = qpos[3 * o + 2];
@@ -629,7 +716,15 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
 O3DML_API size_t o3dml_sparse_conv_lattice_workspace_size(int64_t n_in) {
     int64_t cap = 64;
     while (cap < 2 * n_in) cap <<= 1;
-    return ws_bytes<uint64_t>(cap) + ws_bytes<int32_t>(cap) + ws_bytes<int>(32);
+    return ws_bytes<uint64_t>(cap) + ws_bytes<int32_t>(cap) + ws_bytes<int>(2 * kLatStatBlocks * 12) +
+           ws_bytes<LatticeOffsets>(1);
+}
+
+// Byte offset of the int32 status word inside a map workspace (deferred
+// lattice checks read it later, batched, with one host round trip).
+O3DML_API size_t o3dml_sparse_conv_map_status_offset(int64_t n_out, int64_t n_in, int K) {
+    return ws_bytes<int32_t>(n_out * K) + ws_bytes<float>(n_out * K) + ws_bytes<float>(n_out) +
+           ws_bytes<float>(n_out) + ws_bytes<int32_t>(n_in * K) + ws_bytes<float>(n_in * K);
 }
 
 // Dense kernel map (same workspace layout as o3dml_sparse_conv_build_map) for
@@ -639,9 +734,9 @@ O3DML_API size_t o3dml_sparse_conv_lattice_workspace_size(int64_t n_in) {
 // status_host[0]: 4 = not a lattice set (caller uses the search rulebook).
 O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, const float* query_pos, int64_t n_out,
                                             float voxel_size, int ksize, int mirror, int normalize,
-                                            const float* out_importance, int want_inverse, int* status_host,
-                                            void* workspace, size_t workspace_bytes, void* lattice_workspace,
-                                            size_t lattice_workspace_bytes, void* stream) {
+                                            const float* out_importance, int want_inverse, int defer_status,
+                                            int* status_host, void* workspace, size_t workspace_bytes,
+                                            void* lattice_workspace, size_t lattice_workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
     O3DML_REQUIRE(ksize >= 1 && ksize <= 3, "lattice rulebook: kernel size must be 1..3");
     const int K = ksize * ksize * ksize;
@@ -666,83 +761,40 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     while (cap < 2 * n_in) cap <<= 1;
     uint64_t* keys = lws.take<uint64_t>(cap);
     int32_t* vals = lws.take<int32_t>(cap);
-    int* stats = lws.take<int>(32);
+    int* part = lws.take<int>(2 * kLatStatBlocks * 12);
+    LatticeOffsets* lo = lws.take<LatticeOffsets>(1);
     const float inv_vs = 1.0f / voxel_size;
-    // ---- 1. lattice check (fractions constant per axis, keys in range)
-    int init[16];
-    for (int d = 0; d < 3; ++d) {
-        init[4 * d + 0] = 0x7fffffff;
-        init[4 * d + 1] = 0;
-        init[4 * d + 2] = 0x7fffffff;
-        init[4 * d + 3] = static_cast<int>(0x80000000u);
-    }
-    int h_in[12], h_q[12];
-    O3DML_CHECK_HIP(hipMemcpyAsync(stats, init, sizeof(int) * 12, hipMemcpyHostToDevice, st));
-    O3DML_CHECK_HIP(hipMemcpyAsync(stats + 12, init, sizeof(int) * 12, hipMemcpyHostToDevice, st));
-    lattice_stats_kernel<<<stream_grid(n_in, 256, 512), 256, 0, st>>>(inp_pos, n_in, inv_vs, stats);
+    // ---- 1. lattice check + offsets, on the device (no host round trip)
+    const int nblk = static_cast<int>(std::min<int64_t>(kLatStatBlocks, ceil_div(std::max(n_in, n_out), 256)));
+    lattice_stats_kernel<<<dim3(nblk, 2), 256, 0, st>>>(inp_pos, n_in, query_pos, n_out, inv_vs, part);
     O3DML_LAUNCH_CHECK();
-    lattice_stats_kernel<<<stream_grid(n_out, 256, 512), 256, 0, st>>>(query_pos, n_out, inv_vs, stats + 12);
+    lattice_finalize_kernel<<<1, 64, 0, st>>>(part, nblk, ksize, mirror, lo, status);
     O3DML_LAUNCH_CHECK();
-    O3DML_CHECK_HIP(hipMemcpyAsync(h_in, stats, sizeof(int) * 12, hipMemcpyDeviceToHost, st));
-    O3DML_CHECK_HIP(hipMemcpyAsync(h_q, stats + 12, sizeof(int) * 12, hipMemcpyDeviceToHost, st));
-    O3DML_CHECK_HIP(hipStreamSynchronize(st));
-    LatticeOffsets lo{};
-    const double h = 0.5 * ksize;
-    for (int d = 0; d < 3; ++d) {
-        float fi_lo, fi_hi, fq_lo, fq_hi;
-        std::memcpy(&fi_lo, &h_in[4 * d], 4);
-        std::memcpy(&fi_hi, &h_in[4 * d + 1], 4);
-        std::memcpy(&fq_lo, &h_q[4 * d], 4);
-        std::memcpy(&fq_hi, &h_q[4 * d + 1], 4);
-        const bool keys_ok = h_in[4 * d + 2] > -(1 << 19) && h_in[4 * d + 3] < (1 << 19) &&
-                             h_q[4 * d + 2] > -(1 << 19) && h_q[4 * d + 3] < (1 << 19);
-        if (fi_lo != fi_hi || fq_lo != fq_hi || !keys_ok) {
-            *status_host = 4;
-            return 0;
-        }
-        // lattice offsets d = j + dc within [-h, h]: exactly ksize of them, each
-        // with a distinct in-range kernel index
-        const double dc = static_cast<double>(fi_lo) - static_cast<double>(fq_lo);
-        int n_within = 0;
-        for (int j = -8; j <= 8; ++j) {
-            const double dd = j + dc;
-            if (dd < -h || dd > h) continue;
-            const int kid = mirror ? static_cast<int>(std::floor(h - dd)) : static_cast<int>(std::floor(dd + h));
-            if (kid < 0 || kid >= ksize || n_within >= ksize) {
-                *status_host = 4;
-                return 0;
-            }
-            lo.off[d][kid] = j;
-            ++n_within;
-        }
-        if (n_within != ksize) {
-            *status_host = 4;
-            return 0;
-        }
-    }
     // ---- 2. hash the input voxels, 3. K lookups per output
     O3DML_CHECK_HIP(hipMemsetAsync(keys, 0xff, sizeof(uint64_t) * cap, st));
-    O3DML_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, st));
     lattice_insert_kernel<<<stream_grid(n_in, 256), 256, 0, st>>>(inp_pos, n_in, inv_vs, keys, vals,
                                                                  static_cast<uint32_t>(cap - 1), status);
     O3DML_LAUNCH_CHECK();
     lattice_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(
             inp_pos, query_pos, n_out, inv_vs, 0.5f * voxel_size * static_cast<float>(ksize), ksize, lo, keys, vals,
-            static_cast<uint32_t>(cap - 1), map);
+            static_cast<uint32_t>(cap - 1), status, map);
     O3DML_LAUNCH_CHECK();
     if (normalize) {
         map_count_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(map, n_out, K, norm);
         O3DML_LAUNCH_CHECK();
     }
-    recip_norm_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(normalize ? norm : nullptr, out_importance, n_out,
-                                                              oscale);
-    O3DML_LAUNCH_CHECK();
+    if (normalize || out_importance) {
+        recip_norm_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(normalize ? norm : nullptr, out_importance, n_out,
+                                                                  oscale);
+        O3DML_LAUNCH_CHECK();
+    }
     if (want_inverse) {
         O3DML_CHECK_HIP(hipMemsetAsync(inv, 0xff, sizeof(int32_t) * n_in * K, st));
         build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, nullptr, n_out, K, inv, nullptr,
                                                                             status);
         O3DML_LAUNCH_CHECK();
     }
+    if (defer_status) return 0;  // status stays on the device (o3dml_sparse_conv_map_status_offset)
     O3DML_CHECK_HIP(hipMemcpyAsync(status_host, status, sizeof(int), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
     O3DML_GUARD_END
@@ -757,6 +809,26 @@ static void map_views(void* workspace, size_t bytes, int64_t n_out, int64_t n_in
     *oscale = ws.take<float>(n_out);
     *inv = ws.take<int32_t>(n_in * K);
     *ipscale = ws.take<float>(n_in * K);
+}
+
+// Forward with an input prologue and a residual epilogue (SparseConvUnet eval:
+// out = conv(relu(x * pre_scale + pre_shift)) + residual); pre_scale /
+// pre_shift [cin] and residual [n_out, cout] are each nullable.
+O3DML_API int o3dml_sparse_conv_forward_fused(const float* filters, int K, int cin, int cout,
+                                              const float* inp_features, int64_t n_in, const float* pre_scale,
+                                              const float* pre_shift, const float* residual, const float* bias,
+                                              int64_t n_out, float* out_features, void* map_workspace,
+                                              size_t map_workspace_bytes, void* workspace, size_t workspace_bytes,
+                                              void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE((pre_scale == nullptr) == (pre_shift == nullptr), "pre_scale and pre_shift go together");
+    int32_t *map, *inv;
+    float *pscale, *oscale, *ipscale;
+    map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale);
+    run_gemm(as_stream(stream), map, K, n_out, inp_features, nullptr, nullptr, filters, cin, cout, nullptr, bias,
+             out_features, static_cast<float*>(workspace), workspace_bytes, GemmPrologue{pre_scale, pre_shift},
+             residual);
+    O3DML_GUARD_END
 }
 
 // split-K partial sums of o3dml_sparse_conv_forward (0 when no split is used)

@@ -53,8 +53,9 @@ SIGNATURES = {
                                      c_p]),
     "o3dml_voxelize_fill": (c_i32, [c_i64, c_i32, c_i64, c_p, c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "o3dml_sparse_conv_lattice_workspace_size": (c_sz, [c_i64]),
-    "o3dml_sparse_conv_lattice_map": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i32, c_i32, c_i32, c_p, c_i32, c_p,
-                                              c_p, c_sz, c_p, c_sz, c_p]),
+    "o3dml_sparse_conv_lattice_map": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i32, c_i32, c_i32, c_p, c_i32, c_i32,
+                                              c_p, c_p, c_sz, c_p, c_sz, c_p]),
+    "o3dml_sparse_conv_map_status_offset": (c_sz, [c_i64, c_i64, c_i32]),
     "o3dml_kpconv_weighted_features": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_i32,
                                                c_i32, c_f32, c_i32, c_i32, c_p, c_p, c_p]),
     "o3dml_kpconv_weighted_features_backward": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p,
@@ -81,6 +82,8 @@ SIGNATURES = {
     "o3dml_sparse_conv_build_map": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_i32, c_p, c_p,
                                             c_sz, c_p]),
     "o3dml_sparse_conv_forward_workspace_size": (c_sz, [c_i64, c_i32, c_i32, c_i32]),
+    "o3dml_sparse_conv_forward_fused": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64,
+                                                c_p, c_p, c_sz, c_p, c_sz, c_p]),
     "o3dml_sparse_conv_forward": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i64, c_p,
                                           c_p, c_sz, c_p, c_sz, c_p]),
     "o3dml_sparse_conv_backward_workspace_size": (c_sz, [c_i64, c_i64, c_i32, c_i32, c_i32]),

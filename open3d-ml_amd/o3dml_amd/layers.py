@@ -122,13 +122,36 @@ class SparseConv(torch.nn.Module):
         if hash_table is not None or not self.lattice_rulebook:
             return None
         vs = _voxel_size_scalar(voxel_size, inp_positions)
-        queries = (out_positions - sign * self.offset.to(out_positions.device) * vs).contiguous()
         if getattr(self, "_off_ver", None) != (self.offset._version, self.offset.device):
             self._off_host = tuple(float(v) for v in self.offset.detach().cpu())  # one read per load
             self._off_ver = (self.offset._version, self.offset.device)
         off = self._off_host
+        if not any(off):
+            queries = out_positions
+        else:  # built only when the map is not cached already
+            def queries():
+                return (out_positions - (sign * vs) * self.offset.to(out_positions.device)).contiguous()
         return sc.conv_lattice(self.kernel, kw.pop("bias", self.bias), inp_features, inp_positions, queries, vs,
                                mirror=mirror, cache_key=(inp_positions, out_positions, sign) + off, **kw)
+
+    def forward_fused(self, inp_features, inp_positions, out_positions, voxel_size, pre=None, residual=None):
+        """Inference form used by SparseConvUnet in eval mode:
+        forward(relu(x * pre[0] + pre[1])) + residual with the activation
+        applied while the rows are gathered and the residual added in the
+        GEMM epilogue (lattice rulebook); unfused otherwise."""
+        mirror, sign = (True, -1.0) if isinstance(self, SparseConvTranspose) else (False, 1.0)
+        bias = None if mirror else self.bias
+        out = None
+        if not self.normalize and not (self.activation and residual is not None):
+            out = self._lattice(inp_features, inp_positions, out_positions, voxel_size, None, mirror, sign,
+                                bias=bias, pre=pre, residual=residual)
+        if out is None:
+            x = inp_features if pre is None else torch.relu(inp_features * pre[0] + pre[1])
+            out = self.forward(x, inp_positions, out_positions, voxel_size)
+            return out if residual is None else out + residual
+        if mirror and self.bias is not None:
+            out = out + self.bias
+        return self.activation(out) if self.activation else out
 
     def forward(self, inp_features, inp_positions, out_positions, voxel_size, inp_importance=None,
                 fixed_radius_search_hash_table=None):

@@ -143,25 +143,51 @@ def conv_with_bias(filters, bias, inp_features, neighbors_index, neighbors_kerne
                  _opt(inp_importance, dev), normalize, None)
 
 
-_MAP_CACHE = None  # dict while a rulebook_cache() scope is active
+class _RulebookScope:
+    """Kernel maps of one rulebook_cache() scope, and the lattice checks whose
+    device status words are still to be read (defer_checks)."""
+
+    def __init__(self, defer_checks):
+        self.maps = {}
+        self.defer = defer_checks
+        self.pending = []
+
+    def check(self):
+        """One host round trip for every deferred lattice check of the scope:
+        True when all were lattice sets (their maps are valid)."""
+        if not self.pending:
+            return True
+        st = torch.cat(self.pending).cpu()
+        self.pending.clear()
+        if bool((st & 1).any()):
+            raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index")
+        return not bool((st & 4).any())
+
+
+_SCOPE = None  # the active rulebook_cache() scope
 
 
 @contextlib.contextmanager
-def rulebook_cache():
+def rulebook_cache(defer_checks=False):
     """Reuse dense kernel maps inside the scope: layers with the same input /
     output positions, kernel size and offset (every same-level submanifold
     convolution of a SparseConvUnet) share one rulebook.
-    Entries hold the position tensors, so their identities stay unique."""
-    global _MAP_CACHE
-    prev, _MAP_CACHE = _MAP_CACHE, {}
+    Entries hold the position tensors, so their identities stay unique.
+
+    defer_checks: the lattice test of each new map stays on the device (no
+    host sync per layer; a failed test leaves an all-empty map); the caller
+    must call scope.check() before using the results and recompute without
+    deferral when it returns False."""
+    global _SCOPE
+    prev, _SCOPE = _SCOPE, _RulebookScope(defer_checks)
     try:
-        yield
+        yield _SCOPE
     finally:
-        _MAP_CACHE = prev
+        _SCOPE = prev
 
 
 def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, voxel_size, mirror=False,
-                 inp_importance=None, normalize=False, out_importance=None, cache_key=None):
+                 inp_importance=None, normalize=False, out_importance=None, cache_key=None, pre=None, residual=None):
     """Layer forward with the lattice rulebook (dense kernel map straight from a
     voxel hash; csrc/sparse_conv.hip o3dml_sparse_conv_lattice_map).  Returns
     None when the positions are not on one voxel lattice — the caller then
@@ -172,36 +198,61 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
         return None
     x = to_dev(inp_features, dev)
     ip = to_dev(inp_positions, dev, torch.float32)
-    qp = to_dev(query_positions, dev, torch.float32)
+    lazy_q = callable(query_positions)  # layers pass a builder: only a cache miss needs the queries
+    qp = None if lazy_q else to_dev(query_positions, dev, torch.float32)
     lib = _lib.load()
     K = ks ** 3
-    n_in, n_out = ip.shape[0], qp.shape[0]
+    n_in = ip.shape[0]
+    n_out = cache_key[1].shape[0] if lazy_q else qp.shape[0]
     b = None if bias is None else bias.to(dev)
     want_grad = torch.is_grad_enabled() and (filters.requires_grad or x.requires_grad or
                                              (b is not None and b.requires_grad))
     oimp = _opt(out_importance, dev)
     key = None
-    if _MAP_CACHE is not None and cache_key is not None and out_importance is None:
+    scope = _SCOPE
+    if scope is not None and cache_key is not None and out_importance is None:
         key = (ks, bool(mirror), bool(normalize), bool(want_grad), float(voxel_size)) + tuple(cache_key[2:])
         key = key + (id(cache_key[0]), cache_key[0]._version, id(cache_key[1]), cache_key[1]._version)
-    hit = _MAP_CACHE.get(key) if key is not None else None
+    hit = scope.maps.get(key) if key is not None else None
     if hit is not None:
         mws, status0 = hit[0], hit[1]
     else:
+        if lazy_q:
+            qp = to_dev(query_positions(), dev, torch.float32)
+        defer = scope is not None and scope.defer and n_in > 0 and n_out > 0
         mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
         lws = workspace(lib.o3dml_sparse_conv_lattice_workspace_size(n_in), dev)
         status = np.zeros(1, np.int32)
         _lib.call("o3dml_sparse_conv_lattice_map", ptr(ip), n_in, ptr(qp), n_out, float(voxel_size), ks,
-                  int(bool(mirror)), int(bool(normalize)), ptr(oimp), int(bool(want_grad)), status.ctypes.data,
-                  ptr(mws), mws.numel(), ptr(lws), lws.numel(), stream_handle(dev))
+                  int(bool(mirror)), int(bool(normalize)), ptr(oimp), int(bool(want_grad)), int(defer),
+                  status.ctypes.data, ptr(mws), mws.numel(), ptr(lws), lws.numel(), stream_handle(dev))
         status0 = int(status[0])
+        if defer:
+            off = lib.o3dml_sparse_conv_map_status_offset(n_out, n_in, K)
+            scope.pending.append(mws[off:off + 4].view(torch.int32))
         if key is not None:
-            _MAP_CACHE[key] = (mws, status0, cache_key[0], cache_key[1])
+            scope.maps[key] = (mws, status0, cache_key[0], cache_key[1])
     if status0 & 4:
         return None
     if status0 & 1:
         raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index")
     f = filters.to(dev)
+    if pre is not None or residual is not None:
+        # inference-only fused form: relu(x * pre[0] + pre[1]) gathered, + residual
+        if want_grad or inp_importance is not None or normalize or out_importance is not None:
+            raise RuntimeError("sparse_conv: fused prologue/residual is inference-only without importance")
+        cin, cout = int(f.shape[3]), int(f.shape[4])
+        out = torch.empty((n_out, cout), dtype=torch.float32, device=dev)
+        ps, pb = (None, None) if pre is None else (pre[0].contiguous(), pre[1].contiguous())
+        res = None if residual is None else residual.contiguous()
+        if res is not None and tuple(res.shape) != (n_out, cout):
+            raise ValueError("sparse_conv: residual must be [n_out, cout]")
+        fws = workspace(lib.o3dml_sparse_conv_forward_workspace_size(n_out, K, cin, cout), dev)
+        _lib.call("o3dml_sparse_conv_forward_fused", ptr(f.detach().contiguous()), K, cin, cout,
+                  ptr(x.detach().contiguous()), n_in, ptr(ps), ptr(pb), ptr(res),
+                  ptr(None if b is None else b.detach().contiguous()), n_out, ptr(out), ptr(mws), mws.numel(),
+                  ptr(fws), fws.numel(), stream_handle(dev))
+        return out
     empty = torch.empty(0, dtype=torch.int64, device=dev)
     out = _ConvFn.apply(f, x, b, empty, empty, None, empty, _opt(inp_importance, dev), bool(normalize), oimp,
                         want_grad, (mws, n_out))

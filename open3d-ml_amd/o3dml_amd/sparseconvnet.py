@@ -25,8 +25,29 @@ class BatchNormBlock(nn.Module):
         self.bn = nn.BatchNorm1d(m, eps=eps, momentum=momentum)
 
     def forward(self, feat_list):
+        if len(feat_list) == 1:
+            return [self.bn(feat_list[0])]
         lengths = [f.shape[0] for f in feat_list]
         return list(torch.split(self.bn(torch.cat(feat_list, 0)), lengths))
+
+
+def _folded_bn(block):
+    """Eval-mode BatchNorm1d of a BatchNormBlock as a per-channel affine
+    (scale, shift), cached until a parameter or buffer changes."""
+    bn = block.bn
+    key = (bn.weight._version, bn.bias._version, bn.running_mean._version, bn.running_var._version,
+           bn.weight.device, bn.eps)
+    if getattr(block, "_fold_key", None) != key:
+        with torch.no_grad():
+            scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+            block._fold = (scale.contiguous(), (bn.bias - bn.running_mean * scale).contiguous())
+        block._fold_key = key
+    return block._fold
+
+
+def _fusable(module):
+    """Eval mode without autograd: BN + ReLU go into the next conv's gather."""
+    return not module.training and not torch.is_grad_enabled()
 
 
 class ReLUBlock(nn.Module):
@@ -173,6 +194,14 @@ class ResidualBlock(nn.Module):
 
     def forward(self, feat_list, pos_list):
         out1 = self.lin(feat_list)
+        if _fusable(self):
+            pre1, pre2 = _folded_bn(self.batch_norm1), _folded_bn(self.batch_norm2)
+            c1, c2 = self.sub_sparse_conv1.net, self.sub_sparse_conv2.net
+            out = []
+            for f, p, r in zip(feat_list, pos_list, out1):
+                h = c1.forward_fused(f, p, p, 1.0, pre=pre1)
+                out.append(c2.forward_fused(h, p, p, 1.0, pre=pre2, residual=r))
+            return out
         f = self.relu1(self.batch_norm1(feat_list))
         f = self.sub_sparse_conv1(f, pos_list)
         f = self.relu2(self.batch_norm2(f))
@@ -213,7 +242,32 @@ class UNet(nn.Module):
 
     def forward(self, pos_list, feat_list):
         conv_pos, concat_feat = [], []
-        for m in self.net:
+        mods = list(self.net)
+        fuse = _fusable(self)
+        pre = None  # pending folded BN + ReLU (eval): applied by the next conv's gather
+        for j, m in enumerate(mods):
+            if fuse and isinstance(m, BatchNormBlock) and j + 2 < len(mods) and \
+                    isinstance(mods[j + 1], ReLUBlock) and \
+                    isinstance(mods[j + 2], (SubmanifoldSparseConv, Convolution, DeConvolution)):
+                pre = _folded_bn(m)
+                continue
+            if pre is not None and isinstance(m, ReLUBlock):
+                continue
+            if pre is not None:
+                if isinstance(m, SubmanifoldSparseConv):
+                    feat_list = [m.net.forward_fused(f, p, p, 1.0, pre=pre) for f, p in zip(feat_list, pos_list)]
+                elif isinstance(m, Convolution):
+                    conv_pos.append(pos_list)
+                    outs = [ops.calculate_grid(p) for p in pos_list]
+                    feat_list = [m.net.forward_fused(f, p, o, 1.0, pre=pre)
+                                 for f, p, o in zip(feat_list, pos_list, outs)]
+                    pos_list = [o / 2 for o in outs]
+                else:  # DeConvolution
+                    feat_list = [m.net.forward_fused(f, 2 * p, o, 1.0, pre=pre)
+                                 for f, p, o in zip(feat_list, pos_list, conv_pos[-1])]
+                    pos_list = conv_pos.pop()
+                pre = None
+                continue
             if isinstance(m, (BatchNormBlock, ReLUBlock)):
                 feat_list = m(feat_list)
             elif isinstance(m, (ResidualBlock, SubmanifoldSparseConv)):
@@ -252,15 +306,26 @@ class SparseConvUnet(nn.Module):
         self.output_layer = OutputLayer()
 
     def forward(self, inputs):
+        # lattice checks of all levels are read back once at the end; a
+        # non-lattice input (never produced by the reference preprocess) is
+        # recomputed with per-layer checks and the search rulebook
+        with rulebook_cache(defer_checks=True) as scope:
+            out = self._forward(inputs)
+            ok = scope.check()
+        if ok:
+            return out
         with rulebook_cache():
-            pos_list, feat_list, index_maps = [], [], []
-            for i in range(len(inputs.batch_lengths)):
-                f, p, m = self.input_layer(inputs.feat[i], inputs.point[i])
-                pos_list.append(p)
-                feat_list.append(f)
-                index_maps.append(m)
-            feat_list = self.sub_sparse_conv(feat_list, pos_list, voxel_size=1.0)
-            feat_list = self.unet(pos_list, feat_list)
-            feat_list = self.relu(self.batch_norm(feat_list))
-            feat_list = self.linear(feat_list)
-            return self.output_layer(feat_list, index_maps)
+            return self._forward(inputs)
+
+    def _forward(self, inputs):
+        pos_list, feat_list, index_maps = [], [], []
+        for i in range(len(inputs.batch_lengths)):
+            f, p, m = self.input_layer(inputs.feat[i], inputs.point[i])
+            pos_list.append(p)
+            feat_list.append(f)
+            index_maps.append(m)
+        feat_list = self.sub_sparse_conv(feat_list, pos_list, voxel_size=1.0)
+        feat_list = self.unet(pos_list, feat_list)
+        feat_list = self.relu(self.batch_norm(feat_list))
+        feat_list = self.linear(feat_list)
+        return self.output_layer(feat_list, index_maps)

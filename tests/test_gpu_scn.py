@@ -49,12 +49,11 @@ def test_scn_search_rulebook_equals_lattice(cuda):
     from o3dml_amd import layers
     m = _model(True, cuda)
     inp = _inputs(cuda)
-    with torch.no_grad():
-        a = m(inp)
-        for mod in m.modules():
-            if isinstance(mod, layers.SparseConv):
-                mod.lattice_rulebook = False
-        b = m(inp)
+    a = m(inp).detach()  # autograd on: unfused layers, so only the rulebook differs
+    for mod in m.modules():
+        if isinstance(mod, layers.SparseConv):
+            mod.lattice_rulebook = False
+    b = m(inp).detach()
     assert torch.equal(a, b)
 
 
@@ -69,3 +68,36 @@ def test_input_layer_voxel_map(cuda):
     # voxel mean
     ref = torch.zeros_like(avg).index_add_(0, imap, feat) / torch.bincount(imap, minlength=avg.shape[0])[:, None]
     assert torch.allclose(avg, ref, atol=1e-6)
+
+
+def test_scn_off_lattice_input_recomputes(cuda):
+    """Positions off the half-integer lattice: the deferred lattice check fails,
+    the forward is recomputed with per-layer checks (search rulebook), and the
+    result equals a forward with the lattice rulebook disabled."""
+    from o3dml_amd import layers
+    m = _model(False, cuda)
+    inp = _inputs(cuda)
+    inp.point = [inp.point[0] - 0.1 * (torch.arange(inp.point[0].shape[0], device=cuda) % 2)[:, None]]
+    a = m(inp).detach()
+    for mod in m.modules():
+        if isinstance(mod, layers.SparseConv):
+            mod.lattice_rulebook = False
+    b = m(inp).detach()
+    assert torch.equal(a, b)
+    with torch.no_grad():  # fused eval form, same fallback
+        c = m(inp)
+    assert ((c - b).abs().max() / b.abs().max()).item() < 1e-5
+
+
+@pytest.mark.parametrize("residual", [True, False])
+def test_scn_fused_eval_matches_unfused(cuda, residual):
+    """Eval without autograd folds BN + ReLU into the next convolution's gather
+    and the residual add into its epilogue; with autograd enabled the layers
+    run unfused.  Same logits within fp32 rounding."""
+    m = _model(residual, cuda)
+    inp = _inputs(cuda)
+    with torch.no_grad():
+        a = m(inp)
+    b = m(inp).detach()
+    err = ((a - b).abs().max() / b.abs().max()).item()
+    assert err < 1e-5, err
