@@ -7,16 +7,19 @@
 //   CSR pairs (neighbors_index, neighbors_kernel_index, neighbors_row_splits)
 //     -> dense kernel map  map[o*K + k] = input row or -1   (build_kernel_map)
 //   forward  out[o,:] = oscale[o] * sum_k (src[map[o,k],:] * sscale[i] * pscale[o,k]) @ W[k] + bias
-//            output-stationary implicit GEMM: a workgroup owns TM output rows x
-//            TN output channels, walks the K offsets (skipping offsets no row of
-//            the tile uses) and Cin in KC=32 chunks; the gathered rows and the
-//            W[k] chunk are staged in LDS and multiplied with
-//            v_mfma_f32_32x32x2_f32 (exact fp32 FMA chains; 4 waves, 32x32 each).
-//            No atomics: every output row is written once -> deterministic.
+//            output-stationary implicit GEMM: a wave owns 32 output rows x 32
+//            output channels, walks the K offsets its rows use and Cin in
+//            32-channel stages, operands gathered straight into the
+//            v_mfma_f32_32x32x2_f32 registers (exact fp32 FMA chains); when the
+//            tiles cannot fill the chip the (offset, Cin) stages are split
+//            across waves and the partials reduced in a fixed order.  No
+//            atomics -> deterministic.  Optional eval prologue (folded
+//            BatchNorm + ReLU on the gathered rows) and residual epilogue.
 //   dIn      the same kernel on the inverse map inv[i*K+k] = o with W^T.
 //   dW       per offset k the pair list (o, i) (k-major compaction of the map);
-//            dW[k] = sum_j src[i_j]^T g[o_j] as split-K MFMA tiles into partial
-//            slabs, reduced in a fixed order (deterministic).
+//            dW[k] = sum_j src[i_j]^T g[o_j], one wave per 32x32 tile and pair
+//            chunk with the pairs as the MFMA reduction index (operands gathered
+//            straight into registers), chunk slabs reduced in a fixed order.
 // Roofline: MFMA fp32 (157 TF/s dense) for Cin*Cout >= ~64^2, gather/HBM bound
 // below that.
 #include <algorithm>
@@ -31,7 +34,6 @@ namespace o3dml {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kKC = 32;           // Cin chunk per LDS stage
 constexpr int kGemmThreads = 256; // 4 waves
 
 // --------------------------------------------------------------------------
@@ -114,67 +116,91 @@ __global__ void transpose_filters_kernel(const float* __restrict__ w, int K, int
 // --------------------------------------------------------------------------
 struct GemmStage {
     float a[16], b[16];
+    float sc;  // row factor (importance x pair scale; 0 for a missing neighbour)
 };
 
 // Optional prologue on the gathered rows (eval-mode BatchNorm + ReLU of the
-// layer input, folded to a per-channel affine): a = relu(x * ps[c] + pb[c]).
-// Missing neighbours stay exactly 0 (sc = 0), as the zero padding of the
-// activated features.
+// layer input, folded to a per-channel affine): a = relu(x * ps[c] + pb[c]),
+// staged once per workgroup in LDS.  Missing neighbours stay exactly 0
+// (row factor 0), as the zero padding of the activated features.
 struct GemmPrologue {
     const float* scale;  // [cin] or null
     const float* shift;  // [cin]
 };
+constexpr int kPreMax = 1024;  // max cin with a prologue (LDS staging)
 
 __device__ __forceinline__ float pre_act(float v, float s, float b) { return fmaxf(fmaf(v, s, b), 0.f); }
+
+// Every load below is unconditional and its value is used unconditionally:
+// lanes without data (missing neighbour, channel or column past the end) read
+// from a zero page instead.  A select of "valid ? load : 0" lets the compiler
+// sink the load into a branch with a vmcnt(0) wait per load, which serialises
+// the stage's loads instead of keeping them in flight.  All arithmetic on the
+// loaded values happens in gemm_finish, after the previous stage's MFMAs.
+__device__ __attribute__((aligned(16))) float g_zero_page[16];
 
 template <bool VEC4>
 __device__ __forceinline__ void gemm_load(GemmStage& st, int32_t m, int K, int64_t o, int k, int c0, int h, int col,
                                           const float* __restrict__ src, const float* __restrict__ sscale,
                                           const float* __restrict__ pscale, const float* __restrict__ W, int cin,
-                                          int cout, GemmPrologue pre) {
+                                          int cout) {
     const int cb = c0 + 16 * h;
-    float sc = 0.f;
-    if (m >= 0) sc = (sscale ? sscale[m] : 1.f) * (pscale ? pscale[o * K + k] : 1.f);
-    if (VEC4 && cb + 16 <= cin) {
-        const float4* row = reinterpret_cast<const float4*>(src + static_cast<int64_t>(m >= 0 ? m : 0) * cin + cb);
+    const bool valid = m >= 0;
+    const int64_t mr = valid ? m : 0;
+    float sc = sscale ? sscale[mr] : 1.f;
+    if (pscale) sc *= pscale[(valid ? o : 0) * K + k];
+    st.sc = valid ? sc : 0.f;
+    const float* row = src + mr * cin;
+    if (VEC4) {  // cin % 4 == 0: float4 granules
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            float4 v = m >= 0 ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-            if (pre.scale) {
-                const float4 ps = reinterpret_cast<const float4*>(pre.scale + cb)[q];
-                const float4 pb = reinterpret_cast<const float4*>(pre.shift + cb)[q];
-                v = make_float4(pre_act(v.x, ps.x, pb.x), pre_act(v.y, ps.y, pb.y), pre_act(v.z, ps.z, pb.z),
-                                pre_act(v.w, ps.w, pb.w));
-            }
-            st.a[4 * q] = v.x * sc;
-            st.a[4 * q + 1] = v.y * sc;
-            st.a[4 * q + 2] = v.z * sc;
-            st.a[4 * q + 3] = v.w * sc;
+            const int c = cb + 4 * q;
+            const float4 v = *reinterpret_cast<const float4*>((valid && c < cin) ? row + c : g_zero_page);
+            st.a[4 * q] = v.x;
+            st.a[4 * q + 1] = v.y;
+            st.a[4 * q + 2] = v.z;
+            st.a[4 * q + 3] = v.w;
         }
     } else {
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            float v = (m >= 0 && cb + s < cin) ? src[static_cast<int64_t>(m) * cin + cb + s] : 0.f;
-            if (pre.scale && cb + s < cin) v = pre_act(v, pre.scale[cb + s], pre.shift[cb + s]);
-            st.a[s] = v * sc;
-        }
+        for (int s = 0; s < 16; ++s) st.a[s] = *((valid && cb + s < cin) ? row + cb + s : g_zero_page);
     }
-    const float* wk = W + static_cast<int64_t>(k) * cin * cout;
+    const float* wk = W + static_cast<int64_t>(k) * cin * cout + col;
+    const bool colv = col < cout;
 #pragma unroll
-    for (int s = 0; s < 16; ++s)
-        st.b[s] = (cb + s < cin && col < cout) ? wk[static_cast<int64_t>(cb + s) * cout + col] : 0.f;
+    for (int s = 0; s < 16; ++s) {
+        const int c = cb + s;
+        st.b[s] = *((c < cin && colv) ? wk + static_cast<int64_t>(c) * cout : g_zero_page);
+    }
 }
 
-template <bool VEC4>
+template <bool PRE>
+__device__ __forceinline__ void gemm_finish(GemmStage& st, int c0, int h, const float* lps, const float* lpb) {
+    const int cb = c0 + 16 * h;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) st.a[s] = (PRE ? pre_act(st.a[s], lps[cb + s], lpb[cb + s]) : st.a[s]) * st.sc;
+}
+
+template <bool VEC4, bool PRE>
 __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, const float* __restrict__ src,
                      const float* __restrict__ sscale, const float* __restrict__ pscale,
                      const float* __restrict__ W /*[K][cin][cout]*/, int cin, int cout,
                      const float* __restrict__ oscale, const float* __restrict__ bias, float* __restrict__ out,
                      int nsplit, float* __restrict__ part, GemmPrologue pre, const float* __restrict__ residual) {
+    __shared__ float lpre[PRE ? 2 * (kPreMax + 32) : 1];
+    float* lps = lpre;
+    float* lpb = lpre + (PRE ? kPreMax + 32 : 0);
+    if (PRE) {  // channels past cin stay 0 -> relu(0) * factor = 0
+        for (int c = threadIdx.x; c < kPreMax + 32; c += kGemmThreads) {
+            lps[c] = c < cin ? pre.scale[c] : 0.f;
+            lpb[c] = c < cin ? pre.shift[c] : 0.f;
+        }
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63;
     const int64_t o0 = (static_cast<int64_t>(blockIdx.x) * (kGemmThreads / 64) + (threadIdx.x >> 6)) * 32;
-    if (o0 >= n_out) return;  // whole wave; the kernel has no barriers
+    if (o0 >= n_out) return;  // whole wave; no barriers below
     const int i = lane & 31, h = lane >> 5;
     const int col = blockIdx.y * 32 + i;
     const int64_t o = o0 + i;
@@ -209,7 +235,7 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
         GemmStage cur, nxt;
         int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
-        gemm_load<VEC4>(cur, mtile[i * K + k], K, o, k, c0, h, col, src, sscale, pscale, W, cin, cout, pre);
+        gemm_load<VEC4>(cur, mtile[i * K + k], K, o, k, c0, h, col, src, sscale, pscale, W, cin, cout);
         for (int j = j0 + 1;; ++j) {
             int nk = k, nc = c0 + 32;
             if (nc >= cin) {
@@ -218,8 +244,8 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
                 nk = u ? __builtin_ctz(u) : -1;
             }
             const bool more = j < j1;
-            if (more)
-                gemm_load<VEC4>(nxt, mtile[i * K + nk], K, o, nk, nc, h, col, src, sscale, pscale, W, cin, cout, pre);
+            if (more) gemm_load<VEC4>(nxt, mtile[i * K + nk], K, o, nk, nc, h, col, src, sscale, pscale, W, cin, cout);
+            gemm_finish<PRE>(cur, c0, h, lps, lpb);
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[r], cur.b[r], acc, 0, 0, 0);
             if (!more) break;
@@ -228,7 +254,7 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
             cur = nxt;
         }
     }
-    if (nsplit > 1) {  // raw partial sums; split_reduce_kernel applies oscale / bias
+    if (nsplit > 1) {  // raw partial sums; split_reduce_kernel applies oscale / bias / residual
         float* P = part + static_cast<int64_t>(s) * n_out * cout;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -277,63 +303,102 @@ __global__ void pair_lists_kernel(const int32_t* __restrict__ map, int64_t n_out
     }
 }
 
-// part[(k*nchunk + ch)][cin][cout] for tile (ci0, co0) of 64x64.
-__global__ void __launch_bounds__(kGemmThreads)
+// dW[k] tile (ci0, co0) of 32 x 32 over one chunk of offset k's pair list,
+// one wave per (tile, k, chunk): the pairs are the MFMA reduction index, so
+// lane (i, h) gathers x[in_p][ci0 + i] and g[out_p][co0 + i] of pair
+// 2s + h straight into the v_mfma_f32_32x32x2_f32 operand registers (32
+// consecutive channels of one row per half-wave: coalesced).  The chunk's
+// pair records (out row, in row, scales) are staged in LDS kDwSub at a time,
+// so a stage's gathers depend on LDS reads only and the next stage's gathers
+// are in flight while the current 16 MFMAs run.  No barriers beyond the wave.
+// part[(k*nchunk + ch)][cin][cout].
+constexpr int kDwSub = 512;
+
+struct DwStage {
+    float a[16], b[16];
+};
+
+__device__ __forceinline__ void dw_load(DwStage& st, int base, int h, const int32_t* lo, const int32_t* lm,
+                                        const float* lra, const float* lrb, const float* __restrict__ src,
+                                        const float* __restrict__ g, int cin, int cout, int ci, int co) {
+    // unconditional loads, absent data read from the zero page (see gemm_load)
+    const bool cv = ci < cin, ov = co < cout;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int pp = base + 2 * s + h;
+        const int32_t mo = lo[pp], mi = lm[pp];
+        st.a[s] = *((cv && mi >= 0) ? src + static_cast<int64_t>(mi) * cin + ci : g_zero_page);
+        st.b[s] = *((ov && mo >= 0) ? g + static_cast<int64_t>(mo) * cout + co : g_zero_page);
+    }
+}
+
+__device__ __forceinline__ void dw_finish(DwStage& st, int base, int h, const float* lra, const float* lrb) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int pp = base + 2 * s + h;
+        st.a[s] *= lra[pp];
+        st.b[s] *= lrb[pp];
+    }
+}
+
+__global__ void __launch_bounds__(64)
 dweight_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ po, const int64_t* __restrict__ kstart, int K,
                int nchunk, const float* __restrict__ src, const float* __restrict__ sscale,
                const float* __restrict__ pscale, const float* __restrict__ g, const float* __restrict__ oscale, int cin,
                int cout, float* __restrict__ part) {
-    __shared__ float As[64][kKC + 1];  // [ci][pair]
-    __shared__ float Bs[kKC][64];      // [pair][co]
-    __shared__ int32_t Ri[kKC], Ro[kKC];
-    __shared__ float Rs[kKC], Ro_s[kKC];
-    const int k = blockIdx.z / nchunk, ch = blockIdx.z % nchunk;
-    const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6, wr = w >> 1, wc = w & 1;
-    const int64_t s = kstart[k], e = kstart[k + 1];
-    const int64_t len = (e - s + nchunk - 1) / nchunk;
-    const int64_t js = s + ch * len;
-    const int64_t je = min(e, js + len);
+    __shared__ int32_t lo[kDwSub], lm[kDwSub];
+    __shared__ float lra[kDwSub], lrb[kDwSub];
+    const int ncot = (cout + 31) >> 5;
+    const int ci0 = (blockIdx.x / ncot) * 32, co0 = (blockIdx.x % ncot) * 32;
+    const int k = blockIdx.y, ch = blockIdx.z;
+    const int lane = threadIdx.x, i = lane & 31, h = lane >> 5;
+    const int64_t s0 = kstart[k], e0 = kstart[k + 1];
+    const int64_t len = (e0 - s0 + nchunk - 1) / nchunk;
+    const int64_t js = s0 + ch * len;
+    const int64_t je = min(e0, js + len);
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    for (int64_t j0 = js; j0 < je; j0 += kKC) {
-        if (t < kKC) {
-            const int64_t j = j0 + t;
-            if (j < je) {
-                const int32_t o = po[j];
-                const int32_t i = map[static_cast<int64_t>(o) * K + k];
-                Ro[t] = o;
-                Ri[t] = i;
-                Rs[t] = (sscale ? sscale[i] : 1.f) * (pscale ? pscale[static_cast<int64_t>(o) * K + k] : 1.f);
-                Ro_s[t] = oscale ? oscale[o] : 1.f;
-            } else {
-                Ro[t] = -1;
-                Ri[t] = -1;
-                Rs[t] = 0.f;
-                Ro_s[t] = 0.f;
+    for (int64_t sub = js; sub < je; sub += kDwSub) {
+        const int n = static_cast<int>(min(static_cast<int64_t>(kDwSub), je - sub));
+        for (int t = lane; t < kDwSub; t += 64) {
+            int32_t o = -1, m = -1;
+            float ra = 0.f, rb = 0.f;
+            if (t < n) {
+                o = po[sub + t];
+                m = map[static_cast<int64_t>(o) * K + k];
+                ra = (sscale ? sscale[m] : 1.f) * (pscale ? pscale[static_cast<int64_t>(o) * K + k] : 1.f);
+                rb = oscale ? oscale[o] : 1.f;
             }
+            lo[t] = o;
+            lm[t] = m;
+            lra[t] = ra;
+            lrb[t] = rb;
         }
-        __syncthreads();
-        for (int x = t; x < 64 * kKC; x += kGemmThreads) {
-            const int p = x / 64, c = x - p * 64;  // consecutive threads -> consecutive channels
-            const int32_t i = Ri[p];
-            As[c][p] = (i >= 0 && ci0 + c < cin) ? src[static_cast<int64_t>(i) * cin + ci0 + c] * Rs[p] : 0.f;
-            const int32_t o = Ro[p];
-            Bs[p][c] = (o >= 0 && co0 + c < cout) ? g[static_cast<int64_t>(o) * cout + co0 + c] * Ro_s[p] : 0.f;
-        }
-        __syncthreads();
-        const int ar = wr * 32 + (lane & 31), bc = wc * 32 + (lane & 31), kh = lane >> 5;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int nst = (n + 31) >> 5;
+        DwStage cur, nxt;
+        dw_load(cur, 0, h, lo, lm, lra, lrb, src, g, cin, cout, ci0 + i, co0 + i);
+        for (int j = 0;; ++j) {
+            const bool more = j + 1 < nst;
+            if (more) dw_load(nxt, 32 * (j + 1), h, lo, lm, lra, lrb, src, g, cin, cout, ci0 + i, co0 + i);
+            dw_finish(cur, 32 * j, h, lra, lrb);
 #pragma unroll
-        for (int ss = 0; ss < kKC / 2; ++ss)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[ar][2 * ss + kh], Bs[2 * ss + kh][bc], acc, 0, 0, 0);
-        __syncthreads();
+            for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[r], cur.b[r], acc, 0, 0, 0);
+            if (!more) break;
+            cur = nxt;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // LDS records are rewritten by the next sub-chunk
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    float* P = part + static_cast<int64_t>(blockIdx.z) * cin * cout;
-    const int col = co0 + wc * 32 + (lane & 31);
+    float* P = part + (static_cast<int64_t>(k) * nchunk + ch) * cin * cout;
+    const int col = co0 + i;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int row = ci0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int row = ci0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (row < cin && col < cout) P[static_cast<int64_t>(row) * cout + col] = acc[r];
     }
 }
@@ -423,18 +488,21 @@ static void run_gemm(hipStream_t st, const int32_t* map, int K, int64_t n_out, c
                      float* out, float* part, size_t part_bytes, GemmPrologue pre = {nullptr, nullptr},
                      const float* residual = nullptr) {
     if (n_out == 0 || cout == 0) return;
-    const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0 &&
-                      (reinterpret_cast<uintptr_t>(pre.scale) % 16) == 0 && (reinterpret_cast<uintptr_t>(pre.shift) % 16) == 0;
+    const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0;
     int ns = gemm_splits(n_out, K, cin, cout);
     if (!part || part_bytes < sizeof(float) * static_cast<size_t>(ns) * n_out * cout) ns = 1;
     const dim3 g(static_cast<unsigned>(ceil_div(n_out, 32 * (kGemmThreads / 64))),
                  static_cast<unsigned>(ceil_div(cout, 32)), static_cast<unsigned>(ns));
-    if (vec4)
-        implicit_gemm_kernel<true><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
-                                                               oscale, bias, out, ns, part, pre, residual);
-    else
-        implicit_gemm_kernel<false><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout,
-                                                                oscale, bias, out, ns, part, pre, residual);
+    O3DML_REQUIRE(pre.scale == nullptr || cin <= kPreMax, "sparse_conv: prologue needs cin <= %d", kPreMax);
+#define O3DML_GEMM_LAUNCH(V, P)                                                                                    \
+    implicit_gemm_kernel<V, P><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout, oscale, \
+                                                           bias, out, ns, part, pre, residual)
+    if (pre.scale) {
+        if (vec4) O3DML_GEMM_LAUNCH(true, true); else O3DML_GEMM_LAUNCH(false, true);
+    } else {
+        if (vec4) O3DML_GEMM_LAUNCH(true, false); else O3DML_GEMM_LAUNCH(false, false);
+    }
+#undef O3DML_GEMM_LAUNCH
     O3DML_LAUNCH_CHECK();
     if (ns > 1) {
         split_reduce_kernel<<<stream_grid(n_out * cout, 256), 256, 0, st>>>(part, ns, n_out, cout, oscale, bias,
@@ -854,8 +922,17 @@ O3DML_API int o3dml_sparse_conv_forward(const float* filters, int K, int cin, in
     O3DML_GUARD_END
 }
 
+// dW pair-list chunks per offset: enough waves to fill the chip (~4 per
+// SIMD), but at least ~256 pairs per chunk (each chunk writes a cin x cout slab).
+static int dw_chunks(int64_t n_out, int K, int cin, int cout) {
+    const int64_t tiles = ceil_div(cin, 32) * ceil_div(cout, 32) * static_cast<int64_t>(K);
+    int64_t nc = ceil_div(int64_t(4096), tiles);
+    nc = std::min<int64_t>(nc, std::max<int64_t>(1, n_out / 256));
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(nc, 64)));
+}
+
 O3DML_API size_t o3dml_sparse_conv_backward_workspace_size(int64_t n_out, int64_t n_in, int K, int cin, int cout) {
-    const int nchunk = 16;
+    const int nchunk = dw_chunks(n_out, K, cin, cout);
     return ws_bytes<float>(static_cast<int64_t>(K) * cin * cout) + ws_bytes<float>(n_out * cout) +
            gemm_split_bytes(n_in, K, cout, cin) + ws_bytes<int64_t>(n_out * K) * 2 + ws_bytes<int32_t>(n_out * K) +
            ws_bytes<int64_t>(K + 1) + ws_bytes<float>(static_cast<int64_t>(K) * nchunk * cin * cout) +
@@ -902,23 +979,25 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
         int64_t* incl = ws.take<int64_t>(n_out * K);
         int32_t* po = ws.take<int32_t>(n_out * K);
         int64_t* kstart = ws.take<int64_t>(K + 1);
-        const int nchunk = 16;
-        float* part = ws.take<float>(static_cast<int64_t>(K) * nchunk * cin * cout);
+        const int nchunk = dw_chunks(n_out, K, cin, cout);
+        float* part = nchunk > 1 ? ws.take<float>(static_cast<int64_t>(K) * nchunk * cin * cout) : grad_filters;
         pair_flags_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, n_out, K, flags);
         O3DML_LAUNCH_CHECK();
         Workspace sws = ws;
         prim::scan<int64_t, int64_t>(flags, incl, n_out * K, true, sws, st);
         pair_lists_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, n_out, K, incl, po, kstart);
         O3DML_LAUNCH_CHECK();
-        dim3 gg(static_cast<unsigned>(ceil_div(cin, 64)), static_cast<unsigned>(ceil_div(cout, 64)),
-                static_cast<unsigned>(K * nchunk));
-        dweight_kernel<<<gg, kGemmThreads, 0, st>>>(map, po, kstart, K, nchunk, inp_features, inp_importance,
+        dim3 gg(static_cast<unsigned>(ceil_div(cin, 32) * ceil_div(cout, 32)), static_cast<unsigned>(K),
+                static_cast<unsigned>(nchunk));
+        dweight_kernel<<<gg, 64, 0, st>>>(map, po, kstart, K, nchunk, inp_features, inp_importance,
                                                     has_neighbors_importance ? pscale : nullptr, grad_out, os, cin,
                                                     cout, part);
         O3DML_LAUNCH_CHECK();
-        reduce_slabs_kernel<<<stream_grid(KC, 256), 256, 0, st>>>(part, K, nchunk,
-                                                                  static_cast<int64_t>(cin) * cout, grad_filters);
-        O3DML_LAUNCH_CHECK();
+        if (nchunk > 1) {
+            reduce_slabs_kernel<<<stream_grid(KC, 256), 256, 0, st>>>(part, K, nchunk,
+                                                                      static_cast<int64_t>(cin) * cout, grad_filters);
+            O3DML_LAUNCH_CHECK();
+        }
     }
     O3DML_GUARD_END
 }

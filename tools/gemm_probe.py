@@ -1,0 +1,48 @@
+"""Sparse-conv GEMM microbenchmark on the C4 room voxels: the lattice map is
+built once (rulebook_cache), then the forward GEMM alone is timed for several
+channel widths, plus the backward (dIn + dW) with autograd."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "open3d-ml_amd"))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from o3dml_amd import layers, sparse_conv as sc  # noqa: E402
+
+dev = torch.device("cuda", 0)
+pos = torch.from_numpy(bench.make_room(0)[0]).to(dev)
+reps = int(os.environ.get("REPS", "20"))
+for cin, cout in [(32, 32), (64, 64), (128, 128), (64, 32)]:
+    torch.manual_seed(0)
+    conv = layers.SparseConv(cin, cout, [3, 3, 3], use_bias=False).to(dev)
+    x = torch.rand((pos.shape[0], cin), device=dev)
+    with sc.rulebook_cache():
+        with torch.no_grad():
+            conv(x, pos, pos, 1.0)
+            nb, _ = conv._rulebook(pos, pos, 1.0, None, False, 1.0)
+            pairs = int(nb.neighbors_index.shape[0])
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                conv(x, pos, pos, 1.0)
+            e1.record()
+            torch.cuda.synchronize()
+            fwd = e0.elapsed_time(e1) / reps
+        xg = x.clone().requires_grad_(True)
+        out = conv(xg, pos, pos, 1.0)
+        g = torch.rand_like(out)
+        out.backward(g, retain_graph=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps):
+            torch.autograd.grad(out, [xg, conv.kernel], g, retain_graph=True)
+        e1.record()
+        torch.cuda.synchronize()
+        bwd = e0.elapsed_time(e1) / reps
+    fl = 2.0 * pairs * cin * cout
+    print(f"cin {cin:4d} cout {cout:4d} pairs {pairs} fwd {fwd * 1e3:8.1f} us {fl / fwd / 1e9:7.2f} TF/s | "
+          f"bwd {bwd * 1e3:8.1f} us {2 * fl / bwd / 1e9:7.2f} TF/s", flush=True)
