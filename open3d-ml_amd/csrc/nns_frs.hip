@@ -931,23 +931,21 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
 
 // Final rows from the temp rows of path G (already in canonical order, temp
 // row = query id, so both sides stream in order).  A wave owns 64
-// consecutive rows: every lane fetches one row's (count, row start), then the
-// wave copies the rows 8 at a time with all 8 loads in flight, lanes =
-// entries.  Rows longer than kRowCap are written by the MODE 1 re-run.
+// consecutive rows; lanes = entries of one row, 8 rows in flight: one
+// coalesced 4-B-per-lane load of the row's live entries (lanes past the count
+// read a zero word, so no load sits under a branch) and one coalesced store.
+// Rows longer than kRowCap are written by the MODE 1 re-run.
+__device__ uint32_t g_frs_zero[4];
+
 template <bool DIST, class TIdx>
 __global__ void __launch_bounds__(256) group_rows_copy_kernel(int64_t m, const int64_t* __restrict__ counts,
                                                               const int64_t* __restrict__ rs,
                                                               const uint32_t* __restrict__ tidx,
                                                               const float* __restrict__ tdist,
                                                               TIdx* __restrict__ idx, float* __restrict__ dist) {
-    // lane = (row r of 4, quarter-row qq of 16): 16-B loads of 4 entries from the
-    // 256-B temp row, 4 consecutive stores; 8 rows in flight per wave
     const int lane = threadIdx.x & 63;
-    const int sub = lane >> 4, qq = lane & 15;
     const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
-    const uint4* __restrict__ t4 = reinterpret_cast<const uint4*>(tidx);
-    const float4* __restrict__ d4 = reinterpret_cast<const float4*>(tdist);
     for (int64_t base = wave * 64; base < m; base += nwaves * 64) {
         const int64_t t = base + lane;
         int n = 0;
@@ -958,34 +956,25 @@ __global__ void __launch_bounds__(256) group_rows_copy_kernel(int64_t m, const i
             o = rs[t];
         }
         for (int k = 0; k < 64; k += 8) {
-            uint4 v[2];
-            float4 dv[2];
-            int nn[2];
-            int64_t oo[2];
+            uint32_t v[8];
+            float dv[8];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int rr = k + u * 4 + sub;
-                nn[u] = __shfl(n, rr, 64);
-                oo[u] = __shfl(o, rr, 64);
-                const bool ok = base + rr < m && qq * 4 < nn[u];
-                const int64_t src = (base + rr) * (kRowCap / 4) + qq;
-                v[u] = ok ? t4[src] : make_uint4(0u, 0u, 0u, 0u);
-                if constexpr (DIST) dv[u] = ok ? d4[src] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int u = 0; u < 8; ++u) {
+                const int nu = __builtin_amdgcn_readlane(n, k + u);
+                const int64_t src = (base + k + u) * kRowCap + lane;
+                const bool live = lane < nu;
+                v[u] = *(live ? tidx + src : g_frs_zero);
+                if constexpr (DIST) dv[u] = *(live ? tdist + src : reinterpret_cast<const float*>(g_frs_zero));
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int rr = k + u * 4 + sub;
-                if (base + rr < m) {
-                    const int j0 = qq * 4;
-                    const uint32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-                    const float dd[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        if (j0 + e < nn[u]) {
-                            idx[oo[u] + j0 + e] = static_cast<TIdx>(vv[e]);
-                            if constexpr (DIST) dist[oo[u] + j0 + e] = dd[e];
-                        }
-                    }
+            for (int u = 0; u < 8; ++u) {
+                const int nu = __builtin_amdgcn_readlane(n, k + u);
+                const int64_t ou = static_cast<int64_t>(
+                        (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(o >> 32), k + u))) << 32) |
+                        static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(o), k + u)));
+                if (lane < nu) {
+                    idx[ou + lane] = static_cast<TIdx>(v[u]);
+                    if constexpr (DIST) dist[ou + lane] = dv[u];
                 }
             }
         }
