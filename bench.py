@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--randla-frames", type=int, default=3, help="RandLA-Net frames timed (0: skip)")
+    ap.add_argument("--kpconv-steps", type=int, default=5, help="C3 KPFCNN training steps timed (0: skip)")
     ap.add_argument("--sparse-conv-reps", type=int, default=10, help="C4 sparse-conv forwards timed (0: skip)")
     return ap.parse_args()
 
@@ -154,6 +155,76 @@ def randla_frames(dev, frames):
             "patches_per_frame": round(patches / frames, 2), "frames": frames,
             "config": "C2: 120,000-pt synthetic 64-beam scan, RandLANet semantickitti cfg, fp32, random init",
             "cpu_reference_s_per_frame_8cores_survey": 10.6}
+
+
+def make_c3(seed=0, n=20000):
+    """C3-shaped KPConv batch: two indoor spheres of radius 1.5 m
+    (kpconv_s3dis.yml in_radius) with n points each sampled uniformly on a floor, a
+    ceiling and three walls (~25 neighbours at the first conv radius, as on
+    0.04-subsampled S3DIS), 5 input features (1, colour + height
+    proxies), 13 labels — fed directly to segmentation_inputs."""
+    rng = np.random.default_rng(seed)
+    clouds = []
+    for _ in range(2):
+        pts = []
+        while sum(len(p) for p in pts) < n:
+            m = 4 * n
+            s = rng.integers(0, 5, m)
+            u, v = rng.uniform(-1.5, 1.5, (2, m))
+            h = rng.normal(0, 0.005, m)
+            p = np.select([s[:, None] == 0, s[:, None] == 1, s[:, None] == 2, s[:, None] == 3],
+                          [np.stack([u, v, h - 0.6], 1), np.stack([u, v, h + 0.7], 1),
+                           np.stack([h - 0.5, u, v], 1), np.stack([u, h + 0.6, v], 1)],
+                          np.stack([h + 0.8, u, v], 1))
+            pts.append(p[np.linalg.norm(p, axis=1) < 1.5])
+        clouds.append(np.concatenate(pts)[:n].astype(np.float32))
+    pts = np.concatenate(clouds)
+    feats = np.concatenate([np.ones((len(pts), 1), np.float32), rng.random((len(pts), 4), dtype=np.float32)], 1)
+    return pts, feats, rng.integers(0, 13, len(pts)).astype(np.int64), np.array([n, n], np.int32)
+
+
+def kpconv_bench(dev, steps):
+    """C3: KPFCNN semantic segmentation training step on the GPU, reference
+    kpconv_s3dis.yml model (5 layers, K=15, dl0 0.04, first_features_dim 128,
+    BN in training mode, random init): GPU collate (segmentation_inputs:
+    neighbour searches + grid subsampling per layer) + forward + cross entropy
+    + backward + SGD step, ~40k stacked input points per step."""
+    from o3dml_amd.kpfcnn import KPFCNN, S3DIS, segmentation_inputs
+    torch.manual_seed(0)
+    np.random.seed(0)
+    model = KPFCNN(**S3DIS).to(dev).train()
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.98, weight_decay=0.001)
+    pts_np, feat_np, lab_np, lengths = make_c3(0)
+    pts = torch.from_numpy(pts_np).to(dev)
+    feat = torch.from_numpy(feat_np).to(dev)
+    lab = torch.from_numpy(lab_np).to(dev)
+
+    def step():
+        batch = segmentation_inputs(model.cfg, pts, feat, lab, lengths)
+        loss = model.get_loss(model(batch), batch.labels)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return batch
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    for _ in range(steps):
+        batch = step()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t) / steps
+    t = time.perf_counter()
+    for _ in range(steps):
+        segmentation_inputs(model.cfg, pts, feat, lab, lengths)
+    torch.cuda.synchronize(dev)
+    dt_collate = (time.perf_counter() - t) / steps
+    return {"ms_per_step": round(dt * 1e3, 2), "mpoints_per_s": round(len(pts_np) / dt / 1e6, 3),
+            "ms_collate": round(dt_collate * 1e3, 2), "layer_points": [int(p.shape[0]) for p in batch.points],
+            "neighbor_widths": [int(nb.shape[1]) for nb in batch.neighbors],
+            "config": "C3: 2 x 20,000-pt indoor spheres, KPFCNN kpconv_s3dis.yml, fp32, train step "
+                      "(GPU collate + fwd + CE + bwd + SGD)"}
 
 
 def make_room(seed=0):
@@ -325,6 +396,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline()
         if world == 1 and args.sparse_conv_reps > 0:
             out["sparse_conv"] = sparse_conv_bench(dev, args.sparse_conv_reps)
+        if world == 1 and args.kpconv_steps > 0:
+            out["kpconv"] = kpconv_bench(dev, args.kpconv_steps)
         if world == 1 and args.randla_frames > 0:
             out["randlanet"] = randla_frames(dev, args.randla_frames)
         print(json.dumps(out), flush=True)

@@ -251,6 +251,17 @@ int o3dml_kpconv_weighted_features_backward(const float* q_pts, int64_t n, const
                                             float extent, int influence, int closest, float* grad_features,
                                             void* stream);
 
+/* ---- KPFCNN pooling (kpconv.py:821-858 max_pool /
+ * closest_pool).  x f32 [n_support, c]; inds [n, ld] int32/int64 (index
+ * n_support = shadow row of zeros); the first nb columns are pooled
+ * (closest_pool: nb = 1) -> out f32 [n, c], argmax int32 [n, c] (nullable;
+ * winning support index, n_support = shadow).  Backward adds grad_out into
+ * grad_x [n_support, c] (must be zeroed) at argmax with fp32 atomics. */
+int o3dml_kpconv_pool_max(const float* x, int64_t n_support, int c, const void* inds, int index_bits, int64_t ld,
+                          int64_t n, int nb, float* out, int32_t* argmax, void* stream);
+int o3dml_kpconv_pool_max_backward(const float* grad_out, const int32_t* argmax, int64_t n, int c, int64_t n_support,
+                                   float* grad_x, void* stream);
+
 /* ---- RandLA-Net neighbour gathers (ml3d/torch/models/
  * randlanet.py).  Channels-last: coords f32 [N,3], neighbour indices int32
  * [N,K], per-pair tensors [N,K,C], per-point [N,C].

@@ -146,6 +146,51 @@ __global__ void __launch_bounds__(256) kpconv_wf_backward_kernel(const float* __
     }
 }
 
+
+// KPFCNN pooling (kpconv.py:821-858): out[q, c] = max over the first nb
+// columns j of row q of x_pad[inds[q, j], c], where x_pad is x with one zero
+// row appended (index n_support = shadow).  closest_pool is nb = 1 (column 0
+// only).  argmax[q, c] keeps the winning support index (n_support = the
+// shadow row) for the backward; the first maximum wins.  Lanes own channels,
+// so each gathered row is a coalesced read.
+template <class TI>
+__global__ void __launch_bounds__(256) pool_max_kernel(const float* __restrict__ x, int64_t n_support, int c,
+                                                       const TI* __restrict__ inds, int64_t ld, int64_t n, int nb,
+                                                       float* __restrict__ out, int32_t* __restrict__ argmax) {
+    const int64_t total = n * c;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t q = e / c;
+        const int ch = static_cast<int>(e - q * c);
+        const TI* row = inds + q * ld;
+        float best = -INFINITY;
+        int64_t arg = n_support;
+        for (int j = 0; j < nb; ++j) {
+            int64_t id = static_cast<int64_t>(row[j]);
+            if (id < 0 || id > n_support) id = n_support;
+            const float v = id < n_support ? x[id * c + ch] : 0.f;
+            if (v > best) {
+                best = v;
+                arg = id;
+            }
+        }
+        if (nb == 0) best = 0.f;
+        out[e] = best;
+        if (argmax) argmax[e] = static_cast<int32_t>(arg);
+    }
+}
+
+__global__ void __launch_bounds__(256) pool_max_backward_kernel(const float* __restrict__ g,
+                                                                const int32_t* __restrict__ argmax, int64_t n, int c,
+                                                                int64_t n_support, float* __restrict__ dx) {
+    const int64_t total = n * c;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t a = argmax[e];
+        if (a >= 0 && a < n_support) atomicAdd(dx + a * c + (e % c), g[e]);
+    }
+}
+
 template <bool BWD, class TI>
 static void launch_kp(int influence, int closest, unsigned g, hipStream_t st, const float* qp, const float* sp,
                       int64_t ns, const void* nbr, int64_t n, int nb, const float* in, int cin, const float* kp, int K,
@@ -211,5 +256,34 @@ O3DML_API int o3dml_kpconv_weighted_features_backward(const float* q_pts, int64_
     else
         launch_kp<true, int64_t>(influence, closest, g, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
                                  grad_wf, cin, kernel_points, K, kp_per_query, extent, nullptr, grad_features);
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_kpconv_pool_max(const float* x, int64_t n_support, int c, const void* inds, int index_bits,
+                                    int64_t ld, int64_t n, int nb, float* out, int32_t* argmax, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(c > 0, "pool: channels must be > 0");
+    O3DML_REQUIRE(nb >= 0 && nb <= ld, "pool: columns (%d) must be in [0, row stride %lld]", nb, (long long)ld);
+    O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
+    if (n == 0) return 0;
+    const unsigned g = stream_grid(n * c, 256, 256 * 16);
+    if (index_bits == 32)
+        pool_max_kernel<int32_t><<<g, 256, 0, as_stream(stream)>>>(x, n_support, c, static_cast<const int32_t*>(inds),
+                                                                   ld, n, nb, out, argmax);
+    else
+        pool_max_kernel<int64_t><<<g, 256, 0, as_stream(stream)>>>(x, n_support, c, static_cast<const int64_t*>(inds),
+                                                                   ld, n, nb, out, argmax);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_kpconv_pool_max_backward(const float* grad_out, const int32_t* argmax, int64_t n, int c,
+                                             int64_t n_support, float* grad_x, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(c > 0, "pool: channels must be > 0");
+    if (n == 0) return 0;
+    pool_max_backward_kernel<<<stream_grid(n * c, 256, 256 * 16), 256, 0, as_stream(stream)>>>(grad_out, argmax, n, c,
+                                                                                            n_support, grad_x);
+    O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }
