@@ -9,8 +9,11 @@ to first_features_dim 32) evaluated with deterministic parameters
 
 Stored (data only): the inputs, the random grid rotations the reference drew
 (seeded np.random), every layer's points / neighbours / pools / upsamples,
-the eval-mode logits, and for one training-mode forward + cross-entropy
-backward the loss and the gradients of a few parameters."""
+the kernel-point dispositions (the reference's own, from load_kernels —
+random fills would put every kernel point out of reach), the eval-mode
+logits, loss and the gradients of a few parameters under a cross-entropy
+loss, and the same in training mode (batch statistics).  Both are well
+conditioned: the reference in fp32 and fp64 agree to ~1e-6 relative."""
 import os
 import sys
 import types
@@ -98,19 +101,30 @@ def main():
 
     sd = model.state_dict()
     keys = list(sd.keys())
-    model.load_state_dict(randla_weights.state_dict_for([(k, tuple(v.shape)) for k, v in sd.items()], sd))
+    new = randla_weights.state_dict_for([(k, tuple(v.shape)) for k, v in sd.items()], sd)
+    for k in keys:
+        if k.endswith("kernel_points"):
+            new[k] = sd[k].clone()
+            out["kp:" + k] = sd[k].numpy().astype(np.float32)
+    model.load_state_dict(new)
     model.eval()
-    with torch.no_grad():
-        out["eval_logits"] = model(batch).numpy().astype(np.float32)
+    logits = model(batch)
+    out["eval_logits"] = logits.detach().numpy().astype(np.float32)
+    loss = torch.nn.functional.cross_entropy(logits, batch.labels)
+    loss.backward()
+    params = dict(model.named_parameters())
+    out["eval_loss"] = np.float32(loss.item())
+    for k in GRAD_KEYS:
+        out["grad_" + k] = params[k].grad.numpy().astype(np.float32)
+    model.zero_grad()
     model.train()
     logits = model(batch)
     loss = torch.nn.functional.cross_entropy(logits, batch.labels)
     loss.backward()
-    params = dict(model.named_parameters())
     out["train_logits"] = logits.detach().numpy().astype(np.float32)
     out["train_loss"] = np.float32(loss.item())
     for k in GRAD_KEYS:
-        out["grad_" + k] = params[k].grad.numpy().astype(np.float32)
+        out["tgrad_" + k] = params[k].grad.numpy().astype(np.float32)
     out["keys"] = np.array(keys)
     out["shapes"] = np.array([",".join(map(str, sd[k].shape)) for k in keys])
     print("layers", [len(li[l]) for l in range(L)], "nb widths", [li[L + l].shape[1] for l in range(L)],

@@ -5,12 +5,10 @@ randla_weights.fill, S3DIS configuration at first_features_dim 32).
 * segmentation_inputs on the GPU (with the rotations the reference drew):
   every layer's points bit-exact, neighbour / pool / upsample matrices
   bit-exact (same canonical neighbour order, same shadow padding and width);
-* eval logits on the reference batch within 1e-4 of the logit range;
-* training mode (batch statistics): logits within 1e-3 of the logit range,
-  cross-entropy loss within 1e-4 relative, parameter gradients within 2e-3
-  relative.  Batch-norm statistics over as few as 59 points (layer 4) amplify
-  the fp32 reduction-order differences between the reference's CPU BatchNorm
-  and the GPU one, and the backward gathers use fp32 atomics.
+* eval mode and training mode (batch statistics): logits within 1e-4 of the
+  logit range, cross-entropy loss within 1e-5 relative, parameter gradients
+  within 1e-4 of their range (the reference in fp32 and fp64 agree to ~1e-6,
+  so these bounds leave room only for fp32 reduction order and atomics).
 Also the HIP max_pool / closest_pool against a torch restatement of
 kpconv.py:821-858 with gradients."""
 import os
@@ -33,7 +31,11 @@ def _model(dev):
     from o3dml_amd.kpfcnn import KPFCNN
     m = KPFCNN(**CFG)
     sd = m.state_dict()
-    m.load_state_dict(randla_weights.state_dict_for([(k, tuple(v.shape)) for k, v in sd.items()], sd))
+    new = randla_weights.state_dict_for([(k, tuple(v.shape)) for k, v in sd.items()], sd)
+    for k in sd:
+        if k.endswith("kernel_points"):
+            new[k] = torch.from_numpy(G["kp:" + k])
+    m.load_state_dict(new)
     return m.to(dev)
 
 
@@ -69,26 +71,24 @@ def test_segmentation_inputs_match_reference(cuda):
             assert g.shape == ref.shape and np.array_equal(g, ref), f"{name} layer {l}"
 
 
-def test_eval_logits_match_reference(cuda):
-    m = _model(cuda).eval()
-    with torch.no_grad():
-        out = m(_ref_batch(cuda)).cpu().numpy()
-    assert out.shape == G["eval_logits"].shape
-    assert _rel(out, G["eval_logits"]) < 1e-4
-
-
-def test_train_step_matches_reference(cuda):
-    m = _model(cuda).train()
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_step_matches_reference(cuda, mode):
+    m = _model(cuda)
+    m.train(mode == "train")
     b = _ref_batch(cuda)
     logits = m(b)
     loss = torch.nn.functional.cross_entropy(logits, b.labels)
     loss.backward()
-    assert _rel(logits.detach().cpu().numpy(), G["train_logits"]) < 1e-3
-    assert abs(loss.item() - float(G["train_loss"])) < 1e-4 * abs(float(G["train_loss"]))
+    assert logits.shape == G[f"{mode}_logits"].shape
+    assert _rel(logits.detach().cpu().numpy(), G[f"{mode}_logits"]) < 1e-4
+    assert abs(loss.item() - float(G[f"{mode}_loss"])) < 1e-5 * abs(float(G[f"{mode}_loss"]))
     params = dict(m.named_parameters())
-    for k in [k[5:] for k in G.files if k.startswith("grad_")]:
-        err = _rel(params[k].grad.cpu().numpy(), G["grad_" + k])
-        assert err < 2e-3, (k, err)
+    pre = "grad_" if mode == "eval" else "tgrad_"
+    keys = [k[len(pre):] for k in G.files if k.startswith(pre)]
+    assert keys
+    for k in keys:
+        err = _rel(params[k].grad.cpu().numpy(), G[pre + k])
+        assert err < 1e-4, (k, err)
 
 
 @pytest.mark.parametrize("dtype", [torch.int32, torch.int64])
