@@ -112,8 +112,13 @@ __global__ void __launch_bounds__(256) kpconv_wf_kernel(const float* __restrict_
     }
 }
 
-// Backward of the aggregation for the features: dx[ids[j]][c] += sum_k w[j][k]
-// * dWF[q][k][c] (fp32 atomics; modulations folded into dWF by the caller).
+// Backward of the aggregation for the features: dx[ids[j]][c] += sum_k
+// w[j][k] * dWF[q][k][c] (fp32 atomics; modulations folded into dWF by the
+// caller).  Same shape as the forward: one wave per query, the influences of
+// 64 neighbours at a time computed lane-per-neighbour into LDS, then lanes own
+// channels with the query's K gradient rows held in registers (read once),
+// one atomic per (neighbour, channel).  Shadow neighbours are skipped
+// wave-uniformly.
 template <int INFL, bool CLOSEST, class TI>
 __global__ void __launch_bounds__(256) kpconv_wf_backward_kernel(const float* __restrict__ q_pts,
                                                                  const float* __restrict__ s_pts, int64_t n_support,
@@ -121,31 +126,54 @@ __global__ void __launch_bounds__(256) kpconv_wf_backward_kernel(const float* __
                                                                  const float* __restrict__ dwf, int cin,
                                                                  const float* __restrict__ kp, int K, int kp_per_query,
                                                                  float extent, float* __restrict__ dx) {
+    __shared__ float w_all[4][64][kKpMaxK + 1];
+    __shared__ int32_t id_all[4][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float(*w)[kKpMaxK + 1] = w_all[wv];
+    int32_t* ids = id_all[wv];
     const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
     for (int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + wv; q < n; q += nwaves) {
         const float qx = q_pts[3 * q], qy = q_pts[3 * q + 1], qz = q_pts[3 * q + 2];
         const float* kq = kp + (kp_per_query ? q * K * 3 : 0);
-        for (int j = 0; j < nb; ++j) {
-            const int64_t idx = static_cast<int64_t>(nbr[q * nb + j]);
-            if (idx < 0 || idx >= n_support) continue;
-            const float dxp = s_pts[3 * idx] - qx, dyp = s_pts[3 * idx + 1] - qy, dzp = s_pts[3 * idx + 2] - qz;
-            float wk[kKpMaxK];
+        for (int c0 = 0; c0 < cin; c0 += 64) {
+            const int c = c0 + lane;
+            float gk[kKpMaxK];
+            const float* g = dwf + q * static_cast<int64_t>(K) * cin + c;
 #pragma unroll
-            for (int k = 0; k < kKpMaxK; ++k) wk[k] = 0.f;
-            kp_influences<INFL, CLOSEST>(dxp, dyp, dzp, kq, K, extent, wk);
-            for (int c = lane; c < cin; c += 64) {
-                float s = 0.f;
-                const float* g = dwf + q * static_cast<int64_t>(K) * cin + c;
+            for (int k = 0; k < kKpMaxK; ++k) gk[k] = (k < K && c < cin) ? g[static_cast<int64_t>(k) * cin] : 0.f;
+            for (int j0 = 0; j0 < nb; j0 += 64) {
+                const int j = j0 + lane;
+                int64_t idx = -1;
+                if (j < nb) {
+                    const int64_t v = static_cast<int64_t>(nbr[q * nb + j]);
+                    if (v >= 0 && v < n_support) idx = v;
+                }
+                ids[lane] = static_cast<int32_t>(idx);
+                if (idx >= 0)
+                    kp_influences<INFL, CLOSEST>(s_pts[3 * idx] - qx, s_pts[3 * idx + 1] - qy, s_pts[3 * idx + 2] - qz,
+                                                 kq, K, extent, w[lane]);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int jn = nb - j0 < 64 ? nb - j0 : 64;
+                if (c < cin) {
+                    for (int jj = 0; jj < jn; ++jj) {
+                        const int32_t id = ids[jj];
+                        if (id < 0) continue;
+                        float sum = 0.f;
 #pragma unroll
-                for (int k = 0; k < kKpMaxK; ++k)
-                    if (k < K) s = __builtin_fmaf(wk[k], g[static_cast<int64_t>(k) * cin], s);
-                atomicAdd(dx + idx * cin + c, s);
+                        for (int k = 0; k < kKpMaxK; ++k)
+                            if (k < K) sum = __builtin_fmaf(w[jj][k], gk[k], sum);
+                        atomicAdd(dx + static_cast<int64_t>(id) * cin + c, sum);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
         }
     }
 }
-
 
 // KPFCNN pooling (kpconv.py:821-858): out[q, c] = max over the first nb
 // columns j of row q of x_pad[inds[q, j], c], where x_pad is x with one zero
