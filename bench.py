@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--kernel-reps", type=int, default=5)
     ap.add_argument("--randla-frames", type=int, default=3, help="RandLA-Net frames timed (0: skip)")
     ap.add_argument("--kpconv-steps", type=int, default=5, help="C3 KPFCNN training steps timed (0: skip)")
+    ap.add_argument("--pointpillars-steps", type=int, default=5,
+                    help="C5 PointPillars DDP training steps timed on every rank (0: skip)")
     ap.add_argument("--sparse-conv-reps", type=int, default=10, help="C4 sparse-conv forwards timed (0: skip)")
     return ap.parse_args()
 
@@ -227,6 +229,63 @@ def kpconv_bench(dev, steps):
                       "(GPU collate + fwd + CE + bwd + SGD)"}
 
 
+def make_kitti_scene(seed, n=20000, n_boxes=10):
+    """C5 KITTI-shaped scene: the 64-beam synthetic scan of
+    seed `seed` cropped to the camera field of view (|azimuth| < 45 deg) and
+    pointpillars_kitti.yml's range [0,69.12] x [-39.68,39.68] x [-3,1], at
+    most n points, intensity U[0,1); n_boxes ground-truth boxes (xyzwhlr,
+    KITTI class sizes) on the ground with labels 0..2."""
+    pts, _ = make_scan(seed)
+    keep = (pts[:, 0] > 0) & (np.abs(pts[:, 1]) < pts[:, 0]) & (pts[:, 0] < 69.12) & (np.abs(pts[:, 1]) < 39.68) \
+        & (pts[:, 2] > -3) & (pts[:, 2] < 1)
+    pts = pts[keep][:n]
+    rng = np.random.default_rng(seed + 7)
+    pts = np.concatenate([pts, rng.random((len(pts), 1), dtype=np.float32)], 1)
+    sizes = ((0.6, 0.8, 1.73), (0.6, 1.76, 1.73), (1.6, 3.9, 1.56))
+    labels = rng.integers(0, 3, n_boxes)
+    boxes = np.array([[rng.uniform(5, 60), rng.uniform(-25, 25), -1.73, sizes[c][0], sizes[c][2], sizes[c][1],
+                       rng.uniform(-np.pi, np.pi)] for c in labels], np.float32)
+    return pts.astype(np.float32), boxes, labels.astype(np.int64)
+
+
+def pointpillars_bench(dev, world, rank, steps, scenes_per_gpu=2):
+    """C5: PointPillars (pointpillars_kitti.yml: 3 classes, 432 x 496 pillars,
+    random init) training step data-parallel over all ranks: each rank holds
+    scenes_per_gpu KITTI-shaped scenes (16 scenes at 8 GPUs); batched GPU
+    voxelize + HIP pillar decoration/scatter + SECOND/FPN/head + get_loss +
+    backward with the DDP gradient all-reduce over RCCL (bucketed, overlapped
+    with backward) + AdamW step."""
+    import types
+    from o3dml_amd.pointpillars import PointPillars
+    torch.manual_seed(0)
+    model = PointPillars().to(dev).train()
+    ddp = model
+    if world > 1:
+        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
+    opt = torch.optim.AdamW(model.parameters(), lr=0.001, betas=(0.95, 0.99), weight_decay=0.01)
+    scenes = [make_kitti_scene(1000 + rank * scenes_per_gpu + i) for i in range(scenes_per_gpu)]
+    inp = types.SimpleNamespace(point=[torch.from_numpy(s[0]).to(dev) for s in scenes],
+                                bboxes=[torch.from_numpy(s[1]).to(dev) for s in scenes],
+                                labels=[torch.from_numpy(s[2]).to(dev) for s in scenes])
+
+    def step():
+        losses = model.get_loss(ddp(inp), inp)
+        loss = sum(losses.values())
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    elapsed, _ = timed_run(step, steps, 2, world, lambda: torch.cuda.synchronize(dev))
+    n_params = sum(p.numel() for p in model.parameters())
+    return {"scenes_per_s": round(world * scenes_per_gpu * steps / elapsed, 3),
+            "ms_per_step": round(elapsed / steps * 1e3, 2), "n_gpus": world, "scenes_per_gpu": scenes_per_gpu,
+            "global_batch": world * scenes_per_gpu, "points_per_scene": int(scenes[0][0].shape[0]),
+            "grad_allreduce_mb": round(n_params * 4 / 2**20, 2) if world > 1 else 0.0,
+            "config": "C5: PointPillars pointpillars_kitti.yml train step, KITTI-shaped synthetic scenes, fp32, "
+                      + (f"DDP over RCCL x{world}" if world > 1 else "1 GPU")}
+
+
 def make_room(seed=0):
     """C4-shaped voxel set: ~80k active 2 cm voxels on room surfaces
     (4 m x 3 m floor, 1.2 m walls, four boxes), half-integer positions in voxel
@@ -360,6 +419,7 @@ def main():
     elapsed, res = timed_run(step, args.steps, args.warmup, world, lambda: torch.cuda.synchronize(dev))
     pairs = int(res.neighbors_row_splits[-1].item())
 
+    pp = pointpillars_bench(dev, world, rank, args.pointpillars_steps) if args.pointpillars_steps > 0 else None
     out = None
     if rank == 0:
         queries_total = world * args.scenes * N_POINTS * args.steps
@@ -396,6 +456,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline()
         if world == 1 and args.sparse_conv_reps > 0:
             out["sparse_conv"] = sparse_conv_bench(dev, args.sparse_conv_reps)
+        if pp is not None:
+            out["pointpillars"] = pp
         if world == 1 and args.kpconv_steps > 0:
             out["kpconv"] = kpconv_bench(dev, args.kpconv_steps)
         if world == 1 and args.randla_frames > 0:

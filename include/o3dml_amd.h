@@ -262,6 +262,26 @@ int o3dml_kpconv_pool_max(const float* x, int64_t n_support, int c, const void* 
 int o3dml_kpconv_pool_max_backward(const float* grad_out, const int32_t* argmax, int64_t n, int c, int64_t n_support,
                                    float* grad_x, void* stream);
 
+/* ---- PointPillars pillars (point_pillars.py:352-380,
+ * 509-552, 567-601).
+ * pillar_features: points f32 [n_points, cdim] (x, y, z, features...), the
+ *   voxelize output (voxel_point_indices int64, voxel_point_row_splits int64
+ *   [V+1], voxel_coords int32 [V,3] in x,y,z order) -> out f32
+ *   [V, max_points, cdim + 5]: raw point, offset to the pillar mean (3),
+ *   offset to the pillar centre ix*vx + x_offset, iy*vy + y_offset (2);
+ *   padded slots zero.
+ * pillar_scatter: features f32 [V, C], coords int32 [V, 4] (batch, z, y, x)
+ *   -> canvas f32 [B, C, ny, nx] (zeroed by the caller) at [b, :, y, x].
+ * pillar_gather: the adjoint (canvas -> features). */
+int o3dml_pillar_features(const float* points, int64_t n_points, int cdim, const int64_t* voxel_point_indices,
+                          const int64_t* voxel_point_row_splits, const int32_t* voxel_coords_xyz, int64_t n_voxels,
+                          int max_points, float vx, float vy, float x_offset, float y_offset, float* out,
+                          void* stream);
+int o3dml_pillar_scatter(const float* features, const int32_t* coords_bzyx, int64_t n_voxels, int channels, int ny,
+                         int nx, float* canvas, void* stream);
+int o3dml_pillar_gather(const float* canvas, const int32_t* coords_bzyx, int64_t n_voxels, int channels, int ny,
+                        int nx, float* features, void* stream);
+
 /* ---- RandLA-Net neighbour gathers (ml3d/torch/models/
  * randlanet.py).  Channels-last: coords f32 [N,3], neighbour indices int32
  * [N,K], per-pair tensors [N,K,C], per-point [N,C].

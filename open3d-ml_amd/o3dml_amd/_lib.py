@@ -62,6 +62,10 @@ SIGNATURES = {
                                                         c_i32, c_i32, c_f32, c_i32, c_i32, c_p, c_p]),
     "o3dml_kpconv_pool_max": (c_i32, [c_p, c_i64, c_i32, c_p, c_i32, c_i64, c_i64, c_i32, c_p, c_p, c_p]),
     "o3dml_kpconv_pool_max_backward": (c_i32, [c_p, c_p, c_i64, c_i32, c_i64, c_p, c_p]),
+    "o3dml_pillar_features": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32,
+                                      c_p, c_p]),
+    "o3dml_pillar_scatter": (c_i32, [c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p]),
+    "o3dml_pillar_gather": (c_i32, [c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p]),
     "o3dml_randla_relative_encoding": (c_i32, [c_p, c_i64, c_p, c_i32, c_p, c_p]),
     "o3dml_randla_attentive_pool": (c_i32, [c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p]),
     "o3dml_randla_gather_max": (c_i32, [c_p, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
