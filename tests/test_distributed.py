@@ -73,3 +73,65 @@ def test_make_batch_is_rank_seeded():
     ref = np.random.default_rng(100003).random((bench.N_POINTS, 3), dtype=np.float32)
     assert torch.equal(b, torch.from_numpy(ref))
     assert a.shape == (2 * bench.N_POINTS, 3) and rs.tolist() == [0, bench.N_POINTS, 2 * bench.N_POINTS]
+
+
+def _ddp_worker(rank, world, port, q):
+    """PointPillars' dense part (SECOND + FPN + anchor head + get_loss) under
+    DistributedDataParallel on gloo: after one backward every rank holds the
+    average of the per-rank gradients (bench.py pointpillars_bench's C5 path;
+    the pillar ops themselves need the GPU)."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "open3d-ml_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import types
+
+    from make_golden_pointpillars import CFG
+    from o3dml_amd.pointpillars import PointPillars
+
+    class Dense(torch.nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.backbone, self.neck, self.bbox_head = m.backbone, m.neck, m.bbox_head
+
+        def forward(self, canvas):
+            return self.bbox_head(self.neck(self.backbone(canvas)))
+
+    def batch(r):
+        g = torch.Generator().manual_seed(r)
+        canvas = torch.relu(torch.randn((1, 64, 64, 64), generator=g))
+        boxes = torch.tensor([[3.0 + r, 0.5, -1.7, 1.6, 1.56, 3.9, 0.3], [6.0, -2.0 + r, -0.6, 0.6, 1.73, 0.8, 1.2]])
+        return canvas, types.SimpleNamespace(bboxes=[boxes], labels=[torch.tensor([2, 0])])
+
+    grads = []
+    for r in range(world):  # single-process reference gradients of every rank's batch
+        torch.manual_seed(0)
+        m = PointPillars(**CFG).eval()
+        canvas, inp = batch(r)
+        sum(m.get_loss(Dense(m)(canvas), inp).values()).backward()
+        grads.append(torch.cat([p.grad.reshape(-1) for p in Dense(m).parameters()]))
+    torch.manual_seed(0)
+    m = PointPillars(**CFG).eval()
+    ddp = torch.nn.parallel.DistributedDataParallel(Dense(m))
+    canvas, inp = batch(rank)
+    sum(m.get_loss(ddp(canvas), inp).values()).backward()
+    g = torch.cat([p.grad.reshape(-1) for p in ddp.module.parameters()])
+    q.put((rank, float((g - sum(grads) / world).abs().max() / (g.abs().max() + 1e-30))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_pointpillars_ddp_gradients():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, err in out:
+        assert err < 1e-5
