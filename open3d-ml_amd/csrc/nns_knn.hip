@@ -141,13 +141,196 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// k <= 16: G = 8 lanes per query (8 queries per wave).  A lane-per-query walk
+// leaves the chip nearly idle on the sizes RandLA-Net searches (60 k queries
+// = < 1 wave per SIMD, each lane a chain of dependent loads); here the group
+// walks the same rings together, lanes taking every G-th point of each cell
+// into their own sorted top-K.  After each ring the group merges its lists
+// with a butterfly (xor 1, 2, 4): per round a lane takes the K smallest of its
+// list and its partner's as min(a[i], b[K-1-i]) — a bitonic sequence — and
+// sorts it with a register bitonic network; after the last round every lane
+// holds the group's exact top-K, whose k-th entry both prunes the next ring
+// and decides termination.  Lane 0 keeps the merged list, the others restart
+// empty, so no entry is counted twice.  Order: (distance, index) ascending.
+// ---------------------------------------------------------------------------
+constexpr int kKnnG = 8;
+
+template <int K>
+__device__ __forceinline__ void cas_lex(float (&d)[K], uint32_t (&id)[K], int i, int j) {
+    if (lex_less(d[j], id[j], d[i], id[i])) {
+        const float td = d[i];
+        const uint32_t ti = id[i];
+        d[i] = d[j];
+        id[i] = id[j];
+        d[j] = td;
+        id[j] = ti;
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void group_merge(float (&d)[K], uint32_t (&id)[K]) {
+#pragma unroll
+    for (int mask = 1; mask < kKnnG; mask <<= 1) {
+        float od[K];
+        uint32_t oi[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            od[i] = __shfl_xor(d[i], mask, 64);
+            oi[i] = __shfl_xor(id[i], mask, 64);
+        }
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            if (lex_less(od[K - 1 - i], oi[K - 1 - i], d[i], id[i])) {
+                d[i] = od[K - 1 - i];
+                id[i] = oi[K - 1 - i];
+            }
+        }
+#pragma unroll
+        for (int st = K / 2; st >= 1; st >>= 1) {
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                if ((i & st) == 0) cas_lex<K>(d, id, i, i + st);
+        }
+    }
+}
+
+template <int K, int METRIC, bool IGNORE>
+__global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict__ sorted,
+                                                        const uint32_t* __restrict__ splits,
+                                                        const GridBatch* __restrict__ grids,
+                                                        const float* __restrict__ queries, int64_t m,
+                                                        const uint32_t* __restrict__ qorder,
+                                                        const int64_t* __restrict__ qrs, int nb, int k,
+                                                        int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
+                                                        int64_t* __restrict__ counts) {
+    const int gl = threadIdx.x & (kKnnG - 1);
+    const int64_t groups = static_cast<int64_t>(gridDim.x) * (blockDim.x / kKnnG);
+    for (int64_t t = (blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x) / kKnnG; t < m + 0;
+         t += groups) {
+        const int64_t q = qorder ? static_cast<int64_t>(qorder[t]) : t;
+        const GridBatch g = grids[batch_of(q, qrs, nb)];
+        const float qx = queries[3 * q], qy = queries[3 * q + 1], qz = queries[3 * q + 2];
+        const int cx = grid_axis(qx, g.ox, g.inv_h, g.dx);
+        const int cy = grid_axis(qy, g.oy, g.inv_h, g.dy);
+        const int cz = grid_axis(qz, g.oz, g.inv_h, g.dz);
+        float bd[K];
+        uint32_t bi[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            bd[j] = INFINITY;
+            bi[j] = 0xffffffffu;
+        }
+        float kd = INFINITY;  // group k-th best after the last merge (pruning bound)
+        uint32_t ki = 0xffffffffu;
+        bool full = false;
+        auto consider = [&](const float4& p) {
+            if (IGNORE && p.x == qx && p.y == qy && p.z == qz) return;
+            const float d = dist_metric<METRIC>(p.x, p.y, p.z, qx, qy, qz);
+            const uint32_t id = __float_as_uint(p.w);
+            if (!lex_less(d, id, kd, ki) || !lex_less(d, id, bd[K - 1], bi[K - 1])) return;
+#pragma unroll
+            for (int r = K - 1; r >= 0; --r) {
+                const bool lt_prev = r > 0 && lex_less(d, id, bd[r > 0 ? r - 1 : 0], bi[r > 0 ? r - 1 : 0]);
+                const bool lt_cur = lex_less(d, id, bd[r], bi[r]);
+                if (lt_prev) {
+                    bd[r] = bd[r - 1];
+                    bi[r] = bi[r - 1];
+                } else if (lt_cur) {
+                    bd[r] = d;
+                    bi[r] = id;
+                }
+            }
+        };
+        auto visit = [&](int x, int y, int z) {
+            const uint32_t c = g.offset + static_cast<uint32_t>(x + g.dx * (y + g.dy * z));
+            const uint32_t s = splits[c], e = splits[c + 1];
+            uint32_t j = s + gl;
+            for (; j + kKnnG < e; j += 2 * kKnnG) {  // two loads in flight per lane
+                const float4 p0 = sorted[j], p1 = sorted[j + kKnnG];
+                consider(p0);
+                consider(p1);
+            }
+            if (j < e) consider(sorted[j]);
+        };
+        for (int R = 0;; ++R) {
+            const int x0 = cx - R, x1 = cx + R, y0 = cy - R, y1 = cy + R, z0 = cz - R, z1 = cz + R;
+            const int za = max(z0, 0), zb = min(z1, g.dz - 1);
+            const int ya = max(y0, 0), yb = min(y1, g.dy - 1);
+            const int xa = max(x0, 0), xb = min(x1, g.dx - 1);
+            for (int z = za; z <= zb; ++z) {
+                for (int y = ya; y <= yb; ++y) {
+                    if (z == z0 || z == z1 || y == y0 || y == y1) {
+                        for (int x = xa; x <= xb; ++x) visit(x, y, z);
+                    } else {
+                        if (x0 >= 0) visit(x0, y, z);
+                        if (x1 < g.dx) visit(x1, y, z);
+                    }
+                }
+            }
+            group_merge<K>(bd, bi);
+#pragma unroll
+            for (int r = 0; r < K; ++r)
+                if (r == k - 1) {
+                    kd = bd[r];
+                    ki = bi[r];
+                }
+            full = ki != 0xffffffffu;
+            const bool lo_x = x0 <= 0, hi_x = x1 >= g.dx - 1, lo_y = y0 <= 0, hi_y = y1 >= g.dy - 1;
+            const bool lo_z = z0 <= 0, hi_z = z1 >= g.dz - 1;
+            if (lo_x && hi_x && lo_y && hi_y && lo_z && hi_z) break;  // every cell visited
+            if (full) {
+                float lb = INFINITY;
+                if (!lo_x) lb = fminf(lb, qx - (g.ox + static_cast<float>(x0) * g.h));
+                if (!hi_x) lb = fminf(lb, (g.ox + static_cast<float>(x1 + 1) * g.h) - qx);
+                if (!lo_y) lb = fminf(lb, qy - (g.oy + static_cast<float>(y0) * g.h));
+                if (!hi_y) lb = fminf(lb, (g.oy + static_cast<float>(y1 + 1) * g.h) - qy);
+                if (!lo_z) lb = fminf(lb, qz - (g.oz + static_cast<float>(z0) * g.h));
+                if (!hi_z) lb = fminf(lb, (g.oz + static_cast<float>(z1 + 1) * g.h) - qz);
+                lb = lb - 1e-3f * g.h - 1e-6f * (fabsf(qx) + fabsf(qy) + fabsf(qz));
+                if (lb > 0.f) {
+                    const float bound = METRIC == kL2 ? lb * lb : lb;
+                    if (kd < bound) break;
+                }
+            }
+            if (gl != 0) {  // lane 0 carries the merged list into the next ring
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    bd[j] = INFINITY;
+                    bi[j] = 0xffffffffu;
+                }
+            }
+        }
+        int c = 0;
+#pragma unroll
+        for (int r = 0; r < K; ++r) c += (r < k && bi[r] != 0xffffffffu) ? 1 : 0;
+        if (gl == 0) counts[q] = c;
+        int32_t* oi = out_idx + q * static_cast<int64_t>(k);
+        float* od = out_dist + q * static_cast<int64_t>(k);
+#pragma unroll
+        for (int r = 0; r < K; ++r) {
+            if (r < c && (r & (kKnnG - 1)) == gl) {
+                oi[r] = static_cast<int32_t>(bi[r]);
+                od[r] = bd[r];
+            }
+        }
+    }
+}
+
 template <int K>
 static void launch_knn_k(int metric, bool ignore, unsigned grid, hipStream_t st, const GridIndex& gi, const float* q,
                          int64_t m, const uint32_t* qorder, const int64_t* qrs, int nb, int k, int32_t* oi, float* od,
                          int64_t* counts) {
 #define O3DML_KNN(M, I)                                                                                          \
-    knn_grid_kernel<K, M, I><<<grid, 256, 0, st>>>(gi.sorted, gi.splits, gi.params, q, m, qorder, qrs, nb, k, oi, od, \
-                                                   counts)
+    do {                                                                                                         \
+        if constexpr (K <= 16)                                                                                   \
+            knn_group_kernel<K, M, I><<<stream_grid(m * kKnnG, 256, 1 << 20), 256, 0, st>>>(                      \
+                    gi.sorted, gi.splits, gi.params, q, m, qorder, qrs, nb, k, oi, od, counts);                  \
+        else                                                                                                     \
+            knn_grid_kernel<K, M, I><<<grid, 256, 0, st>>>(gi.sorted, gi.splits, gi.params, q, m, qorder, qrs, nb, \
+                                                           k, oi, od, counts);                                   \
+    } while (0)
     if (metric == kL2) {
         if (ignore) O3DML_KNN(kL2, true); else O3DML_KNN(kL2, false);
     } else if (metric == kL1) {

@@ -46,6 +46,29 @@ def test_knn_metrics_ignore_batched(cuda, metric):
     assert np.array_equal(r.neighbors_distance.cpu().numpy(), od)
 
 
+@pytest.mark.parametrize("k", [1, 16])
+def test_knn_lidar_like_batched(cuda, k):
+    """Surface data with a strongly varying density (a 64-beam scan: dense
+    near the sensor, sparse far away) and RandLA-style nested levels batched
+    in one call; bit-exact vs the oracle."""
+    import bench
+    pts, _ = bench.make_scan(3)
+    lv = [pts[:20000], pts[:5000], pts[:1250]]
+    cat = np.concatenate(lv)
+    rs = np.array([0, 20000, 25000, 26250], np.int64)
+    t = torch.from_numpy(cat).to(cuda)
+    r = ops_knn(t, t, k, rs)
+    oi, ors, od = O.knn_search(cat, cat, k, rs, rs, return_distances=True)
+    assert np.array_equal(r.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(r.neighbors_index.cpu().numpy(), oi)
+    assert np.array_equal(r.neighbors_distance.cpu().numpy(), od)
+
+
+def ops_knn(p, q, k, rs):
+    from o3dml_amd import ops
+    return ops.knn_search(p, q, k, torch.from_numpy(rs), torch.from_numpy(rs), return_distances=True)
+
+
 def test_knn_small_batches_and_duplicates(cuda):
     from o3dml_amd import ops
     pts = np.repeat(_cloud(50, 3), 4, axis=0)  # exact duplicates -> ties broken by index
