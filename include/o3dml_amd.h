@@ -295,6 +295,10 @@ int o3dml_randla_relative_encoding(const float* coords, int64_t n, const int32_t
                                    void* stream);
 int o3dml_randla_attentive_pool(const float* x, const float* logits, int64_t n, int k, int c, float* out,
                                 void* stream);
+/* concat_rows: out[r] = [a[ia[r]] (da floats), b[ib[r]] (db floats)] for r <
+ * rows; ia / ib nullable (identity), int32 or int64 per *_bits. */
+int o3dml_concat_rows(const float* a, int da, const void* ia, int ia_bits, const float* b, int db, const void* ib,
+                      int ib_bits, int64_t rows, float* out, void* stream);
 int o3dml_randla_gather_max(const float* feat, int c, const int32_t* idx, int64_t m, int k, float* out,
                             void* stream);
 

@@ -75,6 +75,34 @@ __global__ void gather_max_kernel(const float* __restrict__ feat, int c, const i
     }
 }
 
+
+// Row concatenation with optional gathers: out[r] = [A[ia[r]] (da), B[ib[r]] (db)]
+// (identity when an index array is null).  Replaces the gather + torch.cat
+// pairs of LocalSpatialEncoding (neighbour features | relative features,
+// randlanet.py:598-606) and of the decoder (skip features | 1-NN
+// interpolation, randlanet.py:285-289): one write of the concatenated rows.
+template <class TA, class TB>
+__global__ void concat_rows_kernel(const float* __restrict__ A, int da, const TA* __restrict__ ia,
+                                   const float* __restrict__ B, int db, const TB* __restrict__ ib, int64_t rows,
+                                   float* __restrict__ out) {
+    const int w = da + db;
+    const int64_t total = rows * w;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t r = e / w;
+        const int c = static_cast<int>(e - r * w);
+        float v;
+        if (c < da) {
+            const int64_t src = ia ? static_cast<int64_t>(ia[r]) : r;
+            v = A[src * da + c];
+        } else {
+            const int64_t src = ib ? static_cast<int64_t>(ib[r]) : r;
+            v = B[src * db + (c - da)];
+        }
+        out[e] = v;
+    }
+}
+
 }  // namespace o3dml
 
 using namespace o3dml;
@@ -105,6 +133,27 @@ O3DML_API int o3dml_randla_gather_max(const float* feat, int c, const int32_t* i
     O3DML_REQUIRE(k > 0 && c > 0, "k and c must be > 0");
     if (m == 0) return 0;
     gather_max_kernel<<<stream_grid(m * c, 256), 256, 0, as_stream(stream)>>>(feat, c, idx, m, k, out);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_concat_rows(const float* a, int da, const void* ia, int ia_bits, const float* b, int db,
+                                const void* ib, int ib_bits, int64_t rows, float* out, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(da >= 0 && db >= 0 && da + db > 0, "concat_rows: widths must be >= 0 and not both 0");
+    O3DML_REQUIRE((ia_bits == 32 || ia_bits == 64) && (ib_bits == 32 || ib_bits == 64), "index_bits must be 32 or 64");
+    if (rows == 0) return 0;
+    const unsigned g = stream_grid(rows * (da + db), 256, 256 * 16);
+    hipStream_t st = as_stream(stream);
+#define O3DML_CAT(TA, TB)                                                                                  \
+    concat_rows_kernel<TA, TB><<<g, 256, 0, st>>>(a, da, static_cast<const TA*>(ia), b, db,                 \
+                                                  static_cast<const TB*>(ib), rows, out)
+    if (ia_bits == 32) {
+        if (ib_bits == 32) O3DML_CAT(int32_t, int32_t); else O3DML_CAT(int32_t, int64_t);
+    } else {
+        if (ib_bits == 32) O3DML_CAT(int64_t, int32_t); else O3DML_CAT(int64_t, int64_t);
+    }
+#undef O3DML_CAT
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }

@@ -58,6 +58,18 @@ def gather_max(feat, idx):
     return out
 
 
+def concat_rows(a, ia, b, ib):
+    """[a[ia] | b[ib]] row-wise (ia / ib None = identity), channels-last:
+    a [Na, da], b [Nb, db] -> [rows, da + db]; rows = len(ia) or len(a)."""
+    rows = ia.numel() if ia is not None else a.shape[0]
+    da, db = a.shape[-1], b.shape[-1]
+    out = torch.empty((rows, da + db), dtype=torch.float32, device=a.device)
+    _lib.call("o3dml_concat_rows", ptr(a), da, ptr(ia), 64 if ia is not None and ia.dtype == torch.int64 else 32,
+              ptr(b), db, ptr(ib), 64 if ib is not None and ib.dtype == torch.int64 else 32, rows, ptr(out),
+              stream_handle(a.device))
+    return out
+
+
 def _fused():
     return not torch.is_grad_enabled()
 
@@ -137,6 +149,9 @@ class LocalSpatialEncoding(nn.Module):
         elif relative_features is None:
             raise ValueError("LocalSpatialEncoding: Require relative_features for second pass.")
         relative_features = self.mlp(relative_features)
+        if _fused():
+            cat = concat_rows(features.contiguous(), nbr.reshape(-1), relative_features.contiguous(), None)
+            return cat.view(n, k, -1), relative_features
         neighbor_features = features[nbr.long()]
         return torch.cat([neighbor_features, relative_features], -1), relative_features
 
@@ -255,8 +270,10 @@ class RandLANet(nn.Module):
             x = ys
         x = self.mlp(x)
         for i, layer in enumerate(self.decoder):
-            interp = x[ups[-i - 1]]
-            x = layer(torch.cat([enc[-i - 2], interp], -1))
+            if _fused():
+                x = layer(concat_rows(enc[-i - 2].contiguous(), None, x.contiguous(), ups[-i - 1]))
+            else:
+                x = layer(torch.cat([enc[-i - 2], x[ups[-i - 1]]], -1))
         for m in self.fc1:
             x = m(x)
         return x

@@ -35,6 +35,10 @@ def test_kernels_vs_torch(cuda):
     feat = torch.randn((500, 40), generator=g).to(cuda)
     idx = torch.randint(0, 500, (120, 16), generator=g, dtype=torch.int32).to(cuda)
     torch.testing.assert_close(R.gather_max(feat, idx), feat[idx.long()].max(1).values)
+    b = torch.randn((120 * 16, 7), generator=g).to(cuda)
+    assert torch.equal(R.concat_rows(feat, idx.reshape(-1), b, None), torch.cat([feat[idx.reshape(-1).long()], b], 1))
+    up = torch.randint(0, 120 * 16, (500,), generator=g).to(cuda)
+    assert torch.equal(R.concat_rows(feat, None, b, up), torch.cat([feat, b[up]], 1))
 
 
 def test_inference_pipeline_covers_cloud(cuda):
