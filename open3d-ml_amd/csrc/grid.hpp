@@ -27,10 +27,34 @@ struct GridBatch {
 // Kernels defined in this header get internal linkage (one copy per TU).
 namespace {
 
+// Per-batch bounding boxes [B][6] (min xyz, max xyz).  gridDim = (kBBoxParts,
+// B): block (p, b) reduces a 1/kBBoxParts slice of batch item b and folds it
+// into the item's box with integer atomics on an order-preserving encoding of
+// the floats (so one launch fills the chip even for a single large cloud);
+// bbox_init / bbox_decode bracket it.  Use launch_bbox().
+constexpr int kBBoxParts = 64;
+
+__device__ __forceinline__ uint32_t f2ord(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+__global__ void bbox_init_kernel(uint32_t* __restrict__ out, int nb) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 6 * nb) out[i] = (i % 6) < 3 ? f2ord(INFINITY) : f2ord(-INFINITY);
+}
+
 __global__ void __launch_bounds__(256) bbox_kernel(const float* __restrict__ pts, const int64_t* __restrict__ rs,
-                                                   float* __restrict__ out /*[B][6]*/) {
-    const int b = blockIdx.x;
-    const int64_t s = rs[b], e = rs[b + 1];
+                                                   uint32_t* __restrict__ out /*[B][6] encoded*/) {
+    const int b = blockIdx.y;
+    const int64_t s0 = rs[b], n = rs[b + 1] - s0;
+    const int64_t chunk = (n + kBBoxParts - 1) / kBBoxParts;
+    const int64_t hi = (blockIdx.x + 1) * chunk;
+    const int64_t s = s0 + blockIdx.x * chunk, e = s0 + (hi < n ? hi : n);
+    if (s >= e) return;
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
 #pragma unroll
@@ -40,7 +64,6 @@ __global__ void __launch_bounds__(256) bbox_kernel(const float* __restrict__ pts
             mx[d] = fmaxf(mx[d], v);
         }
     }
-    __shared__ float red[6][4];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
 #pragma unroll
@@ -52,17 +75,26 @@ __global__ void __launch_bounds__(256) bbox_kernel(const float* __restrict__ pts
     if (lane_id() == 0) {
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            red[d][wave_id()] = mn[d];
-            red[3 + d][wave_id()] = mx[d];
+            if (mn[d] <= mx[d]) {  // this wave saw points
+                atomicMin(out + 6 * b + d, f2ord(mn[d]));
+                atomicMax(out + 6 * b + 3 + d, f2ord(mx[d]));
+            }
         }
     }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        const int d = threadIdx.x;
-        float v = red[d][0];
-        for (int w = 1; w < (int)(blockDim.x / 64); ++w) v = d < 3 ? fminf(v, red[d][w]) : fmaxf(v, red[d][w]);
-        out[6 * b + d] = v;
-    }
+}
+
+__global__ void bbox_decode_kernel(uint32_t* __restrict__ io, int nb) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 6 * nb) reinterpret_cast<float*>(io)[i] = ord2f(io[i]);
+}
+
+// bbox[6 * nb] floats (empty items: +inf / -inf) of the points of each batch item.
+inline void launch_bbox(const float* pts, const int64_t* rs_dev, int nb, float* bbox, hipStream_t st) {
+    uint32_t* enc = reinterpret_cast<uint32_t*>(bbox);
+    const unsigned g6 = static_cast<unsigned>((6 * nb + 255) / 256);
+    bbox_init_kernel<<<g6, 256, 0, st>>>(enc, nb);
+    bbox_kernel<<<dim3(kBBoxParts, static_cast<unsigned>(nb)), 256, 0, st>>>(pts, rs_dev, enc);
+    bbox_decode_kernel<<<g6, 256, 0, st>>>(enc, nb);
 }
 
 __device__ __forceinline__ int grid_axis(float p, float o, float inv_h, int n) {
@@ -183,7 +215,7 @@ inline GridIndex build_grid(const float* pts, int64_t n, const int64_t* rs_dev, 
     uint32_t* keys = ws.take<uint32_t>(n);
     uint32_t* skeys = ws.take<uint32_t>(n);
     gi.order = ws.take<uint32_t>(n);
-    bbox_kernel<<<nb, 256, 0, st>>>(pts, rs_dev, bbox_d);
+    launch_bbox(pts, rs_dev, nb, bbox_d, st);
     O3DML_LAUNCH_CHECK();
     std::vector<float> bbox(6 * nb);
     O3DML_CHECK_HIP(hipMemcpyAsync(bbox.data(), bbox_d, sizeof(float) * 6 * nb, hipMemcpyDeviceToHost, st));

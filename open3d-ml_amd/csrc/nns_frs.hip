@@ -1284,7 +1284,7 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
         return 0;
     }
     // ---- plan: bounding boxes -> dense grid / hashed fine grid / segments
-    bbox_kernel<<<static_cast<unsigned>(n_batch), 256, 0, st>>>(points, points_row_splits, fp.bbox);
+    launch_bbox(points, points_row_splits, static_cast<int>(n_batch), fp.bbox, st);
     O3DML_LAUNCH_CHECK();
     std::vector<float> bb(6 * n_batch);
     O3DML_CHECK_HIP(hipMemcpyAsync(bb.data(), fp.bbox, sizeof(float) * 6 * n_batch, hipMemcpyDeviceToHost, st));

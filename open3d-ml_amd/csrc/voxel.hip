@@ -420,7 +420,7 @@ O3DML_API int o3dml_grid_subsample_count(const float* points, int64_t n_points, 
     float* bbox_d = ws.take<float>(6 * nb);
     std::vector<SubBatch> sb(nb);
     if (n_points > 0) {
-        bbox_kernel<<<nb, 256, 0, st>>>(points, row_splits, bbox_d);
+        launch_bbox(points, row_splits, nb, bbox_d, st);
         O3DML_LAUNCH_CHECK();
         std::vector<float> bb(6 * nb);
         O3DML_CHECK_HIP(hipMemcpyAsync(bb.data(), bbox_d, sizeof(float) * 6 * nb, hipMemcpyDeviceToHost, st));
