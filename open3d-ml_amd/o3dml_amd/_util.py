@@ -32,11 +32,17 @@ def ptr(t):
 
 
 def to_dev(t, device, dtype=None):
-    """Contiguous copy (or view) of t on device with dtype."""
+    """Contiguous copy (or view) of t on device with dtype.  Host data goes
+    through a pinned staging copy and a non-blocking transfer on the current
+    stream (torch's caching host allocator keeps the staging buffer alive until
+    the copy has run), so row splits and other small host arrays do not
+    synchronise the stream with the host."""
     if not isinstance(t, torch.Tensor):
         t = torch.as_tensor(np.asarray(t))
     if dtype is not None and t.dtype != dtype:
         t = t.to(dtype)
+    if t.device.type == "cpu" and torch.device(device).type == "cuda":
+        return t.contiguous().pin_memory().to(device, non_blocking=True)
     return t.to(device, non_blocking=False).contiguous()
 
 

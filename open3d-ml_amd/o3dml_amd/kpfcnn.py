@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib, ops
-from ._util import index_bits, ptr, stream_handle
+from ._util import index_bits, ptr, stream_handle, to_dev
 from .kpconv import KPConv
 from .layers import FixedRadiusSearch
 
@@ -400,7 +400,7 @@ def random_rotations(B, rng=np.random):
 def _rotate(points, splits, R, transpose=False):
     """p' = p @ R[b] per batch element in fp32 with the reference's rounding
     ((p0 R0j + p1 R1j) + p2 R2j, each product rounded; kpconv.py:2087-2090)."""
-    Rt = torch.from_numpy(np.ascontiguousarray(R.transpose(0, 2, 1) if transpose else R)).to(points.device)
+    Rt = to_dev(np.ascontiguousarray(R.transpose(0, 2, 1) if transpose else R), points.device)
     b = torch.repeat_interleave(torch.arange(len(splits) - 1, device=points.device),
                                 torch.as_tensor(np.diff(splits), device=points.device))
     Rb = Rt[b]  # [N, 3, 3]

@@ -50,8 +50,8 @@ def build_spatial_hash_table(points, radius, points_row_splits=None, hash_table_
     T = lib.o3dml_hash_table_splits(B, prs.ctypes.data, float(hash_table_size_factor),
                                     int(max_hash_table_size), splits.ctypes.data)
     pts = to_dev(points, dev)
-    prs_d = torch.from_numpy(prs).to(dev)
-    hts_d = torch.from_numpy(splits.view(np.int32)).to(dev)
+    prs_d = to_dev(prs, dev)
+    hts_d = to_dev(splits.view(np.int32), dev)
     index = torch.empty(n, dtype=torch.int32, device=dev)
     cells = torch.empty(T + 1, dtype=torch.int32, device=dev)
     ws = workspace(lib.o3dml_build_spatial_hash_table_workspace_size(n, T), dev)
@@ -97,8 +97,8 @@ def fixed_radius_search(points, queries, radius, points_row_splits=None, queries
     same = _same_cloud(points, queries, prs, qrs)
     pts = to_dev(points, dev)
     qry = pts if same else to_dev(queries, dev)
-    prs_d = torch.from_numpy(prs).to(dev)
-    qrs_d = prs_d if same else torch.from_numpy(qrs).to(dev)
+    prs_d = to_dev(prs, dev)
+    qrs_d = prs_d if same else to_dev(qrs, dev)
     hts_d = to_dev(hash_table_splits, dev, torch.int32)
     hti_d = to_dev(hash_table_index, dev, torch.int32)
     hcs_d = to_dev(hash_table_cell_splits, dev, torch.int32)
@@ -144,8 +144,8 @@ def knn_search(points, queries, k, points_row_splits=None, queries_row_splits=No
     same = _same_cloud(points, queries, prs, qrs)
     pts = to_dev(points, dev)
     qry = pts if same else to_dev(queries, dev)
-    prs_d = torch.from_numpy(prs).to(dev)
-    qrs_d = prs_d if same else torch.from_numpy(qrs).to(dev)
+    prs_d = to_dev(prs, dev)
+    qrs_d = prs_d if same else to_dev(qrs, dev)
     B = len(prs) - 1
     st = stream_handle(dev)
     rs = torch.empty(m + 1, dtype=torch.int64, device=dev)
@@ -231,7 +231,7 @@ def voxelize(points, row_splits, voxel_size, points_range_min, points_range_max,
     mn = _host_f32(points_range_min, ndim, "points_range_min")
     mx = _host_f32(points_range_max, ndim, "points_range_max")
     pts = to_dev(points, dev)
-    rs_d = torch.from_numpy(rs).to(dev)
+    rs_d = to_dev(rs, dev)
     st = stream_handle(dev)
     ws = workspace(lib.o3dml_voxelize_workspace_size(n, B), dev)
     counts = np.zeros(2, np.int64)
@@ -283,7 +283,7 @@ def grid_subsample(points, lengths, sampleDl, features=None, classes=None, max_p
     rs = row_splits_host(rs, n)
     B = len(rs) - 1
     pts = to_dev(points, dev)
-    rs_d = torch.from_numpy(rs).to(dev)
+    rs_d = to_dev(rs, dev)
     st = stream_handle(dev)
     ws = workspace(lib.o3dml_grid_subsample_workspace_size(n, B), dev)
     nout = np.zeros(1, np.int64)
