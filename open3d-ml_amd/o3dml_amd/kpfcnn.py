@@ -26,7 +26,6 @@ import torch.nn.functional as F
 from . import _lib, ops
 from ._util import index_bits, ptr, stream_handle, to_dev
 from .kpconv import KPConv
-from .layers import FixedRadiusSearch
 
 
 # ---------------------------------------------------------------------------
@@ -428,19 +427,19 @@ def batch_grid_subsampling(points, lengths, sampleDl, rotations=None, random_gri
     return s_pts, s_len
 
 
-def batch_neighbors(queries, supports, q_lengths, s_lengths, radius):
+def _splits(lengths):
+    s = np.zeros(len(lengths) + 1, np.int64)
+    s[1:] = np.cumsum(lengths)
+    return torch.from_numpy(s)
+
+
+def batch_neighbors(queries, supports, q_lengths, s_lengths, radius, hash_table=None):
     """Dense neighbour matrix padded with the shadow index len(supports)
     (kpconv.py:2002-2034): fixed-radius search + ragged_to_dense, width =
-    the largest neighbourhood.  int32 on the GPU."""
-    qs = np.zeros(len(q_lengths) + 1, np.int64)
-    ss = np.zeros(len(s_lengths) + 1, np.int64)
-    qs[1:] = np.cumsum(q_lengths)
-    ss[1:] = np.cumsum(s_lengths)
-    res = FixedRadiusSearch()(supports, queries, radius, torch.from_numpy(ss), torch.from_numpy(qs))
-    rs = res.neighbors_row_splits
-    width = int((rs[1:] - rs[:-1]).max().item()) if rs.numel() > 1 else 0
-    return ops.ragged_to_dense(res.neighbors_index.reshape(-1, 1), rs, width,
-                               torch.tensor([supports.shape[0]], dtype=torch.int32)).squeeze(2)
+    the largest neighbourhood.  int32 on the GPU.  ``hash_table`` (built for
+    the supports at this radius) may be shared between searches."""
+    return ops.fixed_radius_search_dense(supports, queries, radius, _splits(s_lengths), _splits(q_lengths),
+                                         hash_table=hash_table)
 
 
 def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_lengths, neighborhood_limits=(),
@@ -466,9 +465,12 @@ def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_len
             layer_blocks.append(block)
             continue
         deform = any("deformable" in b for b in layer_blocks)
+        table = None  # hash table of this layer's points at r_normal: shared by the conv and pool searches
         if layer_blocks:
             r = r_normal * cfg.deform_radius / cfg.conv_radius if deform else r_normal
-            conv_i = batch_neighbors(stacked_points, stacked_points, stack_lengths, stack_lengths, r)
+            if r == r_normal:
+                table = ops.build_spatial_hash_table(stacked_points, r, _splits(stack_lengths))
+            conv_i = batch_neighbors(stacked_points, stacked_points, stack_lengths, stack_lengths, r, table)
         else:
             conv_i = empty
         if "pool" in block or "strided" in block:
@@ -477,7 +479,8 @@ def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_len
             sub_i += 1
             pool_p, pool_b = batch_grid_subsampling(stacked_points, stack_lengths, dl, rotations=rot)
             r = r_normal * cfg.deform_radius / cfg.conv_radius if "deformable" in block else r_normal
-            pool_i = batch_neighbors(pool_p, stacked_points, pool_b, stack_lengths, r)
+            pool_i = batch_neighbors(pool_p, stacked_points, pool_b, stack_lengths, r,
+                                     table if r == r_normal else None)
             up_i = batch_neighbors(stacked_points, pool_p, stack_lengths, pool_b, 2 * r)
         else:
             pool_i = empty

@@ -66,20 +66,13 @@ def _same_cloud(points, queries, prs, qrs):
             and np.array_equal(prs, qrs))
 
 
-def fixed_radius_search(points, queries, radius, points_row_splits=None, queries_row_splits=None,
-                        hash_table_splits=None, hash_table_index=None, hash_table_cell_splits=None,
-                        index_dtype=torch.int32, metric="L2", ignore_query_point=False,
-                        return_distances=False):
-    """Open3D ``ops.fixed_radius_search`` (SURVEY §8a A5): for every query all
-    points with dist <= radius (L2: squared distance <= r^2; L1; Linf), in the
-    query's batch item.  Neighbour order: hash bins ascending, point id
-    ascending inside a bin (the canonical order; DESIGN.md).  Distances are
-    squared for L2.  Returns (neighbors_index [P], neighbors_row_splits int64
-    [M+1], neighbors_distance [P] or [0])."""
+def _frs_count(points, queries, radius, points_row_splits, queries_row_splits, hash_table_splits,
+               hash_table_index, hash_table_cell_splits, metric, ignore_query_point, return_distances):
+    """Phase 1 of fixed_radius_search: neighbour counts -> device row splits.
+    Returns (row_splits int64 [M+1] on the GPU, state for _frs_fill)."""
     dev = gpu_device(points, queries)
     check_points("points", points)
     check_points("queries", queries)
-    bits = index_bits(index_dtype)
     mcode = metric_code(metric)
     lib = _lib.load()
     n, m = points.shape[0], queries.shape[0]
@@ -109,12 +102,55 @@ def fixed_radius_search(points, queries, radius, points_row_splits=None, queries
     common = (ptr(pts), n, ptr(qry), m, r, B, ptr(prs_d), ptr(qrs_d), prs.ctypes.data, ptr(hts_d), ptr(hti_d),
               ptr(hcs_d), mcode, int(bool(ignore_query_point)), int(same), int(bool(return_distances)))
     _lib.call("o3dml_fixed_radius_search_count", *common, ptr(rs), ptr(ws), ws.numel(), st)
-    total = int(rs[-1].item())
+    # keep every buffer the fill phase reads alive in the state
+    return rs, (common, ws, st, dev, (pts, qry, prs_d, qrs_d, hts_d, hti_d, hcs_d), prs, bool(return_distances))
+
+
+def _frs_fill(rs, state, total, index_dtype):
+    common, ws, st, dev, _keep, _prs, with_dist = state
+    bits = index_bits(index_dtype)
     idx = torch.empty(total, dtype=torch.int32 if bits == 32 else torch.int64, device=dev)
-    dist = torch.empty(total if return_distances else 0, dtype=torch.float32, device=dev)
-    _lib.call("o3dml_fixed_radius_search_fill", *common, ptr(rs), bits, ptr(idx),
-              ptr(dist) if return_distances else None, ptr(ws), ws.numel(), st)
+    dist = torch.empty(total if with_dist else 0, dtype=torch.float32, device=dev)
+    _lib.call("o3dml_fixed_radius_search_fill", *common, ptr(rs), bits, ptr(idx), ptr(dist) if with_dist else None,
+              ptr(ws), ws.numel(), st)
+    return idx, dist
+
+
+def fixed_radius_search(points, queries, radius, points_row_splits=None, queries_row_splits=None,
+                        hash_table_splits=None, hash_table_index=None, hash_table_cell_splits=None,
+                        index_dtype=torch.int32, metric="L2", ignore_query_point=False,
+                        return_distances=False):
+    """Open3D ``ops.fixed_radius_search`` (SURVEY §8a A5): for every query all
+    points with dist <= radius (L2: squared distance <= r^2; L1; Linf), in the
+    query's batch item.  Neighbour order: hash bins ascending, point id
+    ascending inside a bin (the canonical order; DESIGN.md).  Distances are
+    squared for L2.  Returns (neighbors_index [P], neighbors_row_splits int64
+    [M+1], neighbors_distance [P] or [0])."""
+    index_bits(index_dtype)
+    rs, state = _frs_count(points, queries, radius, points_row_splits, queries_row_splits, hash_table_splits,
+                           hash_table_index, hash_table_cell_splits, metric, ignore_query_point, return_distances)
+    idx, dist = _frs_fill(rs, state, int(rs[-1].item()), index_dtype)
     return FixedRadiusSearchResult(back_to(idx, points), back_to(rs, points), back_to(dist, points))
+
+
+def fixed_radius_search_dense(points, queries, radius, points_row_splits, queries_row_splits, hash_table=None):
+    """Fixed-radius neighbours as a dense int32 matrix [M, max row length]
+    padded with len(points) — kpconv.py batch_neighbors (:2002-2034) in one
+    call: one host read for both the total and the width (the reference reads
+    them separately), fill, densify.  GPU tensors in and out."""
+    ht = hash_table
+    rs, state = _frs_count(points, queries, radius, points_row_splits, queries_row_splits,
+                           None if ht is None else ht.hash_table_splits,
+                           None if ht is None else ht.hash_table_index,
+                           None if ht is None else ht.hash_table_cell_splits, "L2", False, False)
+    m = queries.shape[0]
+    if m == 0:
+        return torch.zeros((0, 0), dtype=torch.int32, device=rs.device)
+    tw = torch.stack([rs[-1], (rs[1:] - rs[:-1]).max()]).cpu()
+    total, width = int(tw[0]), int(tw[1])
+    idx, _ = _frs_fill(rs, state, total, torch.int32)
+    return ragged_to_dense(idx.reshape(-1, 1), rs, width,
+                           torch.tensor([points.shape[0]], dtype=torch.int32)).squeeze(2)
 
 
 # ---------------------------------------------------------------------------
