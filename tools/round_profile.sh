@@ -8,7 +8,8 @@ ROOTDIR=$(pwd)
 OUT=$ROOTDIR/gpurun_out/${TAG:-prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BARGS="--steps ${STEPS:-10} --warmup 3 --no-cpu-baseline --randla-frames 0"
+BARGS_X="--no-cpu-baseline --randla-frames 0 --sparse-conv-reps 0 --kpconv-steps 0 --pointpillars-steps 0"
+BARGS="--steps ${STEPS:-10} --warmup 3 --no-cpu-baseline --randla-frames 0 --sparse-conv-reps 0 --kpconv-steps 0 --pointpillars-steps 0"
 timeout -k 10 300 python bench.py $BARGS > "$OUT/bench.log" 2>&1 || { echo "bench rc=$?"; exit 1; }
 tail -1 "$OUT/bench.log" | cut -c1-200
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv \
@@ -17,7 +18,7 @@ i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/p$i" -o run --output-format csv \
-      -- python3 "$ROOTDIR/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --randla-frames 0 > "$OUT/p$i.log" 2>&1) \
+      -- python3 "$ROOTDIR/bench.py" --steps 2 --warmup 1 $BARGS_X > "$OUT/p$i.log" 2>&1) \
       || { echo "pmc pass $i rc=$?"; exit 1; }
   echo "pmc pass $i ok"
 done
