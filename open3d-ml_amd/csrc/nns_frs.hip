@@ -1258,7 +1258,9 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
                                                                                pl.pts);
         O3DML_LAUNCH_CHECK();
         const int batch_bits = prim::bits_needed(static_cast<uint64_t>(n_batch - 1));
-        const int cell_bits = std::max(1, std::min(10, (32 - batch_bits) / 3));
+        // <= 24 key bits = 3 radix passes; Morton coordinates wrap modulo 2^cell_bits
+        // (locality only, grouping compares the full bucket lists)
+        const int cell_bits = std::max(1, std::min(8, (24 - batch_bits) / 3));
         group_query_keys_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(
                 queries, n_queries, 2.0f * inv, (int)n_batch, queries_row_splits, cell_bits, fp.keys);
         O3DML_LAUNCH_CHECK();
