@@ -140,36 +140,40 @@ __global__ void gather_float4_kernel(const float* __restrict__ pts, const uint32
 
 }  // namespace
 
-// Host: choose per-batch grids from the bounding boxes.
-inline std::vector<GridBatch> plan_grid(const float* bbox, const int64_t* rs_host, int nb, double target,
-                                        double cap_factor, int64_t* total_cells) {
-    std::vector<GridBatch> g(nb);
+// Choose per-batch grids from the bounding boxes (~target points per cell
+// for a uniform fill of the box, at most cap_factor * n_b + 64 cells per item):
+// one device thread walks the batch items, so building a grid needs no host
+// round trip.  Any grid gives exact results; the plan only sets the cost.
+namespace {
+__global__ void plan_grid_kernel(const float* __restrict__ bbox, const int64_t* __restrict__ rs, int nb,
+                                 double target, double cap_factor, GridBatch* __restrict__ out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
     int64_t off = 0;
     for (int b = 0; b < nb; ++b) {
-        const int64_t n = rs_host[b + 1] - rs_host[b];
-        GridBatch& gb = g[b];
+        const int64_t n = rs[b + 1] - rs[b];
         double ext[3];
         double vol = 1.0, maxe = 0.0;
         for (int d = 0; d < 3; ++d) {
             const double lo = n > 0 ? bbox[6 * b + d] : 0.0, hi = n > 0 ? bbox[6 * b + 3 + d] : 0.0;
-            ext[d] = std::isfinite(hi - lo) ? (hi - lo) : 0.0;
-            maxe = std::max(maxe, ext[d]);
+            ext[d] = isfinite(hi - lo) ? (hi - lo) : 0.0;
+            maxe = fmax(maxe, ext[d]);
         }
         if (maxe <= 0.0) maxe = 1.0;
-        for (int d = 0; d < 3; ++d) vol *= std::max(ext[d], maxe * 1e-3);
-        double h = std::cbrt(vol * target / std::max<int64_t>(n, 1));
-        h = std::max(h, maxe / 1024.0);
+        for (int d = 0; d < 3; ++d) vol *= fmax(ext[d], maxe * 1e-3);
+        double h = cbrt(vol * target / static_cast<double>(n > 1 ? n : 1));
+        h = fmax(h, maxe / 1024.0);
         const int64_t cap = static_cast<int64_t>(cap_factor * static_cast<double>(n)) + 64;
         int64_t dims[3], cells = 1;
         for (int it = 0; it < 64; ++it) {
             cells = 1;
             for (int d = 0; d < 3; ++d) {
-                dims[d] = static_cast<int64_t>(std::floor(ext[d] / h)) + 1;
+                dims[d] = static_cast<int64_t>(floor(ext[d] / h)) + 1;
                 cells *= dims[d];
             }
             if (cells <= cap) break;
-            h *= std::cbrt(static_cast<double>(cells) / static_cast<double>(cap)) * 1.01;
+            h *= cbrt(static_cast<double>(cells) / static_cast<double>(cap)) * 1.01;
         }
+        GridBatch gb;
         gb.ox = n > 0 ? bbox[6 * b] : 0.f;
         gb.oy = n > 0 ? bbox[6 * b + 1] : 0.f;
         gb.oz = n > 0 ? bbox[6 * b + 2] : 0.f;
@@ -179,11 +183,12 @@ inline std::vector<GridBatch> plan_grid(const float* bbox, const int64_t* rs_hos
         gb.dy = static_cast<int>(dims[1]);
         gb.dz = static_cast<int>(dims[2]);
         gb.offset = static_cast<uint32_t>(off);
+        gb.pad[0] = gb.pad[1] = gb.pad[2] = 0;
+        out[b] = gb;
         off += cells;
     }
-    *total_cells = off;
-    return g;
 }
+}  // namespace
 
 inline int64_t grid_cells_cap(int64_t n, int nb, double cap_factor) {
     return static_cast<int64_t>(cap_factor * static_cast<double>(n)) + 64 * static_cast<int64_t>(nb) + 64;
@@ -203,13 +208,16 @@ inline size_t grid_workspace_bytes(int64_t n, int nb, double cap_factor) {
            ws_bytes<float4>(n) + 3 * ws_bytes<uint32_t>(n) + prim::radix_sort_workspace_bytes<uint32_t>(n);
 }
 
-// Builds the grid; synchronises the stream once (bounding boxes -> host).
-inline GridIndex build_grid(const float* pts, int64_t n, const int64_t* rs_dev, const int64_t* rs_host, int nb,
-                            double target, double cap_factor, Workspace& ws, hipStream_t st) {
+// Builds the grid entirely on the device (bounding boxes -> plan -> cell keys
+// -> radix sort -> cell boundaries); no host synchronisation.  Cell ids are
+// bounded by the capacity, which sizes the sort and the boundary array.
+inline GridIndex build_grid(const float* pts, int64_t n, const int64_t* rs_dev, int nb, double target,
+                            double cap_factor, Workspace& ws, hipStream_t st) {
     GridIndex gi;
     gi.params = ws.take<GridBatch>(nb);
     float* bbox_d = ws.take<float>(6 * nb);
     const int64_t cap = grid_cells_cap(n, nb, cap_factor);
+    gi.cells = cap;
     gi.splits = ws.take<uint32_t>(cap + 1);
     gi.sorted = ws.take<float4>(n);
     uint32_t* keys = ws.take<uint32_t>(n);
@@ -217,23 +225,17 @@ inline GridIndex build_grid(const float* pts, int64_t n, const int64_t* rs_dev, 
     gi.order = ws.take<uint32_t>(n);
     launch_bbox(pts, rs_dev, nb, bbox_d, st);
     O3DML_LAUNCH_CHECK();
-    std::vector<float> bbox(6 * nb);
-    O3DML_CHECK_HIP(hipMemcpyAsync(bbox.data(), bbox_d, sizeof(float) * 6 * nb, hipMemcpyDeviceToHost, st));
-    O3DML_CHECK_HIP(hipStreamSynchronize(st));
-    std::vector<GridBatch> plan = plan_grid(bbox.data(), rs_host, nb, target, cap_factor, &gi.cells);
-    O3DML_REQUIRE(gi.cells <= cap, "grid plan exceeds capacity");
-    O3DML_CHECK_HIP(hipMemcpyAsync(gi.params, plan.data(), sizeof(GridBatch) * nb, hipMemcpyHostToDevice, st));
-    // the plan lives in pageable host memory owned by this frame: wait for the copy
-    O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    plan_grid_kernel<<<1, 64, 0, st>>>(bbox_d, rs_dev, nb, target, cap_factor, gi.params);
+    O3DML_LAUNCH_CHECK();
     if (n > 0) {
         grid_key_kernel<<<stream_grid(n, 256), 256, 0, st>>>(pts, n, rs_dev, nb, gi.params, keys);
         O3DML_LAUNCH_CHECK();
         prim::radix_sort_pairs<uint32_t>(keys, nullptr, skeys, gi.order, n,
-                                         prim::bits_needed(static_cast<uint64_t>(gi.cells - 1)), ws, st);
+                                         prim::bits_needed(static_cast<uint64_t>(cap - 1)), ws, st);
         gather_float4_kernel<<<stream_grid(n, 256), 256, 0, st>>>(pts, gi.order, n, gi.sorted);
         O3DML_LAUNCH_CHECK();
     }
-    key_boundaries_kernel<<<stream_grid(gi.cells + 1, 256, 1 << 16), 256, 0, st>>>(skeys, n, gi.cells, gi.splits);
+    key_boundaries_kernel<<<stream_grid(cap + 1, 256, 1 << 16), 256, 0, st>>>(skeys, n, cap, gi.splits);
     O3DML_LAUNCH_CHECK();
     return gi;
 }

@@ -362,9 +362,20 @@ __global__ void compact_rows_kernel(const int32_t* __restrict__ si, const float*
 }
 
 // ---- k > 64: one query at a time, full sort of its batch item's distances ----
+__global__ void bigk_counts_kernel(const int64_t* __restrict__ prs, const int64_t* __restrict__ qrs, int nb,
+                                   int64_t m, int64_t k, int64_t* __restrict__ counts) {
+    for (int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; q < m;
+         q += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int b = batch_of(q, qrs, nb);
+        const int64_t nbp = prs[b + 1] - prs[b];
+        counts[q] = nbp < k ? nbp : k;
+    }
+}
+
 template <int METRIC>
-__global__ void dist_keys_kernel(const float* __restrict__ pts, int64_t s, int64_t n, float qx, float qy, float qz,
+__global__ void dist_keys_kernel(const float* __restrict__ pts, int64_t s, int64_t n, const float* __restrict__ q,
                                  uint32_t* __restrict__ keys) {
+    const float qx = q[0], qy = q[1], qz = q[2];
     for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
          j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int64_t i = s + j;
@@ -405,7 +416,8 @@ static constexpr double kKnnCapFactor = 2.0;
 O3DML_API size_t o3dml_knn_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t k, int64_t n_batch) {
     if (knn_bucket(k) == 0) {
         int64_t maxn = n_points;
-        return 3 * ws_bytes<uint32_t>(maxn) + prim::radix_sort_workspace_bytes<uint32_t>(maxn);
+        return std::max(3 * ws_bytes<uint32_t>(maxn) + prim::radix_sort_workspace_bytes<uint32_t>(maxn),
+                        ws_bytes<int64_t>(n_queries) + prim::scan_workspace_bytes(n_queries));
     }
     return grid_workspace_bytes(n_points, static_cast<int>(n_batch), kKnnCapFactor) +
            3 * ws_bytes<uint32_t>(n_queries) + prim::radix_sort_workspace_bytes<uint32_t>(n_queries) +
@@ -432,24 +444,23 @@ O3DML_API int o3dml_knn_search_count(const float* points, int64_t n_points, cons
     const int K = knn_bucket(k);
     if (K == 0) {
         O3DML_REQUIRE(!ignore_query_point, "ignore_query_point is not supported for k > 64");
-        // rows: min(k, N_b) per query; computed on the host
-        std::vector<int64_t> rs(n_queries + 1, 0);
-        for (int b = 0; b < nb; ++b) {
-            const int64_t nbp = points_row_splits_host[b + 1] - points_row_splits_host[b];
-            for (int64_t q = queries_row_splits_host[b]; q < queries_row_splits_host[b + 1]; ++q)
-                rs[q + 1] = std::min<int64_t>(k, nbp);
-        }
-        for (int64_t q = 0; q < n_queries; ++q) rs[q + 1] += rs[q];
-        O3DML_CHECK_HIP(hipMemcpyAsync(neighbors_row_splits, rs.data(), sizeof(int64_t) * (n_queries + 1),
-                                       hipMemcpyHostToDevice, st));
-        O3DML_CHECK_HIP(hipStreamSynchronize(st));
+        // rows: min(k, N_b) per query, on the device (no host round trip)
+        (void)points_row_splits_host;
+        (void)queries_row_splits_host;
+        O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
+        if (n_queries == 0) return 0;
+        int64_t* cnt = ws.take<int64_t>(n_queries);
+        bigk_counts_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(points_row_splits, queries_row_splits, nb,
+                                                                       n_queries, k, cnt);
+        O3DML_LAUNCH_CHECK();
+        prim::scan<int64_t, int64_t>(cnt, neighbors_row_splits + 1, n_queries, true, ws, st);
         return 0;
     }
     // per-query results first: o3dml_knn_search_fill finds them at the same offsets
     int32_t* si = ws.take<int32_t>(n_queries * k);
     float* sd = ws.take<float>(n_queries * k);
     int64_t* counts = ws.take<int64_t>(n_queries);
-    GridIndex gi = build_grid(points, n_points, points_row_splits, points_row_splits_host, nb, std::max(2.0, k / 2.0),
+    GridIndex gi = build_grid(points, n_points, points_row_splits, nb, std::max(2.0, k / 2.0),
                               kKnnCapFactor, ws, st);
     uint32_t* qkeys = ws.take<uint32_t>(n_queries);
     uint32_t* qskeys = ws.take<uint32_t>(n_queries);
@@ -501,9 +512,6 @@ O3DML_API int o3dml_knn_search_fill(const float* points, int64_t n_points, const
         uint32_t* keys = ws.take<uint32_t>(n_points);
         uint32_t* skeys = ws.take<uint32_t>(n_points);
         uint32_t* sidx = ws.take<uint32_t>(n_points);
-        std::vector<float> qh(3 * n_queries);
-        O3DML_CHECK_HIP(hipMemcpyAsync(qh.data(), queries, sizeof(float) * 3 * n_queries, hipMemcpyDeviceToHost, st));
-        O3DML_CHECK_HIP(hipStreamSynchronize(st));
         int64_t off = 0;
         for (int b = 0; b < nb; ++b) {
             const int64_t ps = points_row_splits_host[b], pn = points_row_splits_host[b + 1] - ps;
@@ -512,11 +520,11 @@ O3DML_API int o3dml_knn_search_fill(const float* points, int64_t n_points, const
                 if (cnt == 0) continue;
                 const unsigned g = stream_grid(pn, 256);
                 if (metric == kL2)
-                    dist_keys_kernel<kL2><<<g, 256, 0, st>>>(points, ps, pn, qh[3 * q], qh[3 * q + 1], qh[3 * q + 2], keys);
+                    dist_keys_kernel<kL2><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, keys);
                 else if (metric == kL1)
-                    dist_keys_kernel<kL1><<<g, 256, 0, st>>>(points, ps, pn, qh[3 * q], qh[3 * q + 1], qh[3 * q + 2], keys);
+                    dist_keys_kernel<kL1><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, keys);
                 else
-                    dist_keys_kernel<kLinf><<<g, 256, 0, st>>>(points, ps, pn, qh[3 * q], qh[3 * q + 1], qh[3 * q + 2], keys);
+                    dist_keys_kernel<kLinf><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, keys);
                 O3DML_LAUNCH_CHECK();
                 Workspace sws = ws;
                 prim::radix_sort_pairs<uint32_t>(keys, nullptr, skeys, sidx, pn, 32, sws, st);

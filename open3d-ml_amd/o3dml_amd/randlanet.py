@@ -330,8 +330,7 @@ class SemSegInference:
         semseg_spatially_regular.py:82-109)."""
         cfg = self.model.cfg
         n_pts = cfg["num_points"]
-        center_id = int(torch.argmin(possibility))
-        center = sub[center_id:center_id + 1]
+        center = sub.index_select(0, torch.argmin(possibility).view(1))  # stays on the device: no host read
         if sub.shape[0] < n_pts:
             extra = torch.randint(0, sub.shape[0], (n_pts - sub.shape[0],), generator=self.gen, device=self.device)
             idxs = torch.cat([torch.arange(sub.shape[0], device=self.device), extra])
