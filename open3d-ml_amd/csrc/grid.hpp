@@ -32,7 +32,7 @@ namespace {
 // into the item's box with integer atomics on an order-preserving encoding of
 // the floats (so one launch fills the chip even for a single large cloud);
 // bbox_init / bbox_decode bracket it.  Use launch_bbox().
-constexpr int kBBoxParts = 64;
+constexpr int kBBoxParts = 32;
 
 __device__ __forceinline__ uint32_t f2ord(float f) {
     const uint32_t u = __float_as_uint(f);
@@ -72,13 +72,23 @@ __global__ void __launch_bounds__(256) bbox_kernel(const float* __restrict__ pts
             mx[d] = fmaxf(mx[d], __shfl_xor(mx[d], o, 64));
         }
     }
+    // block reduction in LDS, then one set of atomics per block (few per address)
+    __shared__ float red[6][4];
     if (lane_id() == 0) {
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            if (mn[d] <= mx[d]) {  // this wave saw points
-                atomicMin(out + 6 * b + d, f2ord(mn[d]));
-                atomicMax(out + 6 * b + 3 + d, f2ord(mx[d]));
-            }
+            red[d][wave_id()] = mn[d];
+            red[3 + d][wave_id()] = mx[d];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int d = threadIdx.x;
+        float v = red[d][0];
+        for (int w = 1; w < static_cast<int>(blockDim.x / 64); ++w) v = d < 3 ? fminf(v, red[d][w]) : fmaxf(v, red[d][w]);
+        if (d < 3 ? v < INFINITY : v > -INFINITY) {
+            if (d < 3) atomicMin(out + 6 * b + d, f2ord(v));
+            else atomicMax(out + 6 * b + d, f2ord(v));
         }
     }
 }

@@ -269,6 +269,16 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
                     }
                 }
             }
+            // merging only pays once the group holds k candidates (it can then
+            // prune and terminate); before that the lists keep accumulating
+            int have = 0;
+#pragma unroll
+            for (int r = 0; r < K; ++r) have += bi[r] != 0xffffffffu ? 1 : 0;
+#pragma unroll
+            for (int mask = 1; mask < kKnnG; mask <<= 1) have += __shfl_xor(have, mask, 64);
+            const bool last_ring = x0 <= 0 && x1 >= g.dx - 1 && y0 <= 0 && y1 >= g.dy - 1 && z0 <= 0 &&
+                                   z1 >= g.dz - 1;
+            if (have < k && !last_ring) continue;
             group_merge<K>(bd, bi);
 #pragma unroll
             for (int r = 0; r < K; ++r)
@@ -412,6 +422,15 @@ static int knn_bucket(int64_t k) {
 }
 
 static constexpr double kKnnCapFactor = 2.0;
+// points per cell of the uniform-fill grid plan = max(min_target, k * factor)
+static double knn_target_factor() {
+    const char* e = std::getenv("O3DML_KNN_TARGET");
+    return e ? std::atof(e) : 0.5;
+}
+static double knn_min_target() {
+    const char* e = std::getenv("O3DML_KNN_MIN_TARGET");
+    return e ? std::atof(e) : 2.0;
+}
 
 O3DML_API size_t o3dml_knn_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t k, int64_t n_batch) {
     if (knn_bucket(k) == 0) {
@@ -460,7 +479,7 @@ O3DML_API int o3dml_knn_search_count(const float* points, int64_t n_points, cons
     int32_t* si = ws.take<int32_t>(n_queries * k);
     float* sd = ws.take<float>(n_queries * k);
     int64_t* counts = ws.take<int64_t>(n_queries);
-    GridIndex gi = build_grid(points, n_points, points_row_splits, nb, std::max(2.0, k / 2.0),
+    GridIndex gi = build_grid(points, n_points, points_row_splits, nb, std::max(knn_min_target(), k * knn_target_factor()),
                               kKnnCapFactor, ws, st);
     uint32_t* qkeys = ws.take<uint32_t>(n_queries);
     uint32_t* qskeys = ws.take<uint32_t>(n_queries);
