@@ -299,6 +299,16 @@ int o3dml_randla_attentive_pool(const float* x, const float* logits, int64_t n, 
  * rows; ia / ib nullable (identity), int32 or int64 per *_bits. */
 int o3dml_concat_rows(const float* a, int da, const void* ia, int ia_bits, const float* b, int db, const void* ib,
                       int ib_bits, int64_t rows, float* out, void* stream);
+/* att_pool: fused LocalSpatialEncoding + AttentivePooling (randlanet.py:
+ * 540-650) for k == 16 neighbours and width d in {16, 32, 64, 128, 256}:
+ * rel_j = leaky_0.2(Wr r_j + br) with r_j the 10-value relative encoding of
+ * (n, neighbors[n, j]) (rel_in null) or rel_in [N, k, d/2];
+ * F_j = [x[neighbors[n, j]] (x [N, d/2]), rel_j]; s_j = Ws F_j + bs;
+ * out[n] = sum_j softmax_j(s_j) * F_j -> out [N, d].  Weights transposed:
+ * wr_t [in][d/2], ws_t [d][d] (in-major).  rel_out [N, k, d/2] nullable. */
+int o3dml_randla_att_pool(const float* coords, const float* x, const int32_t* neighbors, int64_t n, int k, int d,
+                          const float* rel_in, const float* wr_t, const float* br, const float* ws_t,
+                          const float* bs, float* rel_out, float* out, void* stream);
 int o3dml_randla_gather_max(const float* feat, int c, const int32_t* idx, int64_t m, int k, float* out,
                             void* stream);
 

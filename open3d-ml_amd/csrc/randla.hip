@@ -12,6 +12,8 @@
 //     K gathered rows -> [M,C]
 // All are HBM-bound; one thread per output element, channel-fastest so
 // consecutive lanes read consecutive addresses.
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace o3dml {
@@ -103,6 +105,124 @@ __global__ void concat_rows_kernel(const float* __restrict__ A, int da, const TA
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Fused LocalSpatialEncoding + AttentivePooling (randlanet.py:540-650): per
+// point n with neighbours j < K,
+//   rel_j = leaky_0.2(Wr . r_j + br)            r_j = relative encoding of
+//           (n, nbr_j) (first pass, 10 values) or the previous pass's rel_j
+//   F_j   = [x[nbr_j] (D/2), rel_j (D/2)]
+//   s_j   = Ws . F_j + bs                       (score_fn Linear, D x D)
+//   out   = sum_j softmax_j(s_j) * F_j          (per channel)
+// The reference materialises every [N, K, *] tensor (relative encoding, MLP
+// output, gathered features, their concatenation, the scores) in HBM; here F
+// lives in LDS (channel-major, K contiguous, so a lane reads the K values of
+// one input channel with 128-bit broadcast loads) and each lane owns output
+// channels.  Wr / Ws come transposed ([in][out]) so the weight loads of a
+// wave are coalesced.  rel_out (nullable) keeps rel_j for the second pass.
+// ---------------------------------------------------------------------------
+constexpr int kApK = 16;  // neighbours (RandLA num_neighbors)
+
+template <int D, bool RELENC>
+__global__ void __launch_bounds__(64) att_pool_kernel(const float* __restrict__ coords, const float* __restrict__ x,
+                                                      const int32_t* __restrict__ nbr, int64_t n,
+                                                      const float* __restrict__ rel_in,
+                                                      const float* __restrict__ wrt, const float* __restrict__ br,
+                                                      const float* __restrict__ wst, const float* __restrict__ bs,
+                                                      float* __restrict__ rel_out, float* __restrict__ out) {
+    constexpr int H = D / 2;
+    constexpr int IR = RELENC ? 10 : H;           // rel MLP input width
+    constexpr int LP = D < 64 ? D : 64;           // lanes per point
+    constexpr int PPW = 64 / LP;                  // points per wave
+    constexpr int CPL = D / LP;                   // output channels per lane
+    __shared__ __attribute__((aligned(16))) float ft[PPW][D][kApK];  // F, channel-major
+    __shared__ float rin[PPW][kApK][IR];                              // MLP input rows
+    __shared__ int32_t nb_s[PPW][kApK];
+    const int lane = threadIdx.x;
+    const int ps = lane / LP, cl = lane % LP;
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * PPW; base < n;
+         base += static_cast<int64_t>(gridDim.x) * PPW) {
+        const int64_t q = base + ps;
+        const bool valid = q < n;
+        // (a) neighbour ids and the MLP input rows
+        if (valid && cl < kApK) nb_s[ps][cl] = nbr[q * kApK + cl];
+        __syncthreads();
+        if (valid) {
+            if constexpr (RELENC) {
+                if (cl < kApK) {
+                    const int64_t j = nb_s[ps][cl];
+                    const float cx = coords[3 * q], cy = coords[3 * q + 1], cz = coords[3 * q + 2];
+                    const float px = coords[3 * j], py = coords[3 * j + 1], pz = coords[3 * j + 2];
+                    const float rx = cx - px, ry = cy - py, rz = cz - pz;
+                    float* r = rin[ps][cl];
+                    r[0] = sqrtf((rx * rx + ry * ry) + rz * rz);
+                    r[1] = rx;
+                    r[2] = ry;
+                    r[3] = rz;
+                    r[4] = cx;
+                    r[5] = cy;
+                    r[6] = cz;
+                    r[7] = px;
+                    r[8] = py;
+                    r[9] = pz;
+                }
+            } else {
+                for (int e = cl; e < kApK * IR; e += LP) rin[ps][e / IR][e % IR] = rel_in[q * kApK * IR + e];
+            }
+        }
+        __syncthreads();
+        // (b) F = [x[nbr] | leaky(Wr . r + br)], written channel-major into LDS
+        if (valid) {
+            for (int e = cl; e < kApK * H; e += LP) {
+                const int j = e / H, c = e % H;
+                ft[ps][c][j] = x[static_cast<int64_t>(nb_s[ps][j]) * H + c];
+                float acc = br[c];
+#pragma unroll 10
+                for (int i = 0; i < IR; ++i) acc = __builtin_fmaf(wrt[i * H + c], rin[ps][j][i], acc);
+                const float v = acc > 0.f ? acc : 0.2f * acc;
+                ft[ps][H + c][j] = v;
+                if (rel_out) rel_out[(q * kApK + j) * H + c] = v;
+            }
+        }
+        __syncthreads();
+        // (c) scores s[j][c] = bs[c] + sum_i Ws[c][i] F[j][i], then softmax over j and
+        //     the weighted sum, for this lane's channels
+        if (valid) {
+#pragma unroll
+            for (int t = 0; t < CPL; ++t) {
+                const int c = t * LP + cl;
+                float acc[kApK];
+#pragma unroll
+                for (int j = 0; j < kApK; ++j) acc[j] = bs[c];
+                for (int i = 0; i < D; ++i) {
+                    const float w = wst[i * D + c];
+                    const float4* fr = reinterpret_cast<const float4*>(ft[ps][i]);
+#pragma unroll
+                    for (int v = 0; v < kApK / 4; ++v) {
+                        const float4 f = fr[v];
+                        acc[4 * v] = __builtin_fmaf(w, f.x, acc[4 * v]);
+                        acc[4 * v + 1] = __builtin_fmaf(w, f.y, acc[4 * v + 1]);
+                        acc[4 * v + 2] = __builtin_fmaf(w, f.z, acc[4 * v + 2]);
+                        acc[4 * v + 3] = __builtin_fmaf(w, f.w, acc[4 * v + 3]);
+                    }
+                }
+                float mx = acc[0];
+#pragma unroll
+                for (int j = 1; j < kApK; ++j) mx = fmaxf(mx, acc[j]);
+                float den = 0.f, num = 0.f;
+#pragma unroll
+                for (int j = 0; j < kApK; ++j) {
+                    const float e = __expf(acc[j] - mx);
+                    den += e;
+                    num += e * ft[ps][c][j];
+                }
+                out[q * D + c] = num / den;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace o3dml
 
 using namespace o3dml;
@@ -154,6 +274,38 @@ O3DML_API int o3dml_concat_rows(const float* a, int da, const void* ia, int ia_b
         if (ib_bits == 32) O3DML_CAT(int64_t, int32_t); else O3DML_CAT(int64_t, int64_t);
     }
 #undef O3DML_CAT
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_randla_att_pool(const float* coords, const float* x, const int32_t* neighbors, int64_t n, int k,
+                                    int d, const float* rel_in, const float* wr_t, const float* br, const float* ws_t,
+                                    const float* bs, float* rel_out, float* out, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(k == kApK, "fused attentive pooling needs k == %d, got %d", kApK, k);
+    O3DML_REQUIRE(d == 16 || d == 32 || d == 64 || d == 128 || d == 256,
+                  "fused attentive pooling: width %d not in {16, 32, 64, 128, 256}", d);
+    if (n == 0) return 0;
+    hipStream_t st = as_stream(stream);
+    const int ppw = d < 64 ? 64 / d : 1;
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n, ppw), 1 << 20));
+#define O3DML_AP(D)                                                                                              \
+    do {                                                                                                         \
+        if (rel_in)                                                                                              \
+            att_pool_kernel<D, false><<<g, 64, 0, st>>>(coords, x, neighbors, n, rel_in, wr_t, br, ws_t, bs,     \
+                                                        rel_out, out);                                           \
+        else                                                                                                     \
+            att_pool_kernel<D, true><<<g, 64, 0, st>>>(coords, x, neighbors, n, nullptr, wr_t, br, ws_t, bs,     \
+                                                       rel_out, out);                                            \
+    } while (0)
+    switch (d) {
+        case 16: O3DML_AP(16); break;
+        case 32: O3DML_AP(32); break;
+        case 64: O3DML_AP(64); break;
+        case 128: O3DML_AP(128); break;
+        default: O3DML_AP(256); break;
+    }
+#undef O3DML_AP
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }

@@ -69,6 +69,7 @@ SIGNATURES = {
     "o3dml_randla_relative_encoding": (c_i32, [c_p, c_i64, c_p, c_i32, c_p, c_p]),
     "o3dml_randla_attentive_pool": (c_i32, [c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p]),
     "o3dml_concat_rows": (c_i32, [c_p, c_i32, c_p, c_i32, c_p, c_i32, c_p, c_i32, c_i64, c_p, c_p]),
+    "o3dml_randla_att_pool": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "o3dml_randla_gather_max": (c_i32, [c_p, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
     "o3dml_calculate_grid_workspace_size": (c_sz, [c_i64]),
     "o3dml_calculate_grid_count": (c_i32, [c_p, c_i64, c_p, c_p, c_sz, c_p]),

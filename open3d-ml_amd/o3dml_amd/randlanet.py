@@ -190,8 +190,42 @@ class LocalFeatureAggregation(nn.Module):
         self.shortcut = SharedMLP(d_in, 2 * d_out)
         self.lrelu = nn.LeakyReLU()
 
+    _ATT_WIDTHS = (16, 32, 64, 128, 256)
+
+    def _att_weights(self, lse, pool):
+        """(Wr^T, br, Ws^T, bs) for the fused kernel, cached until parameters change."""
+        cache = self.__dict__.setdefault("_t_cache", {})
+        key = id(pool)
+        if key not in cache:
+            with torch.no_grad():
+                wr, br = lse.mlp.folded()
+                lin = pool.score_fn[0]
+                cache[key] = (wr.t().contiguous(), br.contiguous(), lin.weight.float().t().contiguous(),
+                              lin.bias.float().contiguous())
+        return cache[key]
+
+    def _fused_pool(self, coords, x, nbr, lse, pool, rel_in):
+        """LocalSpatialEncoding + AttentivePooling in one HIP pass
+        (csrc/randla.hip att_pool_kernel) -> (pooled [N, d], rel [N, K, d/2])."""
+        n, k = nbr.shape
+        d = pool.score_fn[0].weight.shape[0]
+        wrt, br, wst, bs = self._att_weights(lse, pool)
+        out = torch.empty((n, d), dtype=torch.float32, device=x.device)
+        rel = torch.empty((n, k, d // 2), dtype=torch.float32, device=x.device) if rel_in is None else None
+        _lib.call("o3dml_randla_att_pool", ptr(coords), ptr(x.contiguous()), ptr(nbr), n, k, d,
+                  ptr(rel_in), ptr(wrt), ptr(br), ptr(wst), ptr(bs), ptr(rel), ptr(out), stream_handle(x.device))
+        return out, rel
+
     def forward(self, coords, feat, nbr):
         x = self.mlp1(feat)
+        d = self.pool1.score_fn[0].weight.shape[0]
+        if (_fused() and not self.training and nbr.shape[1] == 16 and d in self._ATT_WIDTHS
+                and nbr.dtype == torch.int32):
+            pooled, rel = self._fused_pool(coords.contiguous(), x, nbr.contiguous(), self.lse1, self.pool1, None)
+            x = self.pool1.mlp(pooled)
+            pooled, _ = self._fused_pool(coords.contiguous(), x, nbr.contiguous(), self.lse2, self.pool2, rel)
+            x = self.pool2.mlp(pooled)
+            return self.lrelu(self.mlp2(x) + self.shortcut(feat))
         x, rel = self.lse1(coords, x, nbr)
         x = self.pool1(x)
         x, _ = self.lse2(coords, x, nbr, relative_features=rel)
@@ -239,6 +273,8 @@ class RandLANet(nn.Module):
         for m in self.modules():
             if isinstance(m, SharedMLP):
                 m._folded = None
+            if isinstance(m, LocalFeatureAggregation):
+                m.__dict__.pop("_t_cache", None)
 
     def train(self, mode=True):
         self._invalidate()
