@@ -124,37 +124,35 @@ __global__ void concat_rows_kernel(const float* __restrict__ A, int da, const TA
 constexpr int kApK = 16;  // neighbours (RandLA num_neighbors)
 
 template <int D, bool RELENC>
-__global__ void __launch_bounds__(64) att_pool_kernel(const float* __restrict__ coords, const float* __restrict__ x,
-                                                      const int32_t* __restrict__ nbr, int64_t n,
-                                                      const float* __restrict__ rel_in,
-                                                      const float* __restrict__ wrt, const float* __restrict__ br,
-                                                      const float* __restrict__ wst, const float* __restrict__ bs,
-                                                      float* __restrict__ rel_out, float* __restrict__ out) {
+__global__ void __launch_bounds__(D > 64 ? D : 64) att_pool_kernel(
+        const float* __restrict__ coords, const float* __restrict__ x, const int32_t* __restrict__ nbr, int64_t n,
+        const float* __restrict__ rel_in, const float* __restrict__ wrt, const float* __restrict__ br,
+        const float* __restrict__ wst, const float* __restrict__ bs, float* __restrict__ rel_out,
+        float* __restrict__ out) {
     constexpr int H = D / 2;
-    constexpr int IR = RELENC ? 10 : H;           // rel MLP input width
-    constexpr int LP = D < 64 ? D : 64;           // lanes per point
-    constexpr int PPW = 64 / LP;                  // points per wave
-    constexpr int CPL = D / LP;                   // output channels per lane
-    __shared__ __attribute__((aligned(16))) float ft[PPW][D][kApK];  // F, channel-major
-    __shared__ float rin[PPW][kApK][IR];                              // MLP input rows
-    __shared__ int32_t nb_s[PPW][kApK];
-    const int lane = threadIdx.x;
-    const int ps = lane / LP, cl = lane % LP;
-    for (int64_t base = static_cast<int64_t>(blockIdx.x) * PPW; base < n;
-         base += static_cast<int64_t>(gridDim.x) * PPW) {
+    constexpr int IR = RELENC ? 10 : H;  // rel MLP input width
+    constexpr int TP = D;                // threads per point: one output channel each
+    constexpr int BS = D > 64 ? D : 64;  // block size
+    constexpr int PPB = BS / TP;         // points per block
+    __shared__ __attribute__((aligned(16))) float ft[PPB][D][kApK];  // F, channel-major
+    __shared__ float rin[PPB][kApK][IR];                              // MLP input rows
+    __shared__ int32_t nb_s[PPB][kApK];
+    const int ps = threadIdx.x / TP, c = threadIdx.x % TP;
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * PPB; base < n;
+         base += static_cast<int64_t>(gridDim.x) * PPB) {
         const int64_t q = base + ps;
         const bool valid = q < n;
         // (a) neighbour ids and the MLP input rows
-        if (valid && cl < kApK) nb_s[ps][cl] = nbr[q * kApK + cl];
+        if (valid && c < kApK) nb_s[ps][c] = nbr[q * kApK + c];
         __syncthreads();
         if (valid) {
             if constexpr (RELENC) {
-                if (cl < kApK) {
-                    const int64_t j = nb_s[ps][cl];
+                if (c < kApK) {
+                    const int64_t j = nb_s[ps][c];
                     const float cx = coords[3 * q], cy = coords[3 * q + 1], cz = coords[3 * q + 2];
                     const float px = coords[3 * j], py = coords[3 * j + 1], pz = coords[3 * j + 2];
                     const float rx = cx - px, ry = cy - py, rz = cz - pz;
-                    float* r = rin[ps][cl];
+                    float* r = rin[ps][c];
                     r[0] = sqrtf((rx * rx + ry * ry) + rz * rz);
                     r[1] = rx;
                     r[2] = ry;
@@ -167,57 +165,54 @@ __global__ void __launch_bounds__(64) att_pool_kernel(const float* __restrict__ 
                     r[9] = pz;
                 }
             } else {
-                for (int e = cl; e < kApK * IR; e += LP) rin[ps][e / IR][e % IR] = rel_in[q * kApK * IR + e];
+                for (int e = c; e < kApK * IR; e += TP) rin[ps][e / IR][e % IR] = rel_in[q * kApK * IR + e];
             }
         }
         __syncthreads();
-        // (b) F = [x[nbr] | leaky(Wr . r + br)], written channel-major into LDS
+        // (b) F = [x[nbr] | leaky(Wr . r + br)], channel-major in LDS (consecutive
+        //     threads = consecutive channels of one neighbour: coalesced rows)
         if (valid) {
-            for (int e = cl; e < kApK * H; e += LP) {
-                const int j = e / H, c = e % H;
-                ft[ps][c][j] = x[static_cast<int64_t>(nb_s[ps][j]) * H + c];
-                float acc = br[c];
+            for (int e = c; e < kApK * H; e += TP) {
+                const int j = e / H, cc = e % H;
+                ft[ps][cc][j] = x[static_cast<int64_t>(nb_s[ps][j]) * H + cc];
+                float acc = br[cc];
 #pragma unroll 10
-                for (int i = 0; i < IR; ++i) acc = __builtin_fmaf(wrt[i * H + c], rin[ps][j][i], acc);
+                for (int i = 0; i < IR; ++i) acc = __builtin_fmaf(wrt[i * H + cc], rin[ps][j][i], acc);
                 const float v = acc > 0.f ? acc : 0.2f * acc;
-                ft[ps][H + c][j] = v;
-                if (rel_out) rel_out[(q * kApK + j) * H + c] = v;
+                ft[ps][H + cc][j] = v;
+                if (rel_out) rel_out[(q * kApK + j) * H + cc] = v;
             }
         }
         __syncthreads();
-        // (c) scores s[j][c] = bs[c] + sum_i Ws[c][i] F[j][i], then softmax over j and
-        //     the weighted sum, for this lane's channels
+        // (c) scores s[j] = bs[c] + sum_i Ws[c][i] F[j][i] for this thread's channel c,
+        //     softmax over j, weighted sum
         if (valid) {
+            float acc[kApK];
 #pragma unroll
-            for (int t = 0; t < CPL; ++t) {
-                const int c = t * LP + cl;
-                float acc[kApK];
+            for (int j = 0; j < kApK; ++j) acc[j] = bs[c];
+            for (int i = 0; i < D; ++i) {
+                const float w = wst[i * D + c];
+                const float4* fr = reinterpret_cast<const float4*>(ft[ps][i]);
 #pragma unroll
-                for (int j = 0; j < kApK; ++j) acc[j] = bs[c];
-                for (int i = 0; i < D; ++i) {
-                    const float w = wst[i * D + c];
-                    const float4* fr = reinterpret_cast<const float4*>(ft[ps][i]);
-#pragma unroll
-                    for (int v = 0; v < kApK / 4; ++v) {
-                        const float4 f = fr[v];
-                        acc[4 * v] = __builtin_fmaf(w, f.x, acc[4 * v]);
-                        acc[4 * v + 1] = __builtin_fmaf(w, f.y, acc[4 * v + 1]);
-                        acc[4 * v + 2] = __builtin_fmaf(w, f.z, acc[4 * v + 2]);
-                        acc[4 * v + 3] = __builtin_fmaf(w, f.w, acc[4 * v + 3]);
-                    }
+                for (int v = 0; v < kApK / 4; ++v) {
+                    const float4 f = fr[v];
+                    acc[4 * v] = __builtin_fmaf(w, f.x, acc[4 * v]);
+                    acc[4 * v + 1] = __builtin_fmaf(w, f.y, acc[4 * v + 1]);
+                    acc[4 * v + 2] = __builtin_fmaf(w, f.z, acc[4 * v + 2]);
+                    acc[4 * v + 3] = __builtin_fmaf(w, f.w, acc[4 * v + 3]);
                 }
-                float mx = acc[0];
-#pragma unroll
-                for (int j = 1; j < kApK; ++j) mx = fmaxf(mx, acc[j]);
-                float den = 0.f, num = 0.f;
-#pragma unroll
-                for (int j = 0; j < kApK; ++j) {
-                    const float e = __expf(acc[j] - mx);
-                    den += e;
-                    num += e * ft[ps][c][j];
-                }
-                out[q * D + c] = num / den;
             }
+            float mx = acc[0];
+#pragma unroll
+            for (int j = 1; j < kApK; ++j) mx = fmaxf(mx, acc[j]);
+            float den = 0.f, num = 0.f;
+#pragma unroll
+            for (int j = 0; j < kApK; ++j) {
+                const float e = __expf(acc[j] - mx);
+                den += e;
+                num += e * ft[ps][c][j];
+            }
+            out[q * D + c] = num / den;
         }
         __syncthreads();
     }
@@ -287,15 +282,15 @@ O3DML_API int o3dml_randla_att_pool(const float* coords, const float* x, const i
                   "fused attentive pooling: width %d not in {16, 32, 64, 128, 256}", d);
     if (n == 0) return 0;
     hipStream_t st = as_stream(stream);
-    const int ppw = d < 64 ? 64 / d : 1;
-    const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n, ppw), 1 << 20));
+    const int ppb = d < 64 ? 64 / d : 1, block = d > 64 ? d : 64;
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n, ppb), 1 << 20));
 #define O3DML_AP(D)                                                                                              \
     do {                                                                                                         \
         if (rel_in)                                                                                              \
-            att_pool_kernel<D, false><<<g, 64, 0, st>>>(coords, x, neighbors, n, rel_in, wr_t, br, ws_t, bs,     \
+            att_pool_kernel<D, false><<<g, block, 0, st>>>(coords, x, neighbors, n, rel_in, wr_t, br, ws_t, bs,     \
                                                         rel_out, out);                                           \
         else                                                                                                     \
-            att_pool_kernel<D, true><<<g, 64, 0, st>>>(coords, x, neighbors, n, nullptr, wr_t, br, ws_t, bs,     \
+            att_pool_kernel<D, true><<<g, block, 0, st>>>(coords, x, neighbors, n, nullptr, wr_t, br, ws_t, bs,     \
                                                        rel_out, out);                                            \
     } while (0)
     switch (d) {
