@@ -15,7 +15,8 @@ sub-modules), so reference state_dicts load unchanged, and the same
   [V, M, 4+5] tensor once (csrc/pillars.hip);
 * BEV scatter / its adjoint in HIP.
 The dense 2-D backbone, neck and head are torch convolutions (MIOpen); the
-anchor assignment is vectorised on the GPU (no per-box host loop).
+anchor assignment and the losses run on dense per-anchor masks on the GPU (no
+per-box host loop, no index lists, no host round trips).
 """
 import numpy as np
 import torch
@@ -142,7 +143,7 @@ class FocalLoss(nn.Module):
     def forward(self, pred, target, weight=None, avg_factor=None):
         p = pred.sigmoid()
         if pred.dim() > 1:
-            target = F.one_hot(target, pred.shape[-1] + 1)[..., :pred.shape[-1]] if target.numel() else \
+            target = F.one_hot(target.clamp(0, pred.shape[-1]), pred.shape[-1] + 1)[..., :pred.shape[-1]] if target.numel() else \
                 pred.new_zeros(pred.shape)
         t = target.type_as(pred)
         pt = (1 - p) * t + p * (1 - t)
@@ -551,9 +552,93 @@ class PointPillars(nn.Module):
     def forward(self, inputs):
         return self.bbox_head(self.extract_feats(inputs.point))
 
+    def dense_targets(self, feat_shape, gt_bboxes, gt_labels):
+        """Per-anchor assignment for every scene at once, as dense masks in the
+        head's flattened row order (scene, y, x, class, rotation): the same
+        positives / negatives / matched target as Anchor3DHead.assign_bboxes
+        (point_pillars.py:826-913) without index lists — no host round trips.
+        Returns (pos, neg, labels, encoded target boxes, target yaw) over rows."""
+        head = self.bbox_head
+        dev = gt_bboxes[0].device if len(gt_bboxes) else torch.device("cuda")
+        anchors = head._anchors(feat_shape, dev)  # [1, H, W, nc, nr, 7]
+        nc, nr = anchors.shape[-3], anchors.shape[-2]
+        anc = anchors.reshape(-1, 7)
+        S = anc.shape[0] // (nc * nr)
+        thr = torch.tensor(head.iou_thr, dtype=torch.float32, device=dev)  # [nc, 2] (neg, pos)
+        neg_th = thr[:, 0].view(1, nc, 1)
+        pos_th = thr[:, 1].view(1, nc, 1)
+        anc_bev = box3d_to_bev2d(anc)
+        pos_l, neg_l, lab_l, box_l, yaw_l = [], [], [], [], []
+        for tb, tl in zip(gt_bboxes, gt_labels):
+            G = tb.shape[0]
+            if G == 0:
+                z = torch.zeros(anc.shape[0], dtype=torch.bool, device=dev)
+                pos_l.append(z)
+                neg_l.append(z)
+                lab_l.append(torch.full((anc.shape[0],), head.num_classes, dtype=torch.long, device=dev))
+                box_l.append(torch.zeros_like(anc))
+                yaw_l.append(torch.zeros(anc.shape[0], device=dev))
+                continue
+            ov = bbox_overlaps(box3d_to_bev2d(tb), anc_bev).view(G, S, nc, nr)
+            max_ov, arg = ov.max(dim=0)                                      # [S, nc, nr]
+            pos = max_ov >= pos_th
+            neg = (max_ov >= 0) & (max_ov < neg_th)
+            gmax, garg = ov.permute(0, 2, 1, 3).reshape(G, nc, S * nr).max(dim=2)   # [G, nc]
+            ok = gmax >= thr[:, 0].view(1, nc)
+            pos |= ((ov == gmax.view(G, 1, nc, 1)) & ok.view(G, 1, nc, 1)).any(dim=0)
+            # low-quality matches: anchor garg[k, j] of class j goes to target k (last k wins)
+            col = (garg // nr) * (nc * nr) + torch.arange(nc, device=dev).view(1, nc) * nr + garg % nr
+            ks = torch.arange(G, device=dev).view(G, 1).expand(G, nc)
+            win = torch.full((S * nc * nr,), -1, dtype=torch.long, device=dev)
+            win.scatter_reduce_(0, col[ok], ks[ok], reduce="amax")
+            arg = torch.where(win >= 0, win, arg.reshape(-1))
+            pos_l.append(pos.reshape(-1))
+            neg_l.append(neg.reshape(-1))
+            lab_l.append(torch.where(pos.reshape(-1), tl[arg].long(), torch.full_like(arg, head.num_classes)))
+            tgt = tb[arg]
+            box_l.append(head.bbox_coder.encode(anc, tgt))
+            yaw_l.append(tgt[:, -1])
+        return torch.cat(pos_l), torch.cat(neg_l), torch.cat(lab_l), torch.cat(box_l), torch.cat(yaw_l)
+
     def get_loss(self, results, inputs):
         """Focal + smooth-L1 (sin-difference) + direction CE
-        (point_pillars.py:140-206)."""
+        (point_pillars.py:140-206), on dense per-anchor masks: the same sums
+        as the reference's gathers over the selected anchors (avg_factor = the
+        number of positives; unnormalised sums when there are none)."""
+        scores, bboxes, dirs = results
+        head = self.bbox_head
+        pos, neg, labels, tboxes, tyaw = self.dense_targets(bboxes.shape[-2:], inputs.bboxes, inputs.labels)
+        scores = scores.permute(0, 2, 3, 1).reshape(-1, head.num_classes)
+        bboxes = bboxes.permute(0, 2, 3, 1).reshape(-1, head.box_code_size)
+        dirs = dirs.permute(0, 2, 3, 1).reshape(-1, 2)
+        npos = pos.sum().float()
+        sel = (pos | neg).float()
+        # focal loss (modules/losses/focal_loss.py) over pos | neg
+        fl = self.loss_cls
+        p = scores.sigmoid()
+        t = F.one_hot(labels.clamp(0, head.num_classes), head.num_classes + 1)[:, :head.num_classes].type_as(scores)
+        pt = (1 - p) * t + p * (1 - t)
+        w = (fl.alpha * t + (1 - fl.alpha) * (1 - t)) * pt.pow(fl.gamma)
+        cls_sum = (F.binary_cross_entropy_with_logits(scores, t, reduction="none") * w * fl.loss_weight
+                   * sel[:, None]).sum()
+        loss_cls = torch.where(npos > 0, cls_sum / npos.clamp(min=1), cls_sum)
+        valid = (pos & (labels >= 0) & (labels < head.num_classes)).float()
+        denom = npos.clamp(min=1)
+        # direction classification (cross entropy) on the valid positives
+        tdir = (limit_period(tyaw, 0, 2 * np.pi) / np.pi).long() % 2
+        loss_dir = (F.cross_entropy(dirs, tdir, reduction="none") * self.loss_dir.loss_weight * valid).sum() / denom
+        # smooth L1 on the sin-difference encoded boxes
+        r0 = torch.sin(bboxes[:, -1:]) * torch.cos(tboxes[:, -1:])
+        r1 = torch.cos(bboxes[:, -1:]) * torch.sin(tboxes[:, -1:])
+        d = torch.abs(torch.cat([bboxes[:, :-1], r0], -1) - torch.cat([tboxes[:, :-1], r1], -1))
+        beta = self.loss_bbox.beta
+        sl1 = torch.where(d < beta, 0.5 * d * d / beta, d - 0.5 * beta) * self.loss_bbox.loss_weight
+        loss_bbox = (sl1.sum(-1) * valid).sum() / denom
+        return {"loss_cls": loss_cls, "loss_bbox": loss_bbox, "loss_dir": loss_dir}
+
+    def get_loss_indexed(self, results, inputs):
+        """The reference's formulation (index lists from assign_bboxes); kept
+        to check the dense get_loss against."""
         scores, bboxes, dirs = results
         gt_labels, gt_bboxes = inputs.labels, inputs.bboxes
         head = self.bbox_head

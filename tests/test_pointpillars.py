@@ -73,3 +73,25 @@ def test_assign_bboxes_matches_reference_loop():
     ref = _loop_assign(head, (32, 32), tbs)
     for a, b in zip(ours, ref):
         assert a.shape == b.shape and torch.equal(a, b)
+
+
+def test_dense_loss_equals_indexed_loss():
+    """The dense per-anchor loss (no index lists) equals the reference's
+    index-list formulation on CPU, including a scene without targets and a
+    target of a label outside the classes."""
+    from o3dml_amd.pointpillars import PointPillars
+    torch.manual_seed(0)
+    m = PointPillars(**CFG).eval()
+    g = torch.Generator().manual_seed(1)
+    out = (torch.randn((3, 18, 32, 32), generator=g), 0.1 * torch.randn((3, 42, 32, 32), generator=g),
+           torch.randn((3, 12, 32, 32), generator=g))
+    tbs = [torch.from_numpy(G[f"bboxes_{i}"]) for i in range(2)] + [torch.zeros((0, 7))]
+    tls = [torch.from_numpy(G[f"labels_{i}"]) for i in range(2)] + [torch.zeros((0,), dtype=torch.long)]
+    tls[1] = tls[1].clone()
+    tls[1][0] = 3  # not one of the 3 classes
+    import types
+    inp = types.SimpleNamespace(bboxes=tbs, labels=tls)
+    a = m.get_loss(out, inp)
+    b = m.get_loss_indexed(out, inp)
+    for k in a:
+        assert torch.allclose(a[k], b[k], rtol=1e-5, atol=1e-7), (k, a[k], b[k])
