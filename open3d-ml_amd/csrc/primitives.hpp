@@ -119,7 +119,10 @@ void scan(const TIn* in, TOut* out, int64_t n, bool inclusive, Workspace& ws, hi
 // Stable LSD radix sort, 8-bit digits, 2048-key tiles.
 // ---------------------------------------------------------------------------
 constexpr int kRsBlock = 256;
-constexpr int kRsItems = 8;
+#ifndef O3DML_RS_ITEMS
+#define O3DML_RS_ITEMS 8
+#endif
+constexpr int kRsItems = O3DML_RS_ITEMS;
 constexpr int kRsTile = kRsBlock * kRsItems;
 constexpr int kRsWaves = kRsBlock / 64;
 
@@ -139,51 +142,64 @@ __global__ void __launch_bounds__(kRsBlock) radix_hist(const K* __restrict__ key
     hist[static_cast<int64_t>(threadIdx.x) * tiles + blockIdx.x] = h[threadIdx.x];
 }
 
-// Stable scatter: rows of 256 keys are ranked in order; inside a row the
-// rank is (earlier waves) + (earlier lanes with the same digit), found with
-// eight 64-bit ballots per key.  Keys are first placed in LDS in tile-local
-// digit order (tile digit offsets = exclusive scan of this tile's histogram),
-// then written out in LDS order: consecutive threads write consecutive
-// addresses of each digit run, so the global writes coalesce.
+// Stable scatter.  Each wave ranks its own contiguous 512 keys of the tile,
+// row by row (64 keys; peers with the same digit found with eight 64-bit
+// ballots), keeping its running per-digit counts in LDS — LDS operations of
+// one wave execute in order, so no barrier is needed between rows.  One
+// block scan then turns (digit, wave) counts into tile-local bases (tile
+// digit offset + counts of earlier waves: stable), the keys are placed in
+// LDS in tile-local digit order and written out so that consecutive threads
+// write consecutive addresses of each digit run (coalesced).  Four barriers
+// per tile.
 template <class K>
 __global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                           K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                           int64_t n, int shift,
                                                           const int64_t* __restrict__ offsets,
                                                           const uint32_t* __restrict__ hist, int64_t tiles) {
+    constexpr int kRowsPerWave = kRsItems * kRsBlock / 64 / kRsWaves;  // = kRsItems
     __shared__ uint32_t wcnt[kRsWaves][256];
-    __shared__ uint32_t running[256];
+    __shared__ uint32_t wsum[kRsWaves];
     __shared__ uint32_t toff[256];
     __shared__ int64_t goff[256];
     __shared__ K lkey[kRsTile];
     __shared__ uint32_t lval[kRsTile];
     const int t = threadIdx.x;
     const int w = wave_id();
+    const int lane = lane_id();
     const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile;
     const int tile_n = static_cast<int>(n - base < kRsTile ? n - base : kRsTile);
     {
         // tile digit offsets: exclusive scan of this tile's histogram
         const uint32_t c = hist[static_cast<int64_t>(t) * tiles + blockIdx.x];
         const uint32_t inc = wave_inclusive_scan(c);
-        if (lane_id() == 63) wcnt[0][w] = inc;
-        __syncthreads();
-        uint32_t before = 0;
-        for (int ww = 0; ww < w; ++ww) before += wcnt[0][ww];
-        toff[t] = before + inc - c;
-        goff[t] = offsets[static_cast<int64_t>(t) * tiles + blockIdx.x];
-        running[t] = 0;
-        __syncthreads();
+        if (lane == 63) wsum[w] = inc;
 #pragma unroll
         for (int ww = 0; ww < kRsWaves; ++ww) wcnt[ww][t] = 0;
+        goff[t] = offsets[static_cast<int64_t>(t) * tiles + blockIdx.x];
         __syncthreads();
+        uint32_t before = 0;
+        for (int ww = 0; ww < w; ++ww) before += wsum[ww];
+        toff[t] = before + inc - c;
     }
+    // phase 1: each wave ranks its rows in order, counts per digit in LDS
     const uint64_t lt = lanemask_lt();
-    for (int r = 0; r < kRsItems; ++r) {
-        const int64_t i = base + r * kRsBlock + t;
+    K key[kRowsPerWave];
+    uint32_t val[kRowsPerWave], loff[kRowsPerWave];
+    uint32_t dig[kRowsPerWave];
+#pragma unroll
+    for (int r = 0; r < kRowsPerWave; ++r) {
+        const int64_t i = base + (static_cast<int64_t>(w) * kRowsPerWave + r) * 64 + lane;
         const bool valid = i < n;
-        const K key = valid ? kin[i] : K(0);
-        const uint32_t val = valid ? (vin ? vin[i] : static_cast<uint32_t>(i)) : 0u;
-        const uint32_t d = static_cast<uint32_t>(key >> shift) & 255u;
+        key[r] = valid ? kin[i] : K(0);
+        val[r] = valid ? (vin ? vin[i] : static_cast<uint32_t>(i)) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kRowsPerWave; ++r) {
+        const int64_t i = base + (static_cast<int64_t>(w) * kRowsPerWave + r) * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = static_cast<uint32_t>(key[r] >> shift) & 255u;
+        dig[r] = d;
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -192,34 +208,39 @@ __global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* __restrict__ 
             peers &= bit ? m : ~m;
         }
         const uint32_t rank = __popcll(peers & lt);
-        if (valid && rank == 0) wcnt[w][d] = __popcll(peers);
-        __syncthreads();
-        {
-            uint32_t acc = running[t];
-#pragma unroll
-            for (int ww = 0; ww < kRsWaves; ++ww) {
-                const uint32_t c = wcnt[ww][t];
-                wcnt[ww][t] = acc;
-                acc += c;
-            }
-            running[t] = acc;
-        }
-        __syncthreads();
-        if (valid) {
-            const uint32_t lp = toff[d] + wcnt[w][d] + rank;
-            lkey[lp] = key;
-            lval[lp] = val;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int ww = 0; ww < kRsWaves; ++ww) wcnt[ww][t] = 0;
-        __syncthreads();
+        const uint32_t before = valid ? wcnt[w][d] : 0u;
+        loff[r] = before + rank;
+        if (valid && rank == 0) wcnt[w][d] = before + static_cast<uint32_t>(__popcll(peers));
     }
+    __syncthreads();
+    // phase 2: (digit, wave) counts -> tile-local bases
+    {
+        uint32_t acc = toff[t];
+#pragma unroll
+        for (int ww = 0; ww < kRsWaves; ++ww) {
+            const uint32_t c = wcnt[ww][t];
+            wcnt[ww][t] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    // phase 3: place in tile-local digit order
+#pragma unroll
+    for (int r = 0; r < kRowsPerWave; ++r) {
+        const int64_t i = base + (static_cast<int64_t>(w) * kRowsPerWave + r) * 64 + lane;
+        if (i < n) {
+            const uint32_t lp = wcnt[w][dig[r]] + loff[r];
+            lkey[lp] = key[r];
+            lval[lp] = val[r];
+        }
+    }
+    __syncthreads();
+    // phase 4: coalesced runs out
     for (int j = t; j < tile_n; j += kRsBlock) {
-        const K key = lkey[j];
-        const uint32_t d = static_cast<uint32_t>(key >> shift) & 255u;
+        const K k2 = lkey[j];
+        const uint32_t d = static_cast<uint32_t>(k2 >> shift) & 255u;
         const int64_t pos = goff[d] + (j - static_cast<int64_t>(toff[d]));
-        kout[pos] = key;
+        kout[pos] = k2;
         vout[pos] = lval[j];
     }
 }
