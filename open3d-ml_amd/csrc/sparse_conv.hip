@@ -92,6 +92,40 @@ __global__ void recip_norm_kernel(const float* __restrict__ norm, const float* _
     }
 }
 
+// --------------------------------------------------------------------------
+// tile order: the GEMM wave walks the UNION of the offsets its 32 rows use, so
+// rows with different neighbour masks in one tile cost MFMA work on zero
+// operands (C4 room voxels in voxelize order: 67 % useful).  The rows are
+// stably sorted by a 16-bit hash of their offset mask once per map; tiles then
+// take 32 consecutive rows of that order (98 % useful), spatial order kept
+// within a mask class.  Absent offsets only ever added exact zeros, so the
+// per-row sums are unchanged.
+// --------------------------------------------------------------------------
+constexpr int64_t kOrderMinRows = 2048;
+static bool use_order(int64_t n, int K) { return K > 8 && n >= kOrderMinRows; }
+
+__global__ void mask_keys_kernel(const int32_t* __restrict__ map, int64_t n, int K, uint32_t* __restrict__ keys) {
+    for (int64_t o = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; o < n;
+         o += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        uint32_t m = 0u;
+        for (int k = 0; k < K; ++k) m |= (map[o * K + k] >= 0 ? 1u : 0u) << k;
+        keys[o] = (m * 0x9E3779B1u) >> 16;
+    }
+}
+
+static size_t order_scratch_bytes(int64_t n) {
+    return 2 * ws_bytes<uint32_t>(n) + prim::radix_sort_workspace_bytes<uint32_t>(n);
+}
+
+static void build_order(const int32_t* map, int64_t n, int K, int32_t* order, Workspace scratch, hipStream_t st) {
+    if (!use_order(n, K)) return;
+    uint32_t* kin = scratch.take<uint32_t>(n);
+    uint32_t* kout = scratch.take<uint32_t>(n);
+    mask_keys_kernel<<<stream_grid(n, 256), 256, 0, st>>>(map, n, K, kin);
+    O3DML_LAUNCH_CHECK();
+    prim::radix_sort_pairs<uint32_t>(kin, nullptr, kout, reinterpret_cast<uint32_t*>(order), n, 16, scratch, st);
+}
+
 // W [K][Cin][Cout] -> Wt [K][Cout][Cin]
 __global__ void transpose_filters_kernel(const float* __restrict__ w, int K, int cin, int cout, float* __restrict__ wt) {
     const int64_t total = static_cast<int64_t>(K) * cin * cout;
@@ -183,7 +217,8 @@ __device__ __forceinline__ void gemm_finish(GemmStage& st, int c0, int h, const 
 
 template <bool VEC4, bool PRE>
 __global__ void __launch_bounds__(kGemmThreads)
-implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, const float* __restrict__ src,
+implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, int K, int64_t n_out,
+                     const float* __restrict__ src,
                      const float* __restrict__ sscale, const float* __restrict__ pscale,
                      const float* __restrict__ W /*[K][cin][cout]*/, int cin, int cout,
                      const float* __restrict__ oscale, const float* __restrict__ bias, float* __restrict__ out,
@@ -203,13 +238,30 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
     if (o0 >= n_out) return;  // whole wave; no barriers below
     const int i = lane & 31, h = lane >> 5;
     const int col = blockIdx.y * 32 + i;
-    const int64_t o = o0 + i;
-    // the wave's 32 map rows -> LDS (one coalesced sweep), offsets in use
+    // the wave's 32 rows: positions o0.. of the tile order (identity without
+    // one); their output row ids and map rows -> LDS, offsets in use
     __shared__ int32_t mtile_all[kGemmThreads / 64][32 * 32];
+    __shared__ int32_t orow_all[kGemmThreads / 64][32];
     int32_t* mtile = mtile_all[threadIdx.x >> 6];
-    for (int e = lane; e < 32 * K; e += 64) {
-        const int64_t oo = o0 + e / K;
-        mtile[e] = oo < n_out ? map[o0 * K + e] : -1;
+    int32_t* orow = orow_all[threadIdx.x >> 6];
+    if (lane < 32) {
+        const int64_t oo = o0 + lane;
+        orow[lane] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (order) {
+        for (int e = lane; e < 32 * K; e += 64) {
+            const int rr = e / K;
+            const int32_t orr = orow[rr];
+            mtile[e] = orr >= 0 ? map[static_cast<int64_t>(orr) * K + (e - rr * K)] : -1;
+        }
+    } else {
+        for (int e = lane; e < 32 * K; e += 64) {
+            const int64_t oo = o0 + e / K;
+            mtile[e] = oo < n_out ? map[o0 * K + e] : -1;
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -220,6 +272,7 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
         used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
     }
     used |= __builtin_amdgcn_readlane(used, 32) | __builtin_amdgcn_readlane(used, 0);
+    const int64_t o = orow[i] >= 0 ? orow[i] : 0;  // this lane's output row (pair scales)
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -258,8 +311,8 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
         float* P = part + static_cast<int64_t>(s) * n_out * cout;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int64_t orr = o0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (orr < n_out && col < cout) P[orr * cout + col] = acc[r];
+            const int64_t orr = orow[(r & 3) + 8 * (r >> 2) + 4 * h];
+            if (orr >= 0 && col < cout) P[orr * cout + col] = acc[r];
         }
         return;
     }
@@ -267,8 +320,8 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out, cons
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int64_t orr = o0 + row;
-        if (orr < n_out && col < cout) {
+        const int64_t orr = orow[row];
+        if (orr >= 0 && col < cout) {
             float v = acc[r];
             if (oscale) v *= oscale[orr];
             if (bias) v += bias[col];
@@ -483,7 +536,8 @@ static size_t gemm_split_bytes(int64_t n_out, int K, int cin, int cout) {
     return ns > 1 ? ws_bytes<float>(ns * n_out * cout) : 0;
 }
 
-static void run_gemm(hipStream_t st, const int32_t* map, int K, int64_t n_out, const float* src, const float* sscale,
+static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, int K, int64_t n_out, const float* src,
+                     const float* sscale,
                      const float* pscale, const float* W, int cin, int cout, const float* oscale, const float* bias,
                      float* out, float* part, size_t part_bytes, GemmPrologue pre = {nullptr, nullptr},
                      const float* residual = nullptr) {
@@ -495,7 +549,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, int K, int64_t n_out, c
                  static_cast<unsigned>(ceil_div(cout, 32)), static_cast<unsigned>(ns));
     O3DML_REQUIRE(pre.scale == nullptr || cin <= kPreMax, "sparse_conv: prologue needs cin <= %d", kPreMax);
 #define O3DML_GEMM_LAUNCH(V, P)                                                                                    \
-    implicit_gemm_kernel<V, P><<<g, kGemmThreads, 0, st>>>(map, K, n_out, src, sscale, pscale, W, cin, cout, oscale, \
+    implicit_gemm_kernel<V, P><<<g, kGemmThreads, 0, st>>>(map, order, K, n_out, src, sscale, pscale, W, cin, cout, oscale, \
                                                            bias, out, ns, part, pre, residual)
     if (pre.scale) {
         if (vec4) O3DML_GEMM_LAUNCH(true, true); else O3DML_GEMM_LAUNCH(false, true);
@@ -730,7 +784,22 @@ using namespace o3dml;
 // ---------------------------------------------------------------------------
 O3DML_API size_t o3dml_sparse_conv_map_workspace_size(int64_t n_out, int64_t n_in, int K) {
     return ws_bytes<int32_t>(n_out * K) + ws_bytes<float>(n_out * K) + ws_bytes<float>(n_out) +
-           ws_bytes<float>(n_out) + ws_bytes<int32_t>(n_in * K) + ws_bytes<float>(n_in * K) + ws_bytes<int>(4);
+           ws_bytes<float>(n_out) + ws_bytes<int32_t>(n_in * K) + ws_bytes<float>(n_in * K) + ws_bytes<int>(4) +
+           ws_bytes<int32_t>(n_out) + ws_bytes<int32_t>(n_in) + order_scratch_bytes(std::max(n_out, n_in));
+}
+
+// Tile orders of the map and the inverse map (after the status words) and the
+// scratch their sorts use.
+struct MapOrders {
+    int32_t* order;
+    int32_t* iorder;
+    Workspace scratch;
+};
+
+static MapOrders map_orders(Workspace& ws, int64_t n_out, int64_t n_in) {
+    int32_t* order = ws.take<int32_t>(n_out);
+    int32_t* iorder = ws.take<int32_t>(n_in);
+    return MapOrders{order, iorder, Workspace(ws.base + ws.used, ws.size - ws.used)};
 }
 
 // Builds the dense kernel map (and, with want_inverse, the inverse map used by
@@ -756,6 +825,7 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
     int32_t* inv = ws.take<int32_t>(n_in * K);
     float* ipscale = ws.take<float>(n_in * K);
     int* status = ws.take<int>(4);
+    MapOrders ord = map_orders(ws, n_out, n_in);
     O3DML_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, st));
     if (n_out > 0) {
         O3DML_CHECK_HIP(hipMemsetAsync(map, 0xff, sizeof(int32_t) * n_out * K, st));
@@ -775,7 +845,9 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
                     neighbors_importance ? ipscale : nullptr, status);
             O3DML_LAUNCH_CHECK();
         }
+        build_order(inv, n_in, K, ord.iorder, ord.scratch, st);
     }
+    build_order(map, n_out, K, ord.order, ord.scratch, st);
     O3DML_CHECK_HIP(hipMemcpyAsync(status_host, status, sizeof(int), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
     O3DML_GUARD_END
@@ -817,6 +889,7 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     int32_t* inv = ws.take<int32_t>(n_in * K);
     float* ipscale = ws.take<float>(n_in * K);
     int* status = ws.take<int>(4);
+    MapOrders ord = map_orders(ws, n_out, n_in);
     (void)pscale;
     (void)ipscale;
     *status_host = 0;
@@ -861,7 +934,9 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
         build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, nullptr, n_out, K, inv, nullptr,
                                                                             status);
         O3DML_LAUNCH_CHECK();
+        build_order(inv, n_in, K, ord.iorder, ord.scratch, st);
     }
+    build_order(map, n_out, K, ord.order, ord.scratch, st);
     if (defer_status) return 0;  // status stays on the device (o3dml_sparse_conv_map_status_offset)
     O3DML_CHECK_HIP(hipMemcpyAsync(status_host, status, sizeof(int), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
@@ -869,7 +944,8 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
 }
 
 static void map_views(void* workspace, size_t bytes, int64_t n_out, int64_t n_in, int K, int32_t** map,
-                      float** pscale, float** oscale, int32_t** inv, float** ipscale) {
+                      float** pscale, float** oscale, int32_t** inv, float** ipscale, const int32_t** order,
+                      const int32_t** iorder) {
     Workspace ws(workspace, bytes);
     *map = ws.take<int32_t>(n_out * K);
     *pscale = ws.take<float>(n_out * K);
@@ -877,6 +953,10 @@ static void map_views(void* workspace, size_t bytes, int64_t n_out, int64_t n_in
     *oscale = ws.take<float>(n_out);
     *inv = ws.take<int32_t>(n_in * K);
     *ipscale = ws.take<float>(n_in * K);
+    ws.take<int>(4);
+    const MapOrders ord = map_orders(ws, n_out, n_in);
+    *order = use_order(n_out, K) ? ord.order : nullptr;
+    *iorder = use_order(n_in, K) ? ord.iorder : nullptr;
 }
 
 // Forward with an input prologue and a residual epilogue (SparseConvUnet eval:
@@ -892,8 +972,10 @@ O3DML_API int o3dml_sparse_conv_forward_fused(const float* filters, int K, int c
     O3DML_REQUIRE((pre_scale == nullptr) == (pre_shift == nullptr), "pre_scale and pre_shift go together");
     int32_t *map, *inv;
     float *pscale, *oscale, *ipscale;
-    map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale);
-    run_gemm(as_stream(stream), map, K, n_out, inp_features, nullptr, nullptr, filters, cin, cout, nullptr, bias,
+    const int32_t *order, *iorder;
+    map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
+              &iorder);
+    run_gemm(as_stream(stream), map, order, K, n_out, inp_features, nullptr, nullptr, filters, cin, cout, nullptr, bias,
              out_features, static_cast<float*>(workspace), workspace_bytes, GemmPrologue{pre_scale, pre_shift},
              residual);
     O3DML_GUARD_END
@@ -915,8 +997,10 @@ O3DML_API int o3dml_sparse_conv_forward(const float* filters, int K, int cin, in
     O3DML_GUARD_BEGIN
     int32_t *map, *inv;
     float *pscale, *oscale, *ipscale;
-    map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale);
-    run_gemm(as_stream(stream), map, K, n_out, inp_features, inp_importance, has_neighbors_importance ? pscale : nullptr,
+    const int32_t *order, *iorder;
+    map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
+              &iorder);
+    run_gemm(as_stream(stream), map, order, K, n_out, inp_features, inp_importance, has_neighbors_importance ? pscale : nullptr,
              filters, cin, cout, use_out_scale ? oscale : nullptr, bias, out_features,
              static_cast<float*>(workspace), workspace_bytes);
     O3DML_GUARD_END
@@ -951,7 +1035,9 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
     hipStream_t st = as_stream(stream);
     int32_t *map, *inv;
     float *pscale, *oscale, *ipscale;
-    map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale);
+    const int32_t *order, *iorder;
+    map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
+              &iorder);
     Workspace ws(workspace, workspace_bytes);
     float* wt = ws.take<float>(static_cast<int64_t>(K) * cin * cout);
     float* g = ws.take<float>(n_out * cout);  // unused slot kept for layout stability
@@ -966,7 +1052,7 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
         O3DML_LAUNCH_CHECK();
         // the per-row out-scale belongs to the gathered rows (source = grad_out):
         // fold it in as sscale; pair importance via the inverse pscale.
-        run_gemm(st, inv, K, n_in, grad_out, os, has_neighbors_importance ? ipscale : nullptr, wt, cout, cin,
+        run_gemm(st, inv, iorder, K, n_in, grad_out, os, has_neighbors_importance ? ipscale : nullptr, wt, cout, cin,
                  inp_importance, nullptr, grad_inp, split, split_bytes);
     }
     if (grad_filters) {
