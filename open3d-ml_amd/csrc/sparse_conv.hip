@@ -150,7 +150,8 @@ __global__ void transpose_filters_kernel(const float* __restrict__ w, int K, int
 // --------------------------------------------------------------------------
 struct GemmStage {
     float a[16], b[16];
-    float sc;  // row factor (importance x pair scale; 0 for a missing neighbour)
+    float s1, s2;  // row importance, pair scale (1 without them)
+    float v;       // 1 for a present neighbour, 0 for a missing one
 };
 
 // Optional prologue on the gathered rows (eval-mode BatchNorm + ReLU of the
@@ -172,18 +173,21 @@ __device__ __forceinline__ float pre_act(float v, float s, float b) { return fma
 // the stage's loads instead of keeping them in flight.  All arithmetic on the
 // loaded values happens in gemm_finish, after the previous stage's MFMAs.
 __device__ __attribute__((aligned(16))) float g_zero_page[16];
+__device__ float g_one_page[1] = {1.f};
 
 template <bool VEC4>
 __device__ __forceinline__ void gemm_load(GemmStage& st, int32_t m, int K, int64_t o, int k, int c0, int h, int col,
                                           const float* __restrict__ src, const float* __restrict__ sscale,
-                                          const float* __restrict__ pscale, const float* __restrict__ W, int cin,
-                                          int cout) {
+                                          const float* __restrict__ pscale, const float* __restrict__ Wt, int cin,
+                                          int cout, bool live = true) {
     const int cb = c0 + 16 * h;
     const bool valid = m >= 0;
     const int64_t mr = valid ? m : 0;
-    float sc = sscale ? sscale[mr] : 1.f;
-    if (pscale) sc *= pscale[(valid ? o : 0) * K + k];
-    st.sc = valid ? sc : 0.f;
+    // scales: pointer selects (no branch, so the waitcnt placement stays exact);
+    // they are uniform per launch, the loads hit a one-word page without them
+    st.s1 = *(sscale ? sscale + mr : g_one_page);
+    st.s2 = *(pscale ? pscale + (valid ? o : 0) * K + k : g_one_page);
+    st.v = valid ? 1.f : 0.f;
     const float* row = src + mr * cin;
     if (VEC4) {  // cin % 4 == 0: float4 granules
 #pragma unroll
@@ -199,20 +203,32 @@ __device__ __forceinline__ void gemm_load(GemmStage& st, int32_t m, int K, int64
 #pragma unroll
         for (int s = 0; s < 16; ++s) st.a[s] = *((valid && cb + s < cin) ? row + cb + s : g_zero_page);
     }
-    const float* wk = W + static_cast<int64_t>(k) * cin * cout + col;
-    const bool colv = col < cout;
+    // B from the transposed filters Wt[k][col][c]: column col's 16 weights are
+    // contiguous, so the same four 16-B loads as the A side
+    const bool colv = live && col < cout;  // a dead stage reads only the zero page
+    const float* wr = Wt + (static_cast<int64_t>(k) * cout + (colv ? col : 0)) * cin;
+    if (VEC4) {
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-        const int c = cb + s;
-        st.b[s] = *((c < cin && colv) ? wk + static_cast<int64_t>(c) * cout : g_zero_page);
+        for (int q = 0; q < 4; ++q) {
+            const int c = cb + 4 * q;
+            const float4 v = *reinterpret_cast<const float4*>((colv && c < cin) ? wr + c : g_zero_page);
+            st.b[4 * q] = v.x;
+            st.b[4 * q + 1] = v.y;
+            st.b[4 * q + 2] = v.z;
+            st.b[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) st.b[s] = *((colv && cb + s < cin) ? wr + cb + s : g_zero_page);
     }
 }
 
 template <bool PRE>
 __device__ __forceinline__ void gemm_finish(GemmStage& st, int c0, int h, const float* lps, const float* lpb) {
     const int cb = c0 + 16 * h;
+    const float sc = st.v != 0.f ? st.s1 * st.s2 : 0.f;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) st.a[s] = (PRE ? pre_act(st.a[s], lps[cb + s], lpb[cb + s]) : st.a[s]) * st.sc;
+    for (int s = 0; s < 16; ++s) st.a[s] = (PRE ? pre_act(st.a[s], lps[cb + s], lpb[cb + s]) : st.a[s]) * sc;
 }
 
 template <bool VEC4, bool PRE>
@@ -220,7 +236,7 @@ __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, int K, int64_t n_out,
                      const float* __restrict__ src,
                      const float* __restrict__ sscale, const float* __restrict__ pscale,
-                     const float* __restrict__ W /*[K][cin][cout]*/, int cin, int cout,
+                     const float* __restrict__ Wt /*[K][cout][cin]*/, int cin, int cout,
                      const float* __restrict__ oscale, const float* __restrict__ bias, float* __restrict__ out,
                      int nsplit, float* __restrict__ part, GemmPrologue pre, const float* __restrict__ residual) {
     __shared__ float lpre[PRE ? 2 * (kPreMax + 32) : 1];
@@ -286,25 +302,45 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict_
     if (j0 < j1) {
         unsigned u = used;
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
-        GemmStage cur, nxt;
-        int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
-        gemm_load<VEC4>(cur, mtile[i * K + k], K, o, k, c0, h, col, src, sscale, pscale, W, cin, cout);
-        for (int j = j0 + 1;; ++j) {
-            int nk = k, nc = c0 + 32;
-            if (nc >= cin) {
-                nc = 0;
+        // two stage buffers in ping-pong (no register copy between stages, so
+        // the loads of stage j+1 stay in flight under the MFMAs of stage j)
+        auto advance = [&](int& kk, int& cc) {
+            cc += 32;
+            if (cc >= cin) {
+                cc = 0;
                 u &= u - 1u;
-                nk = u ? __builtin_ctz(u) : -1;
+                kk = u ? __builtin_ctz(u) : 0;
             }
-            const bool more = j < j1;
-            if (more) gemm_load<VEC4>(nxt, mtile[i * K + nk], K, o, nk, nc, h, col, src, sscale, pscale, W, cin, cout);
-            gemm_finish<PRE>(cur, c0, h, lps, lpb);
+        };
+        GemmStage sa, sb;
+        int ka = __builtin_ctz(u), ca = (j0 % nch) * 32, kb = 0, cb = 0;
+        gemm_load<VEC4>(sa, mtile[i * K + ka], K, o, ka, ca, h, col, src, sscale, pscale, Wt, cin, cout);
+        for (int j = j0;; j += 2) {
+            kb = ka;
+            cb = ca;
+            advance(kb, cb);
+            // loads are issued unconditionally (a stage past the end reads the zero
+            // page): a skipped load on one path makes the compiler's wait counts
+            // conservative at the join and the MFMAs would wait for these loads
+            const bool lb = j + 1 < j1;
+            gemm_load<VEC4>(sb, lb ? mtile[i * K + kb] : -1, K, o, kb, cb, h, col, src, sscale, pscale, Wt, cin, cout,
+                            lb);
+            __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs
+            gemm_finish<PRE>(sa, ca, h, lps, lpb);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[r], cur.b[r], acc, 0, 0, 0);
-            if (!more) break;
-            k = nk;
-            c0 = nc;
-            cur = nxt;
+            for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sa.a[r], sa.b[r], acc, 0, 0, 0);
+            if (j + 1 >= j1) break;
+            ka = kb;
+            ca = cb;
+            advance(ka, ca);
+            const bool la = j + 2 < j1;
+            gemm_load<VEC4>(sa, la ? mtile[i * K + ka] : -1, K, o, ka, ca, h, col, src, sscale, pscale, Wt, cin, cout,
+                            la);
+            __builtin_amdgcn_sched_barrier(0);
+            gemm_finish<PRE>(sb, cb, h, lps, lpb);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sb.a[r], sb.b[r], acc, 0, 0, 0);
+            if (j + 2 >= j1) break;
         }
     }
     if (nsplit > 1) {  // raw partial sums; split_reduce_kernel applies oscale / bias / residual
@@ -321,6 +357,190 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict_
     for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
         const int64_t orr = orow[row];
+        if (orr >= 0 && col < cout) {
+            float v = acc[r];
+            if (oscale) v *= oscale[orr];
+            if (bias) v += bias[col];
+            if (residual) v += residual[orr * cout + col];
+            out[orr * cout + col] = v;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// implicit GEMM, LDS-staged (cin % 4 == 0, the common case): the same tiles,
+// stage order and MFMA reduction order as implicit_gemm_kernel (so the same
+// fp32 sums bit for bit), but each stage's operands travel global -> LDS as
+// full 128-B lines with global_load_lds_dwordx4 (8 lanes per row, 8 rows per
+// instruction) instead of fragment-shaped 16-B loads (32 rows x 16 B per
+// instruction, every line touched by 4 instructions): 4x fewer L1 accesses
+// per stage, which bounded the register-staged kernel (PMC: 512 TCP accesses
+// per 16-MFMA stage, MFMA pipes 34 % busy at 128 channels).
+// LDS image per operand: [32 rows][8 pieces of 16 B], piece p of row r in slot
+// p ^ (r & 7) — the swizzle sits on the global source address because the
+// DMA's LDS destination is lane-linear — read back in the MFMA layout with
+// ds_read_b128 (lane (i, h): pieces 4h .. 4h+3 of row i), conflict-free over
+// any 8 consecutive rows.  One buffer per operand and wave: stage j is read
+// into registers, then stage j+1's DMA is issued into the same buffer and
+// runs under stage j's 16 MFMAs.
+// --------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+__device__ __forceinline__ void glds16(const float* g, float* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds(g, (lds_void_ptr)(lds_wave_base), 16, 0, 0);
+}
+
+// DMA of one stage (offset k, channels [c0, c0+32)) into abuf / bbuf, plus the
+// row factors of lane (i, h)'s row i into st.
+__device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_t* mtile, int K, int k, int c0,
+                                          int lane, int64_t o, int i, int col0, const float* __restrict__ src,
+                                          const float* __restrict__ sscale, const float* __restrict__ pscale,
+                                          const float* __restrict__ Wt, int cin, int cout, bool live, GemmStage& st) {
+    const int sl = lane & 7;
+    // all LDS reads of the map first (a DMA in between would order after them)
+    int32_t mq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) mq[q] = live ? mtile[(8 * q + (lane >> 3)) * K + k] : -1;
+    const int32_t mi = live ? mtile[i * K + k] : -1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int r = 8 * q + (lane >> 3);
+        const int c = c0 + 4 * (sl ^ (r & 7));
+        const int32_t m = mq[q];
+        const float* ga = (m >= 0 && c < cin) ? src + static_cast<int64_t>(m) * cin + c : g_zero_page;
+        glds16(ga, abuf + 256 * q);
+        const int cc = col0 + r;
+        const float* gb = (live && cc < cout && c < cin) ? Wt + (static_cast<int64_t>(k) * cout + cc) * cin + c
+                                                          : g_zero_page;
+        glds16(gb, bbuf + 256 * q);
+    }
+    const bool valid = mi >= 0;
+    st.s1 = *(sscale ? sscale + (valid ? mi : 0) : g_one_page);
+    st.s2 = *(pscale ? pscale + (valid ? o : 0) * K + k : g_one_page);
+    st.v = valid ? 1.f : 0.f;
+}
+
+__device__ __forceinline__ void lds_read(const float* abuf, const float* bbuf, int i, int h, GemmStage& st) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int slot = (4 * h + q) ^ (i & 7);
+        const float4 va = *reinterpret_cast<const float4*>(abuf + 32 * i + 4 * slot);
+        const float4 vb = *reinterpret_cast<const float4*>(bbuf + 32 * i + 4 * slot);
+        st.a[4 * q] = va.x;
+        st.a[4 * q + 1] = va.y;
+        st.a[4 * q + 2] = va.z;
+        st.a[4 * q + 3] = va.w;
+        st.b[4 * q] = vb.x;
+        st.b[4 * q + 1] = vb.y;
+        st.b[4 * q + 2] = vb.z;
+        st.b[4 * q + 3] = vb.w;
+    }
+}
+
+template <bool PRE>
+__global__ void __launch_bounds__(kGemmThreads)
+implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, int K, int64_t n_out,
+                         const float* __restrict__ src, const float* __restrict__ sscale,
+                         const float* __restrict__ pscale, const float* __restrict__ Wt /*[K][cout][cin]*/, int cin,
+                         int cout, const float* __restrict__ oscale, const float* __restrict__ bias,
+                         float* __restrict__ out, int nsplit, float* __restrict__ part, GemmPrologue pre,
+                         const float* __restrict__ residual) {
+    __shared__ float lpre[PRE ? 2 * (kPreMax + 32) : 1];
+    __shared__ __attribute__((aligned(16))) float stage_all[kGemmThreads / 64][2][32 * 32];
+    __shared__ int32_t mtile_all[kGemmThreads / 64][32 * 32];
+    __shared__ int32_t orow_all[kGemmThreads / 64][32];
+    float* lps = lpre;
+    float* lpb = lpre + (PRE ? kPreMax + 32 : 0);
+    if (PRE) {
+        for (int c = threadIdx.x; c < kPreMax + 32; c += kGemmThreads) {
+            lps[c] = c < cin ? pre.scale[c] : 0.f;
+            lpb[c] = c < cin ? pre.shift[c] : 0.f;
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int64_t o0 = (static_cast<int64_t>(blockIdx.x) * (kGemmThreads / 64) + w) * 32;
+    if (o0 >= n_out) return;  // whole wave; no barriers below
+    const int i = lane & 31, h = lane >> 5;
+    const int col0 = blockIdx.y * 32;
+    const int col = col0 + i;
+    int32_t* mtile = mtile_all[w];
+    int32_t* orow = orow_all[w];
+    float* abuf = stage_all[w][0];
+    float* bbuf = stage_all[w][1];
+    if (lane < 32) {
+        const int64_t oo = o0 + lane;
+        orow[lane] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int e = lane; e < 32 * K; e += 64) {
+        const int rr = e / K;
+        const int32_t orr = orow[rr];
+        mtile[e] = orr >= 0 ? map[static_cast<int64_t>(orr) * K + (e - rr * K)] : -1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    unsigned used = 0u;
+    for (int k = h; k < K; k += 2) {
+        const uint64_t b = __ballot(mtile[i * K + k] >= 0);
+        used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
+    }
+    used = __builtin_amdgcn_readlane(used, 32) | __builtin_amdgcn_readlane(used, 0);
+    const int64_t o = orow[i] >= 0 ? orow[i] : 0;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int nch = (cin + 31) >> 5;
+    const int nst = __builtin_popcount(used) * nch;
+    const int s = blockIdx.z;
+    const int j0 = static_cast<int>(static_cast<int64_t>(s) * nst / nsplit);
+    const int j1 = static_cast<int>(static_cast<int64_t>(s + 1) * nst / nsplit);
+    if (j0 < j1) {
+        unsigned u = used;
+        for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
+        int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
+        GemmStage nx, cu;
+        lds_issue(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout, true, nx);
+        for (int j = j0; j < j1; ++j) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage j in LDS, its row factors in nx
+            lds_read(abuf, bbuf, i, h, cu);
+            cu.s1 = nx.s1;
+            cu.s2 = nx.s2;
+            cu.v = nx.v;
+            const int kj = k, cj = c0;
+            c0 += 32;
+            if (c0 >= cin) {
+                c0 = 0;
+                u &= u - 1u;
+                k = u ? __builtin_ctz(u) : 0;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffer read out before the next DMA
+            lds_issue(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout, j + 1 < j1,
+                      nx);
+            __builtin_amdgcn_sched_barrier(0);
+            (void)kj;
+            gemm_finish<PRE>(cu, cj, h, lps, lpb);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cu.a[r], cu.b[r], acc, 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead DMA has landed before the wave exits
+    }
+    if (nsplit > 1) {
+        float* P = part + static_cast<int64_t>(s) * n_out * cout;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t orr = orow[(r & 3) + 8 * (r >> 2) + 4 * h];
+            if (orr >= 0 && col < cout) P[orr * cout + col] = acc[r];
+        }
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t orr = orow[(r & 3) + 8 * (r >> 2) + 4 * h];
         if (orr >= 0 && col < cout) {
             float v = acc[r];
             if (oscale) v *= oscale[orr];
@@ -538,20 +758,34 @@ static size_t gemm_split_bytes(int64_t n_out, int K, int cin, int cout) {
 
 static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, int K, int64_t n_out, const float* src,
                      const float* sscale,
-                     const float* pscale, const float* W, int cin, int cout, const float* oscale, const float* bias,
+                     const float* pscale, const float* Wt, int cin, int cout, const float* oscale, const float* bias,
                      float* out, float* part, size_t part_bytes, GemmPrologue pre = {nullptr, nullptr},
                      const float* residual = nullptr) {
     if (n_out == 0 || cout == 0) return;
-    const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0;
+    const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0 &&
+                      (reinterpret_cast<uintptr_t>(Wt) % 16) == 0;
     int ns = gemm_splits(n_out, K, cin, cout);
     if (!part || part_bytes < sizeof(float) * static_cast<size_t>(ns) * n_out * cout) ns = 1;
     const dim3 g(static_cast<unsigned>(ceil_div(n_out, 32 * (kGemmThreads / 64))),
                  static_cast<unsigned>(ceil_div(cout, 32)), static_cast<unsigned>(ns));
     O3DML_REQUIRE(pre.scale == nullptr || cin <= kPreMax, "sparse_conv: prologue needs cin <= %d", kPreMax);
 #define O3DML_GEMM_LAUNCH(V, P)                                                                                    \
-    implicit_gemm_kernel<V, P><<<g, kGemmThreads, 0, st>>>(map, order, K, n_out, src, sscale, pscale, W, cin, cout, oscale, \
+    implicit_gemm_kernel<V, P><<<g, kGemmThreads, 0, st>>>(map, order, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, \
                                                            bias, out, ns, part, pre, residual)
-    if (pre.scale) {
+    static const bool lds_path = [] {
+        const char* e = std::getenv("O3DML_GEMM_LDS");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    if (vec4 && lds_path) {
+        if (pre.scale)
+            implicit_gemm_lds_kernel<true><<<g, kGemmThreads, 0, st>>>(map, order, K, n_out, src, sscale, pscale, Wt,
+                                                                      cin, cout, oscale, bias, out, ns, part, pre,
+                                                                      residual);
+        else
+            implicit_gemm_lds_kernel<false><<<g, kGemmThreads, 0, st>>>(map, order, K, n_out, src, sscale, pscale, Wt,
+                                                                       cin, cout, oscale, bias, out, ns, part, pre,
+                                                                       residual);
+    } else if (pre.scale) {
         if (vec4) O3DML_GEMM_LAUNCH(true, true); else O3DML_GEMM_LAUNCH(false, true);
     } else {
         if (vec4) O3DML_GEMM_LAUNCH(true, false); else O3DML_GEMM_LAUNCH(false, false);
@@ -943,6 +1177,15 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     O3DML_GUARD_END
 }
 
+// Wt [K][cout][cin] at the front of a forward workspace; the rest -> split
+static float* forward_filters(const float* filters, int K, int cin, int cout, Workspace& ws, hipStream_t st) {
+    float* wt = ws.take<float>(static_cast<int64_t>(K) * cin * cout);
+    transpose_filters_kernel<<<stream_grid(static_cast<int64_t>(K) * cin * cout, 256), 256, 0, st>>>(filters, K, cin,
+                                                                                                  cout, wt);
+    O3DML_LAUNCH_CHECK();
+    return wt;
+}
+
 static void map_views(void* workspace, size_t bytes, int64_t n_out, int64_t n_in, int K, int32_t** map,
                       float** pscale, float** oscale, int32_t** inv, float** ipscale, const int32_t** order,
                       const int32_t** iorder) {
@@ -975,15 +1218,18 @@ O3DML_API int o3dml_sparse_conv_forward_fused(const float* filters, int K, int c
     const int32_t *order, *iorder;
     map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
               &iorder);
-    run_gemm(as_stream(stream), map, order, K, n_out, inp_features, nullptr, nullptr, filters, cin, cout, nullptr, bias,
-             out_features, static_cast<float*>(workspace), workspace_bytes, GemmPrologue{pre_scale, pre_shift},
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    const float* wt = forward_filters(filters, K, cin, cout, ws, st);
+    run_gemm(st, map, order, K, n_out, inp_features, nullptr, nullptr, wt, cin, cout, nullptr, bias, out_features,
+             reinterpret_cast<float*>(ws.base + ws.used), ws.size - ws.used, GemmPrologue{pre_scale, pre_shift},
              residual);
     O3DML_GUARD_END
 }
 
 // split-K partial sums of o3dml_sparse_conv_forward (0 when no split is used)
 O3DML_API size_t o3dml_sparse_conv_forward_workspace_size(int64_t n_out, int K, int cin, int cout) {
-    return gemm_split_bytes(n_out, K, cin, cout);
+    return ws_bytes<float>(static_cast<int64_t>(K) * cin * cout) + gemm_split_bytes(n_out, K, cin, cout);
 }
 
 // out [n_out, cout] = oscale * sum_k gather(inp) @ W[k] (+ bias).  filters:
@@ -1000,9 +1246,12 @@ O3DML_API int o3dml_sparse_conv_forward(const float* filters, int K, int cin, in
     const int32_t *order, *iorder;
     map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
               &iorder);
-    run_gemm(as_stream(stream), map, order, K, n_out, inp_features, inp_importance, has_neighbors_importance ? pscale : nullptr,
-             filters, cin, cout, use_out_scale ? oscale : nullptr, bias, out_features,
-             static_cast<float*>(workspace), workspace_bytes);
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    const float* wt = forward_filters(filters, K, cin, cout, ws, st);
+    run_gemm(st, map, order, K, n_out, inp_features, inp_importance, has_neighbors_importance ? pscale : nullptr, wt,
+             cin, cout, use_out_scale ? oscale : nullptr, bias, out_features,
+             reinterpret_cast<float*>(ws.base + ws.used), ws.size - ws.used);
     O3DML_GUARD_END
 }
 
@@ -1046,13 +1295,13 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
     float* split = split_bytes ? ws.take<float>(static_cast<int64_t>(split_bytes / sizeof(float))) : nullptr;
     const float* os = use_out_scale ? oscale : nullptr;
     if (grad_inp && n_in > 0) {
-        // dIn[i] = sscale[i] * sum_k (g[inv[i,k]] * oscale[o] * pscale) @ W[k]^T
-        transpose_filters_kernel<<<stream_grid(static_cast<int64_t>(K) * cin * cout, 256), 256, 0, st>>>(
-                filters, K, cin, cout, wt);
-        O3DML_LAUNCH_CHECK();
-        // the per-row out-scale belongs to the gathered rows (source = grad_out):
+        // dIn[i] = sscale[i] * sum_k (g[inv[i,k]] * oscale[o] * pscale) @ W[k]^T: a
+        // GEMM with weights W[k]^T [cout][cin], whose transposed form (what
+        // the kernel reads) is W itself.
+        // The per-row out-scale belongs to the gathered rows (source = grad_out):
         // fold it in as sscale; pair importance via the inverse pscale.
-        run_gemm(st, inv, iorder, K, n_in, grad_out, os, has_neighbors_importance ? ipscale : nullptr, wt, cout, cin,
+        (void)wt;
+        run_gemm(st, inv, iorder, K, n_in, grad_out, os, has_neighbors_importance ? ipscale : nullptr, filters, cout, cin,
                  inp_importance, nullptr, grad_inp, split, split_bytes);
     }
     if (grad_filters) {

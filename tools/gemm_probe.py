@@ -15,7 +15,8 @@ from o3dml_amd import layers, sparse_conv as sc  # noqa: E402
 dev = torch.device("cuda", 0)
 pos = torch.from_numpy(bench.make_room(0)[0]).to(dev)
 reps = int(os.environ.get("REPS", "20"))
-for cin, cout in [(32, 32), (64, 64), (128, 128), (64, 32)]:
+shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ.get("SHAPES", "32x32,64x64,128x128,64x32").split(",")]
+for cin, cout in shapes:
     torch.manual_seed(0)
     conv = layers.SparseConv(cin, cout, [3, 3, 3], use_bias=False).to(dev)
     x = torch.rand((pos.shape[0], cin), device=dev)
