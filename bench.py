@@ -350,8 +350,40 @@ def sparse_conv_bench(dev, reps):
     return {"voxels": int(n), "pairs": pairs, "mvoxels_per_s_layer": round(n / t_layer / 1e6, 2),
             "ms_layer": round(t_layer * 1e3, 4), "ms_gemm": round(t_gemm * 1e3, 4),
             "tflops_gemm": round(flops / t_gemm / 1e12, 3),
+            "mfma_roofline": [gemm_roofline(dev, pos, nb, kidx, pairs, c, reps) for c in (32, 128)],
             "config": "C4: ~80k 2 cm room voxels, SparseConv 3^3 32->32 fp32, rulebook rebuilt per call",
             "unet": scn_bench(dev, pos, reps)}
+
+
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32-input MFMA (MI355X_MICROARCH.md)
+
+
+def gemm_roofline(dev, pos, nb, kidx, pairs, ch, reps):
+    """MFMA roofline of the sparse-conv GEMM kernel alone (HIP events around the
+    launch inside the library, o3dml_timing_*) on the C4 3^3 map (lattice
+    rulebook, cached and tile-ordered as in SparseConvUnet) at ch -> ch
+    channels: useful flops 2 * pairs * ch^2 per launch over the kernel time,
+    against the fp32 MFMA peak."""
+    from o3dml_amd import _lib, layers, sparse_conv as sc
+    torch.manual_seed(0)
+    conv = layers.SparseConv(ch, ch, [3, 3, 3], use_bias=False).to(dev)
+    feat = torch.rand((pos.shape[0], ch), device=dev)
+    lib = _lib.load()
+    with torch.no_grad(), sc.rulebook_cache():  # the map as SparseConvUnet uses it: cached, tile-ordered
+        conv(feat, pos, pos, 1.0)
+        torch.cuda.synchronize(dev)
+        lib.o3dml_timing_reset()
+        lib.o3dml_timing_enable(1)
+        for _ in range(reps):
+            conv(feat, pos, pos, 1.0)
+        torch.cuda.synchronize(dev)
+        ms, cnt = _lib.kernel_times(["sparse_conv_gemm"])["sparse_conv_gemm"]
+        lib.o3dml_timing_enable(0)
+    t = ms / max(cnt, 1) / 1e3
+    tf = 2.0 * pairs * ch * ch / t / 1e12 if t > 0 else 0.0
+    return {"channels": ch, "kernel": "implicit_gemm_lds_kernel", "kernel_us": round(t * 1e6, 2),
+            "bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4)}
 
 
 def scn_bench(dev, pos, reps):

@@ -196,8 +196,10 @@ int o3dml_sparse_conv_forward(const float* filters, int K, int cin, int cout, co
                               size_t map_workspace_bytes, void* workspace, size_t workspace_bytes, void* stream);
 /* forward with an input prologue relu(x * pre_scale + pre_shift) (eval-mode
  * BatchNorm + ReLU folded per channel) and a residual added in the epilogue;
- * pre_* [cin] and residual [n_out, cout] nullable; no importance / normalize */
-int o3dml_sparse_conv_forward_fused(const float* filters, int K, int cin, int cout, const float* inp_features,
+ * pre_* [cin] and residual [n_out, cout] nullable; no importance / normalize.
+ * filters_t: the filters TRANSPOSED, [K][cout][cin] (constant eval weights,
+ * transposed once by the host). */
+int o3dml_sparse_conv_forward_fused(const float* filters_t, int K, int cin, int cout, const float* inp_features,
                                     int64_t n_in, const float* pre_scale, const float* pre_shift,
                                     const float* residual, const float* bias, int64_t n_out, float* out_features,
                                     void* map_workspace, size_t map_workspace_bytes, void* workspace,
@@ -224,6 +226,14 @@ int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* quer
  * stays 0 unless a set is empty) and leaves the status word in the map
  * workspace at o3dml_sparse_conv_map_status_offset — a failed test leaves an
  * all-empty (safe) map. */
+/* Tile order of a built kernel map (and of its inverse with inverse = 1): the
+ * map rows stably sorted by a hash of their offset mask, so that every
+ * 32-row GEMM tile walks (almost) only offsets all its rows use; the GEMMs
+ * use it from then on (a device flag in the map workspace).  Optional; pays
+ * off when the map serves several convolutions or wide channels.  Results
+ * are unchanged (absent offsets only ever added exact zeros). */
+int o3dml_sparse_conv_tile_order(void* map_workspace, size_t map_workspace_bytes, int64_t n_out, int64_t n_in, int K,
+                                 int inverse, void* stream);
 size_t o3dml_sparse_conv_lattice_workspace_size(int64_t n_in);
 size_t o3dml_sparse_conv_map_status_offset(int64_t n_out, int64_t n_in, int K);
 int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, const float* query_pos, int64_t n_out,

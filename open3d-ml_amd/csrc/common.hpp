@@ -74,12 +74,14 @@ struct TimedRegion {
         else
             a = b = nullptr;
     }
-    ~TimedRegion() {
+    void end() {  // close the region early (idempotent)
         if (a) {
             (void)hipEventRecord(b, st);
             timing_record(name, a, b);
+            a = nullptr;
         }
     }
+    ~TimedRegion() { end(); }
 };
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

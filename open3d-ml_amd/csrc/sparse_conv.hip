@@ -104,7 +104,9 @@ __global__ void recip_norm_kernel(const float* __restrict__ norm, const float* _
 constexpr int64_t kOrderMinRows = 2048;
 static bool use_order(int64_t n, int K) { return K > 8 && n >= kOrderMinRows; }
 
-__global__ void mask_keys_kernel(const int32_t* __restrict__ map, int64_t n, int K, uint32_t* __restrict__ keys) {
+__global__ void mask_keys_kernel(const int32_t* __restrict__ map, int64_t n, int K, uint32_t* __restrict__ keys,
+                                 int* __restrict__ flag) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *flag = 1;  // the sort below completes before any GEMM reads it
     for (int64_t o = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; o < n;
          o += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         uint32_t m = 0u;
@@ -117,11 +119,12 @@ static size_t order_scratch_bytes(int64_t n) {
     return 2 * ws_bytes<uint32_t>(n) + prim::radix_sort_workspace_bytes<uint32_t>(n);
 }
 
-static void build_order(const int32_t* map, int64_t n, int K, int32_t* order, Workspace scratch, hipStream_t st) {
+static void build_order(const int32_t* map, int64_t n, int K, int32_t* order, int* flag, Workspace scratch,
+                        hipStream_t st) {
     if (!use_order(n, K)) return;
     uint32_t* kin = scratch.take<uint32_t>(n);
     uint32_t* kout = scratch.take<uint32_t>(n);
-    mask_keys_kernel<<<stream_grid(n, 256), 256, 0, st>>>(map, n, K, kin);
+    mask_keys_kernel<<<stream_grid(n, 256), 256, 0, st>>>(map, n, K, kin, flag);
     O3DML_LAUNCH_CHECK();
     prim::radix_sort_pairs<uint32_t>(kin, nullptr, kout, reinterpret_cast<uint32_t*>(order), n, 16, scratch, st);
 }
@@ -223,6 +226,19 @@ __device__ __forceinline__ void gemm_load(GemmStage& st, int32_t m, int K, int64
     }
 }
 
+// Split s of nsplit owns the global stages (offset k, chunk c), g = k*nch + c,
+// in [s*G/nsplit, (s+1)*G/nsplit) with G = K*nch — a partition of the
+// (offset, Cin) reduction that does not depend on which rows share a tile, so
+// every row's partial sums (and the fixed-order reduce) are the same for any
+// tile order.  Returns the number of the wave's used stages before split s.
+__device__ __forceinline__ int split_stage(unsigned used, int nch, int K, int s, int nsplit) {
+    const int g = static_cast<int>(static_cast<int64_t>(s) * K * nch / nsplit);
+    const int kk = g / nch, cc = g - kk * nch;
+    const unsigned below = kk >= 32 ? used : (used & ((1u << kk) - 1u));
+    const bool own = kk < 32 && ((used >> kk) & 1u);
+    return __builtin_popcount(below) * nch + (own ? cc : 0);
+}
+
 template <bool PRE>
 __device__ __forceinline__ void gemm_finish(GemmStage& st, int c0, int h, const float* lps, const float* lpb) {
     const int cb = c0 + 16 * h;
@@ -233,7 +249,8 @@ __device__ __forceinline__ void gemm_finish(GemmStage& st, int c0, int h, const 
 
 template <bool VEC4, bool PRE>
 __global__ void __launch_bounds__(kGemmThreads)
-implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, int K, int64_t n_out,
+implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, const int* order_flag,
+                     int K, int64_t n_out,
                      const float* __restrict__ src,
                      const float* __restrict__ sscale, const float* __restrict__ pscale,
                      const float* __restrict__ Wt /*[K][cout][cin]*/, int cin, int cout,
@@ -260,6 +277,7 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict_
     __shared__ int32_t orow_all[kGemmThreads / 64][32];
     int32_t* mtile = mtile_all[threadIdx.x >> 6];
     int32_t* orow = orow_all[threadIdx.x >> 6];
+    if (order && *order_flag == 0) order = nullptr;  // map built without a tile order
     if (lane < 32) {
         const int64_t oo = o0 + lane;
         orow[lane] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
@@ -293,12 +311,11 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict_
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     // the wave's stage stream = (used offset, 32-channel chunk) in order; split
-    // s of nsplit takes stages [s*n/nsplit, (s+1)*n/nsplit)
+    // s of nsplit takes its stages in [j0, j1) (split_stage)
     const int nch = (cin + 31) >> 5;
-    const int nst = __builtin_popcount(used) * nch;
     const int s = blockIdx.z;
-    const int j0 = static_cast<int>(static_cast<int64_t>(s) * nst / nsplit);
-    const int j1 = static_cast<int>(static_cast<int64_t>(s + 1) * nst / nsplit);
+    const int j0 = split_stage(used, nch, K, s, nsplit);
+    const int j1 = split_stage(used, nch, K, s + 1, nsplit);
     if (j0 < j1) {
         unsigned u = used;
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
@@ -439,7 +456,8 @@ __device__ __forceinline__ void lds_read(const float* abuf, const float* bbuf, i
 
 template <bool PRE>
 __global__ void __launch_bounds__(kGemmThreads)
-implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, int K, int64_t n_out,
+implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order,
+                         const int* order_flag, int K, int64_t n_out,
                          const float* __restrict__ src, const float* __restrict__ sscale,
                          const float* __restrict__ pscale, const float* __restrict__ Wt /*[K][cout][cin]*/, int cin,
                          int cout, const float* __restrict__ oscale, const float* __restrict__ bias,
@@ -469,6 +487,7 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     int32_t* orow = orow_all[w];
     float* abuf = stage_all[w][0];
     float* bbuf = stage_all[w][1];
+    if (order && *order_flag == 0) order = nullptr;  // map built without a tile order
     if (lane < 32) {
         const int64_t oo = o0 + lane;
         orow[lane] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
@@ -495,10 +514,9 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     const int nch = (cin + 31) >> 5;
-    const int nst = __builtin_popcount(used) * nch;
     const int s = blockIdx.z;
-    const int j0 = static_cast<int>(static_cast<int64_t>(s) * nst / nsplit);
-    const int j1 = static_cast<int>(static_cast<int64_t>(s + 1) * nst / nsplit);
+    const int j0 = split_stage(used, nch, K, s, nsplit);
+    const int j1 = split_stage(used, nch, K, s + 1, nsplit);
     if (j0 < j1) {
         unsigned u = used;
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
@@ -756,7 +774,7 @@ static size_t gemm_split_bytes(int64_t n_out, int K, int cin, int cout) {
     return ns > 1 ? ws_bytes<float>(ns * n_out * cout) : 0;
 }
 
-static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, int K, int64_t n_out, const float* src,
+static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, const int* order_flag, int K, int64_t n_out, const float* src,
                      const float* sscale,
                      const float* pscale, const float* Wt, int cin, int cout, const float* oscale, const float* bias,
                      float* out, float* part, size_t part_bytes, GemmPrologue pre = {nullptr, nullptr},
@@ -770,19 +788,20 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, i
                  static_cast<unsigned>(ceil_div(cout, 32)), static_cast<unsigned>(ns));
     O3DML_REQUIRE(pre.scale == nullptr || cin <= kPreMax, "sparse_conv: prologue needs cin <= %d", kPreMax);
 #define O3DML_GEMM_LAUNCH(V, P)                                                                                    \
-    implicit_gemm_kernel<V, P><<<g, kGemmThreads, 0, st>>>(map, order, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, \
+    implicit_gemm_kernel<V, P><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, \
                                                            bias, out, ns, part, pre, residual)
     static const bool lds_path = [] {
         const char* e = std::getenv("O3DML_GEMM_LDS");
         return e ? std::atoi(e) != 0 : true;
     }();
+    TimedRegion tr("sparse_conv_gemm", st);  // the GEMM kernel alone (bench roofline)
     if (vec4 && lds_path) {
         if (pre.scale)
-            implicit_gemm_lds_kernel<true><<<g, kGemmThreads, 0, st>>>(map, order, K, n_out, src, sscale, pscale, Wt,
+            implicit_gemm_lds_kernel<true><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, pscale, Wt,
                                                                       cin, cout, oscale, bias, out, ns, part, pre,
                                                                       residual);
         else
-            implicit_gemm_lds_kernel<false><<<g, kGemmThreads, 0, st>>>(map, order, K, n_out, src, sscale, pscale, Wt,
+            implicit_gemm_lds_kernel<false><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, pscale, Wt,
                                                                        cin, cout, oscale, bias, out, ns, part, pre,
                                                                        residual);
     } else if (pre.scale) {
@@ -792,6 +811,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, i
     }
 #undef O3DML_GEMM_LAUNCH
     O3DML_LAUNCH_CHECK();
+    tr.end();
     if (ns > 1) {
         split_reduce_kernel<<<stream_grid(n_out * cout, 256), 256, 0, st>>>(part, ns, n_out, cout, oscale, bias,
                                                                            residual, out);
@@ -929,6 +949,8 @@ __global__ void __launch_bounds__(64) lattice_finalize_kernel(const int* __restr
     }
     *lo_out = lo;
     status[0] = ok ? 0 : 4;
+    status[2] = 0;  // no tile orders yet (o3dml_sparse_conv_tile_order)
+    status[3] = 0;
 }
 
 __global__ void lattice_insert_kernel(const float* __restrict__ pos, int64_t n, float inv_vs, uint64_t* __restrict__ keys,
@@ -1059,8 +1081,7 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
     int32_t* inv = ws.take<int32_t>(n_in * K);
     float* ipscale = ws.take<float>(n_in * K);
     int* status = ws.take<int>(4);
-    MapOrders ord = map_orders(ws, n_out, n_in);
-    O3DML_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, st));
+    O3DML_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, st));  // [2], [3]: no tile orders yet
     if (n_out > 0) {
         O3DML_CHECK_HIP(hipMemsetAsync(map, 0xff, sizeof(int32_t) * n_out * K, st));
         build_kernel_map_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(
@@ -1079,9 +1100,7 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
                     neighbors_importance ? ipscale : nullptr, status);
             O3DML_LAUNCH_CHECK();
         }
-        build_order(inv, n_in, K, ord.iorder, ord.scratch, st);
     }
-    build_order(map, n_out, K, ord.order, ord.scratch, st);
     O3DML_CHECK_HIP(hipMemcpyAsync(status_host, status, sizeof(int), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
     O3DML_GUARD_END
@@ -1123,7 +1142,6 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     int32_t* inv = ws.take<int32_t>(n_in * K);
     float* ipscale = ws.take<float>(n_in * K);
     int* status = ws.take<int>(4);
-    MapOrders ord = map_orders(ws, n_out, n_in);
     (void)pscale;
     (void)ipscale;
     *status_host = 0;
@@ -1168,9 +1186,7 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
         build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, nullptr, n_out, K, inv, nullptr,
                                                                             status);
         O3DML_LAUNCH_CHECK();
-        build_order(inv, n_in, K, ord.iorder, ord.scratch, st);
     }
-    build_order(map, n_out, K, ord.order, ord.scratch, st);
     if (defer_status) return 0;  // status stays on the device (o3dml_sparse_conv_map_status_offset)
     O3DML_CHECK_HIP(hipMemcpyAsync(status_host, status, sizeof(int), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
@@ -1188,7 +1204,7 @@ static float* forward_filters(const float* filters, int K, int cin, int cout, Wo
 
 static void map_views(void* workspace, size_t bytes, int64_t n_out, int64_t n_in, int K, int32_t** map,
                       float** pscale, float** oscale, int32_t** inv, float** ipscale, const int32_t** order,
-                      const int32_t** iorder) {
+                      const int32_t** iorder, const int** order_flag, const int** iorder_flag) {
     Workspace ws(workspace, bytes);
     *map = ws.take<int32_t>(n_out * K);
     *pscale = ws.take<float>(n_out * K);
@@ -1196,16 +1212,41 @@ static void map_views(void* workspace, size_t bytes, int64_t n_out, int64_t n_in
     *oscale = ws.take<float>(n_out);
     *inv = ws.take<int32_t>(n_in * K);
     *ipscale = ws.take<float>(n_in * K);
-    ws.take<int>(4);
+    int* status = ws.take<int>(4);
     const MapOrders ord = map_orders(ws, n_out, n_in);
+    // device flags status[2] / status[3] say whether the orders were built
     *order = use_order(n_out, K) ? ord.order : nullptr;
     *iorder = use_order(n_in, K) ? ord.iorder : nullptr;
+    *order_flag = status + 2;
+    *iorder_flag = status + 3;
+}
+
+// Tile orders for a built map (and its inverse with `inverse` = 1): worth it
+// when the map serves several GEMMs or wide channels (host decides).
+O3DML_API int o3dml_sparse_conv_tile_order(void* map_workspace, size_t map_workspace_bytes, int64_t n_out,
+                                           int64_t n_in, int K, int inverse, void* stream) {
+    O3DML_GUARD_BEGIN
+    hipStream_t st = as_stream(stream);
+    Workspace ws(map_workspace, map_workspace_bytes);
+    const int32_t* map = ws.take<int32_t>(n_out * K);
+    ws.take<float>(n_out * K);
+    ws.take<float>(n_out);
+    ws.take<float>(n_out);
+    const int32_t* inv = ws.take<int32_t>(n_in * K);
+    ws.take<float>(n_in * K);
+    int* status = ws.take<int>(4);
+    MapOrders ord = map_orders(ws, n_out, n_in);
+    build_order(map, n_out, K, ord.order, status + 2, ord.scratch, st);
+    if (inverse) build_order(inv, n_in, K, ord.iorder, status + 3, ord.scratch, st);
+    O3DML_GUARD_END
 }
 
 // Forward with an input prologue and a residual epilogue (SparseConvUnet eval:
 // out = conv(relu(x * pre_scale + pre_shift)) + residual); pre_scale /
-// pre_shift [cin] and residual [n_out, cout] are each nullable.
-O3DML_API int o3dml_sparse_conv_forward_fused(const float* filters, int K, int cin, int cout,
+// pre_shift [cin] and residual [n_out, cout] are each nullable.  The filters
+// come TRANSPOSED, filters_t [K][cout][cin] (eval weights are constant: the
+// host keeps the transposed copy instead of a transpose launch per call).
+O3DML_API int o3dml_sparse_conv_forward_fused(const float* filters_t, int K, int cin, int cout,
                                               const float* inp_features, int64_t n_in, const float* pre_scale,
                                               const float* pre_shift, const float* residual, const float* bias,
                                               int64_t n_out, float* out_features, void* map_workspace,
@@ -1216,12 +1257,14 @@ O3DML_API int o3dml_sparse_conv_forward_fused(const float* filters, int K, int c
     int32_t *map, *inv;
     float *pscale, *oscale, *ipscale;
     const int32_t *order, *iorder;
+    const int *oflag, *ioflag;
     map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
-              &iorder);
+              &iorder, &oflag, &ioflag);
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
-    const float* wt = forward_filters(filters, K, cin, cout, ws, st);
-    run_gemm(st, map, order, K, n_out, inp_features, nullptr, nullptr, wt, cin, cout, nullptr, bias, out_features,
+    ws.take<float>(static_cast<int64_t>(K) * cin * cout);  // (unused Wt slot: filters_t comes transposed)
+    run_gemm(st, map, order, oflag, K, n_out, inp_features, nullptr, nullptr, filters_t, cin, cout, nullptr, bias,
+             out_features,
              reinterpret_cast<float*>(ws.base + ws.used), ws.size - ws.used, GemmPrologue{pre_scale, pre_shift},
              residual);
     O3DML_GUARD_END
@@ -1244,12 +1287,13 @@ O3DML_API int o3dml_sparse_conv_forward(const float* filters, int K, int cin, in
     int32_t *map, *inv;
     float *pscale, *oscale, *ipscale;
     const int32_t *order, *iorder;
+    const int *oflag, *ioflag;
     map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
-              &iorder);
+              &iorder, &oflag, &ioflag);
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
     const float* wt = forward_filters(filters, K, cin, cout, ws, st);
-    run_gemm(st, map, order, K, n_out, inp_features, inp_importance, has_neighbors_importance ? pscale : nullptr, wt,
+    run_gemm(st, map, order, oflag, K, n_out, inp_features, inp_importance, has_neighbors_importance ? pscale : nullptr, wt,
              cin, cout, use_out_scale ? oscale : nullptr, bias, out_features,
              reinterpret_cast<float*>(ws.base + ws.used), ws.size - ws.used);
     O3DML_GUARD_END
@@ -1285,8 +1329,9 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
     int32_t *map, *inv;
     float *pscale, *oscale, *ipscale;
     const int32_t *order, *iorder;
+    const int *oflag, *ioflag;
     map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
-              &iorder);
+              &iorder, &oflag, &ioflag);
     Workspace ws(workspace, workspace_bytes);
     float* wt = ws.take<float>(static_cast<int64_t>(K) * cin * cout);
     float* g = ws.take<float>(n_out * cout);  // unused slot kept for layout stability
@@ -1301,7 +1346,7 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
         // The per-row out-scale belongs to the gathered rows (source = grad_out):
         // fold it in as sscale; pair importance via the inverse pscale.
         (void)wt;
-        run_gemm(st, inv, iorder, K, n_in, grad_out, os, has_neighbors_importance ? ipscale : nullptr, filters, cout, cin,
+        run_gemm(st, inv, iorder, ioflag, K, n_in, grad_out, os, has_neighbors_importance ? ipscale : nullptr, filters, cout, cin,
                  inp_importance, nullptr, grad_inp, split, split_bytes);
     }
     if (grad_filters) {

@@ -56,6 +56,7 @@ SIGNATURES = {
     "o3dml_sparse_conv_lattice_map": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i32, c_i32, c_i32, c_p, c_i32, c_i32,
                                               c_p, c_p, c_sz, c_p, c_sz, c_p]),
     "o3dml_sparse_conv_map_status_offset": (c_sz, [c_i64, c_i64, c_i32]),
+    "o3dml_sparse_conv_tile_order": (c_i32, [c_p, c_sz, c_i64, c_i64, c_i32, c_i32, c_p]),
     "o3dml_kpconv_weighted_features": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_i32,
                                                c_i32, c_f32, c_i32, c_i32, c_p, c_p, c_p]),
     "o3dml_kpconv_weighted_features_backward": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p,

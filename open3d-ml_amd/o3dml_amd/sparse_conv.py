@@ -20,6 +20,11 @@ def _opt(t, dev, dtype=torch.float32):
     return to_dev(t, dev, dtype)
 
 
+
+# Tile order (o3dml_sparse_conv_tile_order) for a map used once: only when the
+# GEMM is wide enough that the saved MFMA work beats the sort's few launches.
+TILE_ORDER_MIN_CHANNELS = 64 * 64
+
 class _ConvFn(torch.autograd.Function):
     """out = oscale * sum_k gather(x * sscale * pscale) @ W[k] (+ bias)."""
 
@@ -49,6 +54,8 @@ class _ConvFn(torch.autograd.Function):
             if status[0] & 1:
                 raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index "
                                    "(non-lattice neighbourhood); not representable by the dense kernel map")
+            if cin * cout >= TILE_ORDER_MIN_CHANNELS:
+                _lib.call("o3dml_sparse_conv_tile_order", ptr(mws), mws.numel(), n_out, n_in, K, want_inv, st)
         W = filters.detach().contiguous()
         x = inp_features.detach().contiguous()
         out = torch.empty((n_out, cout), dtype=torch.float32, device=dev)
@@ -227,6 +234,11 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
                   int(bool(mirror)), int(bool(normalize)), ptr(oimp), int(bool(want_grad)), int(defer),
                   status.ctypes.data, ptr(mws), mws.numel(), ptr(lws), lws.numel(), stream_handle(dev))
         status0 = int(status[0])
+        if (scope is not None or int(filters.shape[3]) * int(filters.shape[4]) >= TILE_ORDER_MIN_CHANNELS) \
+                and not status0 & 4:
+            # cached maps serve several convolutions: sort the GEMM tiles by offset mask once
+            _lib.call("o3dml_sparse_conv_tile_order", ptr(mws), mws.numel(), n_out, n_in, K, int(bool(want_grad)),
+                      stream_handle(dev))
         if defer:
             off = lib.o3dml_sparse_conv_map_status_offset(n_out, n_in, K)
             scope.pending.append(mws[off:off + 4].view(torch.int32))
@@ -248,7 +260,7 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
         if res is not None and tuple(res.shape) != (n_out, cout):
             raise ValueError("sparse_conv: residual must be [n_out, cout]")
         fws = workspace(lib.o3dml_sparse_conv_forward_workspace_size(n_out, K, cin, cout), dev)
-        _lib.call("o3dml_sparse_conv_forward_fused", ptr(f.detach().contiguous()), K, cin, cout,
+        _lib.call("o3dml_sparse_conv_forward_fused", ptr(_transposed_filters(f)), K, cin, cout,
                   ptr(x.detach().contiguous()), n_in, ptr(ps), ptr(pb), ptr(res),
                   ptr(None if b is None else b.detach().contiguous()), n_out, ptr(out), ptr(mws), mws.numel(),
                   ptr(fws), fws.numel(), stream_handle(dev))
@@ -257,6 +269,18 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
     out = _ConvFn.apply(f, x, b, empty, empty, None, empty, _opt(inp_importance, dev), bool(normalize), oimp,
                         want_grad, (mws, n_out))
     return out if inp_features.is_cuda else out.cpu()
+
+
+def _transposed_filters(f):
+    """[k,k,k,Cin,Cout] -> contiguous [K, Cout, Cin] (what the GEMM reads),
+    cached on the tensor until its data changes (eval weights: once)."""
+    key = (f._version, f.data_ptr(), tuple(f.shape))
+    hit = getattr(f, "_o3dml_wt", None)
+    if hit is None or hit[0] != key:
+        wt = f.detach().reshape(-1, f.shape[-2], f.shape[-1]).transpose(1, 2).contiguous()
+        f._o3dml_wt = (key, wt)
+        return wt
+    return hit[1]
 
 
 def kernel_index(inp_positions, query_positions, neighbors_index, neighbors_row_splits, kernel_size, voxel_size,
