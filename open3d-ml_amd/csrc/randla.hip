@@ -13,6 +13,7 @@
 // All are HBM-bound; one thread per output element, channel-fastest so
 // consecutive lanes read consecutive addresses.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -218,6 +219,152 @@ __global__ void __launch_bounds__(D > 64 ? D : 64) att_pool_kernel(
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// D >= 64: the same fused pass with both GEMMs on MFMA.  The per-point work is
+// two small GEMMs over the K = 16 neighbour rows — the rel MLP (second pass:
+// [16 x D/2] x [D/2 x D/2]) and the scores ([16 x D] x [D x D]) — which the
+// lane-per-channel kernel runs as VALU FMA chains (7-20 TF/s at D = 256).
+// Here a workgroup takes 2 points = 32 rows, one wave per 64 output channels
+// (D / 64 waves); every 32 x 32 tile is a chain of v_mfma_f32_32x32x2_f32 with
+// A read from the LDS rows (F channel-major [pt][ch][j], rin row-major
+// [row][i]) and B = the transposed weights ([in][out], coalesced, L2-resident).
+// Accumulator layout: lane l, register r holds column l % 32 of row
+// (r & 3) + 8 (r >> 2) + 4 (l >> 5), so point p's 16 rows are registers
+// 8p .. 8p+7 of lanes l and l ^ 32 — softmax and the weighted sum combine
+// those two lanes with one xor-32 shuffle.
+// ---------------------------------------------------------------------------
+typedef float ap_f32x16 __attribute__((ext_vector_type(16)));
+
+template <int D, bool RELENC>
+__global__ void __launch_bounds__(D) att_pool_mfma_kernel(
+        const float* __restrict__ coords, const float* __restrict__ x, const int32_t* __restrict__ nbr, int64_t n,
+        const float* __restrict__ rel_in, const float* __restrict__ wrt, const float* __restrict__ br,
+        const float* __restrict__ wst, const float* __restrict__ bs, float* __restrict__ rel_out,
+        float* __restrict__ out) {
+    constexpr int H = D / 2;
+    constexpr int IR = RELENC ? 10 : H;
+    constexpr int NT = D;  // threads: D / 64 waves
+    // F of the two points, point 1 shifted by 32 banks (the MFMA A reads of the
+    // two points' rows hit distinct banks)
+    constexpr int PS = D * kApK + 32;
+    __shared__ __attribute__((aligned(16))) float ft_s[2 * PS];
+#define FT(p, ch, j) ft_s[(p) * PS + (ch) * kApK + (j)]
+    __shared__ float rin[2 * kApK][IR + (RELENC ? 0 : 1)];  // +1: rows on distinct banks
+    __shared__ int32_t nb_s[2 * kApK];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int li = lane & 31, lh = lane >> 5;
+    for (int64_t base = static_cast<int64_t>(blockIdx.x) * 2; base < n; base += static_cast<int64_t>(gridDim.x) * 2) {
+        const int np = n - base >= 2 ? 2 : 1;
+        // (a) neighbour ids and the MLP input rows (rows of a missing 2nd point: 0)
+        if (tid < 2 * kApK) nb_s[tid] = tid < np * kApK ? nbr[base * kApK + tid] : 0;
+        __syncthreads();
+        if constexpr (RELENC) {
+            if (tid < 2 * kApK) {
+                const int64_t q = base + (tid >> 4);
+                const bool ok = tid < np * kApK;
+                const int64_t j = nb_s[tid];
+                const float cx = ok ? coords[3 * q] : 0.f, cy = ok ? coords[3 * q + 1] : 0.f,
+                            cz = ok ? coords[3 * q + 2] : 0.f;
+                const float px = coords[3 * j], py = coords[3 * j + 1], pz = coords[3 * j + 2];
+                const float rx = cx - px, ry = cy - py, rz = cz - pz;
+                float* r = rin[tid];
+                r[0] = sqrtf((rx * rx + ry * ry) + rz * rz);
+                r[1] = rx;
+                r[2] = ry;
+                r[3] = rz;
+                r[4] = cx;
+                r[5] = cy;
+                r[6] = cz;
+                r[7] = px;
+                r[8] = py;
+                r[9] = pz;
+            }
+        } else {
+            for (int e = tid; e < 2 * kApK * IR; e += NT) {
+                const int row = e / IR;
+                rin[row][e % IR] = row < np * kApK ? rel_in[base * kApK * IR + e] : 0.f;
+            }
+        }
+        // gathered half of F
+        for (int e = tid; e < 2 * kApK * H; e += NT) {
+            const int row = e / H, cc = e % H;
+            FT(row >> 4, cc, row & 15) = x[static_cast<int64_t>(nb_s[row]) * H + cc];
+        }
+        __syncthreads();
+        // (b) relative half of F: leaky(Wr . r + br)
+        if constexpr (RELENC) {
+            for (int e = tid; e < 2 * kApK * H; e += NT) {
+                const int row = e / H, cc = e % H;
+                float acc = br[cc];
+#pragma unroll
+                for (int i = 0; i < IR; ++i) acc = __builtin_fmaf(wrt[i * H + cc], rin[row][i], acc);
+                const float v = acc > 0.f ? acc : 0.2f * acc;
+                FT(row >> 4, H + cc, row & 15) = v;
+                if (rel_out && row < np * kApK) rel_out[(base * kApK + row) * H + cc] = v;
+            }
+        } else {
+            // H / 32 = D / 64 column tiles: one per wave
+            const int col = 32 * w + li;
+            ap_f32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll 8
+            for (int k = 0; k < IR; k += 2) {
+                const float a = rin[li][k + lh];
+                const float b = wrt[(k + lh) * H + col];
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+            }
+            const float bb = br[col];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+                const float v0 = acc[r] + bb;
+                const float v = v0 > 0.f ? v0 : 0.2f * v0;
+                FT(row >> 4, H + col, row & 15) = v;
+                if (rel_out && row < np * kApK) rel_out[(base * kApK + row) * H + col] = v;
+            }
+        }
+        __syncthreads();
+        // (c) scores: wave w owns output columns [64w, 64w + 64)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int col = 64 * w + 32 * t + li;
+            ap_f32x16 acc;
+            const float b0 = bs[col];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = b0;
+#pragma unroll 8
+            for (int k = 0; k < D; k += 2) {
+                const float a = FT(li >> 4, k + lh, li & 15);
+                const float b = wst[(k + lh) * D + col];
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+            }
+            // softmax over the 16 neighbours of each point, weighted sum of F
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                float mx = acc[8 * p];
+#pragma unroll
+                for (int r = 1; r < 8; ++r) mx = fmaxf(mx, acc[8 * p + r]);
+                mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+                float den = 0.f, num = 0.f;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int j = (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    const float e = __expf(acc[8 * p + r] - mx);
+                    den += e;
+                    num += e * FT(p, col, j);
+                }
+                den += __shfl_xor(den, 32, 64);
+                num += __shfl_xor(num, 32, 64);
+                if (lh == 0 && p < np) out[(base + p) * D + col] = num / den;
+            }
+        }
+        __syncthreads();
+    }
+}
+#undef FT
+
 }  // namespace o3dml
 
 using namespace o3dml;
@@ -282,6 +429,26 @@ O3DML_API int o3dml_randla_att_pool(const float* coords, const float* x, const i
                   "fused attentive pooling: width %d not in {16, 32, 64, 128, 256}", d);
     if (n == 0) return 0;
     hipStream_t st = as_stream(stream);
+    static const bool mfma = [] {
+        const char* e = std::getenv("O3DML_ATT_MFMA");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    if (mfma && d >= 64) {
+        const unsigned gm = static_cast<unsigned>(std::min<int64_t>(ceil_div(n, 2), 1 << 20));
+#define O3DML_APM(D)                                                                                             \
+    do {                                                                                                         \
+        if (rel_in)                                                                                              \
+            att_pool_mfma_kernel<D, false><<<gm, D, 0, st>>>(coords, x, neighbors, n, rel_in, wr_t, br, ws_t, bs,  \
+                                                             rel_out, out);                                      \
+        else                                                                                                     \
+            att_pool_mfma_kernel<D, true><<<gm, D, 0, st>>>(coords, x, neighbors, n, nullptr, wr_t, br, ws_t, bs,  \
+                                                            rel_out, out);                                       \
+    } while (0)
+        if (d == 64) O3DML_APM(64); else if (d == 128) O3DML_APM(128); else O3DML_APM(256);
+#undef O3DML_APM
+        O3DML_LAUNCH_CHECK();
+        return 0;
+    }
     const int ppb = d < 64 ? 64 / d : 1, block = d > 64 ? d : 64;
     const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n, ppb), 1 << 20));
 #define O3DML_AP(D)                                                                                              \

@@ -55,3 +55,26 @@ def test_inference_pipeline_covers_cloud(cuda):
     assert torch.isfinite(probs).all() and (probs.sum(1) > 0).all()
     labels2, _ = SemSegInference(m, seed=0).run(pts)
     assert torch.equal(labels, labels2)  # seeded -> reproducible patch sequence
+
+
+@pytest.mark.parametrize("d_out", [16, 64, 128, 256])
+def test_fused_pooling_widths_vs_torch(cuda, d_out):
+    """Fused LSE + attentive pooling (VALU kernel below 64 channels, MFMA kernel
+    from 64 up) against the module's own torch path, eval mode, odd point count
+    (the MFMA kernel's half-filled last pair of points)."""
+    from o3dml_amd.randlanet import LocalFeatureAggregation
+    torch.manual_seed(d_out)
+    n = 301
+    m = LocalFeatureAggregation(d_out // 2, d_out, 16).to(cuda).eval()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_mean.uniform_(-0.2, 0.2)
+            mod.running_var.uniform_(0.5, 1.5)
+    coords = torch.rand((n, 3), device=cuda) * 4.0
+    feat = torch.randn((n, d_out // 2), device=cuda)
+    nbr = torch.randint(0, n, (n, 16), device=cuda, dtype=torch.int32)
+    with torch.no_grad():
+        fused = m(coords, feat, nbr)
+    with torch.enable_grad():
+        ref = m(coords, feat, nbr).detach()
+    torch.testing.assert_close(fused, ref, rtol=1e-4, atol=1e-4)
