@@ -19,6 +19,8 @@ is grid-subsampled and projected ONCE, then patches are cropped, recentred,
 searched (kNN k=16 / k=1 per layer), inferred and accumulated on the GPU
 until every sub-point's possibility exceeds 0.5.
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -346,8 +348,11 @@ class SemSegInference:
     sampler.  ``run(points)`` -> (predicted labels [N] int64, probabilities
     [N, C] float32), both on the GPU; ``stats`` records patches per frame."""
 
-    def __init__(self, model, device=None, seed=0, test_smooth=0.95):
+    def __init__(self, model, device=None, seed=0, test_smooth=0.95, use_graph=None):
         self.model = model
+        if use_graph is None:
+            use_graph = os.environ.get("O3DML_RANDLA_GRAPH", "1") != "0"
+        self.use_graph = use_graph
         self.device = device or next(model.parameters()).device
         self.test_smooth = test_smooth
         self.gen = torch.Generator(device=self.device)
@@ -393,14 +398,50 @@ class SemSegInference:
         sup = torch.cat(levels[1:]).contiguous()
         srs = np.concatenate([[0], np.cumsum(sizes[1:])]).astype(np.int64)
         up_all = ops.knn_search(sup, cat, 1, srs, rs).neighbors_index.long()
+        return pc, idxs, nb_all, up_all, (sizes, rs, srs)
+
+    def _levels(self, pc, nb_all, up_all, plan):
+        """Per-layer (coords, nbrs, subs, ups) views of the batched kNN results."""
+        sizes, rs, srs = plan
         coords, nbrs, subs, ups = [], [], [], []
-        for i in range(L):
+        for i in range(self.model.cfg["num_layers"]):
             nb = (nb_all[rs[i]:rs[i + 1]] - int(rs[i])).contiguous()
-            coords.append(levels[i].contiguous())
+            coords.append(pc[:sizes[i]].contiguous())
             nbrs.append(nb)
             subs.append(nb[:sizes[i + 1]].contiguous())
             ups.append(up_all[rs[i]:rs[i + 1]] - int(srs[i]))
-        return pc, idxs, coords, nbrs, subs, ups
+        return coords, nbrs, subs, ups
+
+    def _patch_probs(self, pc, nb_all, up_all, plan):
+        coords, nbrs, subs, ups = self._levels(pc, nb_all, up_all, plan)
+        return torch.softmax(self.model.forward_points(pc, coords, nbrs, subs, ups), -1)
+
+    def _graph_probs(self, pc, nb_all, up_all, plan):
+        """The network part of a patch (per-layer views, forward, softmax: ~100
+        launches) replayed as one HIP graph: every full-size patch has the same
+        shapes, so the graph is captured once per (model, patch plan) and its
+        static inputs are refreshed with three device copies.  The graph lives on
+        the model (one per patch plan and device), so later frames reuse it."""
+        key = (str(self.device), tuple(plan[0]))
+        g = self.model.__dict__.get("_o3dml_patch_graph")
+        if g is None or g[0] != key:
+            st = {"pc": pc.clone(), "nb": nb_all.clone(), "up": up_all.clone()}
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):
+                for _ in range(2):  # warm-up outside the capture (caches, allocator)
+                    self._patch_probs(st["pc"], st["nb"], st["up"], plan)
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = self._patch_probs(st["pc"], st["nb"], st["up"], plan)
+            g = self.model.__dict__["_o3dml_patch_graph"] = (key, graph, st, out)
+        _, graph, st, out = g
+        st["pc"].copy_(pc)
+        st["nb"].copy_(nb_all)
+        st["up"].copy_(up_all)
+        graph.replay()
+        return out
 
     @torch.no_grad()
     def run(self, points):
@@ -413,9 +454,11 @@ class SemSegInference:
         test_probs = torch.zeros((n_sub, C), dtype=torch.float32, device=self.device)
         patches = 0
         while float(possibility.min()) <= 0.5:
-            pc, idxs, coords, nbrs, subs, ups = self.transform(sub, possibility)
-            logits = self.model.forward_points(pc, coords, nbrs, subs, ups)
-            probs = torch.softmax(logits, -1)
+            pc, idxs, nb_all, up_all, plan = self.transform(sub, possibility)
+            if self.use_graph and n_sub >= self.model.cfg["num_points"]:
+                probs = self._graph_probs(pc, nb_all, up_all, plan)
+            else:
+                probs = self._patch_probs(pc, nb_all, up_all, plan)
             test_probs[idxs] = self.test_smooth * test_probs[idxs] + (1 - self.test_smooth) * probs
             patches += 1
         self.stats = {"patches": patches, "sub_points": n_sub}

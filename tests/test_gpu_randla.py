@@ -78,3 +78,17 @@ def test_fused_pooling_widths_vs_torch(cuda, d_out):
     with torch.enable_grad():
         ref = m(coords, feat, nbr).detach()
     torch.testing.assert_close(fused, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_inference_graph_replay_matches_eager(cuda):
+    """The patch network replayed as a HIP graph gives the eager path's result."""
+    from o3dml_amd.randlanet import RandLANet, SemSegInference
+    torch.manual_seed(0)
+    m = RandLANet(num_points=4096).to(cuda)
+    rng = np.random.default_rng(2)
+    pts = np.stack([rng.uniform(-20, 20, 20000), rng.uniform(-20, 20, 20000), rng.uniform(-2, 2, 20000)], 1)
+    pts = torch.from_numpy(pts.astype(np.float32)).to(cuda)
+    lg, pg = SemSegInference(m, seed=0, use_graph=True).run(pts)
+    le, pe = SemSegInference(m, seed=0, use_graph=False).run(pts)
+    torch.testing.assert_close(pg, pe, rtol=0, atol=1e-6)
+    assert torch.equal(lg, le)
