@@ -40,6 +40,11 @@ N_POINTS = 65536
 RADIUS = 0.05
 
 
+
+def _fused_opt():
+    """Single-kernel (fused) optimizer steps; O3DML_FUSED_OPT=0 for torch's foreach path."""
+    return os.environ.get("O3DML_FUSED_OPT", "1") != "0"
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -195,7 +200,7 @@ def kpconv_bench(dev, steps):
     torch.manual_seed(0)
     np.random.seed(0)
     model = KPFCNN(**S3DIS).to(dev).train()
-    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.98, weight_decay=0.001)
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.98, weight_decay=0.001, fused=_fused_opt())
     pts_np, feat_np, lab_np, lengths = make_c3(0)
     pts = torch.from_numpy(pts_np).to(dev)
     feat = torch.from_numpy(feat_np).to(dev)
@@ -262,7 +267,7 @@ def pointpillars_bench(dev, world, rank, steps, scenes_per_gpu=2):
     ddp = model
     if world > 1:
         ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index])
-    opt = torch.optim.AdamW(model.parameters(), lr=0.001, betas=(0.95, 0.99), weight_decay=0.01)
+    opt = torch.optim.AdamW(model.parameters(), lr=0.001, betas=(0.95, 0.99), weight_decay=0.01, fused=_fused_opt())
     scenes = [make_kitti_scene(1000 + rank * scenes_per_gpu + i) for i in range(scenes_per_gpu)]
     inp = types.SimpleNamespace(point=[torch.from_numpy(s[0]).to(dev) for s in scenes],
                                 bboxes=[torch.from_numpy(s[1]).to(dev) for s in scenes],
