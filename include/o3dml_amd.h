@@ -169,6 +169,15 @@ int o3dml_three_interpolate(const float* features, const int32_t* idx, const flo
 int o3dml_three_interpolate_grad(const float* grad_out, const int32_t* idx, const float* weight, int64_t B, int64_t C,
                                  int64_t n, int64_t m, float* grad_features, void* stream);
 
+/* ---- rotated BEV NMS: replaces open3d.ml.torch.ops.nms
+ * (ml3d/torch/utils/objdet_helper.py:27, called by multiclass_nms :346 from
+ * point_pillars.py:1005).  boxes f32 [N,5] (x1,y1,x2,y2,yaw), scores f32 [N];
+ * keep int64 [N] receives the kept original indices in descending-score order
+ * and *keep_count (device int64) their number.  N <= 65536. -------------- */
+size_t o3dml_nms_workspace_size(int64_t n);
+int o3dml_nms(const float* boxes, const float* scores, int64_t n, float nms_overlap_thresh, int64_t* keep,
+              int64_t* keep_count, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- sparse convolution: replaces open3d.ml.torch.ops.sparse_conv,
  * sparse_conv_transpose and their gradients, bound by layers.SparseConv /
  * layers.SparseConvTranspose (ml3d/torch/models/sparseconvnet.py:344-482;

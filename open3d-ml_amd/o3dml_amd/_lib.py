@@ -86,6 +86,8 @@ SIGNATURES = {
     "o3dml_three_nn": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "o3dml_three_interpolate": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     "o3dml_three_interpolate_grad": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
+    "o3dml_nms_workspace_size": (c_sz, [c_i64]),
+    "o3dml_nms": (c_i32, [c_p, c_p, c_i64, c_f32, c_p, c_p, c_p, c_sz, c_p]),
     # sparse_conv.hip
     "o3dml_sparse_conv_map_workspace_size": (c_sz, [c_i64, c_i64, c_i32]),
     "o3dml_sparse_conv_build_map": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_i32, c_p, c_p,

@@ -422,11 +422,32 @@ def three_interpolate_grad(grad_out, idx, weights, M):
 
 # ---------------------------------------------------------------------------
 # sparse convolution — see sparse_conv.py
+def nms(boxes, scores, nms_overlap_thresh):
+    """Open3D ``ops.nms`` (objdet_helper.py:27, called at :346): rotated BEV NMS.
+    boxes f32 [N,5] (x1,y1,x2,y2,yaw), scores f32 [N] -> int64 kept indices in
+    descending-score order (stable for ties); IoU > threshold suppresses."""
+    dev = gpu_device(boxes, scores)
+    if boxes.dim() != 2 or boxes.shape[1] != 5:
+        raise RuntimeError("nms: boxes must be [N, 5], got %s" % (tuple(boxes.shape),))
+    if scores.dim() != 1 or scores.shape[0] != boxes.shape[0]:
+        raise RuntimeError("nms: scores must be [N] matching boxes")
+    lib = _lib.load()
+    n = boxes.shape[0]
+    b = to_dev(boxes, dev, torch.float32)
+    s = to_dev(scores, dev, torch.float32)
+    keep = torch.empty((max(n, 1),), dtype=torch.int64, device=dev)
+    count = torch.zeros((1,), dtype=torch.int64, device=dev)
+    ws = workspace(lib.o3dml_nms_workspace_size(n), dev)
+    _lib.call("o3dml_nms", ptr(b), ptr(s), n, float(nms_overlap_thresh), ptr(keep), ptr(count), ptr(ws),
+              ws.numel(), stream_handle(dev))
+    return back_to(keep[:int(count.item())], boxes)
+
+
 # ---------------------------------------------------------------------------
 from .sparse_conv import sparse_conv, sparse_conv_transpose  # noqa: E402,F401
 
 
 __all__ = ["build_spatial_hash_table", "fixed_radius_search", "knn_search", "ragged_to_dense",
            "reduce_subarrays_sum", "voxelize", "grid_subsample", "calculate_grid", "furthest_point_sampling",
-           "ball_query", "three_nn", "three_interpolate", "three_interpolate_grad", "sparse_conv",
+           "ball_query", "three_nn", "three_interpolate", "three_interpolate_grad", "nms", "sparse_conv",
            "sparse_conv_transpose"]

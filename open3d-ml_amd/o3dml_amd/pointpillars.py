@@ -411,6 +411,24 @@ class SECONDFPN(nn.Module):
         return torch.cat(ups, dim=1) if len(ups) > 1 else ups[0]
 
 
+def multiclass_nms(boxes, scores, score_thr):
+    """Per-class rotated BEV NMS (objdet_helper.py:316-349): boxes [N,7] xyzwhlr,
+    scores [N,C] -> list of C int64 index tensors.  Score filter, then the HIP
+    ``ops.nms`` at IoU 0.01 on (x-w/2, y-l/2, x+w/2, y+l/2, yaw)."""
+    idxs = []
+    bev = boxes[:, [0, 1, 3, 4, 6]]
+    half = bev[:, 2:4] / 2
+    xyxyr = torch.cat([bev[:, :2] - half, bev[:, :2] + half, bev[:, 4:5]], 1)
+    for c in range(scores.shape[1]):
+        sel = torch.nonzero(scores[:, c] > score_thr).squeeze(1)
+        if sel.numel() == 0:
+            idxs.append(torch.empty((0,), dtype=torch.long, device=boxes.device))
+            continue
+        keep = ops.nms(xyxyr[sel].contiguous(), scores[sel, c].contiguous(), 0.01)
+        idxs.append(sel[keep])
+    return idxs
+
+
 class Anchor3DHead(nn.Module):
     """Anchor head + target assignment (point_pillars.py:743-1025)."""
 
@@ -451,6 +469,32 @@ class Anchor3DHead(nn.Module):
         if key not in self._anchor_cache:
             self._anchor_cache[key] = self.anchor_generator.grid_anchors(fs, device=device)
         return self._anchor_cache[key]
+
+    def get_bboxes(self, cls_scores, bbox_preds, dir_preds):
+        """Decoded, NMS-filtered boxes per scene (point_pillars.py:946-966)."""
+        out = [self.get_bboxes_single(c, b, d) for c, b, d in zip(cls_scores, bbox_preds, dir_preds)]
+        return [o[0] for o in out], [o[1] for o in out], [o[2] for o in out]
+
+    def get_bboxes_single(self, cls_scores, bbox_preds, dir_preds):
+        """point_pillars.py:968-1025: top-nms_pre anchors by max class score,
+        decode, multiclass rotated NMS (HIP), direction-bin yaw fix-up."""
+        anchors = self._anchors(cls_scores.shape[-2:], cls_scores.device).reshape(-1, self.box_code_size)
+        dir_scores = torch.max(dir_preds.permute(1, 2, 0).reshape(-1, 2), dim=-1)[1]
+        scores = cls_scores.permute(1, 2, 0).reshape(-1, self.num_classes).sigmoid()
+        bbox_preds = bbox_preds.permute(1, 2, 0).reshape(-1, self.box_code_size)
+        if scores.shape[0] > self.nms_pre:
+            _, topk = scores.max(dim=1)[0].topk(self.nms_pre)
+            anchors, bbox_preds, scores, dir_scores = anchors[topk], bbox_preds[topk], scores[topk], dir_scores[topk]
+        bboxes = self.bbox_coder.decode(anchors, bbox_preds)
+        idxs = multiclass_nms(bboxes, scores, self.score_thr)
+        labels = torch.cat([torch.full((len(idxs[i]),), i, dtype=torch.long) for i in range(self.num_classes)])
+        scores = torch.cat([scores[idxs[i], i] for i in range(self.num_classes)])
+        idxs = torch.cat(idxs)
+        bboxes, dir_scores = bboxes[idxs], dir_scores[idxs]
+        if bboxes.shape[0] > 0:
+            dir_rot = limit_period(bboxes[..., 6] - self.dir_offset, 1, np.pi)
+            bboxes[..., 6] = dir_rot + self.dir_offset + np.pi * dir_scores.to(bboxes.dtype)
+        return bboxes, scores, labels
 
     def assign_bboxes(self, pred_bboxes, target_bboxes):
         """Per scene and class: IoU of the BEV boxes of the targets and the

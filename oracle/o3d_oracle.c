@@ -737,3 +737,120 @@ ORC_API void orc_kernel_index(const float* inp_pos, const float* query_pos,
             kidx[e] = (id[2] * ksize[1] + id[1]) * ksize[2] + id[0];
         }
 }
+
+/* ---- nms (open3d.ml.torch.ops.nms, bound at ml3d/torch/utils/objdet_helper.py:27,
+ * called by multiclass_nms :346 from PointPillars.get_bboxes_single
+ * point_pillars.py:1005).  † Open3D NmsImpl / IoUImpl (OpenPCDet rotated BEV
+ * IoU): boxes (x1,y1,x2,y2,yaw) rotated about their centre; intersection =
+ * convex polygon of edge crossings + contained corners (margin 1e-5), sorted by
+ * ascending atan2 about their mean, shoelace area; IoU = inter/max(sa+sb-inter,
+ * 1e-8).  Greedy in stable descending score order; a box is dropped when its
+ * IoU with an earlier kept box is > thresh.  Returns the kept count; keep[]
+ * holds original indices in score order. */
+typedef struct { float x, y; } orc_p2;
+
+static float orc_cross3(orc_p2 p1, orc_p2 p2, orc_p2 p0) {
+    return (p1.x - p0.x) * (p2.y - p0.y) - (p2.x - p0.x) * (p1.y - p0.y);
+}
+
+static int orc_rect_cross(orc_p2 p1, orc_p2 p2, orc_p2 q1, orc_p2 q2) {
+    return fminf(p1.x, p2.x) <= fmaxf(q1.x, q2.x) && fminf(q1.x, q2.x) <= fmaxf(p1.x, p2.x) &&
+           fminf(p1.y, p2.y) <= fmaxf(q1.y, q2.y) && fminf(q1.y, q2.y) <= fmaxf(p1.y, p2.y);
+}
+
+static int orc_in_box(const float* b, orc_p2 p) {
+    const float margin = 1e-5f;
+    const float cx = (b[0] + b[2]) * 0.5f, cy = (b[1] + b[3]) * 0.5f;
+    const float c = cosf(-b[4]), s = sinf(-b[4]);
+    const float rx = (p.x - cx) * c + (p.y - cy) * s + cx;
+    const float ry = -(p.x - cx) * s + (p.y - cy) * c + cy;
+    return rx > b[0] - margin && rx < b[2] + margin && ry > b[1] - margin && ry < b[3] + margin;
+}
+
+static int orc_seg_cross(orc_p2 p1, orc_p2 p0, orc_p2 q1, orc_p2 q0, orc_p2* ans) {
+    if (!orc_rect_cross(p0, p1, q0, q1)) return 0;
+    const float s1 = orc_cross3(q0, p1, p0), s2 = orc_cross3(p1, q1, p0);
+    const float s3 = orc_cross3(p0, q1, q0), s4 = orc_cross3(q1, p1, q0);
+    if (!(s1 * s2 > 0.f && s3 * s4 > 0.f)) return 0;
+    const float s5 = orc_cross3(q1, p1, p0);
+    if (fabsf(s5 - s1) > 1e-8f) {
+        ans->x = (s5 * q0.x - s1 * q1.x) / (s5 - s1);
+        ans->y = (s5 * q0.y - s1 * q1.y) / (s5 - s1);
+    } else {
+        const float a0 = p0.y - p1.y, b0 = p1.x - p0.x, c0 = p0.x * p1.y - p1.x * p0.y;
+        const float a1 = q0.y - q1.y, b1 = q1.x - q0.x, c1 = q0.x * q1.y - q1.x * q0.y;
+        const float d = a0 * b1 - a1 * b0;
+        ans->x = (b0 * c1 - b1 * c0) / d;
+        ans->y = (a1 * c0 - a0 * c1) / d;
+    }
+    return 1;
+}
+
+static void orc_box_corners(const float* b, orc_p2* c) {
+    const float cx = (b[0] + b[2]) * 0.5f, cy = (b[1] + b[3]) * 0.5f;
+    const float co = cosf(b[4]), si = sinf(b[4]);
+    const float xs[4] = {b[0], b[2], b[2], b[0]}, ys[4] = {b[1], b[1], b[3], b[3]};
+    for (int k = 0; k < 4; ++k) {
+        c[k].x = (xs[k] - cx) * co + (ys[k] - cy) * si + cx;
+        c[k].y = -(xs[k] - cx) * si + (ys[k] - cy) * co + cy;
+    }
+    c[4] = c[0];
+}
+
+ORC_API float orc_bev_iou(const float* a, const float* b) {
+    orc_p2 ca[5], cb[5], pts[16], ctr = {0.f, 0.f};
+    int cnt = 0;
+    orc_box_corners(a, ca);
+    orc_box_corners(b, cb);
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            if (orc_seg_cross(ca[i + 1], ca[i], cb[j + 1], cb[j], &pts[cnt])) {
+                ctr.x += pts[cnt].x;
+                ctr.y += pts[cnt].y;
+                ++cnt;
+            }
+    for (int k = 0; k < 4; ++k) {
+        if (orc_in_box(a, cb[k])) { ctr.x += cb[k].x; ctr.y += cb[k].y; pts[cnt++] = cb[k]; }
+        if (orc_in_box(b, ca[k])) { ctr.x += ca[k].x; ctr.y += ca[k].y; pts[cnt++] = ca[k]; }
+    }
+    float area = 0.f;
+    if (cnt > 2) {
+        ctr.x /= cnt;
+        ctr.y /= cnt;
+        for (int j = 0; j < cnt - 1; ++j)
+            for (int i = 0; i < cnt - j - 1; ++i)
+                if (atan2f(pts[i].y - ctr.y, pts[i].x - ctr.x) > atan2f(pts[i + 1].y - ctr.y, pts[i + 1].x - ctr.x)) {
+                    orc_p2 t = pts[i];
+                    pts[i] = pts[i + 1];
+                    pts[i + 1] = t;
+                }
+        for (int k = 0; k < cnt - 1; ++k) {
+            const float ux = pts[k].x - pts[0].x, uy = pts[k].y - pts[0].y;
+            const float vx = pts[k + 1].x - pts[0].x, vy = pts[k + 1].y - pts[0].y;
+            area += ux * vy - uy * vx;
+        }
+    }
+    const float inter = fabsf(area) * 0.5f;
+    const float sa = (a[2] - a[0]) * (a[3] - a[1]), sb = (b[2] - b[0]) * (b[3] - b[1]);
+    return inter / fmaxf(sa + sb - inter, 1e-8f);
+}
+
+ORC_API int64_t orc_nms(const float* boxes, const float* scores, int64_t n, float thresh, int64_t* keep) {
+    int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+    char* gone = (char*)calloc((size_t)(n > 0 ? n : 1), 1);
+    for (int64_t i = 0; i < n; ++i) { /* stable descending: rank by comparison count */
+        int64_t r = 0;
+        for (int64_t j = 0; j < n; ++j) r += scores[j] > scores[i] || (scores[j] == scores[i] && j < i);
+        order[r] = i;
+    }
+    int64_t cnt = 0;
+    for (int64_t a = 0; a < n; ++a) {
+        if (gone[a]) continue;
+        keep[cnt++] = order[a];
+        for (int64_t b = a + 1; b < n; ++b)
+            if (!gone[b] && orc_bev_iou(boxes + order[a] * 5, boxes + order[b] * 5) > thresh) gone[b] = 1;
+    }
+    free(order);
+    free(gone);
+    return cnt;
+}

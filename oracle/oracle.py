@@ -32,6 +32,8 @@ def lib():
         _lib = ctypes.CDLL(_LIB_PATH)
         _lib.orc_hash_table_splits.restype = ctypes.c_int64
         _lib.orc_grid_subsample.restype = ctypes.c_int64
+        _lib.orc_nms.restype = ctypes.c_int64
+        _lib.orc_bev_iou.restype = ctypes.c_float
     return _lib
 
 
@@ -367,3 +369,19 @@ def calculate_grid(in_positions):
     out = out[~(out % 2).astype(bool).any(1)]
     out = np.unique(out, axis=0)
     return (out + 0.5).astype(np.float32)
+
+
+def bev_iou(a, b):
+    """Rotated BEV IoU of two (x1,y1,x2,y2,yaw) boxes (o3d_oracle.c orc_bev_iou)."""
+    a, b = _f32(a), _f32(b)
+    return float(lib().orc_bev_iou(_p(a), _p(b)))
+
+
+def nms(boxes, scores, thresh):
+    """open3d.ml.torch.ops.nms (objdet_helper.py:27,346): kept original indices, int64,
+    in stable descending score order (o3d_oracle.c orc_nms)."""
+    boxes, scores = _f32(boxes).reshape(-1, 5), _f32(scores).reshape(-1)
+    n = scores.shape[0]
+    keep = np.zeros(max(n, 1), np.int64)
+    cnt = lib().orc_nms(_p(boxes), _p(scores), ctypes.c_int64(n), ctypes.c_float(thresh), _p(keep))
+    return keep[:cnt].copy()

@@ -8,7 +8,7 @@ IMPORTS = [
     ("open3d.ml.torch.ops", ["voxelize", "ragged_to_dense", "reduce_subarrays_sum", "knn_search",
                              "fixed_radius_search", "build_spatial_hash_table", "furthest_point_sampling",
                              "ball_query", "three_nn", "three_interpolate", "three_interpolate_grad",
-                             "sparse_conv", "sparse_conv_transpose"]),
+                             "nms", "sparse_conv", "sparse_conv_transpose"]),
     ("open3d.ml.torch.layers", ["FixedRadiusSearch", "KNNSearch", "SparseConv", "SparseConvTranspose"]),
     ("open3d.ml.contrib", ["subsample", "subsample_batch"]),
     ("open3d.core", ["Tensor", "nns", "cuda"]),
