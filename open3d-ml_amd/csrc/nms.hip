@@ -11,11 +11,12 @@
 //   1. rank kernel: stable descending score order (rank = #{higher score} +
 //      #{equal score with lower index}), O(N^2) compares over an LDS-staged
 //      score tile — N is a few hundred per class (nms_pre = 100 upstream);
-//   2. mask kernel: one 64-lane wavefront per (row block, column block) pair
-//      of the upper triangle; the 64 column boxes are staged in LDS and each
-//      lane writes one 64-bit suppression word (bit j: box j overlaps box i);
+//   2. mask kernel: one 64-lane wavefront per (row, column block) of the upper
+//      triangle; lane l tests column block*64+l and the wave ballot is the
+//      64-bit suppression word (bit l: box block*64+l overlaps box row);
 //   3. sweep kernel: one wavefront walks the sorted boxes in order, keeping
-//      the running "removed" bitmap in LDS and OR-ing in each kept box's row.
+//      the running "removed" bitmap (and, up to 64 KiB, the mask) in LDS and
+//      OR-ing in each kept box's row.
 #include "common.hpp"
 
 namespace o3dml {
@@ -151,43 +152,56 @@ __global__ void __launch_bounds__(256) nms_rank_kernel(const float* __restrict__
     if (i < n) order[rank] = i;
 }
 
-// mask[i * words + cb] bit t: sorted box (cb*64 + t) > i overlaps sorted box i.
-__global__ void __launch_bounds__(kNmsBlock) nms_mask_kernel(const float* __restrict__ boxes,
-                                                             const int32_t* __restrict__ order, int n, int words,
-                                                             float thresh, uint64_t* __restrict__ mask) {
-    const int rb = blockIdx.y, cb = blockIdx.x;
-    if (cb < rb) return;
-    __shared__ float cols[kNmsBlock * 5];
-    const int t = threadIdx.x;
-    const int jc = cb * kNmsBlock + t;
-    if (jc < n) {
-        const float* src = boxes + static_cast<int64_t>(order[jc]) * 5;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) cols[t * 5 + k] = src[k];
-    }
-    __syncthreads();
-    const int i = rb * kNmsBlock + t;
-    if (i >= n) return;
-    float me[5];
+// mask[i * words + cb] bit l: sorted box (cb*64 + l) > i overlaps sorted box i.
+// One wavefront per (row i, column block cb): lane l evaluates column cb*64+l
+// and the 64-bit word is the wave ballot, so the n*words words come from
+// n*words independent waves (the IoU is ~200 dependent ALU ops with a small
+// private polygon array; wave-level parallelism is what hides it).
+constexpr int kNmsRowsPerBlock = 4;
+__global__ void __launch_bounds__(kNmsBlock* kNmsRowsPerBlock)
+        nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ order, int n, int words,
+                        float thresh, uint64_t* __restrict__ mask) {
+    const int lane = threadIdx.x & (kNmsBlock - 1);
+    const int i = blockIdx.y * kNmsRowsPerBlock + (threadIdx.x >> 6);
+    const int cb = blockIdx.x;
+    if (i >= n || cb < (i >> 6)) return;  // wave-uniform
+    const int j = cb * kNmsBlock + lane;
+    float me[5], other[5];
     const float* src = boxes + static_cast<int64_t>(order[i]) * 5;
 #pragma unroll
     for (int k = 0; k < 5; ++k) me[k] = src[k];
-    const int ncols = min(kNmsBlock, n - cb * kNmsBlock);
-    const int start = (cb == rb) ? t + 1 : 0;
-    uint64_t bits = 0;
-    for (int c = start; c < ncols; ++c)
-        if (bev_iou(me, cols + c * 5) > thresh) bits |= 1ull << c;
-    mask[static_cast<int64_t>(i) * words + cb] = bits;
+    bool hit = false;
+    if (j > i && j < n) {
+        const float* o = boxes + static_cast<int64_t>(order[j]) * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) other[k] = o[k];
+        hit = bev_iou(me, other) > thresh;
+    }
+    const uint64_t bits = __ballot(hit);
+    if (lane == 0) mask[static_cast<int64_t>(i) * words + cb] = bits;
 }
 
 // One wavefront: greedy sweep in score order.  keep[] gets original indices.
+// STAGE: the whole upper-triangular mask is first copied into LDS (coalesced),
+// so the sequential loop touches no global memory; otherwise each kept row is
+// read from global memory.
+template <bool STAGE>
 __global__ void __launch_bounds__(kNmsBlock) nms_sweep_kernel(const uint64_t* __restrict__ mask,
                                                               const int32_t* __restrict__ order, int n, int words,
                                                               int64_t* __restrict__ keep,
                                                               int64_t* __restrict__ keep_count) {
-    extern __shared__ uint64_t removed[];
+    extern __shared__ uint64_t lds[];
+    uint64_t* removed = lds;
+    uint64_t* rows = lds + words;
     const int t = threadIdx.x;
     for (int w = t; w < words; w += kNmsBlock) removed[w] = 0;
+    if (STAGE) {
+        const int64_t total = static_cast<int64_t>(n) * words;
+        for (int64_t e = t; e < total; e += kNmsBlock) {
+            const int r = static_cast<int>(e / words), w = static_cast<int>(e - static_cast<int64_t>(r) * words);
+            if (w >= (r >> 6)) rows[e] = mask[e];
+        }
+    }
     __syncthreads();
     int64_t cnt = 0;
     for (int i = 0; i < n; ++i) {
@@ -196,7 +210,7 @@ __global__ void __launch_bounds__(kNmsBlock) nms_sweep_kernel(const uint64_t* __
         if (gone) continue;
         if (t == 0) keep[cnt] = order[i];
         ++cnt;
-        const uint64_t* row = mask + static_cast<int64_t>(i) * words;
+        const uint64_t* row = (STAGE ? rows : mask) + static_cast<int64_t>(i) * words;
         for (int w = (i >> 6) + t; w < words; w += kNmsBlock) removed[w] |= row[w];
         __syncthreads();
     }
@@ -209,6 +223,7 @@ using namespace o3dml;
 
 namespace {
 constexpr int64_t kNmsMaxBoxes = 1 << 16;  // mask = N^2/8 bytes (512 MiB at the cap)
+constexpr size_t kNmsStageBytes = 64 * 1024;  // mask staged in LDS up to ~700 boxes
 inline int64_t nms_words(int64_t n) { return ceil_div(n, kNmsBlock); }
 }  // namespace
 
@@ -235,9 +250,15 @@ O3DML_API int o3dml_nms(const float* boxes, const float* scores, int64_t n, floa
     uint64_t* mask = ws.take<uint64_t>(n * words);
     nms_rank_kernel<<<static_cast<unsigned>(ceil_div(n, 256)), 256, 0, st>>>(scores, ni, order);
     O3DML_LAUNCH_CHECK();
-    nms_mask_kernel<<<dim3(words, words), kNmsBlock, 0, st>>>(boxes, order, ni, words, nms_overlap_thresh, mask);
+    nms_mask_kernel<<<dim3(words, static_cast<unsigned>(ceil_div(n, kNmsRowsPerBlock))), kNmsBlock * kNmsRowsPerBlock,
+                      0, st>>>(boxes, order, ni, words, nms_overlap_thresh, mask);
     O3DML_LAUNCH_CHECK();
-    nms_sweep_kernel<<<1, kNmsBlock, sizeof(uint64_t) * words, st>>>(mask, order, ni, words, keep, keep_count);
+    const size_t staged = sizeof(uint64_t) * (static_cast<size_t>(words) + static_cast<size_t>(n) * words);
+    if (staged <= kNmsStageBytes)
+        nms_sweep_kernel<true><<<1, kNmsBlock, staged, st>>>(mask, order, ni, words, keep, keep_count);
+    else
+        nms_sweep_kernel<false><<<1, kNmsBlock, sizeof(uint64_t) * words, st>>>(mask, order, ni, words, keep,
+                                                                                keep_count);
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }
