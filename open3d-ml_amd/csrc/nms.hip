@@ -79,7 +79,7 @@ __device__ __forceinline__ void box_corners(const float* b, P2* c) {
 }
 
 __device__ float bev_iou(const float* a, const float* b) {
-    P2 ca[5], cb[5], pts[16];
+    P2 ca[5], cb[5], pts[24];  // <= 16 edge crossings + 8 contained corners
     box_corners(a, ca);
     box_corners(b, cb);
     int cnt = 0;
@@ -131,21 +131,31 @@ __device__ float bev_iou(const float* a, const float* b) {
     return inter / fmaxf(sa + sb - inter, kNmsEps);
 }
 
-// order[rank(i)] = i, stable descending by score.
+// Total-order sort key of a score: ascending floats map to ascending keys,
+// -0 and +0 share a key (they compare equal), every NaN maps to 0, below -inf.
+// With the index tie-break the ranks are a permutation for any input, so
+// order[] is always fully written.
+__device__ __forceinline__ uint32_t score_key(float s) {
+    if (s != s) return 0u;
+    const uint32_t u = __float_as_uint(s + 0.0f);  // -0 -> +0
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// order[rank(i)] = i, stable descending by score_key.
 __global__ void __launch_bounds__(256) nms_rank_kernel(const float* __restrict__ scores, int n,
                                                         int32_t* __restrict__ order) {
-    __shared__ float tile[256];
+    __shared__ uint32_t tile[256];
     const int i = blockIdx.x * 256 + threadIdx.x;
-    const float si = i < n ? scores[i] : 0.f;
+    const uint32_t ki = i < n ? score_key(scores[i]) : 0u;
     int rank = 0;
     for (int base = 0; base < n; base += 256) {
         const int j = base + threadIdx.x;
-        tile[threadIdx.x] = j < n ? scores[j] : 0.f;
+        tile[threadIdx.x] = j < n ? score_key(scores[j]) : 0u;
         __syncthreads();
         const int lim = min(256, n - base);
         for (int t = 0; t < lim; ++t) {
-            const float sj = tile[t];
-            rank += (sj > si) || (sj == si && base + t < i);
+            const uint32_t kj = tile[t];
+            rank += (kj > ki) || (kj == ki && base + t < i);
         }
         __syncthreads();
     }

@@ -425,7 +425,13 @@ def three_interpolate_grad(grad_out, idx, weights, M):
 def nms(boxes, scores, nms_overlap_thresh):
     """Open3D ``ops.nms`` (objdet_helper.py:27, called at :346): rotated BEV NMS.
     boxes f32 [N,5] (x1,y1,x2,y2,yaw), scores f32 [N] -> int64 kept indices in
-    descending-score order (stable for ties); IoU > threshold suppresses."""
+    descending-score order (stable for ties); IoU > threshold suppresses.
+
+    Scores are ranked by a total order: -0 equals +0 and NaN ranks below -inf
+    (so a NaN-scored box is visited last, never first).  The suppression mask
+    is N*ceil(N/64)*8 bytes of workspace (N^2/8: 1.25 MiB at 3,200 boxes,
+    512 MiB at the cap); N is limited to 65,536 boxes and a larger call raises
+    RuntimeError before anything is allocated."""
     dev = gpu_device(boxes, scores)
     if boxes.dim() != 2 or boxes.shape[1] != 5:
         raise RuntimeError("nms: boxes must be [N, 5], got %s" % (tuple(boxes.shape),))
@@ -433,6 +439,8 @@ def nms(boxes, scores, nms_overlap_thresh):
         raise RuntimeError("nms: scores must be [N] matching boxes")
     lib = _lib.load()
     n = boxes.shape[0]
+    if n > 65536:
+        raise RuntimeError("nms: %d boxes exceed the 65,536-box cap (N^2/8-byte suppression mask)" % n)
     b = to_dev(boxes, dev, torch.float32)
     s = to_dev(scores, dev, torch.float32)
     keep = torch.empty((max(n, 1),), dtype=torch.int64, device=dev)

@@ -798,7 +798,7 @@ static void orc_box_corners(const float* b, orc_p2* c) {
 }
 
 ORC_API float orc_bev_iou(const float* a, const float* b) {
-    orc_p2 ca[5], cb[5], pts[16], ctr = {0.f, 0.f};
+    orc_p2 ca[5], cb[5], pts[24], ctr = {0.f, 0.f}; /* <= 16 crossings + 8 corners */
     int cnt = 0;
     orc_box_corners(a, ca);
     orc_box_corners(b, cb);
@@ -835,12 +835,26 @@ ORC_API float orc_bev_iou(const float* a, const float* b) {
     return inter / fmaxf(sa + sb - inter, 1e-8f);
 }
 
+/* Total-order score key: ascending floats -> ascending keys, -0 == +0, every
+ * NaN -> 0 (below -inf), so the ranks below are a permutation for any input. */
+static uint32_t orc_score_key(float s) {
+    if (s != s) return 0u;
+    float z = s + 0.0f; /* -0 -> +0 */
+    uint32_t u;
+    memcpy(&u, &z, sizeof u);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
 ORC_API int64_t orc_nms(const float* boxes, const float* scores, int64_t n, float thresh, int64_t* keep) {
     int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
     char* gone = (char*)calloc((size_t)(n > 0 ? n : 1), 1);
     for (int64_t i = 0; i < n; ++i) { /* stable descending: rank by comparison count */
+        const uint32_t ki = orc_score_key(scores[i]);
         int64_t r = 0;
-        for (int64_t j = 0; j < n; ++j) r += scores[j] > scores[i] || (scores[j] == scores[i] && j < i);
+        for (int64_t j = 0; j < n; ++j) {
+            const uint32_t kj = orc_score_key(scores[j]);
+            r += kj > ki || (kj == ki && j < i);
+        }
         order[r] = i;
     }
     int64_t cnt = 0;
