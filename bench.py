@@ -69,7 +69,7 @@ def make_batch(rank, scenes, dev):
     return torch.from_numpy(pts).to(dev), torch.from_numpy(rs)
 
 
-KERNELS = ("frs_group_search", "frs_group_rows", "frs_fine_search", "frs_row_sort")
+KERNELS = ("frs_group_search", "frs_group_rows")
 
 
 def kernel_profile(step, n_queries, pairs, reps):

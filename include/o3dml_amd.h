@@ -32,7 +32,7 @@ const char* o3dml_last_error(void);
 int o3dml_version(void);
 int o3dml_device_info(int device, int* cu_count, int* arch_major, int* arch_minor);
 /* Optional kernel timing: HIP events on the launch stream around the main
- * kernels (names e.g. "frs_fine_count", "frs_fine_fill", "frs_row_sort");
+ * kernels (names e.g. "frs_group_search", "frs_group_rows");
  * o3dml_timing_get synchronises on the recorded events. */
 void o3dml_timing_enable(int on);
 void o3dml_timing_reset(void);

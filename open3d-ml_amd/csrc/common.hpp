@@ -84,7 +84,7 @@ struct TimedRegion {
     ~TimedRegion() { end(); }
 };
 
-inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Grid size for grid-stride streaming kernels: enough workgroups to fill the
 // 256 CUs several times over, capped (cdna_hip_programming.md Guideline 11).
@@ -180,6 +180,50 @@ __device__ __forceinline__ int batch_of(int64_t i, const int64_t* __restrict__ s
         if (splits[mid] <= i) lo = mid; else hi = mid - 1;
     }
     return lo;
+}
+
+// v_writelane: set lane LANE of v to the uniform value x (one instruction;
+// the lane select is an inline constant, the value an SGPR).
+template <int LANE>
+__device__ __forceinline__ int write_lane(int v, int x) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(LANE));
+    return v;
+}
+
+// Fourth word of a raw buffer resource on gfx950 (32-bit data format, no
+// swizzle/stride): used with __builtin_amdgcn_make_buffer_rsrc.
+constexpr int kBufferFlags = 0x00020000;
+
+// Row splits staged in LDS for the batch lookups of a streaming kernel (the
+// binary search then costs LDS latency, not a chain of global loads); splits
+// that do not fit are searched in global memory.  Call from every thread.
+constexpr int kLdsSplits = 1024;
+__device__ __forceinline__ const int64_t* stage_splits(int64_t* lds, const int64_t* __restrict__ splits,
+                                                       int n_batch) {
+    if (n_batch + 1 > kLdsSplits) return splits;
+    for (int i = threadIdx.x; i <= n_batch; i += blockDim.x) lds[i] = splits[i];
+    __syncthreads();
+    return lds;
+}
+
+// XCD-contiguous block order for streaming kernels whose blocks each take one
+// contiguous range: workgroups are dealt round-robin to the 8 XCDs, so with a
+// grid that is a multiple of 8, XCD x runs blocks x, x+8, ... — remapped here
+// to ranges x*G/8 ... (x+1)*G/8-1, i.e. one contiguous slice of the array per
+// XCD (its L2 then holds the data that slice touches).
+__device__ __forceinline__ int64_t xcd_block() {
+    const int64_t g = gridDim.x, b = blockIdx.x;
+    return (g & 7) ? b : (b & 7) * (g >> 3) + (b >> 3);
+}
+
+// Grid for xcd_block() kernels: a multiple of 8, ~4 block-strides of work per
+// block, at most 2048 blocks.
+inline unsigned xcd_grid(int64_t n, int block) {
+    int64_t g = ceil_div(n, 4 * static_cast<int64_t>(block));
+    g = ((g + 7) / 8) * 8;
+    if (g < 8) g = 8;
+    if (g > 2048) g = 2048;
+    return static_cast<unsigned>(g);
 }
 
 }  // namespace o3dml

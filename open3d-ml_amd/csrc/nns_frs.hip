@@ -4,716 +4,70 @@
 // search sparseconvnet.py:362-367).
 //
 // Output: per query every point of its batch item with dist <= r (L2 squared /
-// L1 / Linf), in the canonical order of oracle/o3d_oracle.c (Open3D hash bins
-// ascending, point ids ascending inside a bin).  Two paths:
-//   A (default) fine r-cell hash grid + per-row sort      (see below)
-//   B (fallback) Open3D-cell segments through LDS windows (cells beyond +-2^30)
+// L1 / Linf) among the points of the hash buckets Open3D visits (the bucket of
+// the query's own 2r-cell and of the cells of the 8 corners q +- r), in the
+// canonical order of oracle/o3d_oracle.c: buckets ascending, point ids
+// ascending inside a bucket — i.e. ascending position in hash_table_index.
+//
+// Query groups over Open3D's own buckets.  Two queries whose 9 visited
+// buckets are identical visit exactly the same points in the same order.  A
+// wave takes 64 consecutive queries in (batch, Morton r-cell) order, splits
+// them into such groups (typically the queries of one octant of a 2r-cell)
+// and, per group:
+//   1. streams the group's buckets in ascending order — Open3D's visit order —
+//      with coalesced 16-B loads, keeping only points within the metric's
+//      distance of the group's bounding box (the box test uses the same fp32
+//      operations as the exact test on smaller operands, so it never drops a
+//      neighbour), compacted IN ORDER into an LDS list;
+//   2. tests the list against the group's queries with S = 64 / G lanes per
+//      query (G = group size rounded up to a power of two): lane (g, s) tests
+//      entries s, s + S, ... of query g; a ballot + mbcnt ranks every hit, so
+//      rows come out in canonical order with no sort.
+// The first kRowCap neighbours of a query go to its temp row (indexed by
+// query id), the count to counts[qid]; the fill phase copies the temp rows
+// into the final CSR and re-runs the rare longer rows straight into place.
 #include <algorithm>
 #include <cstdlib>
-#include <vector>
 
-#include "grid.hpp"
 #include "primitives.hpp"
 #include "spatial_hash.hpp"
 
 namespace o3dml {
 
-__global__ void gather_sorted_points_kernel(const float* __restrict__ points, const uint32_t* __restrict__ index,
-                                            int64_t n, float4* __restrict__ out) {
-    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
-         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+// out[j] = (points[index[j]], index[j]) — the points in Open3D bucket order, so
+// one bucket is one contiguous 16-B-per-point stream.  XCD-contiguous: the
+// workgroups of one XCD gather one contiguous range (one or two batch items at
+// a time), so the random reads inside a batch item stay in that XCD's L2.
+__global__ void __launch_bounds__(256) gather_sorted_points_kernel(const float* __restrict__ points,
+                                                                   const uint32_t* __restrict__ index, int64_t n,
+                                                                   float4* __restrict__ out, int sentinel) {
+    const int64_t per = ceil_div(n, static_cast<int64_t>(gridDim.x));
+    const int64_t blk = xcd_block();
+    const int64_t e = min(n, (blk + 1) * per);
+    for (int64_t j = blk * per + threadIdx.x; j < e; j += blockDim.x) {
         const uint32_t i = index[j];
         out[j] = make_float4(points[3 * static_cast<int64_t>(i)], points[3 * static_cast<int64_t>(i) + 1],
                              points[3 * static_cast<int64_t>(i) + 2], __uint_as_float(i));
     }
-}
-
-
-// ===========================================================================
-// Path A (default): fine r-cell hash grid + per-row canonical sort.
-//
-// The canonical order (bins ascending, ids ascending in a bin) is exactly the
-// order of the points' positions in the Open3D-sorted array (hash_table_index),
-// so the search may use any exact structure and restore order afterwards:
-//   * cells of edge r (double precision), one hash table per batch item
-//     (nextpow2(2 N_b) bins); each query scans the 2-3 cells per axis that
-//     intersect [q - r', q + r'] (r' = r(1+1e-6) covers fp32 rounding of the
-//     distance test), ~8x fewer candidates than Open3D's 2r bins;
-//   * a 30-bit cell fingerprint (cell coords mod 1024) in each record skips
-//     points of colliding cells — the only cells that could be visited twice
-//     lie within 2 cells, so the fingerprint makes every visit exact;
-//   * fill writes each neighbour's Open3D position; a wave-level segmented
-//     bitonic sort per row restores the canonical order and maps position ->
-//     point id.
-// ===========================================================================
-__device__ __forceinline__ uint32_t fine_mix(int32_t x, int32_t y, int32_t z) {
-    uint32_t h = (static_cast<uint32_t>(x) * 0x9E3779B1u) ^ (static_cast<uint32_t>(y) * 0x85EBCA77u) ^
-                 (static_cast<uint32_t>(z) * 0xC2B2AE3Du);
-    h ^= h >> 16;
-    h *= 0x7FEB352Du;
-    h ^= h >> 15;
-    h *= 0x846CA68Bu;
-    h ^= h >> 16;
-    return h;
-}
-
-__device__ __forceinline__ uint32_t fine_fp(int32_t x, int32_t y, int32_t z) {
-    return (static_cast<uint32_t>(x) & 1023u) | ((static_cast<uint32_t>(y) & 1023u) << 10) |
-           ((static_cast<uint32_t>(z) & 1023u) << 20);
-}
-
-__device__ __forceinline__ int32_t fine_cell(float p, double inv_h) {
-    return static_cast<int32_t>(floor(static_cast<double>(p) * inv_h));
-}
-
-// fine bin of every point (+ range flag when a cell coordinate leaves +-2^30)
-__global__ void fine_keys_kernel(const float* __restrict__ pts, int64_t n, const int64_t* __restrict__ rs, int nb,
-                                 const uint32_t* __restrict__ foff, double inv_h, uint32_t* __restrict__ keys,
-                                 int64_t* __restrict__ flag) {
-    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
-         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int b = batch_of(i, rs, nb);
-        const double cx = floor(static_cast<double>(pts[3 * i]) * inv_h);
-        const double cy = floor(static_cast<double>(pts[3 * i + 1]) * inv_h);
-        const double cz = floor(static_cast<double>(pts[3 * i + 2]) * inv_h);
-        const double lim = 1073741824.0;
-        if (!(fabs(cx) < lim && fabs(cy) < lim && fabs(cz) < lim)) *flag = 1;
-        const uint32_t base = foff[b], mask = foff[b + 1] - base - 1;
-        keys[i] = base + (fine_mix(static_cast<int32_t>(cx), static_cast<int32_t>(cy), static_cast<int32_t>(cz)) & mask);
-    }
-}
-
-__global__ void bin_bounds_kernel(const uint32_t* __restrict__ skeys, int64_t n, int64_t total,
-                                  uint32_t* __restrict__ splits) {
-    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
-         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t k = skeys[j];
-        const int64_t kp = j == 0 ? -1 : static_cast<int64_t>(skeys[j - 1]);
-        for (int64_t b = kp + 1; b <= k; ++b) splits[b] = static_cast<uint32_t>(j);
-        if (j == n - 1)
-            for (int64_t b = k + 1; b <= total; ++b) splits[b] = static_cast<uint32_t>(n);
-    }
-}
-
-// o3d position of every point: inv[hash_table_index[j]] = j
-__global__ void inverse_perm_kernel(const uint32_t* __restrict__ perm, int64_t n, uint32_t* __restrict__ inv) {
-    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
-         j += static_cast<int64_t>(gridDim.x) * blockDim.x)
-        inv[perm[j]] = static_cast<uint32_t>(j);
-}
-
-__global__ void fine_records_kernel(const float* __restrict__ pts, const uint32_t* __restrict__ order, int64_t n,
-                                    const uint32_t* __restrict__ o3dpos, double inv_h, float4* __restrict__ rec,
-                                    uint2* __restrict__ rid) {
-    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
-         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t i = order[j];
-        const float x = pts[3 * i], y = pts[3 * i + 1], z = pts[3 * i + 2];
-        rec[j] = make_float4(x, y, z, __uint_as_float(fine_fp(fine_cell(x, inv_h), fine_cell(y, inv_h),
-                                                              fine_cell(z, inv_h))));
-        rid[j] = make_uint2(o3dpos[i], static_cast<uint32_t>(i));
-    }
-}
-
-
-
-// ---- dense per-batch cell grid (used when sum of cells <= 8 N): cells are
-// x-fastest linear ids, so the 2-3 x-neighbour cells of a query row are one
-// contiguous run of records and spatial neighbours are neighbours in memory.
-struct DenseBatch {
-    double ox, oy, oz;
-    int32_t dx, dy, dz;
-    uint32_t offset;
-};
-
-__device__ __forceinline__ int32_t dense_axis(float p, double o, double inv_h, int32_t n) {
-    const int32_t c = static_cast<int32_t>(floor((static_cast<double>(p) - o) * inv_h));
-    return c < 0 ? 0 : (c >= n ? n - 1 : c);
-}
-
-__global__ void dense_keys_kernel(const float* __restrict__ pts, int64_t n, const int64_t* __restrict__ rs, int nb,
-                                  const DenseBatch* __restrict__ g, double inv_h, uint32_t* __restrict__ keys) {
-    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
-         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const DenseBatch d = g[batch_of(i, rs, nb)];
-        const int32_t cx = dense_axis(pts[3 * i], d.ox, inv_h, d.dx);
-        const int32_t cy = dense_axis(pts[3 * i + 1], d.oy, inv_h, d.dy);
-        const int32_t cz = dense_axis(pts[3 * i + 2], d.oz, inv_h, d.dz);
-        keys[i] = d.offset + static_cast<uint32_t>(cx + d.dx * (cy + d.dy * cz));
+    if (sentinel && blockIdx.x == 0 && threadIdx.x == 0) {  // out[n]: beyond every radius
+        const float inf = __builtin_huge_valf();
+        out[n] = make_float4(inf, inf, inf, 0.f);
     }
 }
 
 constexpr int kRowCap = 64;  // neighbours kept per query in the temp rows
 
-// Open3D visit-set membership of a hit p for query q: Open3D tests only the
-// points of the bins of q's own cell and of the cells of the 8 corners q+-r.
-// Exact: cell test first; the rare boundary case falls back to the bin test.
-struct O3dVisit {
-    int32_t lo[3], hi[3], c[3];
-};
-
-__device__ __forceinline__ O3dVisit o3d_visit(float qx, float qy, float qz, float r, float inv) {
-    O3dVisit v;
-    const float q[3] = {qx, qy, qz};
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        v.lo[a] = static_cast<int32_t>(floorf((q[a] - r) * inv));
-        v.hi[a] = static_cast<int32_t>(floorf((q[a] + r) * inv));
-        v.c[a] = static_cast<int32_t>(floorf(q[a] * inv));
-    }
-    return v;
-}
-
-__device__ __noinline__ bool o3d_bin_member(float px, float py, float pz, float qx, float qy, float qz, float r,
-                                            float inv, uint32_t first, uint32_t tsize) {
-    const uint32_t pb = first + point_bin(px, py, pz, inv, tsize);
-    const QueryBins qb = query_bins(qx, qy, qz, r, inv, first, tsize);
-    bool m = false;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) m |= qb.b[k] == pb;
-    return m;
-}
-
-__device__ __forceinline__ bool o3d_visited(const O3dVisit& v, float px, float py, float pz, float qx, float qy,
-                                            float qz, float r, float inv, uint32_t first, uint32_t tsize) {
-    const int32_t x = static_cast<int32_t>(floorf(px * inv));
-    const int32_t y = static_cast<int32_t>(floorf(py * inv));
-    const int32_t z = static_cast<int32_t>(floorf(pz * inv));
-    const bool corner = (x == v.lo[0] || x == v.hi[0]) && (y == v.lo[1] || y == v.hi[1]) &&
-                        (z == v.lo[2] || z == v.hi[2]);
-    if (corner || (x == v.c[0] && y == v.c[1] && z == v.c[2])) return true;
-    return o3d_bin_member(px, py, pz, qx, qy, qz, r, inv, first, tsize);
-}
-
-// MODE 0: one pass over every query, neighbours as (o3d position, id) into a
-//         kRowCap temp row, the full count into counts[q]; queries with more
-//         than kRowCap neighbours are appended to `over`.
-// MODE 1: re-run of the overflow queries, positions straight into the final
-//         rows (sorted afterwards by row_sort_long_kernel).
-template <bool DENSE, int METRIC, bool IGNORE, bool DIST, int MODE, class TIdx>
-__global__ void __launch_bounds__(256)
-frs_fine_search(const float4* __restrict__ rec, const uint2* __restrict__ rid, const uint32_t* __restrict__ fs,
-                const uint32_t* __restrict__ foff, const DenseBatch* __restrict__ dg, const float* __restrict__ queries,
-                int64_t m,
-                const uint32_t* __restrict__ qorder, const int64_t* __restrict__ n_over_in, double inv_h,
-                double rmargin, float r, float inv, float thr, int nb, const int64_t* __restrict__ qrs,
-                const uint32_t* __restrict__ hts, int64_t* __restrict__ counts, uint32_t* __restrict__ tpos,
-                uint32_t* __restrict__ tid, float* __restrict__ tdist, uint32_t* __restrict__ over,
-                int64_t* __restrict__ n_over, const int64_t* __restrict__ rs, TIdx* __restrict__ out_idx,
-                float* __restrict__ out_dist) {
-    const int64_t mm = MODE == 0 ? m : *n_over_in;
-    for (int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; t < mm;
-         t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t q = MODE == 0 ? static_cast<int64_t>(qorder[t]) : static_cast<int64_t>(over[t]);
-        const float qx = queries[3 * q], qy = queries[3 * q + 1], qz = queries[3 * q + 2];
-        const int b = batch_of(q, qrs, nb);
-        const uint32_t first = hts[b], tsize = hts[b + 1] - first;
-        const O3dVisit vis = o3d_visit(qx, qy, qz, r, inv);
-        int64_t cnt = 0;
-        const int64_t row = q * kRowCap;
-        const int64_t o = MODE == 1 ? rs[q] : 0;
-        auto test = [&](const float4& p, uint32_t j) {
-            if (IGNORE && p.x == qx && p.y == qy && p.z == qz) return;
-            const float d = dist_metric<METRIC>(p.x, p.y, p.z, qx, qy, qz);
-            if (d <= thr && o3d_visited(vis, p.x, p.y, p.z, qx, qy, qz, r, inv, first, tsize)) {
-                const uint2 pi = rid[j];
-                if constexpr (MODE == 0) {
-                    if (cnt < kRowCap) {
-                        tpos[row + cnt] = pi.x;
-                        tid[row + cnt] = pi.y;
-                        if constexpr (DIST) tdist[row + cnt] = d;
-                    }
-                } else {
-                    out_idx[o + cnt] = static_cast<TIdx>(pi.x);
-                    if constexpr (DIST) out_dist[o + cnt] = d;
-                }
-                ++cnt;
-            }
-        };
-        if constexpr (DENSE) {
-            const DenseBatch g = dg[b];
-            const double lx = (static_cast<double>(qx) - g.ox) * inv_h, ly = (static_cast<double>(qy) - g.oy) * inv_h,
-                         lz = (static_cast<double>(qz) - g.oz) * inv_h, rm = rmargin * inv_h;
-            const int32_t x0 = max(static_cast<int32_t>(floor(lx - rm)), 0);
-            const int32_t x1 = min(static_cast<int32_t>(floor(lx + rm)), g.dx - 1);
-            const int32_t y0 = max(static_cast<int32_t>(floor(ly - rm)), 0);
-            const int32_t y1 = min(static_cast<int32_t>(floor(ly + rm)), g.dy - 1);
-            const int32_t z0 = max(static_cast<int32_t>(floor(lz - rm)), 0);
-            const int32_t z1 = min(static_cast<int32_t>(floor(lz + rm)), g.dz - 1);
-            if (x0 <= x1)
-                for (int32_t cz = z0; cz <= z1; ++cz)
-                    for (int32_t cy = y0; cy <= y1; ++cy) {
-                        const uint32_t rowc = g.offset + static_cast<uint32_t>(g.dx * (cy + g.dy * cz));
-                        const uint32_t s0 = fs[rowc + x0], e0 = fs[rowc + x1 + 1];
-                        uint32_t j = s0;
-                        for (; j + 4 <= e0; j += 4) {  // 4 loads in flight per lane
-                            const float4 p0 = rec[j], p1 = rec[j + 1], p2 = rec[j + 2], p3 = rec[j + 3];
-                            test(p0, j);
-                            test(p1, j + 1);
-                            test(p2, j + 2);
-                            test(p3, j + 3);
-                        }
-                        for (; j < e0; ++j) test(rec[j], j);
-                    }
-        } else {
-            const uint32_t base = foff[b], mask = foff[b + 1] - base - 1;
-            const int32_t x0 = static_cast<int32_t>(floor((static_cast<double>(qx) - rmargin) * inv_h));
-            const int32_t x1 = static_cast<int32_t>(floor((static_cast<double>(qx) + rmargin) * inv_h));
-            const int32_t y0 = static_cast<int32_t>(floor((static_cast<double>(qy) - rmargin) * inv_h));
-            const int32_t y1 = static_cast<int32_t>(floor((static_cast<double>(qy) + rmargin) * inv_h));
-            const int32_t z0 = static_cast<int32_t>(floor((static_cast<double>(qz) - rmargin) * inv_h));
-            const int32_t z1 = static_cast<int32_t>(floor((static_cast<double>(qz) + rmargin) * inv_h));
-            for (int32_t cz = z0; cz <= z1; ++cz)
-                for (int32_t cy = y0; cy <= y1; ++cy)
-                    for (int32_t cx = x0; cx <= x1; ++cx) {
-                        const uint32_t bin = base + (fine_mix(cx, cy, cz) & mask);
-                        const uint32_t fp = fine_fp(cx, cy, cz);
-                        const uint32_t s0 = fs[bin], e0 = fs[bin + 1];
-                        for (uint32_t j = s0; j < e0; ++j) {
-                            const float4 p = rec[j];
-                            if (__float_as_uint(p.w) == fp) test(p, j);
-                        }
-                    }
-        }
-        if constexpr (MODE == 0) {
-            counts[q] = cnt;
-            if (cnt > kRowCap) over[atomicAdd(reinterpret_cast<unsigned long long*>(n_over), 1ull)] =
-                    static_cast<uint32_t>(q);
-        }
-    }
-}
-
-// Sort every temp row (<= kRowCap) by Open3D position and compact it into the
-// final CSR: one wave per row; every lane holds one entry and computes its
-// rank by counting the smaller keys of the row (keys are unique positions),
-// broadcast by v_readlane — no LDS permutes — then scatters to s + rank.
-template <bool DIST, class TIdx>
-__global__ void __launch_bounds__(256) row_sort_compact_kernel(const int64_t* __restrict__ rs, int64_t m,
-                                                               const uint32_t* __restrict__ tpos,
-                                                               const uint32_t* __restrict__ tid,
-                                                               const float* __restrict__ tdist,
-                                                               TIdx* __restrict__ idx, float* __restrict__ dist) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-    const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
-    // two rows per iteration: both rows' loads are issued before either is ranked
-    for (int64_t r0 = 2 * wave; r0 < m; r0 += 2 * nwaves) {
-        const int64_t r1 = r0 + 1;
-        const int64_t sA = rs[r0];
-        const int64_t eA = rs[r0 + 1];
-        const int64_t eB = r1 < m ? rs[r1 + 1] : eA;
-        const int lenA = static_cast<int>(eA - sA), lenB = static_cast<int>(eB - eA);
-        const bool okA = lenA <= kRowCap && lane < lenA;
-        const bool okB = lenB <= kRowCap && lane < lenB;
-        const int64_t srcA = r0 * kRowCap + lane, srcB = r1 * kRowCap + lane;
-        const uint32_t kA = okA ? tpos[srcA] : 0xffffffffu, kB = okB ? tpos[srcB] : 0xffffffffu;
-        const uint32_t vA = okA ? tid[srcA] : 0u, vB = okB ? tid[srcB] : 0u;
-        float dA = 0.f, dB = 0.f;
-        if constexpr (DIST) {
-            dA = okA ? tdist[srcA] : 0.f;
-            dB = okB ? tdist[srcB] : 0.f;
-        }
-        int rankA = 0, rankB = 0;
-        const int nA = lenA <= kRowCap ? lenA : 0, nB = lenB <= kRowCap ? lenB : 0;
-        for (int j = 0; j < nA; ++j) rankA += static_cast<uint32_t>(__builtin_amdgcn_readlane(kA, j)) < kA;
-        for (int j = 0; j < nB; ++j) rankB += static_cast<uint32_t>(__builtin_amdgcn_readlane(kB, j)) < kB;
-        if (okA) {
-            idx[sA + rankA] = static_cast<TIdx>(vA);
-            if constexpr (DIST) dist[sA + rankA] = dA;
-        }
-        if (okB) {
-            idx[eA + rankB] = static_cast<TIdx>(vB);
-            if constexpr (DIST) dist[eA + rankB] = dB;
-        }
-    }
-}
-
-// Rows longer than 64: one 1024-thread workgroup per row, bitonic in LDS
-// (<= 8192 entries), global-memory odd-even transposition beyond that.
-template <class TIdx>
-__global__ void __launch_bounds__(1024) row_sort_long_kernel(const int64_t* __restrict__ rs, const uint32_t* __restrict__ rows,
-                                                             const int64_t* __restrict__ n_long, TIdx* __restrict__ idx,
-                                                             float* __restrict__ dist, const uint32_t* __restrict__ hti) {
-    __shared__ uint32_t sk[8192];
-    __shared__ float sd[8192];
-    const int64_t nl = *n_long;
-    for (int64_t w = blockIdx.x; w < nl; w += gridDim.x) {
-        const int64_t r = rows[w];
-        const int64_t s = rs[r];
-        const int64_t len = rs[r + 1] - s;
-        if (len <= 8192) {
-            int P = 128;
-            while (P < len) P <<= 1;
-            for (int i = threadIdx.x; i < P; i += blockDim.x) {
-                sk[i] = i < len ? static_cast<uint32_t>(idx[s + i]) : 0xffffffffu;
-                sd[i] = (i < len && dist) ? dist[s + i] : 0.f;
-            }
-            __syncthreads();
-            for (int k = 2; k <= P; k <<= 1) {
-                for (int j = k >> 1; j > 0; j >>= 1) {
-                    for (int i = threadIdx.x; i < P; i += blockDim.x) {
-                        const int pr = i ^ j;
-                        if (pr > i) {
-                            const bool asc = (i & k) == 0;
-                            const uint32_t a = sk[i], bb = sk[pr];
-                            if ((a > bb) == asc) {
-                                sk[i] = bb;
-                                sk[pr] = a;
-                                const float t = sd[i];
-                                sd[i] = sd[pr];
-                                sd[pr] = t;
-                            }
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-            for (int i = threadIdx.x; i < len; i += blockDim.x) {
-                idx[s + i] = static_cast<TIdx>(hti[sk[i]]);
-                if (dist) dist[s + i] = sd[i];
-            }
-            __syncthreads();
-        } else {
-            // odd-even transposition sort in global memory (rare: > 8192 neighbours)
-            for (int64_t ph = 0; ph < len; ++ph) {
-                for (int64_t i = 2 * threadIdx.x + (ph & 1); i + 1 < len; i += 2 * blockDim.x) {
-                    const uint32_t a = static_cast<uint32_t>(idx[s + i]), bb = static_cast<uint32_t>(idx[s + i + 1]);
-                    if (a > bb) {
-                        idx[s + i] = static_cast<TIdx>(bb);
-                        idx[s + i + 1] = static_cast<TIdx>(a);
-                        if (dist) {
-                            const float t = dist[s + i];
-                            dist[s + i] = dist[s + i + 1];
-                            dist[s + i + 1] = t;
-                        }
-                    }
-                }
-                __threadfence_block();
-                __syncthreads();
-            }
-            for (int64_t i = threadIdx.x; i < len; i += blockDim.x)
-                idx[s + i] = static_cast<TIdx>(hti[static_cast<uint32_t>(idx[s + i])]);
-            __syncthreads();
-        }
-    }
-}
-
-// fine bin of each query's own cell (coherent processing order)
-__global__ void fine_query_keys_kernel(const float* __restrict__ q, int64_t m, const int64_t* __restrict__ qrs, int nb,
-                                       const uint32_t* __restrict__ foff, double inv_h, uint32_t* __restrict__ keys) {
-    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < m;
-         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int b = batch_of(i, qrs, nb);
-        const uint32_t base = foff[b], mask = foff[b + 1] - base - 1;
-        keys[i] = base + (fine_mix(fine_cell(q[3 * i], inv_h), fine_cell(q[3 * i + 1], inv_h),
-                                   fine_cell(q[3 * i + 2], inv_h)) &
-                          mask);
-    }
-}
-// ---------------------------------------------------------------------------
-// fixed-radius search kernels
-// ---------------------------------------------------------------------------
-// Per-query body over global memory (fallback for the rare chunks whose bins
-// are not in their segment's directory, i.e. two cells merged by the 13-bit
-// segment hash).
-template <int METRIC, bool IGNORE, bool FILL, class TIdx>
-__device__ __forceinline__ void frs_query_global(const float4* __restrict__ pts, const uint32_t* __restrict__ cs,
-                                                 const QueryBins& bins, float qx, float qy, float qz, float thr,
-                                                 int64_t& cnt, int64_t& o, TIdx* __restrict__ out_idx,
-                                                 float* __restrict__ out_dist) {
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        if (bins.b[k] == 0xffffffffu) continue;
-        const uint32_t s = cs[bins.b[k]], e = cs[bins.b[k] + 1];
-        for (uint32_t j = s; j < e; ++j) {
-            const float4 p = pts[j];
-            if (IGNORE && p.x == qx && p.y == qy && p.z == qz) continue;
-            const float d = dist_metric<METRIC>(p.x, p.y, p.z, qx, qy, qz);
-            if (d <= thr) {
-                if constexpr (FILL) {
-                    out_idx[o] = static_cast<TIdx>(__float_as_uint(p.w));
-                    if (out_dist) out_dist[o] = d;
-                    ++o;
-                } else {
-                    ++cnt;
-                }
-            }
-        }
-    }
-}
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ uint32_t wave_sort_u32(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint32_t o = __shfl_xor(v, j, 64);
-            const bool asc = (lane & k) == 0;
-            const bool lower = (lane & j) == 0;
-            const uint32_t mn = o < v ? o : v, mx = o < v ? v : o;
-            v = (lower == asc) ? mn : mx;
-        }
-    }
-    return v;
-}
-
-// Sorted, duplicate-free 9-bin list of a query (UINT_MAX padding at the end).
-__device__ __forceinline__ QueryBins unique_query_bins(float qx, float qy, float qz, float r, float inv,
-                                                       uint32_t first, uint32_t tsize) {
-    QueryBins bins = query_bins(qx, qy, qz, r, inv, first, tsize);
-#pragma unroll
-    for (int i = 8; i >= 1; --i)
-        if (bins.b[i] == bins.b[i - 1]) bins.b[i] = 0xffffffffu;
-#pragma unroll
-    for (int st = 0; st < 9; ++st) {
-#pragma unroll
-        for (int i = (st & 1); i + 1 < 9; i += 2) cswap(bins.b[i], bins.b[i + 1]);
-    }
-    return bins;
-}
-
-constexpr int kFrsWaves = 4;
-
-// One wave per cell segment (queries of one Open3D cell, sorted by octant).
-// The ascending union U of the bins of the cell's 27 neighbour cells is
-// streamed through an LDS window of WIN points per wave (coalesced 16-B
-// loads, each point fetched once per segment); every lane reads its own
-// (<= 9) bins from LDS.  Windows sweep U in bin order and each lane consumes
-// its bins in that order, so the output keeps the canonical order.
-template <int WIN, int METRIC, bool IGNORE, bool FILL, class TIdx>
-__global__ void __launch_bounds__(64 * kFrsWaves)
-frs_cell_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs, const float* __restrict__ queries,
-                int64_t m, const uint32_t* __restrict__ qord, const int32_t* __restrict__ seg_start,
-                const int64_t* __restrict__ nseg_ptr, float r, float inv, float thr, int n_batch,
-                const int64_t* __restrict__ qrs, const uint32_t* __restrict__ hts, int64_t* __restrict__ row_splits,
-                TIdx* __restrict__ out_idx, float* __restrict__ out_dist) {
-    __shared__ float4 win_all[kFrsWaves][WIN];
-    __shared__ uint32_t dir_all[kFrsWaves][4][32];  // bin, union offset, global start, count
-    const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    float4* win = win_all[wv];
-    uint32_t(*dir)[32] = dir_all[wv];
-    const int64_t nseg = *nseg_ptr;
-    const int64_t sg = static_cast<int64_t>(blockIdx.x) * kFrsWaves + wv;
-    if (sg >= nseg) return;
-    const int64_t qs = seg_start[sg];
-    const int64_t qe = sg + 1 < nseg ? seg_start[sg + 1] : m;
-    // ---- directory: bins of the 27 neighbour cells of the segment's cell
-    const int64_t q0 = qord[qs];
-    const int b0 = batch_of(q0, qrs, n_batch);
-    const uint32_t first = hts[b0], tsize = hts[b0 + 1] - first;
-    const int cx = static_cast<int>(floorf(queries[3 * q0] * inv));
-    const int cy = static_cast<int>(floorf(queries[3 * q0 + 1] * inv));
-    const int cz = static_cast<int>(floorf(queries[3 * q0 + 2] * inv));
-    uint32_t v = 0xffffffffu;
-    if (lane < 27) v = first + spatial_bin(cx + lane % 3 - 1, cy + (lane / 3) % 3 - 1, cz + lane / 9 - 1, tsize);
-    v = wave_sort_u32(v);
-    const uint32_t pv = __shfl_up(v, 1, 64);
-    if (lane > 0 && pv == v) v = 0xffffffffu;
-    v = wave_sort_u32(v);
-    const bool has = v != 0xffffffffu;
-    const int u = __popcll(__ballot(has));
-    const uint32_t gs = has ? cs[v] : 0u;
-    const uint32_t cnt_b = has ? cs[v + 1] - gs : 0u;
-    const uint32_t incl = wave_inclusive_scan(cnt_b);
-    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    if (lane < 32) {
-        dir[0][lane] = v;
-        dir[1][lane] = incl - cnt_b;
-        dir[2][lane] = gs;
-        dir[3][lane] = cnt_b;
-    }
-    wave_sync();
-    for (int64_t c0 = qs; c0 < qe; c0 += 64) {
-        const int64_t t = c0 + lane;
-        const bool valid = t < qe;
-        int64_t q = 0;
-        float qx = 0.f, qy = 0.f, qz = 0.f;
-        QueryBins bins;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) bins.b[i] = 0xffffffffu;
-        if (valid) {
-            q = qord[t];
-            qx = queries[3 * q];
-            qy = queries[3 * q + 1];
-            qz = queries[3 * q + 2];
-            bins = unique_query_bins(qx, qy, qz, r, inv, first, tsize);
-        }
-        // resolve each bin to its range in U (ascending walk of both lists)
-        uint32_t uo[9], uc[9];
-        bool missing = false;
-        int p = 0;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            uo[k] = 0;
-            uc[k] = 0;
-            if (bins.b[k] != 0xffffffffu) {
-                while (p < u && dir[0][p] < bins.b[k]) ++p;
-                if (p < u && dir[0][p] == bins.b[k]) {
-                    uo[k] = dir[1][p];
-                    uc[k] = dir[3][p];
-                } else {
-                    missing = true;
-                }
-            }
-        }
-        int64_t cnt = 0;
-        int64_t o = 0;
-        if constexpr (FILL) {
-            if (valid) o = row_splits[q];
-        }
-        if (__any(missing)) {
-            if (valid) frs_query_global<METRIC, IGNORE, FILL, TIdx>(pts, cs, bins, qx, qy, qz, thr, cnt, o, out_idx,
-                                                                   out_dist);
-        } else {
-            for (uint32_t w0 = 0; w0 < total; w0 += WIN) {
-                const uint32_t w1 = min(w0 + static_cast<uint32_t>(WIN), total);
-                wave_sync();  // previous window fully consumed
-                for (int i = 0; i < u; ++i) {
-                    const uint32_t doff = dir[1][i], dcnt = dir[3][i];
-                    const uint32_t a = max(doff, w0), e = min(doff + dcnt, w1);
-                    const uint32_t g = dir[2][i];
-                    for (uint32_t x = a + lane; x < e; x += 64) win[x - w0] = pts[g + (x - doff)];
-                }
-                wave_sync();
-                // each lane consumes its bins overlapping [w0, w1)
-                while (uc[0] != 0 || uo[0] != 0 || bins.b[0] != 0xffffffffu) {
-                    const uint32_t a = max(uo[0], w0), e = min(uo[0] + uc[0], w1);
-                    for (uint32_t x = a; x < e; ++x) {
-                        const float4 pp = win[x - w0];
-                        if (IGNORE && pp.x == qx && pp.y == qy && pp.z == qz) continue;
-                        const float d = dist_metric<METRIC>(pp.x, pp.y, pp.z, qx, qy, qz);
-                        if (d <= thr) {
-                            if constexpr (FILL) {
-                                out_idx[o] = static_cast<TIdx>(__float_as_uint(pp.w));
-                                if (out_dist) out_dist[o] = d;
-                                ++o;
-                            } else {
-                                ++cnt;
-                            }
-                        }
-                    }
-                    if (uo[0] + uc[0] > w1) break;  // bin continues in the next window
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        uo[k] = uo[k + 1];
-                        uc[k] = uc[k + 1];
-                        bins.b[k] = bins.b[k + 1];
-                    }
-                    uo[8] = 0;
-                    uc[8] = 0;
-                    bins.b[8] = 0xffffffffu;
-                }
-            }
-        }
-        if constexpr (!FILL) {
-            if (valid) row_splits[q + 1] = cnt;
-        }
-        wave_sync();
-    }
-}
-
-// Sort key of every query: (own bin, 13-bit hash of its cell, octant).  Equal
-// (bin, cell hash) = one cell segment; octant order inside a segment groups
-// lanes with identical bin lists (LDS broadcast reads).
-__global__ void query_order_keys_kernel(const float* __restrict__ queries, int64_t m, float inv, int n_batch,
-                                        const int64_t* __restrict__ qrs, const uint32_t* __restrict__ hts,
-                                        uint64_t* __restrict__ keys) {
-    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < m;
-         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int b = batch_of(i, qrs, n_batch);
-        const uint32_t first = hts[b], tsize = hts[b + 1] - first;
-        const float qx = queries[3 * i], qy = queries[3 * i + 1], qz = queries[3 * i + 2];
-        const int32_t cx = static_cast<int32_t>(floorf(qx * inv));
-        const int32_t cy = static_cast<int32_t>(floorf(qy * inv));
-        const int32_t cz = static_cast<int32_t>(floorf(qz * inv));
-        const uint32_t center = first + spatial_bin(cx, cy, cz, tsize);
-        uint32_t h = (static_cast<uint32_t>(cx) * 0x9E3779B1u) ^ (static_cast<uint32_t>(cy) * 0x85EBCA77u) ^
-                     (static_cast<uint32_t>(cz) * 0xC2B2AE3Du);
-        h = (h ^ (h >> 15)) * 0x2C1B3C6Du;
-        const float i2 = inv * 2.0f;
-        const uint32_t oct = (static_cast<uint32_t>(static_cast<int32_t>(floorf(qx * i2))) & 1u) |
-                             ((static_cast<uint32_t>(static_cast<int32_t>(floorf(qy * i2))) & 1u) << 1) |
-                             ((static_cast<uint32_t>(static_cast<int32_t>(floorf(qz * i2))) & 1u) << 2);
-        keys[i] = (static_cast<uint64_t>(center) << 16) | ((h >> 19) << 3) | oct;
-    }
-}
-
-__global__ void segment_heads_kernel(const uint64_t* __restrict__ sk, int64_t m, int64_t* __restrict__ head) {
-    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < m;
-         j += static_cast<int64_t>(gridDim.x) * blockDim.x)
-        head[j] = (j == 0 || (sk[j] >> 3) != (sk[j - 1] >> 3)) ? 1 : 0;
-}
-
-__global__ void segment_starts_kernel(const int64_t* __restrict__ head, const int64_t* __restrict__ incl, int64_t m,
-                                      int32_t* __restrict__ starts, int64_t* __restrict__ nseg) {
-    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < m;
-         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        if (head[j]) starts[incl[j] - 1] = static_cast<int32_t>(j);
-        if (j == m - 1) *nseg = incl[j];
-    }
-}
-
-constexpr int kFrsWin = 512;
-
-template <bool FILL, class TIdx>
-static void launch_frs(int metric, bool ignore, unsigned grid, hipStream_t st, const float4* pts, const uint32_t* cs,
-                       const float* queries, int64_t m, const uint32_t* qord, const int32_t* seg, const int64_t* nseg,
-                       float r, float inv, float thr, int nb, const int64_t* qrs, const uint32_t* hts, int64_t* rs,
-                       TIdx* idx, float* dist) {
-#define O3DML_FRS(M, I)                                                                                          \
-    frs_cell_kernel<kFrsWin, M, I, FILL, TIdx><<<grid, 64 * kFrsWaves, 0, st>>>(pts, cs, queries, m, qord, seg,     \
-                                                                                 nseg, r, inv, thr, nb, qrs, hts, rs, \
-                                                                                 idx, dist)
-    if (metric == kL2) {
-        if (ignore) O3DML_FRS(kL2, true); else O3DML_FRS(kL2, false);
-    } else if (metric == kL1) {
-        if (ignore) O3DML_FRS(kL1, true); else O3DML_FRS(kL1, false);
-    } else {
-        if (ignore) O3DML_FRS(kLinf, true); else O3DML_FRS(kLinf, false);
-    }
-#undef O3DML_FRS
-    O3DML_LAUNCH_CHECK();
-}
-
-// ===========================================================================
-// Path G (default): query groups over Open3D's own buckets.
-//
-// Two queries whose 9 visited buckets (own cell + the 8 corners q +- r) are
-// identical visit exactly the same points, in the same order.  A wave takes
-// 64 consecutive queries in bucket order (self search: Open3D's own
-// hash_table_index order), splits them into such groups (typically the
-// queries of one cell octant) and, per group:
-//   1. streams the group's buckets in ascending order — Open3D's visit order —
-//      with coalesced 16-B loads, keeping only points within the metric's
-//      distance of the group's bounding box (the box test uses the same fp32
-//      operations as the exact test on smaller operands, so it can never drop
-//      a neighbour), compacted IN ORDER into an LDS list;
-//   2. tests the list against the group's queries with S = 64 / G lanes per
-//      query (G = group size rounded up to a power of two): lane (g, s)
-//      tests entries s, s + S, ... of query g; a ballot + mbcnt gives every
-//      hit its rank, so rows are written directly in canonical order.
-// No sort, no temp rows, no visit-set check: the candidate list IS Open3D's
-// visit sequence.  Count pass = the same walk with counting only.
-// ===========================================================================
 #ifndef O3DML_DIAG
-#define O3DML_DIAG 0
-#endif
-#ifndef O3DML_GROUP_CAP
-#define O3DML_GROUP_CAP 256
+#define O3DML_DIAG 0  // 1: skip the candidate test loop (instruction-split diagnostics)
 #endif
 #ifndef O3DML_STREAM_U
 #define O3DML_STREAM_U 2
 #endif
-constexpr int kGroupCap = O3DML_GROUP_CAP;  // LDS candidate list per wave (float4)
-constexpr int kStreamU = O3DML_STREAM_U;    // 64-point loads in flight per lane while streaming buckets
+constexpr int kStreamU = O3DML_STREAM_U;  // 64-point loads in flight per lane while streaming buckets
+// LDS candidate list per wave (float4), incl. the padding of the last slice:
+// 4 KiB + 1 KiB of query slots keeps 32 waves per CU (LDS no tighter than the
+// 64-VGPR limit of 8 waves per SIMD)
+constexpr int kCandCap = 256;
 
 // Wave-wide float min / max: DPP within rows of 16 lanes, then the 4 row
 // results through v_readlane (uniform result, no LDS round trip).
@@ -758,70 +112,106 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
 }
 
+__device__ __forceinline__ uint32_t rdlane(int v, uint32_t lane) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(v, static_cast<int>(lane)));
+}
+
+// Lanes K..8 of the group's bucket table (see frs_group_kernel): flat start
+// and start - flat start of each deduplicated bucket, written with v_writelane.
+template <int K>
+__device__ __forceinline__ void bucket_table(const uint32_t* __restrict__ cs, const uint32_t* lb, int& vpre,
+                                             int& vdel, uint32_t& total) {
+    if constexpr (K < 9) {
+        const uint32_t s0 = cs[lb[K]];
+        const uint32_t len = (K == 0 || lb[K] != lb[K > 0 ? K - 1 : 0]) ? cs[lb[K] + 1] - s0 : 0u;
+        vpre = write_lane<K>(vpre, static_cast<int>(total));
+        vdel = write_lane<K>(vdel, static_cast<int>(s0 - total));
+        total += len;
+        bucket_table<K + 1>(cs, lb, vpre, vdel, total);
+    }
+}
+
 // MODE 0: every query of the (sorted) query array; its first kRowCap
 //         neighbours go to temp row qid, the full count to counts[qid]; ids of
 //         queries with more than kRowCap neighbours are listed in `over` for
-//         a MODE 1 re-run.
-// MODE 1: the queries of qpts[0 .. *m_dev) written straight into the final
-//         rows at rs[qid].
+//         a MODE 1 re-run.  qkeys >> bshift is the query's batch item.
+// MODE 1: the queries of qpts[0 .. *m_dev) (one per wave) written straight
+//         into the final rows at rs[qid].
+#ifndef O3DML_FRS_NUM_SGPR
+#define O3DML_FRS_NUM_SGPR 80  // <= 80 SGPRs keep 8 waves per SIMD (the 800-entry SGPR file)
+#endif
+#ifndef O3DML_FRS_WAVES
+#define O3DML_FRS_WAVES 0
+#endif
+#if O3DML_FRS_WAVES > 0
+#define O3DML_FRS_ATTR __attribute__((amdgpu_num_sgpr(O3DML_FRS_NUM_SGPR), amdgpu_waves_per_eu(O3DML_FRS_WAVES, 8)))
+#else
+#define O3DML_FRS_ATTR __attribute__((amdgpu_num_sgpr(O3DML_FRS_NUM_SGPR)))
+#endif
 template <int METRIC, bool IGNORE, bool DIST, int MODE, class TIdx>
-__global__ void __launch_bounds__(64)
-frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs, const float4* __restrict__ qpts,
-                 int64_t m_host, const int64_t* __restrict__ m_dev, float r, float inv, float thr, int nb,
-                 const int64_t* __restrict__ qrs, const uint32_t* __restrict__ hts, int64_t* __restrict__ counts,
-                 uint32_t* __restrict__ tidx, float* __restrict__ tdist, uint32_t* __restrict__ over,
-                 int64_t* __restrict__ n_over, const int64_t* __restrict__ rs, TIdx* __restrict__ out_idx,
-                 float* __restrict__ out_dist) {
-    __shared__ float4 cand[kGroupCap];
+__global__ void __launch_bounds__(64) O3DML_FRS_ATTR
+frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t* __restrict__ cs,
+                 const float4* __restrict__ qpts,
+                 const uint32_t* __restrict__ qkeys, int bshift, int64_t m_host, const int64_t* __restrict__ m_dev,
+                 float r, float inv, float thr, int nb, const int64_t* __restrict__ qrs,
+                 const uint32_t* __restrict__ hts, int64_t* __restrict__ counts, uint32_t* __restrict__ tidx,
+                 float* __restrict__ tdist, uint32_t* __restrict__ over, int64_t* __restrict__ n_over,
+                 const int64_t* __restrict__ rs, TIdx* __restrict__ out_idx, float* __restrict__ out_dist) {
+    __shared__ float4 cand[kCandCap];
     __shared__ float4 qsh[64];
-    __shared__ int64_t qrow[64];
+    __shared__ int64_t qrow[MODE == 0 ? 1 : 64];  // MODE 0: the row is the query id (qsh .w)
     const int lane = threadIdx.x;
+    const float inf = __builtin_huge_valf();
+    const float4 far = make_float4(inf, inf, inf, 0.f);  // never within any radius of a finite query
     const int64_t m = m_dev ? *m_dev : m_host;
-    // MODE 1 (few, long rows): one query per wave, so the re-runs proceed in parallel
-    const int64_t nchunks = MODE == 0 ? (m + 63) >> 6 : m;
-    // XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so block b
-    // takes chunk (b % 8) * per + b / 8 — every XCD sweeps one contiguous,
-    // spatially coherent range and its L2 keeps the shared buckets.
+    const int64_t nchunks = MODE == 0 ? (m + 63) >> 6 : m;  // MODE 1: one query per wave
+    // buffer resource over pts[0 .. n_pts] when its byte size fits the 32-bit range
+    const bool pts_rsrc_ok = n_pts < 0x0FFFFFFFu;
+    const __amdgpu_buffer_rsrc_t pts_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float4*>(pts), static_cast<short>(0), static_cast<int>((n_pts + 1u) * 16u), kBufferFlags);
+    // XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so with a grid
+    // of exactly 8 * per blocks, block b takes chunk (b % 8) * per + b / 8 —
+    // every XCD sweeps one contiguous, spatially coherent range and its L2
+    // keeps the shared buckets.  Otherwise plain grid stride.
     const int64_t per = (nchunks + 7) >> 3;
-    const bool xcd_map = gridDim.x >= 8 * per;  // host launches 8 * per blocks when it can
+    const bool xcd_map = static_cast<int64_t>(gridDim.x) == 8 * per;
     int64_t chunk = xcd_map ? static_cast<int64_t>(blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
     for (; chunk < nchunks; chunk = xcd_map ? nchunks : chunk + gridDim.x) {
         const int64_t t = MODE == 0 ? (chunk << 6) + lane : chunk;
         const bool valid = t < m && (MODE == 0 || lane == 0);
-        float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 q4 = far;
         QueryBins qb;
 #pragma unroll
         for (int k = 0; k < 9; ++k) qb.b[k] = 0xffffffffu;
-        int64_t row = 0;
+        int64_t row = 0;  // MODE 1: the query's final row start
         if (valid) {
             q4 = qpts[t];
             const uint32_t qid = __float_as_uint(q4.w);
-            const int b = batch_of(qid, qrs, nb);
+            const int b = qkeys ? (bshift >= 32 ? 0 : static_cast<int>(qkeys[t] >> bshift)) : batch_of(qid, qrs, nb);
             const uint32_t first = hts[b], tsize = hts[b + 1] - first;
             qb = query_bins(q4.x, q4.y, q4.z, r, inv, first, tsize);
-            row = MODE == 0 ? static_cast<int64_t>(qid) : rs[qid];
+            if constexpr (MODE == 1) row = rs[qid];
         }
-        uint64_t todo = __ballot(valid);
+        uint64_t todo = __builtin_amdgcn_ballot_w64(valid);
         while (todo) {
             const int leader = __builtin_ctzll(todo);
             uint32_t lb[9];
             bool same = valid;
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
-                lb[k] = __builtin_amdgcn_readlane(qb.b[k], leader);
+                lb[k] = rdlane(static_cast<int>(qb.b[k]), leader);
                 same = same && qb.b[k] == lb[k];
             }
-            const uint64_t gm = __ballot(same);
+            const uint64_t gm = __builtin_amdgcn_ballot_w64(same);
             todo &= ~gm;
             const int ng = __popcll(gm);
             __syncthreads();  // previous group done with qsh / cand
             if (same) {
                 const uint32_t slot = mbcnt64(gm);
                 qsh[slot] = q4;
-                qrow[slot] = row;
+                if constexpr (MODE == 1) qrow[slot] = row;
             }
             // group bounding box
-            const float inf = __builtin_huge_valf();
             const float lx = wave_min_f(same ? q4.x : inf), ly = wave_min_f(same ? q4.y : inf),
                         lz = wave_min_f(same ? q4.z : inf);
             const float hx = wave_max_f(same ? q4.x : -inf), hy = wave_max_f(same ? q4.y : -inf),
@@ -831,96 +221,128 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
             const int ls = 6 - lg;                                                         // log2 S
             const int S = 1 << ls;
             const int g = lane >> ls, sl = lane & (S - 1);
-            const bool active = g < ng;
             __syncthreads();
-            float4 mq = make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 mq = far;  // lanes past the group test the far point: never a hit
             int64_t mrow = 0;
-            if (active) {
+            if (g < ng) {
                 mq = qsh[g];
-                mrow = qrow[g];
+                mrow = MODE == 0 ? static_cast<int64_t>(__float_as_uint(mq.w)) : qrow[g];
             }
-            int cnt = 0;  // neighbours of query g so far (uniform over its S lanes)
-            int nc = 0;
-            uint32_t* const trow = MODE == 0 ? tidx + mrow * kRowCap : nullptr;
-            float* const tdrow = (MODE == 0 && DIST) ? tdist + mrow * kRowCap : nullptr;
+            uint32_t cnt = 0;  // neighbours of query g so far (uniform over its S lanes)
             const uint64_t gmask = ls == 6 ? ~0ull : (((1ull << S) - 1ull) << (g << ls));
             const uint32_t gm_lo = static_cast<uint32_t>(gmask), gm_hi = static_cast<uint32_t>(gmask >> 32);
-            // stream the group's buckets (ascending, deduplicated): Open3D's visit order
-            uint32_t pre[10];
-            int32_t delta[9];  // bucket start - flat offset
-            pre[0] = 0;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                const uint32_t s0 = cs[lb[k]];
-                const uint32_t len = (k == 0 || lb[k] != lb[k - 1]) ? cs[lb[k] + 1] - s0 : 0u;
-                delta[k] = static_cast<int32_t>(s0 - pre[k]);
-                pre[k + 1] = pre[k] + len;
-            }
-            const uint32_t total = pre[9];
-            uint32_t f0 = 0;
-            while (true) {
-                // 1. fill the LDS list: rounds of kStreamU x 64 loads, all in flight
-                while (f0 < total && nc + 64 * kStreamU <= kGroupCap) {
-                    float4 c[kStreamU];
-#pragma unroll
-                    for (int u = 0; u < kStreamU; ++u) {
-                        const uint32_t f = f0 + u * 64 + lane;
-                        int32_t dl = delta[0];
-#pragma unroll
-                        for (int k = 1; k < 9; ++k) dl = f >= pre[k] ? delta[k] : dl;
-                        c[u] = pts[f < total ? static_cast<uint32_t>(static_cast<int32_t>(f) + dl) : 0u];
+            // Bucket table of the group, one bucket per lane: lane k < 9 holds
+            // the flat start pre[k] of bucket k in the concatenated stream and
+            // delta[k] = its start in pts - pre[k]; lane 9 holds the stream
+            // length, lanes > 9 hold UINT_MAX.  Looked up with v_readlane by
+            // the uniform stream cursor.
+            int vpre = -1, vdel = 0;
+            uint32_t total = 0;
+            bucket_table<0>(cs, lb, vpre, vdel, total);
+            vpre = write_lane<9>(vpre, static_cast<int>(total));
+            // stop filling while the next round (and the test padding) might not fit
+            const int fill_lim = kCandCap - 64 * kStreamU - (S - 1);
+            // stream cursor: source index of this lane's point in the round of
+            // 64 starting at flat position fb (rounds are requested in order;
+            // lanes past the stream read the far sentinel pts[n_pts])
+            uint32_t kcur = 0;
+            auto round_src = [&](uint32_t fb) -> uint32_t {
+                uint32_t p1 = rdlane(vpre, kcur + 1);
+                while (p1 <= fb) p1 = rdlane(vpre, ++kcur + 1);  // kcur: bucket holding fb
+                const uint32_t f = fb + lane;
+                uint32_t dl = rdlane(vdel, kcur);
+                const uint32_t d1 = rdlane(vdel, kcur + 1);
+                dl = f >= p1 ? d1 : dl;  // no lane matches when p1 lies past the round
+                if (p1 < fb + 64) {      // p1 inside the round: later boundaries may be too (rare)
+                    for (uint32_t kk = kcur + 2;; ++kk) {
+                        const uint32_t pk = rdlane(vpre, kk);
+                        if (pk >= fb + 64) break;
+                        const uint32_t dk = rdlane(vdel, kk);
+                        dl = f >= pk ? dk : dl;
                     }
+                }
+                return f < total ? f + dl : n_pts;
+            };
+            // all addresses of a step first, then all its loads (in flight together)
+            auto load_step = [&](uint32_t fb, float4* c) {
+                uint32_t src[kStreamU];
+#pragma unroll
+                for (int u = 0; u < kStreamU; ++u) src[u] = round_src(fb + u * 64);
+                if (pts_rsrc_ok) {  // 16-B buffer loads: 32-bit offsets, never split by the compiler
+#pragma unroll
+                    for (int u = 0; u < kStreamU; ++u)
+                        c[u] = __builtin_bit_cast(float4,
+                                                  __builtin_amdgcn_raw_buffer_load_b128(pts_rsrc, src[u] * 16u, 0, 0));
+                } else {
+#pragma unroll
+                    for (int u = 0; u < kStreamU; ++u) c[u] = pts[src[u]];
+                }
+            };
+            uint32_t f0 = 0;
+            int nc = 0;
+            while (true) {
+                // 1. fill the LDS list: steps of kStreamU x 64 loads, all in flight
+                //    (a software-pipelined variant that issued the next step before
+                //    filtering this one measured 8 % slower: more VGPRs, fewer waves)
+                while (f0 < total && nc <= fill_lim) {
+                    float4 c[kStreamU];
+                    load_step(f0, c);
 #pragma unroll
                     for (int u = 0; u < kStreamU; ++u) {
-                        const bool keep = f0 + u * 64 + lane < total &&
-                                          box_dist<METRIC>(c[u], lx, ly, lz, hx, hy, hz) <= thr;
-                        const uint64_t km = __ballot(keep);
+                        const bool keep = box_dist<METRIC>(c[u], lx, ly, lz, hx, hy, hz) <= thr;
+                        const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
                         if (keep) cand[nc + mbcnt64(km)] = c[u];
                         nc += __popcll(km);
                     }
                     f0 += 64 * kStreamU;
                 }
-                // 2. test the list against the group's queries, in order; hits are
-                //    ranked by ballot so every row is written in canonical order
+                // 2. pad to whole S-entry slices with the far point, then test the
+                //    list against the group's queries, in order (4 slices per
+                //    step, then single slices); hits are ranked by ballot so every
+                //    row is written in canonical order
+                const int ncp = (nc + S - 1) & ~(S - 1);
+                if (nc + lane < ncp) cand[nc + lane] = far;
                 __syncthreads();
 #if O3DML_DIAG != 1
-                for (int e0 = 0; e0 < nc; e0 += 4 * S) {
+                auto test = [&](const float4& p) {
+                    const float d = dist_metric<METRIC>(p.x, p.y, p.z, mq.x, mq.y, mq.z);
+                    const bool hit = d <= thr && !(IGNORE && p.x == mq.x && p.y == mq.y && p.z == mq.z);
+                    const uint64_t bal = __builtin_amdgcn_ballot_w64(hit);
+                    const uint32_t mlo = static_cast<uint32_t>(bal) & gm_lo;
+                    const uint32_t mhi = static_cast<uint32_t>(bal >> 32) & gm_hi;
+                    if (hit) {
+                        const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+                        if constexpr (MODE == 0) {
+                            // rows longer than kRowCap are re-run (MODE 1), so their
+                            // temp row may take anything in its last slot
+                            const uint32_t ps = min(pos, static_cast<uint32_t>(kRowCap - 1));
+                            tidx[mrow * kRowCap + ps] = __float_as_uint(p.w);
+                            if constexpr (DIST) tdist[mrow * kRowCap + ps] = d;
+                        } else {
+                            out_idx[mrow + pos] = static_cast<TIdx>(__float_as_uint(p.w));
+                            if constexpr (DIST) out_dist[mrow + pos] = d;
+                        }
+                    }
+                    cnt += __popc(mlo) + __popc(mhi);
+                };
+                int e0 = 0;
+                for (; e0 + 4 * S <= ncp; e0 += 4 * S) {
                     float4 p[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) p[u] = cand[(e0 + u * S + sl) & (kGroupCap - 1)];
+                    for (int u = 0; u < 4; ++u) p[u] = cand[e0 + u * S + sl];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const float d = dist_metric<METRIC>(p[u].x, p[u].y, p[u].z, mq.x, mq.y, mq.z);
-                        const bool hit = active && e0 + u * S + sl < nc && d <= thr &&
-                                         !(IGNORE && p[u].x == mq.x && p[u].y == mq.y && p[u].z == mq.z);
-                        const uint64_t bal = __ballot(hit);
-                        const uint32_t mlo = static_cast<uint32_t>(bal) & gm_lo;
-                        const uint32_t mhi = static_cast<uint32_t>(bal >> 32) & gm_hi;
-                        if (hit) {
-                            const int pos = cnt + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
-                                                      mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u)));
-                            if constexpr (MODE == 0) {
-                                if (pos < kRowCap) {
-                                    trow[pos] = __float_as_uint(p[u].w);
-                                    if constexpr (DIST) tdrow[pos] = d;
-                                }
-                            } else {
-                                out_idx[mrow + pos] = static_cast<TIdx>(__float_as_uint(p[u].w));
-                                if constexpr (DIST) out_dist[mrow + pos] = d;
-                            }
-                        }
-                        cnt += __popc(mlo) + __popc(mhi);
-                    }
+                    for (int u = 0; u < 4; ++u) test(p[u]);
                 }
+                for (; e0 < ncp; e0 += S) test(cand[e0 + sl]);
 #endif
                 __syncthreads();
                 nc = 0;
                 if (f0 >= total) break;
             }
             if constexpr (MODE == 0) {
-                if (active && sl == 0) {
+                if (g < ng && sl == 0) {
                     counts[__float_as_uint(mq.w)] = cnt;
-                    if (cnt > kRowCap)
+                    if (cnt > static_cast<uint32_t>(kRowCap))
                         over[atomicAdd(reinterpret_cast<unsigned long long*>(n_over), 1ull)] =
                                 static_cast<uint32_t>(mrow);
                 }
@@ -929,12 +351,12 @@ frs_group_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ cs
     }
 }
 
-// Final rows from the temp rows of path G (already in canonical order, temp
-// row = query id, so both sides stream in order).  A wave owns 64
-// consecutive rows; lanes = entries of one row, 8 rows in flight: one
-// coalesced 4-B-per-lane load of the row's live entries (lanes past the count
-// read a zero word, so no load sits under a branch) and one coalesced store.
-// Rows longer than kRowCap are written by the MODE 1 re-run.
+// Final rows from the temp rows (already in canonical order, temp row = query
+// id, so both sides stream in order).  A wave owns 64 consecutive rows;
+// lanes = entries of one row, 8 rows in flight: one coalesced 4-B-per-lane
+// load of the row's live entries (lanes past the count read a zero word, so
+// no load sits under a branch) and one coalesced store.  Rows longer than
+// kRowCap are written by the MODE 1 re-run.
 __device__ uint32_t g_frs_zero[4];
 
 template <bool DIST, class TIdx>
@@ -992,19 +414,12 @@ __global__ void gather_over_kernel(const float* __restrict__ queries, const uint
     }
 }
 
-__global__ void set_scalars_kernel(int64_t* s, int64_t a, int64_t b, int64_t c, int64_t d) {
-    s[0] = a;
-    s[1] = b;
-    s[2] = c;
-    s[3] = d;
-}
-
-// Query order for path G: (batch, Morton code of the query's r-cell) — the
-// lowest Morton level is the octant of the Open3D 2r-cell, so queries with
-// identical visit lists (one group) are adjacent, and consecutive chunks are
-// spatial neighbours that share buckets in L2.  Cell coordinates wrap modulo
-// 2^bits (locality only; any order is correct — grouping inside the kernel
-// compares the full bucket lists).
+// Query order: (batch, Morton code of the query's r-cell) — the lowest Morton
+// level is the octant of the Open3D 2r-cell, so queries with identical visit
+// lists (one group) are adjacent, and consecutive chunks are spatial
+// neighbours that share buckets in L2.  Cell coordinates wrap modulo
+// 2^cell_bits (locality only; any order is correct — grouping inside the
+// kernel compares the full bucket lists).
 __device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 10 bits -> every third bit
     v &= 0x3ffu;
     v = (v | (v << 16)) & 0x030000FFu;
@@ -1014,29 +429,21 @@ __device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 10 bits -> every t
     return v;
 }
 
-__global__ void group_query_keys_kernel(const float* __restrict__ queries, int64_t m, float inv2, int n_batch,
-                                        const int64_t* __restrict__ qrs, int cell_bits, uint32_t* __restrict__ keys) {
+__global__ void __launch_bounds__(256) group_query_keys_kernel(const float* __restrict__ queries, int64_t m,
+                                                               float inv2, int n_batch,
+                                                               const int64_t* __restrict__ qrs, int cell_bits,
+                                                               uint32_t* __restrict__ keys) {
+    __shared__ int64_t s_rs[kLdsSplits];
+    const int64_t* rsp = stage_splits(s_rs, qrs, n_batch);
     const uint32_t mask = (1u << cell_bits) - 1u;
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < m;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int b = batch_of(i, qrs, n_batch);
+        const int b = batch_of(i, rsp, n_batch);
         const uint32_t cx = static_cast<uint32_t>(static_cast<int32_t>(floorf(queries[3 * i] * inv2))) & mask;
         const uint32_t cy = static_cast<uint32_t>(static_cast<int32_t>(floorf(queries[3 * i + 1] * inv2))) & mask;
         const uint32_t cz = static_cast<uint32_t>(static_cast<int32_t>(floorf(queries[3 * i + 2] * inv2))) & mask;
         const uint32_t mort = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
         keys[i] = (static_cast<uint32_t>(b) << (3 * cell_bits)) | mort;
-    }
-}
-
-// Queries not identical to the points: key = bucket of the query's own cell.
-__global__ void query_bin_keys_kernel(const float* __restrict__ queries, int64_t m, float inv, int n_batch,
-                                      const int64_t* __restrict__ qrs, const uint32_t* __restrict__ hts,
-                                      uint32_t* __restrict__ keys) {
-    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < m;
-         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int b = batch_of(i, qrs, n_batch);
-        const uint32_t first = hts[b], tsize = hts[b + 1] - first;
-        keys[i] = first + point_bin(queries[3 * i], queries[3 * i + 1], queries[3 * i + 2], inv, tsize);
     }
 }
 
@@ -1047,12 +454,14 @@ static unsigned group_grid(int64_t m, int queries_per_wave = 64) {
 
 template <int MODE, class TIdx>
 static void launch_group(int metric, bool ignore, bool with_dist, hipStream_t st, unsigned grid, const float4* pts,
-                         const uint32_t* cs, const float4* qpts, int64_t m, const int64_t* m_dev, float r, float inv,
-                         float thr, int nb, const int64_t* qrs, const uint32_t* hts, int64_t* counts, uint32_t* tidx,
-                         float* tdist, uint32_t* over, int64_t* n_over, const int64_t* rs, TIdx* idx, float* dist) {
-#define O3DML_GRP(M, I, D)                                                                                      \
-    frs_group_kernel<M, I, D, MODE, TIdx><<<grid, 64, 0, st>>>(pts, cs, qpts, m, m_dev, r, inv, thr, nb, qrs, hts, \
-                                                                counts, tidx, tdist, over, n_over, rs, idx, dist)
+                         uint32_t n_pts, const uint32_t* cs, const float4* qpts, const uint32_t* qkeys, int bshift, int64_t m,
+                         const int64_t* m_dev, float r, float inv, float thr, int nb, const int64_t* qrs,
+                         const uint32_t* hts, int64_t* counts, uint32_t* tidx, float* tdist, uint32_t* over,
+                         int64_t* n_over, const int64_t* rs, TIdx* idx, float* dist) {
+#define O3DML_GRP(M, I, D)                                                                                    \
+    frs_group_kernel<M, I, D, MODE, TIdx><<<grid, 64, 0, st>>>(pts, n_pts, cs, qpts, qkeys, bshift, m, m_dev, r, inv, \
+                                                                thr, nb, qrs, hts, counts, tidx, tdist, over,   \
+                                                                n_over, rs, idx, dist)
 #define O3DML_GRP_D(M, I)              \
     do {                               \
         if (with_dist)                 \
@@ -1072,144 +481,40 @@ static void launch_group(int metric, bool ignore, bool with_dist, hipStream_t st
     O3DML_LAUNCH_CHECK();
 }
 
-static bool frs_legacy() {
-    const char* e = std::getenv("O3DML_FRS_PATH");
-    return e && e[0] == 'l';  // "legacy": fine r-cell grid + row sort (comparison only)
-}
-
-// Search plan kept in the workspace between _count and _fill.
+// Workspace kept between _count and _fill (same layout in both entries).
 struct FrsPlan {
-    float4* pts;
-    float4* qpts;
-    float4* pts_over;
-    uint64_t* keys;
-    uint64_t* skeys;
-    uint32_t* qord;
-    int64_t* head;
-    int64_t* incl;
-    int32_t* seg;
-    int64_t* nseg;
+    int64_t* scalars;  // [0] overflow count
+    float4* pts;       // [N + 1] points in Open3D bucket order + a far sentinel
+    float4* qpts;      // [M] queries in (batch, Morton) order
+    float4* pts_over;  // [M] overflow queries
+    uint32_t* keys;    // [M]
+    uint32_t* skeys;   // [M]
+    uint32_t* qorder;  // [M]
+    int64_t* counts;   // [M]
+    uint32_t* over;    // [M]
+    uint32_t* tidx;    // [M * kRowCap]
+    float* tdist;      // [M * kRowCap] (with distances)
 };
 
-static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m) {
+static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m, bool dist) {
     FrsPlan p;
-    p.pts = ws.take<float4>(n);
+    p.scalars = ws.take<int64_t>(4);
+    p.pts = ws.take<float4>(n + 1);  // + far sentinel
     p.qpts = ws.take<float4>(m);
     p.pts_over = ws.take<float4>(m);
-    p.keys = ws.take<uint64_t>(m);
-    p.skeys = ws.take<uint64_t>(m);
-    p.qord = ws.take<uint32_t>(m);
-    p.head = ws.take<int64_t>(m);
-    p.incl = ws.take<int64_t>(m);
-    p.seg = ws.take<int32_t>(m);
-    p.nseg = ws.take<int64_t>(2);
+    p.keys = ws.take<uint32_t>(m);
+    p.skeys = ws.take<uint32_t>(m);
+    p.qorder = ws.take<uint32_t>(m);
+    p.counts = ws.take<int64_t>(m);
+    p.over = ws.take<uint32_t>(m);
+    p.tidx = ws.take<uint32_t>(m * kRowCap);
+    p.tdist = dist ? ws.take<float>(m * kRowCap) : nullptr;
     return p;
 }
 
 static size_t plan_bytes(int64_t n, int64_t m) {
-    return ws_bytes<float4>(n) + 2 * ws_bytes<float4>(m) + 2 * ws_bytes<uint64_t>(m) + ws_bytes<uint32_t>(m) + 2 * ws_bytes<int64_t>(m) +
-           ws_bytes<int32_t>(m) + ws_bytes<int64_t>(2);
-}
-
-static unsigned frs_grid(int64_t nseg) {
-    const int64_t g = ceil_div(nseg, kFrsWaves);
-    return static_cast<unsigned>(g < 1 ? 1 : g);
-}
-
-
-
-// ---------------------------------------------------------------------------
-// search plan kept in the workspace between _count and _fill
-// ---------------------------------------------------------------------------
-struct FinePlan {
-    int64_t* scalars;   // [0] path (0 fine, 1 segments), [1] range flag, [2] n_over
-    uint32_t* foff;     // [B+1] per-batch fine table offsets (device)
-    uint32_t* o3dpos;   // [N]
-    uint32_t* keys;     // [max(N,M)]
-    uint32_t* skeys;    // [max(N,M)]
-    uint32_t* order;    // [N] point ids in fine order
-    uint32_t* qorder;   // [M]
-    uint32_t* fs;       // [F+1]
-    float4* rec;        // [N]
-    uint2* rid;         // [N] (o3d position, id)
-    int64_t* counts;    // [M]
-    uint32_t* over;     // [M]
-    uint32_t* tpos;     // [M * kRowCap]
-    uint32_t* tid;      // [M * kRowCap]
-    float* tdist;       // [M * kRowCap]
-    DenseBatch* dg;     // [B]
-    float* bbox;        // [B*6]
-};
-
-static int64_t fine_table_cap(int64_t n, int64_t nb) { return 4 * n + 64 * (nb + 1); }
-
-static FinePlan take_fine(Workspace& ws, int64_t n, int64_t m, int64_t nb) {
-    FinePlan p;
-    const int64_t nm = std::max(n, m);
-    p.scalars = ws.take<int64_t>(8);
-    p.foff = ws.take<uint32_t>(nb + 1);
-    p.o3dpos = ws.take<uint32_t>(n);
-    p.keys = ws.take<uint32_t>(nm);
-    p.skeys = ws.take<uint32_t>(nm);
-    p.order = ws.take<uint32_t>(n);
-    p.qorder = ws.take<uint32_t>(m);
-    p.fs = ws.take<uint32_t>(fine_table_cap(n, nb) + 1);
-    p.rec = ws.take<float4>(n);
-    p.rid = ws.take<uint2>(n);
-    p.counts = ws.take<int64_t>(m);
-    p.over = ws.take<uint32_t>(m);
-    p.tpos = ws.take<uint32_t>(m * kRowCap);
-    p.tid = ws.take<uint32_t>(m * kRowCap);
-    p.tdist = ws.take<float>(m * kRowCap);
-    p.dg = ws.take<DenseBatch>(nb);
-    p.bbox = ws.take<float>(6 * nb);
-    return p;
-}
-
-static size_t fine_bytes(int64_t n, int64_t m, int64_t nb) {
-    const int64_t nm = std::max(n, m);
-    return ws_bytes<int64_t>(8) + ws_bytes<uint32_t>(nb + 1) + ws_bytes<uint32_t>(n) + 2 * ws_bytes<uint32_t>(nm) +
-           ws_bytes<uint32_t>(n) + ws_bytes<uint32_t>(m) + ws_bytes<uint32_t>(fine_table_cap(n, nb) + 1) +
-           ws_bytes<float4>(n) + ws_bytes<uint2>(n) + ws_bytes<int64_t>(m) + ws_bytes<uint32_t>(m) +
-           2 * ws_bytes<uint32_t>(m * kRowCap) + ws_bytes<float>(m * kRowCap) + ws_bytes<DenseBatch>(nb) +
-           ws_bytes<float>(6 * nb);
-}
-
-template <int MODE, class TIdx>
-static void launch_fine(bool dense, int metric, bool ignore, bool with_dist, unsigned g, hipStream_t st,
-                        const FinePlan& p,
-                        const float* queries, int64_t m, double inv_h, double rmargin, float r, float inv, float thr,
-                        int nb, const int64_t* qrs, const uint32_t* hts, const int64_t* rs, TIdx* idx, float* dist) {
-#define O3DML_FINE2(DN, M, I, D)                                                                             \
-    frs_fine_search<DN, M, I, D, MODE, TIdx><<<g, 256, 0, st>>>(p.rec, p.rid, p.fs, p.foff, p.dg, queries, m,   \
-                                                                 p.qorder, p.scalars + 2, inv_h, rmargin, r, inv, \
-                                                                 thr, nb, qrs, hts, p.counts, p.tpos, p.tid,      \
-                                                                 p.tdist, p.over, p.scalars + 2, rs, idx, dist)
-#define O3DML_FINE(M, I, D)           \
-    do {                              \
-        if (dense)                    \
-            O3DML_FINE2(true, M, I, D); \
-        else                          \
-            O3DML_FINE2(false, M, I, D); \
-    } while (0)
-#define O3DML_FINE_D(M, I) \
-    do {                   \
-        if (with_dist)     \
-            O3DML_FINE(M, I, true); \
-        else               \
-            O3DML_FINE(M, I, false); \
-    } while (0)
-    if (metric == kL2) {
-        if (ignore) O3DML_FINE_D(kL2, true); else O3DML_FINE_D(kL2, false);
-    } else if (metric == kL1) {
-        if (ignore) O3DML_FINE_D(kL1, true); else O3DML_FINE_D(kL1, false);
-    } else {
-        if (ignore) O3DML_FINE_D(kLinf, true); else O3DML_FINE_D(kLinf, false);
-    }
-#undef O3DML_FINE_D
-#undef O3DML_FINE
-#undef O3DML_FINE2
-    O3DML_LAUNCH_CHECK();
+    return ws_bytes<int64_t>(4) + ws_bytes<float4>(n + 1) + 2 * ws_bytes<float4>(m) + 3 * ws_bytes<uint32_t>(m) +
+           ws_bytes<int64_t>(m) + ws_bytes<uint32_t>(m) + 2 * ws_bytes<uint32_t>(m * kRowCap);
 }
 
 }  // namespace o3dml
@@ -1217,11 +522,9 @@ static void launch_fine(bool dense, int metric, bool ignore, bool with_dist, uns
 using namespace o3dml;
 
 O3DML_API size_t o3dml_fixed_radius_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t n_batch) {
-    const int64_t nm = std::max(n_points, n_queries);
-    return fine_bytes(n_points, n_queries, n_batch) + plan_bytes(n_points, n_queries) +
-           std::max(prim::scan_workspace_bytes(nm),
-                    std::max(prim::radix_sort_workspace_bytes<uint64_t>(n_queries),
-                             prim::radix_sort_workspace_bytes<uint32_t>(nm)));
+    (void)n_batch;
+    return plan_bytes(n_points, n_queries) +
+           std::max(prim::scan_workspace_bytes(n_queries), prim::radix_sort_workspace_bytes<uint32_t>(n_queries));
 }
 
 O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_points, const float* queries,
@@ -1234,187 +537,53 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
                                               int64_t* neighbors_row_splits, void* workspace,
                                               size_t workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
+    (void)points_row_splits;
+    (void)points_row_splits_host;
+    (void)self_search;
     O3DML_REQUIRE(metric >= 0 && metric <= 2, "metric must be L1(0), L2(1) or Linf(2)");
     O3DML_REQUIRE(radius > 0.f, "radius must be > 0");
     O3DML_REQUIRE(n_queries < (int64_t(1) << 31) && n_points < (int64_t(1) << 31), "too many points");
+    O3DML_REQUIRE(n_batch >= 1, "need at least one batch item");
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
-    FinePlan fp = take_fine(ws, n_points, n_queries, n_batch);
-    FrsPlan pl = take_plan(ws, n_points, n_queries);
-    O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
-    O3DML_CHECK_HIP(hipMemsetAsync(fp.scalars, 0, sizeof(int64_t) * 8, st));
-    if (n_queries == 0) return 0;
+    FrsPlan pl = take_plan(ws, n_points, n_queries, with_distances != 0);
+    O3DML_CHECK_HIP(hipMemsetAsync(pl.scalars, 0, sizeof(int64_t) * 4, st));
+    if (n_queries == 0) {
+        O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
+        return 0;
+    }
     if (n_points == 0) {
         O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t) * (n_queries + 1), st));
         return 0;
     }
+    O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
     const float thr = metric == kL2 ? radius * radius : radius;
     const float inv = 1.0f / (2.0f * radius);
-    if (!frs_legacy()) {
-        // ---- path G: query groups over Open3D's buckets (no host sync)
-        set_scalars_kernel<<<1, 1, 0, st>>>(fp.scalars, 3, 0, 0, 0);
-        O3DML_LAUNCH_CHECK();
-        gather_sorted_points_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points,
-                                                                               pl.pts);
-        O3DML_LAUNCH_CHECK();
-        const int batch_bits = prim::bits_needed(static_cast<uint64_t>(n_batch - 1));
-        // <= 24 key bits = 3 radix passes; Morton coordinates wrap modulo 2^cell_bits
-        // (locality only, grouping compares the full bucket lists)
-        const int cell_bits = std::max(1, std::min(8, (24 - batch_bits) / 3));
-        group_query_keys_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(
-                queries, n_queries, 2.0f * inv, (int)n_batch, queries_row_splits, cell_bits, fp.keys);
-        O3DML_LAUNCH_CHECK();
-        {
-            Workspace sws = ws;
-            prim::radix_sort_pairs<uint32_t>(fp.keys, nullptr, fp.skeys, fp.qorder, n_queries,
-                                             batch_bits + 3 * cell_bits, sws, st);
-        }
-        gather_sorted_points_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(queries, fp.qorder, n_queries,
-                                                                                pl.qpts);
-        O3DML_LAUNCH_CHECK();
-        const float4* qp = pl.qpts;
-        {
-            TimedRegion tr("frs_group_search", st);
-            launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0, st,
-                                     group_grid(n_queries), pl.pts,
-                                     hash_table_cell_splits, qp, n_queries, nullptr, radius, inv, thr, (int)n_batch,
-                                     queries_row_splits, hash_table_splits, fp.counts, fp.tpos, fp.tdist, fp.over,
-                                     fp.scalars + 2, nullptr, nullptr, nullptr);
-        }
-        Workspace sws = ws;
-        prim::scan<int64_t, int64_t>(fp.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
-        return 0;
-    }
-    // ---- plan: bounding boxes -> dense grid / hashed fine grid / segments
-    launch_bbox(points, points_row_splits, static_cast<int>(n_batch), fp.bbox, st);
+    gather_sorted_points_kernel<<<xcd_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points, pl.pts, 1);
     O3DML_LAUNCH_CHECK();
-    std::vector<float> bb(6 * n_batch);
-    O3DML_CHECK_HIP(hipMemcpyAsync(bb.data(), fp.bbox, sizeof(float) * 6 * n_batch, hipMemcpyDeviceToHost, st));
-    O3DML_CHECK_HIP(hipStreamSynchronize(st));
-    const double inv_h = 1.0 / static_cast<double>(radius);
-    const double rmargin = static_cast<double>(radius) * (1.0 + 1e-6);
-    std::vector<DenseBatch> dg(n_batch);
-    int64_t dense_cells = 0;
-    double max_abs = 0.0;
-    for (int64_t b = 0; b < n_batch; ++b) {
-        DenseBatch& d = dg[b];
-        const bool empty = points_row_splits_host[b + 1] == points_row_splits_host[b];
-        double o[3], dims[3];
-        for (int a = 0; a < 3; ++a) {
-            const double lo = empty ? 0.0 : bb[6 * b + a], hi = empty ? 0.0 : bb[6 * b + 3 + a];
-            o[a] = lo;
-            dims[a] = std::floor((hi - lo) * inv_h) + 1.0;
-            max_abs = std::max(max_abs, std::max(std::fabs(lo), std::fabs(hi)));
-        }
-        d.ox = o[0];
-        d.oy = o[1];
-        d.oz = o[2];
-        const double cells = dims[0] * dims[1] * dims[2];
-        d.dx = static_cast<int32_t>(std::min(dims[0], 2e9));
-        d.dy = static_cast<int32_t>(std::min(dims[1], 2e9));
-        d.dz = static_cast<int32_t>(std::min(dims[2], 2e9));
-        d.offset = static_cast<uint32_t>(std::min<double>(static_cast<double>(dense_cells), 4e9));
-        dense_cells += static_cast<int64_t>(std::min(cells, 9e15));
-    }
-    const bool dense = std::isfinite(max_abs) && dense_cells <= fine_table_cap(n_points, n_batch);
-    const bool hashed = !dense && std::isfinite(max_abs) && max_abs * inv_h < 1e9;
-    if (dense || hashed) {
-        const int64_t path = dense ? 0 : 2;
-        O3DML_CHECK_HIP(hipMemcpyAsync(fp.scalars, &path, sizeof(int64_t), hipMemcpyHostToDevice, st));
-        const unsigned gn = stream_grid(n_points, 256);
-        uint32_t total_cells;
-        std::vector<uint32_t> foff(n_batch + 1, 0);
-        if (dense) {
-            O3DML_CHECK_HIP(hipMemcpyAsync(fp.dg, dg.data(), sizeof(DenseBatch) * n_batch, hipMemcpyHostToDevice, st));
-            total_cells = static_cast<uint32_t>(dense_cells);
-            dense_keys_kernel<<<gn, 256, 0, st>>>(points, n_points, points_row_splits, (int)n_batch, fp.dg, inv_h,
-                                                  fp.keys);
-        } else {
-            for (int64_t b = 0; b < n_batch; ++b) {
-                const int64_t nbp = points_row_splits_host[b + 1] - points_row_splits_host[b];
-                uint32_t f = 64;
-                while (f < 2 * nbp) f <<= 1;
-                foff[b + 1] = foff[b] + f;
-            }
-            O3DML_CHECK_HIP(hipMemcpyAsync(fp.foff, foff.data(), sizeof(uint32_t) * (n_batch + 1),
-                                           hipMemcpyHostToDevice, st));
-            total_cells = foff[n_batch];
-            fine_keys_kernel<<<gn, 256, 0, st>>>(points, n_points, points_row_splits, (int)n_batch, fp.foff, inv_h,
-                                                 fp.keys, fp.scalars + 1);
-        }
-        O3DML_LAUNCH_CHECK();
-        O3DML_CHECK_HIP(hipStreamSynchronize(st));  // retires the pageable plan copies
-        {
-            Workspace sws = ws;
-            prim::radix_sort_pairs<uint32_t>(fp.keys, nullptr, fp.skeys, fp.order, n_points,
-                                             prim::bits_needed(total_cells - 1), sws, st);
-        }
-        bin_bounds_kernel<<<gn, 256, 0, st>>>(fp.skeys, n_points, total_cells, fp.fs);
-        O3DML_LAUNCH_CHECK();
-        inverse_perm_kernel<<<gn, 256, 0, st>>>(hash_table_index, n_points, fp.o3dpos);
-        O3DML_LAUNCH_CHECK();
-        fine_records_kernel<<<gn, 256, 0, st>>>(points, fp.order, n_points, fp.o3dpos, inv_h, fp.rec, fp.rid);
-        O3DML_LAUNCH_CHECK();
-        if (self_search) {
-            O3DML_CHECK_HIP(hipMemcpyAsync(fp.qorder, fp.order, sizeof(uint32_t) * n_queries,
-                                           hipMemcpyDeviceToDevice, st));
-        } else {
-            if (dense)
-                dense_keys_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(
-                        queries, n_queries, queries_row_splits, (int)n_batch, fp.dg, inv_h, fp.keys);
-            else
-                fine_query_keys_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(
-                        queries, n_queries, queries_row_splits, (int)n_batch, fp.foff, inv_h, fp.keys);
-            O3DML_LAUNCH_CHECK();
-            Workspace sws = ws;
-            prim::radix_sort_pairs<uint32_t>(fp.keys, nullptr, fp.skeys, fp.qorder, n_queries,
-                                             prim::bits_needed(total_cells - 1), sws, st);
-        }
-        {
-            TimedRegion tr("frs_fine_search", st);
-            launch_fine<0, int32_t>(dense, metric, ignore_query_point != 0, with_distances != 0,
-                                    stream_grid(n_queries, 256, 1 << 20), st, fp, queries, n_queries, inv_h, rmargin,
-                                    radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits, nullptr,
-                                    nullptr, nullptr);
-        }
-        Workspace sws = ws;
-        prim::scan<int64_t, int64_t>(fp.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
-        return 0;
-    }
-    // ---- path B: Open3D-cell segments through LDS windows
-    const int64_t one = 1;
-    O3DML_CHECK_HIP(hipMemcpyAsync(fp.scalars, &one, sizeof(int64_t), hipMemcpyHostToDevice, st));
-    gather_sorted_points_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points,
-                                                                           pl.pts);
-    O3DML_LAUNCH_CHECK();
-    const unsigned g = stream_grid(n_queries, 256);
-    query_order_keys_kernel<<<g, 256, 0, st>>>(queries, n_queries, inv, (int)n_batch, queries_row_splits,
-                                              hash_table_splits, pl.keys);
-    O3DML_LAUNCH_CHECK();
-    uint32_t tb = 0;
-    O3DML_CHECK_HIP(hipMemcpyAsync(&tb, hash_table_splits + n_batch, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    O3DML_CHECK_HIP(hipStreamSynchronize(st));
-    {
-        Workspace sws = ws;
-        prim::radix_sort_pairs<uint64_t>(pl.keys, nullptr, pl.skeys, pl.qord, n_queries,
-                                         16 + prim::bits_needed(tb > 0 ? tb - 1 : 0), sws, st);
-    }
-    segment_heads_kernel<<<g, 256, 0, st>>>(pl.skeys, n_queries, pl.head);
+    const int batch_bits = prim::bits_needed(static_cast<uint64_t>(n_batch - 1));
+    // <= 24 key bits = 3 radix passes; Morton coordinates wrap modulo 2^cell_bits
+    const int cell_bits = std::max(1, std::min(8, (24 - batch_bits) / 3));
+    group_query_keys_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(
+            queries, n_queries, 2.0f * inv, (int)n_batch, queries_row_splits, cell_bits, pl.keys);
     O3DML_LAUNCH_CHECK();
     {
         Workspace sws = ws;
-        prim::scan<int64_t, int64_t>(pl.head, pl.incl, n_queries, true, sws, st);
+        prim::radix_sort_pairs<uint32_t>(pl.keys, nullptr, pl.skeys, pl.qorder, n_queries,
+                                         batch_bits + 3 * cell_bits, sws, st);
     }
-    segment_starts_kernel<<<g, 256, 0, st>>>(pl.head, pl.incl, n_queries, pl.seg, pl.nseg);
+    gather_sorted_points_kernel<<<xcd_grid(n_queries, 256), 256, 0, st>>>(queries, pl.qorder, n_queries, pl.qpts, 0);
     O3DML_LAUNCH_CHECK();
-    int64_t nseg = 0;
-    O3DML_CHECK_HIP(hipMemcpyAsync(&nseg, pl.nseg, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    O3DML_CHECK_HIP(hipStreamSynchronize(st));
-    launch_frs<false, int32_t>(metric, ignore_query_point != 0, frs_grid(nseg), st, pl.pts, hash_table_cell_splits,
-                               queries, n_queries, pl.qord, pl.seg, pl.nseg, radius, inv, thr, (int)n_batch,
-                               queries_row_splits, hash_table_splits, neighbors_row_splits, nullptr, nullptr);
+    {
+        TimedRegion tr("frs_group_search", st);
+        launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0, st, group_grid(n_queries),
+                                 pl.pts, static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts, pl.skeys,
+                                 batch_bits == 0 ? 32 : 3 * cell_bits, n_queries, nullptr, radius, inv, thr,
+                                 (int)n_batch, queries_row_splits, hash_table_splits, pl.counts, pl.tidx, pl.tdist,
+                                 pl.over, pl.scalars, nullptr, nullptr, nullptr);
+    }
     Workspace sws = ws;
-    prim::scan<int64_t, int64_t>(neighbors_row_splits + 1, neighbors_row_splits + 1, n_queries, true, sws, st);
+    prim::scan<int64_t, int64_t>(pl.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
     O3DML_GUARD_END
 }
 
@@ -1432,112 +601,50 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
     (void)points;
     (void)points_row_splits;
     (void)points_row_splits_host;
+    (void)hash_table_index;
     (void)self_search;
     O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
     O3DML_REQUIRE(!with_distances || neighbors_distance, "with_distances needs a distance buffer");
     if (n_queries == 0 || n_points == 0) return 0;
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
-    FinePlan fp = take_fine(ws, n_points, n_queries, n_batch);  // built by _count (same workspace)
-    FrsPlan pl = take_plan(ws, n_points, n_queries);
-    int64_t sc[4];
-    O3DML_CHECK_HIP(hipMemcpyAsync(sc, fp.scalars, sizeof(sc), hipMemcpyDeviceToHost, st));
-    O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    FrsPlan pl = take_plan(ws, n_points, n_queries, with_distances != 0);  // built by _count (same workspace)
     const float thr = metric == kL2 ? radius * radius : radius;
     const float inv = 1.0f / (2.0f * radius);
     int64_t* rs = const_cast<int64_t*>(neighbors_row_splits);
     float* dist = with_distances ? neighbors_distance : nullptr;
-    if (sc[0] == 3) {
-        {
-            TimedRegion tr("frs_group_rows", st);
-            const unsigned gc = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_queries, 256), 1 << 16)));
-#define O3DML_GCOPY(T)                                                                                            \
-    do {                                                                                                          \
-        if (dist)                                                                                                 \
-            group_rows_copy_kernel<true, T><<<gc, 256, 0, st>>>(n_queries, fp.counts, rs, fp.tpos,      \
-                                                                fp.tdist, static_cast<T*>(neighbors_index), dist); \
-        else                                                                                                      \
-            group_rows_copy_kernel<false, T><<<gc, 256, 0, st>>>(n_queries, fp.counts, rs, fp.tpos,     \
-                                                                 nullptr, static_cast<T*>(neighbors_index), nullptr); \
+    {
+        TimedRegion tr("frs_group_rows", st);
+        const unsigned gc = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_queries, 256), 1 << 16)));
+#define O3DML_GCOPY(T)                                                                                        \
+    do {                                                                                                      \
+        if (dist)                                                                                             \
+            group_rows_copy_kernel<true, T><<<gc, 256, 0, st>>>(n_queries, pl.counts, rs, pl.tidx, pl.tdist,  \
+                                                                static_cast<T*>(neighbors_index), dist);      \
+        else                                                                                                  \
+            group_rows_copy_kernel<false, T><<<gc, 256, 0, st>>>(n_queries, pl.counts, rs, pl.tidx, nullptr,  \
+                                                                 static_cast<T*>(neighbors_index), nullptr);  \
     } while (0)
-            if (index_bits == 32) O3DML_GCOPY(int32_t); else O3DML_GCOPY(int64_t);
+        if (index_bits == 32) O3DML_GCOPY(int32_t); else O3DML_GCOPY(int64_t);
 #undef O3DML_GCOPY
-            O3DML_LAUNCH_CHECK();
-        }
-        if (sc[2] > 0) {  // rows longer than kRowCap: re-run those queries into the final rows
-            const int64_t n_over = sc[2];
-            gather_over_kernel<<<stream_grid(n_over, 256), 256, 0, st>>>(queries, fp.over, fp.scalars + 2, pl.pts_over);
-            O3DML_LAUNCH_CHECK();
-            const unsigned go = group_grid(n_over, 1);
-            if (index_bits == 32)
-                launch_group<1, int32_t>(metric, ignore_query_point != 0, dist != nullptr, st, go, pl.pts,
-                                         hash_table_cell_splits, pl.pts_over, n_over, nullptr, radius, inv, thr,
-                                         (int)n_batch, queries_row_splits, hash_table_splits, nullptr, nullptr,
-                                         nullptr, nullptr, nullptr, rs, static_cast<int32_t*>(neighbors_index), dist);
-            else
-                launch_group<1, int64_t>(metric, ignore_query_point != 0, dist != nullptr, st, go, pl.pts,
-                                         hash_table_cell_splits, pl.pts_over, n_over, nullptr, radius, inv, thr,
-                                         (int)n_batch, queries_row_splits, hash_table_splits, nullptr, nullptr,
-                                         nullptr, nullptr, nullptr, rs, static_cast<int64_t*>(neighbors_index), dist);
-        }
-        return 0;
+        O3DML_LAUNCH_CHECK();
     }
-    if (sc[0] == 0 || sc[0] == 2) {
-        const bool dense = sc[0] == 0;
-        const double inv_h = 1.0 / static_cast<double>(radius);
-        const double rmargin = static_cast<double>(radius) * (1.0 + 1e-6);
-        const unsigned gs = stream_grid(ceil_div(n_queries, 4), 256, 1 << 20);
-        {
-            TimedRegion tr("frs_row_sort", st);
-#define O3DML_RSC(T)                                                                                              \
-    do {                                                                                                          \
-        if (dist)                                                                                                 \
-            row_sort_compact_kernel<true, T><<<gs, 256, 0, st>>>(rs, n_queries, fp.tpos, fp.tid, fp.tdist,        \
-                                                                 static_cast<T*>(neighbors_index), dist);         \
-        else                                                                                                      \
-            row_sort_compact_kernel<false, T><<<gs, 256, 0, st>>>(rs, n_queries, fp.tpos, fp.tid, fp.tdist,       \
-                                                                  static_cast<T*>(neighbors_index), nullptr);     \
-    } while (0)
-            if (index_bits == 32) O3DML_RSC(int32_t); else O3DML_RSC(int64_t);
-#undef O3DML_RSC
-            O3DML_LAUNCH_CHECK();
-        }
-        const int64_t n_over = sc[2];
-        if (n_over > 0) {
-            const unsigned go = stream_grid(n_over, 256);
-            if (index_bits == 32)
-                launch_fine<1, int32_t>(dense, metric, ignore_query_point != 0, dist != nullptr, go, st, fp, queries,
-                                        n_queries, inv_h, rmargin, radius, inv, thr, (int)n_batch, queries_row_splits,
-                                        hash_table_splits, rs, static_cast<int32_t*>(neighbors_index), dist);
-            else
-                launch_fine<1, int64_t>(dense, metric, ignore_query_point != 0, dist != nullptr, go, st, fp, queries,
-                                        n_queries, inv_h, rmargin, radius, inv, thr, (int)n_batch, queries_row_splits,
-                                        hash_table_splits, rs, static_cast<int64_t*>(neighbors_index), dist);
-            const unsigned gl = static_cast<unsigned>(std::min<int64_t>(n_over, 4096));
-            if (index_bits == 32)
-                row_sort_long_kernel<int32_t><<<gl, 1024, 0, st>>>(rs, fp.over, fp.scalars + 2,
-                                                                   static_cast<int32_t*>(neighbors_index), dist,
-                                                                   hash_table_index);
-            else
-                row_sort_long_kernel<int64_t><<<gl, 1024, 0, st>>>(rs, fp.over, fp.scalars + 2,
-                                                                   static_cast<int64_t*>(neighbors_index), dist,
-                                                                   hash_table_index);
-            O3DML_LAUNCH_CHECK();
-        }
-        return 0;
-    }
-    int64_t nseg = 0;
-    O3DML_CHECK_HIP(hipMemcpyAsync(&nseg, pl.nseg, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    // rows longer than kRowCap: re-run those queries straight into the final
+    // rows; the overflow count stays on the device (no host round trip), so a
+    // fixed grid strides over however many there are (usually none)
+    const unsigned go = static_cast<unsigned>(std::min<int64_t>(n_queries, 1024));
+    gather_over_kernel<<<stream_grid(std::min<int64_t>(n_queries, 1 << 16), 256), 256, 0, st>>>(
+            queries, pl.over, pl.scalars, pl.pts_over);
+    O3DML_LAUNCH_CHECK();
     if (index_bits == 32)
-        launch_frs<true, int32_t>(metric, ignore_query_point != 0, frs_grid(nseg), st, pl.pts, hash_table_cell_splits,
-                                  queries, n_queries, pl.qord, pl.seg, pl.nseg, radius, inv, thr, (int)n_batch,
-                                  queries_row_splits, hash_table_splits, rs, static_cast<int32_t*>(neighbors_index),
-                                  dist);
+        launch_group<1, int32_t>(metric, ignore_query_point != 0, dist != nullptr, st, go, pl.pts,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.pts_over, nullptr, 32, 0, pl.scalars, radius, inv, thr,
+                                 (int)n_batch, queries_row_splits, hash_table_splits, nullptr, nullptr, nullptr,
+                                 nullptr, nullptr, rs, static_cast<int32_t*>(neighbors_index), dist);
     else
-        launch_frs<true, int64_t>(metric, ignore_query_point != 0, frs_grid(nseg), st, pl.pts, hash_table_cell_splits,
-                                  queries, n_queries, pl.qord, pl.seg, pl.nseg, radius, inv, thr, (int)n_batch,
-                                  queries_row_splits, hash_table_splits, rs, static_cast<int64_t*>(neighbors_index),
-                                  dist);
+        launch_group<1, int64_t>(metric, ignore_query_point != 0, dist != nullptr, st, go, pl.pts,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.pts_over, nullptr, 32, 0, pl.scalars, radius, inv, thr,
+                                 (int)n_batch, queries_row_splits, hash_table_splits, nullptr, nullptr, nullptr,
+                                 nullptr, nullptr, rs, static_cast<int64_t*>(neighbors_index), dist);
     O3DML_GUARD_END
 }

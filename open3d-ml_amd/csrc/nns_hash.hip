@@ -19,15 +19,33 @@
 
 namespace o3dml {
 
-__global__ void hash_points_kernel(const float* __restrict__ points, int64_t n, float inv, int n_batch,
-                                   const int64_t* __restrict__ prs, const uint32_t* __restrict__ hts,
-                                   uint32_t* __restrict__ bins) {
+// Bucket of every point.  The row splits and, per batch item, the table
+// offset / size / 2^64 mod size are staged in LDS, so a point costs one LDS
+// binary search and a 32-bit modulo (no 64-bit division, no global search).
+__global__ void __launch_bounds__(256) hash_points_kernel(const float* __restrict__ points, int64_t n, float inv,
+                                                          int n_batch, const int64_t* __restrict__ prs,
+                                                          const uint32_t* __restrict__ hts,
+                                                          uint32_t* __restrict__ bins) {
+    __shared__ int64_t s_rs[kLdsSplits];
+    __shared__ uint32_t s_tab[kLdsSplits][3];  // first, size, 2^64 mod size
+    const int64_t* rsp = stage_splits(s_rs, prs, n_batch);
+    const bool tab = n_batch <= kLdsSplits;
+    if (tab) {
+        for (int b = threadIdx.x; b < n_batch; b += blockDim.x) {
+            const uint32_t first = hts[b], tsize = hts[b + 1] - first;
+            s_tab[b][0] = first;
+            s_tab[b][1] = tsize;
+            s_tab[b][2] = pow64_mod(tsize);
+        }
+        __syncthreads();
+    }
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int b = batch_of(i, prs, n_batch);
-        const uint32_t first = hts[b];
-        const uint32_t tsize = hts[b + 1] - first;
-        bins[i] = first + point_bin(points[3 * i], points[3 * i + 1], points[3 * i + 2], inv, tsize);
+        const int b = batch_of(i, rsp, n_batch);
+        const uint32_t first = tab ? s_tab[b][0] : hts[b];
+        const uint32_t tsize = tab ? s_tab[b][1] : hts[b + 1] - first;
+        const uint32_t k64 = tab ? s_tab[b][2] : pow64_mod(tsize);
+        bins[i] = first + point_bin_k(points[3 * i], points[3 * i + 1], points[3 * i + 2], inv, tsize, k64);
     }
 }
 
