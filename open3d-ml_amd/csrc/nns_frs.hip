@@ -447,6 +447,117 @@ __global__ void __launch_bounds__(256) group_query_keys_kernel(const float* __re
     }
 }
 
+// Self search (queries = points): the queries in Open3D's bucket order (the
+// gathered pts array) with each bucket's entries reordered by (cell, octant),
+// so the queries of one group — same cell, same octant, hence the same 9
+// visited buckets — are adjacent and 64 consecutive queries form few groups,
+// like the Morton order of the general path but with no sort of the queries.
+// One wave per bucket, 128 entries at a time (longer buckets are ordered
+// chunk by chunk: any order is correct, grouping compares the full bucket
+// lists).  qbatch[t] = batch item of query t.
+constexpr int kSelfChunk = 256;  // bucket entries ordered at once (longer buckets: chunk by chunk)
+
+// The chunk's entries get a 5-bit class: the octant (3 bits) and which of the
+// bucket's cells holds the point (first cell seen, second cell seen, any
+// other: 2 bits); a stable counting sort by class (ballot ranking, per-class
+// counts in LDS) makes every (cell, octant) group contiguous.
+__global__ void __launch_bounds__(256) self_query_order_kernel(const float4* __restrict__ pts,
+                                                               const uint32_t* __restrict__ cs,
+                                                               const uint32_t* __restrict__ hts, int nb, float inv2,
+                                                               float4* __restrict__ qpts,
+                                                               uint32_t* __restrict__ qbatch) {
+    constexpr int E = kSelfChunk / 64;
+    __shared__ uint32_t s_hts[kLdsSplits];
+    __shared__ uint32_t wcnt[4][32];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const bool lds_hts = nb + 1 <= kLdsSplits;
+    if (lds_hts)
+        for (int i = threadIdx.x; i <= nb; i += blockDim.x) s_hts[i] = hts[i];
+    __syncthreads();
+    const uint32_t* H = lds_hts ? s_hts : hts;
+    const int64_t nbins = H[nb];
+    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+    const uint64_t lt = lanemask_lt();
+    int64_t bin = static_cast<int64_t>(blockIdx.x) * 4 + wv;
+    uint32_t s = bin < nbins ? cs[bin] : 0u, e = bin < nbins ? cs[bin + 1] : 0u;
+    for (; bin < nbins; bin += nwaves) {
+        // next bucket's bounds in flight while this one is ordered
+        const int64_t nbin = bin + nwaves;
+        const uint32_t ns = nbin < nbins ? cs[nbin] : 0u, ne = nbin < nbins ? cs[nbin + 1] : 0u;
+        int lo = 0, hi = nb - 1;  // batch item of the bucket (uniform)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (H[mid] <= bin) lo = mid; else hi = mid - 1;
+        }
+        for (uint32_t c0 = s; c0 < e; c0 += kSelfChunk) {
+            const uint32_t len = min(e - c0, static_cast<uint32_t>(kSelfChunk));
+            float4 p[E];
+            uint32_t hc[E], oct[E];
+#pragma unroll
+            for (int h = 0; h < E; ++h) {
+                const uint32_t i = lane + 64 * h;
+                p[h] = i < len ? pts[c0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                const int32_t x = static_cast<int32_t>(floorf(p[h].x * inv2)),
+                              y = static_cast<int32_t>(floorf(p[h].y * inv2)),
+                              z = static_cast<int32_t>(floorf(p[h].z * inv2));
+                // 2r-cell = half-cell >> 1, octant = the half-cell parities
+                hc[h] = (static_cast<uint32_t>(x >> 1) * 0x9E3779B1u) ^ (static_cast<uint32_t>(y >> 1) * 0x85EBCA77u) ^
+                        (static_cast<uint32_t>(z >> 1) * 0xC2B2AE3Du);
+                oct[h] = (x & 1) | ((y & 1) << 1) | ((z & 1) << 2);
+            }
+            const uint32_t c1 = rdlane(static_cast<int>(hc[0]), 0);
+            uint32_t c2 = c1;
+#pragma unroll
+            for (int h = E - 1; h >= 0; --h) {  // first entry in another cell (lowest row wins)
+                const uint64_t other = __builtin_amdgcn_ballot_w64(lane + 64 * h < len && hc[h] != c1);
+                if (other) c2 = rdlane(static_cast<int>(hc[h]), __builtin_ctzll(other));
+            }
+            if (lane < 32) wcnt[wv][lane] = 0;
+            __builtin_amdgcn_wave_barrier();
+            uint32_t dig[E], loff[E];
+#pragma unroll
+            for (int h = 0; h < E; ++h) {  // rows in order: stable within a class
+                const bool valid = lane + 64 * h < len;
+                const uint32_t cls = hc[h] == c1 ? 0u : (hc[h] == c2 ? 1u : 2u);
+                const uint32_t d = (cls << 3) | oct[h];
+                dig[h] = d;
+                uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
+#pragma unroll
+                for (int b = 0; b < 5; ++b) {
+                    const bool bit = (d >> b) & 1u;
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(bit);
+                    peers &= bit ? m : ~m;
+                }
+                const uint32_t rank = __popcll(peers & lt);
+                const uint32_t before = valid ? wcnt[wv][d] : 0u;
+                loff[h] = before + rank;
+                if (valid && rank == 0) wcnt[wv][d] = before + static_cast<uint32_t>(__popcll(peers));
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t cnt = lane < 32 ? wcnt[wv][lane] : 0u;
+            const uint32_t base = wave_inclusive_scan(cnt) - cnt;  // class bases
+#pragma unroll
+            for (int h = 0; h < E; ++h) {
+                const uint32_t i = lane + 64 * h;
+                const uint32_t pos =
+                        static_cast<uint32_t>(__shfl(static_cast<int>(base), static_cast<int>(dig[h]), 64)) + loff[h];
+                if (i < len) {
+                    qpts[c0 + pos] = p[h];
+                    qbatch[c0 + pos] = static_cast<uint32_t>(lo);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        s = ns;
+        e = ne;
+    }
+}
+
+static bool frs_self_order() {
+    const char* e = std::getenv("O3DML_FRS_SELF_ORDER");  // "0": Morton-sort the queries of a self search too (A/B)
+    return !(e && e[0] == '0');
+}
+
 static unsigned group_grid(int64_t m, int queries_per_wave = 64) {
     const int64_t per = ((m + queries_per_wave - 1) / queries_per_wave + 7) / 8;
     return static_cast<unsigned>(std::max<int64_t>(8, std::min<int64_t>(8 * per, 1 << 20)));
@@ -559,26 +670,43 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
     const float thr = metric == kL2 ? radius * radius : radius;
     const float inv = 1.0f / (2.0f * radius);
+    const int batch_bits = prim::bits_needed(static_cast<uint64_t>(n_batch - 1));
+    const uint32_t* qkeys;
+    int bshift;
     gather_sorted_points_kernel<<<xcd_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points, pl.pts, 1);
     O3DML_LAUNCH_CHECK();
-    const int batch_bits = prim::bits_needed(static_cast<uint64_t>(n_batch - 1));
-    // <= 24 key bits = 3 radix passes; Morton coordinates wrap modulo 2^cell_bits
-    const int cell_bits = std::max(1, std::min(8, (24 - batch_bits) / 3));
-    group_query_keys_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(
-            queries, n_queries, 2.0f * inv, (int)n_batch, queries_row_splits, cell_bits, pl.keys);
-    O3DML_LAUNCH_CHECK();
-    {
-        Workspace sws = ws;
-        prim::radix_sort_pairs<uint32_t>(pl.keys, nullptr, pl.skeys, pl.qorder, n_queries,
-                                         batch_bits + 3 * cell_bits, sws, st);
+    if (self_search && frs_self_order()) {
+        // queries = points: Open3D's bucket order, octant groups made adjacent
+        // inside each bucket — no sort of the queries at all
+        self_query_order_kernel<<<static_cast<unsigned>(std::min<int64_t>(ceil_div(n_points, 64 * 4), 1 << 16)), 256,
+                                  0, st>>>(pl.pts, hash_table_cell_splits, hash_table_splits, (int)n_batch,
+                                           2.0f * inv, pl.qpts, pl.keys);
+        O3DML_LAUNCH_CHECK();
+        qkeys = pl.keys;
+        bshift = 0;
+    } else {
+        // (batch, Morton r-cell) order: <= 24 key bits = 3 radix passes;
+        // Morton coordinates wrap modulo 2^cell_bits
+        const int cell_bits = std::max(1, std::min(8, (24 - batch_bits) / 3));
+        group_query_keys_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(
+                queries, n_queries, 2.0f * inv, (int)n_batch, queries_row_splits, cell_bits, pl.keys);
+        O3DML_LAUNCH_CHECK();
+        {
+            Workspace sws = ws;
+            prim::radix_sort_pairs<uint32_t>(pl.keys, nullptr, pl.skeys, pl.qorder, n_queries,
+                                             batch_bits + 3 * cell_bits, sws, st);
+        }
+        gather_sorted_points_kernel<<<xcd_grid(n_queries, 256), 256, 0, st>>>(queries, pl.qorder, n_queries,
+                                                                             pl.qpts, 0);
+        O3DML_LAUNCH_CHECK();
+        qkeys = pl.skeys;
+        bshift = batch_bits == 0 ? 32 : 3 * cell_bits;
     }
-    gather_sorted_points_kernel<<<xcd_grid(n_queries, 256), 256, 0, st>>>(queries, pl.qorder, n_queries, pl.qpts, 0);
-    O3DML_LAUNCH_CHECK();
     {
         TimedRegion tr("frs_group_search", st);
         launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0, st, group_grid(n_queries),
-                                 pl.pts, static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts, pl.skeys,
-                                 batch_bits == 0 ? 32 : 3 * cell_bits, n_queries, nullptr, radius, inv, thr,
+                                 pl.pts, static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts, qkeys,
+                                 bshift, n_queries, nullptr, radius, inv, thr,
                                  (int)n_batch, queries_row_splits, hash_table_splits, pl.counts, pl.tidx, pl.tdist,
                                  pl.over, pl.scalars, nullptr, nullptr, nullptr);
     }

@@ -126,6 +126,45 @@ constexpr int kRsItems = O3DML_RS_ITEMS;
 constexpr int kRsTile = kRsBlock * kRsItems;
 constexpr int kRsWaves = kRsBlock / 64;
 
+// offs[d * tiles + j] = number of digit-d keys in tiles < j, dtot[d] = all
+// digit-d keys: one block per digit scans its row of the tile histogram (the
+// digits' global bases are a 256-entry scan the scatter kernel does itself).
+static __global__ void __launch_bounds__(kRsBlock) radix_digit_scan(const uint32_t* __restrict__ hist, int64_t tiles,
+                                                             uint32_t* __restrict__ offs,
+                                                             uint32_t* __restrict__ dtot) {
+    __shared__ uint32_t wsum[kRsWaves];
+    const int64_t row = static_cast<int64_t>(blockIdx.x) * tiles;
+    uint32_t carry = 0;
+    for (int64_t c0 = 0; c0 < tiles; c0 += kRsBlock * 8) {
+        uint32_t v[8];
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {  // blocked: thread t owns entries t*8 .. t*8+7 of the chunk
+            const int64_t j = c0 + threadIdx.x * 8 + k;
+            v[k] = j < tiles ? hist[row + j] : 0u;
+            acc += v[k];
+        }
+        const uint32_t inc = wave_inclusive_scan(acc);
+        if (lane_id() == 63) wsum[wave_id()] = inc;
+        __syncthreads();
+        uint32_t run = carry + inc - acc, tot = 0;
+#pragma unroll
+        for (int w = 0; w < kRsWaves; ++w) {
+            run += w < wave_id() ? wsum[w] : 0u;
+            tot += wsum[w];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int64_t j = c0 + threadIdx.x * 8 + k;
+            if (j < tiles) offs[row + j] = run;
+            run += v[k];
+        }
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) dtot[blockIdx.x] = carry;
+}
+
 template <class K>
 __global__ void __launch_bounds__(kRsBlock) radix_hist(const K* __restrict__ keys, int64_t n, int shift,
                                                        uint32_t* __restrict__ hist, int64_t tiles) {
@@ -155,11 +194,12 @@ template <class K>
 __global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                           K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                           int64_t n, int shift,
-                                                          const int64_t* __restrict__ offsets,
+                                                          const uint32_t* __restrict__ offsets,
+                                                          const uint32_t* __restrict__ dtot,
                                                           const uint32_t* __restrict__ hist, int64_t tiles) {
     constexpr int kRowsPerWave = kRsItems * kRsBlock / 64 / kRsWaves;  // = kRsItems
     __shared__ uint32_t wcnt[kRsWaves][256];
-    __shared__ uint32_t wsum[kRsWaves];
+    __shared__ uint32_t wsum[kRsWaves], dsum[kRsWaves];
     __shared__ uint32_t toff[256];
     __shared__ int64_t goff[256];
     __shared__ K lkey[kRsTile];
@@ -173,14 +213,22 @@ __global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* __restrict__ 
         // tile digit offsets: exclusive scan of this tile's histogram
         const uint32_t c = hist[static_cast<int64_t>(t) * tiles + blockIdx.x];
         const uint32_t inc = wave_inclusive_scan(c);
-        if (lane == 63) wsum[w] = inc;
+        const uint32_t dt = dtot[t];
+        const uint32_t dinc = wave_inclusive_scan(dt);  // digit bases: scan of the digit totals
+        if (lane == 63) {
+            wsum[w] = inc;
+            dsum[w] = dinc;
+        }
 #pragma unroll
         for (int ww = 0; ww < kRsWaves; ++ww) wcnt[ww][t] = 0;
-        goff[t] = offsets[static_cast<int64_t>(t) * tiles + blockIdx.x];
         __syncthreads();
-        uint32_t before = 0;
-        for (int ww = 0; ww < w; ++ww) before += wsum[ww];
+        uint32_t before = 0, dbefore = 0;
+        for (int ww = 0; ww < w; ++ww) {
+            before += wsum[ww];
+            dbefore += dsum[ww];
+        }
         toff[t] = before + inc - c;
+        goff[t] = static_cast<int64_t>(dbefore + dinc - dt) + offsets[static_cast<int64_t>(t) * tiles + blockIdx.x];
     }
     // phase 1: each wave ranks its rows in order, counts per digit in LDS
     const uint64_t lt = lanemask_lt();
@@ -311,8 +359,7 @@ inline int bits_needed(uint64_t max_key) {
 template <class K>
 size_t radix_sort_workspace_bytes(int64_t n) {
     const int64_t tiles = ceil_div(n > 0 ? n : 1, kRsTile);
-    return ws_bytes<K>(n) + ws_bytes<uint32_t>(n) + ws_bytes<uint32_t>(256 * tiles) +
-           ws_bytes<int64_t>(256 * tiles) + scan_workspace_bytes(256 * tiles);
+    return ws_bytes<K>(n) + ws_bytes<uint32_t>(n) + 2 * ws_bytes<uint32_t>(256 * tiles) + ws_bytes<uint32_t>(256);
 }
 
 // Sorts (keys_in, vals_in) by key bits [0, end_bit) into (keys_out, vals_out).
@@ -339,7 +386,8 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
     K* ktmp = ws.take<K>(n);
     uint32_t* vtmp = ws.take<uint32_t>(n);
     uint32_t* hist = ws.take<uint32_t>(256 * tiles);
-    int64_t* offs = ws.take<int64_t>(256 * tiles);
+    uint32_t* offs = ws.take<uint32_t>(256 * tiles);
+    uint32_t* dtot = ws.take<uint32_t>(256);
     const K* ksrc = keys_in;
     const uint32_t* vsrc = vals_in;
     for (int p = 0; p < passes; ++p) {
@@ -349,10 +397,10 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
         const int shift = 8 * p;
         radix_hist<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(ksrc, n, shift, hist, tiles);
         O3DML_LAUNCH_CHECK();
-        Workspace sws = ws;  // scan scratch is transient per pass
-        scan<uint32_t, int64_t>(hist, offs, 256 * tiles, false, sws, st);
+        radix_digit_scan<<<256, kRsBlock, 0, st>>>(hist, tiles, offs, dtot);
+        O3DML_LAUNCH_CHECK();
         radix_scatter<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift,
-                                                                          offs, hist, tiles);
+                                                                          offs, dtot, hist, tiles);
         O3DML_LAUNCH_CHECK();
         ksrc = kdst;
         vsrc = vdst;
