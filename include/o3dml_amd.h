@@ -48,13 +48,15 @@ int64_t o3dml_hash_table_splits(int64_t n_batch, const int64_t* points_row_split
                                 uint32_t* hash_table_splits_host);
 size_t o3dml_build_spatial_hash_table_workspace_size(int64_t n_points, int64_t total_bins);
 /* points f32[N,3]; hash_table_splits u32[B+1] (device copy of the host
- * helper's output) -> hash_table_index u32[N] (point ids by bin, ascending id
+ * helper's output; hash_table_splits_host: the host copy, nullable — with it,
+ * tables of <= 4096 bins per batch item take a chunked counting sort instead
+ * of radix passes) -> hash_table_index u32[N] (point ids by bin, ascending id
  * inside a bin), hash_table_cell_splits u32[T+1]. */
 int o3dml_build_spatial_hash_table(const float* points, int64_t n_points, float radius, int64_t n_batch,
                                    const int64_t* points_row_splits, const uint32_t* hash_table_splits,
-                                   int64_t total_bins, uint32_t* hash_table_index,
-                                   uint32_t* hash_table_cell_splits, void* workspace, size_t workspace_bytes,
-                                   void* stream);
+                                   const uint32_t* hash_table_splits_host, int64_t total_bins,
+                                   uint32_t* hash_table_index, uint32_t* hash_table_cell_splits, void* workspace,
+                                   size_t workspace_bytes, void* stream);
 
 /* ---- fixed radius search: replaces open3d.ml.torch.ops.fixed_radius_search
  * (layers.FixedRadiusSearch; kpconv.py:2016-2034 batch_neighbors, called from

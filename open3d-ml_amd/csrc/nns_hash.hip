@@ -68,6 +68,226 @@ __global__ void bin_boundaries_kernel(const uint32_t* __restrict__ skeys, int64_
     }
 }
 
+// ---------------------------------------------------------------------------
+// Small-table path (every batch item has <= kSmallTable bins): a stable
+// counting sort per batch item, split into chunks of kHashChunk points so the
+// whole GPU works on it — no radix passes.
+//   plan:    chunk_start[b] (chunks of items < b, at least one per item) and
+//            hist_off[b] (offset of item b's chunk histograms);
+//   hist:    per chunk, the bin of every point (kept for the scatter) and the
+//            chunk's bin histogram (LDS atomics: order-free);
+//   scan:    per item, each bin's column of chunk counts -> the chunks'
+//            first slots (bin start inside the item + earlier chunks), and
+//            the item's cell_splits;
+//   scatter: per chunk, the points ranked stably inside the chunk (ballot
+//            peers, per-wave counts in LDS), ids written to their slots.
+// ---------------------------------------------------------------------------
+constexpr int kSmallTable = 4096;
+constexpr int kHashChunk = 4096;  // points per chunk = 4 waves x 16 rows of 64
+constexpr int kHashWaves = 4;
+
+__global__ void __launch_bounds__(256) hash_plan_kernel(const int64_t* __restrict__ prs, int nb,
+                                                        const uint32_t* __restrict__ hts,
+                                                        int64_t* __restrict__ chunk_start,
+                                                        int64_t* __restrict__ hist_off) {
+    __shared__ int64_t wsum[2][4];
+    int64_t carry_c = 0, carry_h = 0;
+    for (int b0 = 0; b0 < nb; b0 += 256) {
+        const int b = b0 + threadIdx.x;
+        int64_t c = 0, h = 0;
+        if (b < nb) {
+            const int64_t n = prs[b + 1] - prs[b];
+            c = n > kHashChunk ? ceil_div(n, kHashChunk) : 1;
+            h = c * static_cast<int64_t>(hts[b + 1] - hts[b]);
+        }
+        const int64_t ic = wave_inclusive_scan(c), ih = wave_inclusive_scan(h);
+        if (lane_id() == 63) {
+            wsum[0][wave_id()] = ic;
+            wsum[1][wave_id()] = ih;
+        }
+        __syncthreads();
+        int64_t bc = carry_c, bh = carry_h, tc = 0, th = 0;
+        for (int w = 0; w < 4; ++w) {
+            if (w < wave_id()) {
+                bc += wsum[0][w];
+                bh += wsum[1][w];
+            }
+            tc += wsum[0][w];
+            th += wsum[1][w];
+        }
+        if (b < nb) {
+            chunk_start[b] = bc + ic - c;
+            hist_off[b] = bh + ih - h;
+        }
+        carry_c += tc;
+        carry_h += th;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        chunk_start[nb] = carry_c;
+        hist_off[nb] = carry_h;
+    }
+}
+
+// Batch item and chunk of workgroup blockIdx.x (false: past the last chunk).
+__device__ __forceinline__ bool hash_chunk_of(const int64_t* __restrict__ chunk_start, int nb, int& b, int64_t& c) {
+    const int64_t w = blockIdx.x;
+    if (w >= chunk_start[nb]) return false;
+    int lo = 0, hi = nb - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (chunk_start[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    b = lo;
+    c = w - chunk_start[lo];
+    return true;
+}
+
+__global__ void __launch_bounds__(256) hash_chunk_hist_kernel(const float* __restrict__ points, float inv, int nb,
+                                                              const int64_t* __restrict__ prs,
+                                                              const uint32_t* __restrict__ hts,
+                                                              const int64_t* __restrict__ chunk_start,
+                                                              const int64_t* __restrict__ hist_off,
+                                                              uint32_t* __restrict__ bins, uint32_t* __restrict__ hist) {
+    extern __shared__ uint32_t h[];  // [max bins per item]
+    int b;
+    int64_t c;
+    if (!hash_chunk_of(chunk_start, nb, b, c)) return;
+    const uint32_t tsize = hts[b + 1] - hts[b];
+    const uint32_t k64 = pow64_mod(tsize);
+    for (uint32_t i = threadIdx.x; i < tsize; i += 256) h[i] = 0;
+    __syncthreads();
+    const int64_t p0 = prs[b] + c * kHashChunk, p1 = min(prs[b + 1], p0 + kHashChunk);
+    for (int64_t i = p0 + threadIdx.x; i < p1; i += 256) {
+        const uint32_t bin = point_bin_k(points[3 * i], points[3 * i + 1], points[3 * i + 2], inv, tsize, k64);
+        bins[i] = bin;
+        atomicAdd(&h[bin], 1u);
+    }
+    __syncthreads();
+    uint32_t* out = hist + hist_off[b] + c * tsize;
+    for (uint32_t i = threadIdx.x; i < tsize; i += 256) out[i] = h[i];
+}
+
+// Per batch item (one workgroup): every bin's column of chunk counts becomes
+// the chunk's first slot of that bin (exclusive scan over the chunks plus the
+// bin's start inside the item, a scan over the bins); cell_splits too.
+__global__ void __launch_bounds__(1024) hash_hist_scan_kernel(int nb, const int64_t* __restrict__ prs,
+                                                              const uint32_t* __restrict__ hts,
+                                                              const int64_t* __restrict__ chunk_start,
+                                                              const int64_t* __restrict__ hist_off,
+                                                              uint32_t* __restrict__ hist,
+                                                              uint32_t* __restrict__ cell_splits) {
+    __shared__ uint32_t wsum[16];
+    const int b = blockIdx.x;
+    const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+    const uint32_t first = hts[b], tsize = hts[b + 1] - first;
+    const int64_t item0 = prs[b];
+    const int64_t nchunks = chunk_start[b + 1] - chunk_start[b];
+    uint32_t* H = hist + hist_off[b];
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < tsize; b0 += 1024) {  // bins b0 + t
+        const uint32_t bin = b0 + t;
+        uint32_t tot = 0;
+        if (bin < tsize) {
+            int64_t cc = 0;
+            for (; cc + 4 <= nchunks; cc += 4) {  // independent loads in flight
+                const uint32_t v0 = H[cc * tsize + bin], v1 = H[(cc + 1) * tsize + bin],
+                               v2 = H[(cc + 2) * tsize + bin], v3 = H[(cc + 3) * tsize + bin];
+                tot += (v0 + v1) + (v2 + v3);
+            }
+            for (; cc < nchunks; ++cc) tot += H[cc * tsize + bin];
+        }
+        const uint32_t inc = wave_inclusive_scan(tot);
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        uint32_t start = carry + inc - tot, all = 0;
+        for (int ww = 0; ww < 16; ++ww) {
+            start += ww < w ? wsum[ww] : 0u;
+            all += wsum[ww];
+        }
+        if (bin < tsize) {
+            cell_splits[first + bin] = static_cast<uint32_t>(item0 + start);
+            uint32_t run = start;
+            for (int64_t cc = 0; cc < nchunks; ++cc) {
+                const uint32_t v = H[cc * tsize + bin];
+                H[cc * tsize + bin] = run;
+                run += v;
+            }
+        }
+        carry += all;
+        __syncthreads();
+    }
+    if (b == nb - 1 && t == 0) cell_splits[first + tsize] = static_cast<uint32_t>(prs[nb]);
+}
+
+// Per chunk: ranks the chunk's points stably and writes their ids; the chunk's
+// first slot per bin comes from hash_hist_scan_kernel.
+__global__ void __launch_bounds__(256) hash_chunk_scatter_kernel(int nb, const int64_t* __restrict__ prs,
+                                                                 const uint32_t* __restrict__ hts,
+                                                                 const int64_t* __restrict__ chunk_start,
+                                                                 const int64_t* __restrict__ hist_off,
+                                                                 const uint32_t* __restrict__ bins,
+                                                                 const uint32_t* __restrict__ hist,
+                                                                 uint32_t* __restrict__ hti, int max_bins) {
+    constexpr int kRows = kHashChunk / 64 / kHashWaves;  // rows of 64 per wave
+    extern __shared__ uint32_t wc_all[];                // [kHashWaves][max_bins]: counts, then bases
+    int b;
+    int64_t c;
+    if (!hash_chunk_of(chunk_start, nb, b, c)) return;
+    const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+    const uint32_t tsize = hts[b + 1] - hts[b];
+    const int64_t item0 = prs[b], item_end = prs[b + 1];
+    const uint32_t* base = hist + hist_off[b] + c * tsize;
+    uint32_t* wc = wc_all + w * max_bins;
+    for (uint32_t i = t; i < tsize; i += 256)
+#pragma unroll
+        for (int ww = 0; ww < kHashWaves; ++ww) wc_all[ww * max_bins + i] = 0;
+    __syncthreads();
+    // each wave ranks its contiguous rows in order (peers = same bin, found
+    // with one ballot per bin bit), running per-bin counts in LDS — LDS
+    // operations of one wave execute in order, no barrier between rows
+    const int64_t p0 = item0 + c * kHashChunk;
+    const int64_t pend = min(item_end, p0 + kHashChunk);
+    const int nbits = tsize > 1 ? 32 - __builtin_clz(tsize - 1) : 0;
+    const uint64_t lt = lanemask_lt();
+    uint32_t dig[kRows], loff[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int64_t i = p0 + (static_cast<int64_t>(w) * kRows + r) * 64 + lane;
+        const bool valid = i < pend;
+        const uint32_t d = valid ? bins[i] : 0u;
+        dig[r] = d;
+        uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
+        for (int bit = 0; bit < nbits; ++bit) {
+            const bool on = (d >> bit) & 1u;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(on);
+            peers &= on ? m : ~m;
+        }
+        const uint32_t rank = __popcll(peers & lt);
+        const uint32_t before = valid ? wc[d] : 0u;
+        loff[r] = before + rank;
+        if (valid && rank == 0) wc[d] = before + static_cast<uint32_t>(__popcll(peers));
+    }
+    __syncthreads();
+    // per-wave bases: chunk base + counts of the earlier waves (stable)
+    for (uint32_t i = t; i < tsize; i += 256) {
+        uint32_t a = base[i];
+#pragma unroll
+        for (int ww = 0; ww < kHashWaves; ++ww) {
+            const uint32_t cw = wc_all[ww * max_bins + i];
+            wc_all[ww * max_bins + i] = a;
+            a += cw;
+        }
+    }
+    __syncthreads();
+    // ids to their slots (scattered inside the item's range)
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int64_t i = p0 + (static_cast<int64_t>(w) * kRows + r) * 64 + lane;
+        if (i < pend) hti[item0 + wc[dig[r]] + loff[r]] = static_cast<uint32_t>(i);
+    }
+}
+
 }  // namespace o3dml
 
 using namespace o3dml;
@@ -87,15 +307,22 @@ O3DML_API int64_t o3dml_hash_table_splits(int64_t n_batch, const int64_t* points
 }
 
 O3DML_API size_t o3dml_build_spatial_hash_table_workspace_size(int64_t n_points, int64_t total_bins) {
-    (void)total_bins;
-    return ws_bytes<uint32_t>(n_points) * 2 + prim::radix_sort_workspace_bytes<uint32_t>(n_points);
+    // radix path: bins + sorted keys + sort scratch; small-table path: bins,
+    // chunk histograms (<= n_points + total_bins entries when every table has
+    // <= kSmallTable bins: sum_b chunks_b T_b <= sum_b (N_b / chunk + 1) T_b)
+    // and the plan — the larger of the two
+    const size_t radix = ws_bytes<uint32_t>(n_points) * 2 + prim::radix_sort_workspace_bytes<uint32_t>(n_points);
+    const int64_t nb_ub = total_bins;  // every batch item has >= 1 bin
+    const size_t small = ws_bytes<uint32_t>(n_points) + ws_bytes<uint32_t>(n_points + total_bins) +
+                         2 * ws_bytes<int64_t>(nb_ub + 1);
+    return std::max(radix, small);
 }
 
 O3DML_API int o3dml_build_spatial_hash_table(const float* points, int64_t n_points, float radius, int64_t n_batch,
                                              const int64_t* points_row_splits, const uint32_t* hash_table_splits,
-                                             int64_t total_bins, uint32_t* hash_table_index,
-                                             uint32_t* hash_table_cell_splits, void* workspace,
-                                             size_t workspace_bytes, void* stream) {
+                                             const uint32_t* hash_table_splits_host, int64_t total_bins,
+                                             uint32_t* hash_table_index, uint32_t* hash_table_cell_splits,
+                                             void* workspace, size_t workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
     O3DML_REQUIRE(radius > 0.f, "radius must be > 0");
     O3DML_REQUIRE(n_batch >= 1, "need at least one batch item");
@@ -104,6 +331,35 @@ O3DML_API int o3dml_build_spatial_hash_table(const float* points, int64_t n_poin
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
     const float inv = 1.0f / (2.0f * radius);
+    bool small = hash_table_splits_host != nullptr && n_points > 0;
+    uint32_t max_bins = 1;
+    for (int64_t b = 0; small && b < n_batch; ++b) {
+        const uint32_t tb = hash_table_splits_host[b + 1] - hash_table_splits_host[b];
+        max_bins = std::max(max_bins, tb);
+        small = tb <= static_cast<uint32_t>(kSmallTable);
+    }
+    if (small) {
+        uint32_t* bins = ws.take<uint32_t>(n_points);
+        uint32_t* hist = ws.take<uint32_t>(n_points + total_bins);
+        int64_t* chunk_start = ws.take<int64_t>(n_batch + 1);
+        int64_t* hist_off = ws.take<int64_t>(n_batch + 1);
+        hash_plan_kernel<<<1, 256, 0, st>>>(points_row_splits, (int)n_batch, hash_table_splits, chunk_start,
+                                            hist_off);
+        O3DML_LAUNCH_CHECK();
+        const unsigned grid = static_cast<unsigned>(ceil_div(n_points, kHashChunk) + n_batch);  // >= chunk count
+        hash_chunk_hist_kernel<<<grid, 256, sizeof(uint32_t) * max_bins, st>>>(
+                points, inv, (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist);
+        O3DML_LAUNCH_CHECK();
+        hash_hist_scan_kernel<<<static_cast<unsigned>(n_batch), 1024, 0, st>>>(
+                (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, hist,
+                hash_table_cell_splits);
+        O3DML_LAUNCH_CHECK();
+        hash_chunk_scatter_kernel<<<grid, 256, sizeof(uint32_t) * kHashWaves * max_bins, st>>>(
+                (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist,
+                hash_table_index, static_cast<int>(max_bins));
+        O3DML_LAUNCH_CHECK();
+        return 0;
+    }
     uint32_t* bins = ws.take<uint32_t>(n_points);
     uint32_t* skeys = ws.take<uint32_t>(n_points);
     if (n_points > 0) {
@@ -118,4 +374,3 @@ O3DML_API int o3dml_build_spatial_hash_table(const float* points, int64_t n_poin
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }
-

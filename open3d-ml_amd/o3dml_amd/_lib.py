@@ -33,7 +33,7 @@ SIGNATURES = {
     # nns_hash.hip
     "o3dml_hash_table_splits": (c_i64, [c_i64, c_p, c_f64, c_i64, c_p]),
     "o3dml_build_spatial_hash_table_workspace_size": (c_sz, [c_i64, c_i64]),
-    "o3dml_build_spatial_hash_table": (c_i32, [c_p, c_i64, c_f32, c_i64, c_p, c_p, c_i64, c_p, c_p,
+    "o3dml_build_spatial_hash_table": (c_i32, [c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p, c_i64, c_p, c_p,
                                                c_p, c_sz, c_p]),
     "o3dml_fixed_radius_search_workspace_size": (c_sz, [c_i64, c_i64, c_i64]),
     "o3dml_fixed_radius_search_count": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p, c_p,

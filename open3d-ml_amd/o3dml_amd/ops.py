@@ -55,8 +55,8 @@ def build_spatial_hash_table(points, radius, points_row_splits=None, hash_table_
     index = torch.empty(n, dtype=torch.int32, device=dev)
     cells = torch.empty(T + 1, dtype=torch.int32, device=dev)
     ws = workspace(lib.o3dml_build_spatial_hash_table_workspace_size(n, T), dev)
-    _lib.call("o3dml_build_spatial_hash_table", ptr(pts), n, r, B, ptr(prs_d), ptr(hts_d), T, ptr(index),
-              ptr(cells), ptr(ws), ws.numel(), stream_handle(dev))
+    _lib.call("o3dml_build_spatial_hash_table", ptr(pts), n, r, B, ptr(prs_d), ptr(hts_d), splits.ctypes.data, T,
+              ptr(index), ptr(cells), ptr(ws), ws.numel(), stream_handle(dev))
     return BuildSpatialHashTableResult(back_to(index, points), back_to(cells, points),
                                        torch.from_numpy(splits.astype(np.int32)))
 
