@@ -44,10 +44,26 @@ __global__ void __launch_bounds__(256) gather_sorted_points_kernel(const float* 
     const int64_t per = ceil_div(n, static_cast<int64_t>(gridDim.x));
     const int64_t blk = xcd_block();
     const int64_t e = min(n, (blk + 1) * per);
-    for (int64_t j = blk * per + threadIdx.x; j < e; j += blockDim.x) {
-        const uint32_t i = index[j];
-        out[j] = make_float4(points[3 * static_cast<int64_t>(i)], points[3 * static_cast<int64_t>(i) + 1],
-                             points[3 * static_cast<int64_t>(i) + 2], __uint_as_float(i));
+    constexpr int U = 4;  // four independent index -> point chains in flight per thread
+    for (int64_t j0 = blk * per + threadIdx.x; j0 < e; j0 += U * static_cast<int64_t>(blockDim.x)) {
+        uint32_t id[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = j0 + u * static_cast<int64_t>(blockDim.x);
+            id[u] = j < e ? index[j] : 0u;
+        }
+        float x[U], y[U], z[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            x[u] = points[3 * static_cast<int64_t>(id[u])];
+            y[u] = points[3 * static_cast<int64_t>(id[u]) + 1];
+            z[u] = points[3 * static_cast<int64_t>(id[u]) + 2];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = j0 + u * static_cast<int64_t>(blockDim.x);
+            if (j < e) out[j] = make_float4(x[u], y[u], z[u], __uint_as_float(id[u]));
+        }
     }
     if (sentinel && blockIdx.x == 0 && threadIdx.x == 0) {  // out[n]: beyond every radius
         const float inf = __builtin_huge_valf();
@@ -58,7 +74,7 @@ __global__ void __launch_bounds__(256) gather_sorted_points_kernel(const float* 
 constexpr int kRowCap = 64;  // neighbours kept per query in the temp rows
 
 #ifndef O3DML_DIAG
-#define O3DML_DIAG 0  // 1: skip the candidate test loop (instruction-split diagnostics)
+#define O3DML_DIAG 0  // 1: skip the candidate test loop, 2: also skip streaming (cost-split diagnostics)
 #endif
 #ifndef O3DML_STREAM_U
 #define O3DML_STREAM_U 2
@@ -240,6 +256,9 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
             uint32_t total = 0;
             bucket_table<0>(cs, lb, vpre, vdel, total);
             vpre = write_lane<9>(vpre, static_cast<int>(total));
+#if O3DML_DIAG == 2
+            total = 0;  // diagnostics: grouping and bucket tables only, no streaming
+#endif
             // stop filling while the next round (and the test padding) might not fit
             const int fill_lim = kCandCap - 64 * kStreamU - (S - 1);
             // stream cursor: source index of this lane's point in the round of
@@ -303,7 +322,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 const int ncp = (nc + S - 1) & ~(S - 1);
                 if (nc + lane < ncp) cand[nc + lane] = far;
                 __syncthreads();
-#if O3DML_DIAG != 1
+#if O3DML_DIAG == 0
                 auto test = [&](const float4& p) {
                     const float d = dist_metric<METRIC>(p.x, p.y, p.z, mq.x, mq.y, mq.z);
                     const bool hit = d <= thr && !(IGNORE && p.x == mq.x && p.y == mq.y && p.z == mq.z);
