@@ -164,13 +164,14 @@ __device__ __forceinline__ void bucket_table(const uint32_t* __restrict__ cs, co
 #else
 #define O3DML_FRS_ATTR __attribute__((amdgpu_num_sgpr(O3DML_FRS_NUM_SGPR)))
 #endif
-template <int METRIC, bool IGNORE, bool DIST, int MODE, class TIdx>
+template <int METRIC, bool IGNORE, bool DIST, int MODE, class TIdx, bool REL16>
 __global__ void __launch_bounds__(64) O3DML_FRS_ATTR
 frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t* __restrict__ cs,
                  const float4* __restrict__ qpts,
                  const uint32_t* __restrict__ qkeys, int bshift, int64_t m_host, const int64_t* __restrict__ m_dev,
                  float r, float inv, float thr, int nb, const int64_t* __restrict__ qrs,
-                 const uint32_t* __restrict__ hts, int64_t* __restrict__ counts, uint32_t* __restrict__ tidx,
+                 const uint32_t* __restrict__ hts, const int64_t* __restrict__ prs,
+                 uint32_t* __restrict__ counts, uint32_t* __restrict__ tidx,
                  float* __restrict__ tdist, uint32_t* __restrict__ over, int64_t* __restrict__ n_over,
                  const int64_t* __restrict__ rs, TIdx* __restrict__ out_idx, float* __restrict__ out_dist) {
     __shared__ float4 cand[kCandCap];
@@ -200,10 +201,12 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
 #pragma unroll
         for (int k = 0; k < 9; ++k) qb.b[k] = 0xffffffffu;
         int64_t row = 0;  // MODE 1: the query's final row start
+        uint32_t pbase = 0;  // REL16: first point id of the query's batch item
         if (valid) {
             q4 = qpts[t];
             const uint32_t qid = __float_as_uint(q4.w);
             const int b = qkeys ? (bshift >= 32 ? 0 : static_cast<int>(qkeys[t] >> bshift)) : batch_of(qid, qrs, nb);
+            if constexpr (REL16) pbase = static_cast<uint32_t>(prs[b]);
             const uint32_t first = hts[b], tsize = hts[b + 1] - first;
             qb = query_bins(q4.x, q4.y, q4.z, r, inv, first, tsize);
             if constexpr (MODE == 1) row = rs[qid];
@@ -219,6 +222,8 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 same = same && qb.b[k] == lb[k];
             }
             const uint64_t gm = __builtin_amdgcn_ballot_w64(same);
+            // a group shares its buckets, hence its batch item
+            const uint32_t gbase = REL16 ? rdlane(static_cast<int>(pbase), leader) : 0u;
             todo &= ~gm;
             const int ng = __popcll(gm);
             __syncthreads();  // previous group done with qsh / cand
@@ -335,7 +340,11 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                             // rows longer than kRowCap are re-run (MODE 1), so their
                             // temp row may take anything in its last slot
                             const uint32_t ps = min(pos, static_cast<uint32_t>(kRowCap - 1));
-                            tidx[mrow * kRowCap + ps] = __float_as_uint(p.w);
+                            if constexpr (REL16)  // 16-bit ids relative to the batch item: 128-B rows
+                                reinterpret_cast<uint16_t*>(tidx)[mrow * kRowCap + ps] =
+                                        static_cast<uint16_t>(__float_as_uint(p.w) - gbase);
+                            else
+                                tidx[mrow * kRowCap + ps] = __float_as_uint(p.w);
                             if constexpr (DIST) tdist[mrow * kRowCap + ps] = d;
                         } else {
                             out_idx[mrow + pos] = static_cast<TIdx>(__float_as_uint(p.w));
@@ -372,49 +381,70 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
 
 // Final rows from the temp rows (already in canonical order, temp row = query
 // id, so both sides stream in order).  A wave owns 64 consecutive rows;
-// lanes = entries of one row, 8 rows in flight: one coalesced 4-B-per-lane
-// load of the row's live entries (lanes past the count read a zero word, so
-// no load sits under a branch) and one coalesced store.  Rows longer than
-// kRowCap are written by the MODE 1 re-run.
+// lanes = entries of one row, 8 rows in flight: one coalesced load of the
+// row's live entries (lanes past the count read a zero word, so no load sits
+// under a branch) and one coalesced store.  REL16: the temp rows hold 16-bit
+// ids relative to the batch item's first point (one 128-B line per row), the
+// item base is added back here.  Rows longer than kRowCap are written by the
+// MODE 1 re-run.
 __device__ uint32_t g_frs_zero[4];
+#ifndef O3DML_COPY_ROWS
+#define O3DML_COPY_ROWS 32
+#endif
+constexpr int kCopyRows = O3DML_COPY_ROWS;  // rows whose loads are in flight together
 
-template <bool DIST, class TIdx>
-__global__ void __launch_bounds__(256) group_rows_copy_kernel(int64_t m, const int64_t* __restrict__ counts,
+template <bool DIST, bool REL16, class TIdx>
+__global__ void __launch_bounds__(256) group_rows_copy_kernel(int64_t m, const uint32_t* __restrict__ counts,
                                                               const int64_t* __restrict__ rs,
+                                                              const int64_t* __restrict__ qrs,
+                                                              const int64_t* __restrict__ prs, int nb,
                                                               const uint32_t* __restrict__ tidx,
                                                               const float* __restrict__ tdist,
                                                               TIdx* __restrict__ idx, float* __restrict__ dist) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tidx);
     for (int64_t base = wave * 64; base < m; base += nwaves * 64) {
         const int64_t t = base + lane;
         int n = 0;
         int64_t o = 0;
+        uint32_t pb = 0;
+        if constexpr (REL16) {  // the 64 rows usually share one batch item: one uniform (scalar) search
+            const int64_t ub = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(base >> 6))) << 6;
+            const int b0 = batch_of(ub, qrs, nb);
+            const int64_t last = min(ub + 63, m - 1);
+            pb = static_cast<uint32_t>(prs[b0]);
+            if (qrs[b0 + 1] <= last && t < m) pb = static_cast<uint32_t>(prs[batch_of(t, qrs, nb)]);
+        }
         if (t < m) {
-            const int64_t c = counts[t];
-            n = c <= kRowCap ? static_cast<int>(c) : 0;
+            const uint32_t c = counts[t];
+            n = c <= static_cast<uint32_t>(kRowCap) ? static_cast<int>(c) : 0;
             o = rs[t];
         }
-        for (int k = 0; k < 64; k += 8) {
-            uint32_t v[8];
-            float dv[8];
+        for (int k = 0; k < 64; k += kCopyRows) {
+            uint32_t v[kCopyRows];
+            float dv[kCopyRows];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < kCopyRows; ++u) {
                 const int nu = __builtin_amdgcn_readlane(n, k + u);
                 const int64_t src = (base + k + u) * kRowCap + lane;
                 const bool live = lane < nu;
-                v[u] = *(live ? tidx + src : g_frs_zero);
+                if constexpr (REL16)
+                    v[u] = *(live ? t16 + src : reinterpret_cast<const uint16_t*>(g_frs_zero));
+                else
+                    v[u] = *(live ? tidx + src : g_frs_zero);
                 if constexpr (DIST) dv[u] = *(live ? tdist + src : reinterpret_cast<const float*>(g_frs_zero));
             }
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < kCopyRows; ++u) {
                 const int nu = __builtin_amdgcn_readlane(n, k + u);
                 const int64_t ou = static_cast<int64_t>(
                         (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(o >> 32), k + u))) << 32) |
                         static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(o), k + u)));
+                const uint32_t pbu = REL16 ? static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(pb), k + u)) : 0u;
                 if (lane < nu) {
-                    idx[ou + lane] = static_cast<TIdx>(v[u]);
+                    idx[ou + lane] = static_cast<TIdx>(v[u] + pbu);
                     if constexpr (DIST) dist[ou + lane] = dv[u];
                 }
             }
@@ -583,21 +613,29 @@ static unsigned group_grid(int64_t m, int queries_per_wave = 64) {
 }
 
 template <int MODE, class TIdx>
-static void launch_group(int metric, bool ignore, bool with_dist, hipStream_t st, unsigned grid, const float4* pts,
-                         uint32_t n_pts, const uint32_t* cs, const float4* qpts, const uint32_t* qkeys, int bshift, int64_t m,
-                         const int64_t* m_dev, float r, float inv, float thr, int nb, const int64_t* qrs,
-                         const uint32_t* hts, int64_t* counts, uint32_t* tidx, float* tdist, uint32_t* over,
-                         int64_t* n_over, const int64_t* rs, TIdx* idx, float* dist) {
-#define O3DML_GRP(M, I, D)                                                                                    \
-    frs_group_kernel<M, I, D, MODE, TIdx><<<grid, 64, 0, st>>>(pts, n_pts, cs, qpts, qkeys, bshift, m, m_dev, r, inv, \
-                                                                thr, nb, qrs, hts, counts, tidx, tdist, over,   \
-                                                                n_over, rs, idx, dist)
+static void launch_group(int metric, bool ignore, bool with_dist, bool rel16, hipStream_t st, unsigned grid,
+                         const float4* pts, uint32_t n_pts, const uint32_t* cs, const float4* qpts,
+                         const uint32_t* qkeys, int bshift, int64_t m, const int64_t* m_dev, float r, float inv,
+                         float thr, int nb, const int64_t* qrs, const uint32_t* hts, const int64_t* prs,
+                         uint32_t* counts, uint32_t* tidx, float* tdist, uint32_t* over, int64_t* n_over,
+                         const int64_t* rs, TIdx* idx, float* dist) {
+#define O3DML_GRP(M, I, D, R)                                                                                   \
+    frs_group_kernel<M, I, D, MODE, TIdx, R><<<grid, 64, 0, st>>>(pts, n_pts, cs, qpts, qkeys, bshift, m, m_dev,  \
+                                                                   r, inv, thr, nb, qrs, hts, prs, counts, tidx,  \
+                                                                   tdist, over, n_over, rs, idx, dist)
+#define O3DML_GRP_R(M, I, D)                                  \
+    do {                                                      \
+        if (MODE == 0 && rel16)                               \
+            O3DML_GRP(M, I, D, MODE == 0);                    \
+        else                                                  \
+            O3DML_GRP(M, I, D, false);                        \
+    } while (0)
 #define O3DML_GRP_D(M, I)              \
     do {                               \
         if (with_dist)                 \
-            O3DML_GRP(M, I, true);     \
+            O3DML_GRP_R(M, I, true);   \
         else                           \
-            O3DML_GRP(M, I, false);    \
+            O3DML_GRP_R(M, I, false);  \
     } while (0)
     if (metric == kL2) {
         if (ignore) O3DML_GRP_D(kL2, true); else O3DML_GRP_D(kL2, false);
@@ -607,6 +645,7 @@ static void launch_group(int metric, bool ignore, bool with_dist, hipStream_t st
         if (ignore) O3DML_GRP_D(kLinf, true); else O3DML_GRP_D(kLinf, false);
     }
 #undef O3DML_GRP_D
+#undef O3DML_GRP_R
 #undef O3DML_GRP
     O3DML_LAUNCH_CHECK();
 }
@@ -620,7 +659,7 @@ struct FrsPlan {
     uint32_t* keys;    // [M]
     uint32_t* skeys;   // [M]
     uint32_t* qorder;  // [M]
-    int64_t* counts;   // [M]
+    uint32_t* counts;  // [M]
     uint32_t* over;    // [M]
     uint32_t* tidx;    // [M * kRowCap]
     float* tdist;      // [M * kRowCap] (with distances)
@@ -635,16 +674,28 @@ static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m, bool dist) {
     p.keys = ws.take<uint32_t>(m);
     p.skeys = ws.take<uint32_t>(m);
     p.qorder = ws.take<uint32_t>(m);
-    p.counts = ws.take<int64_t>(m);
+    p.counts = ws.take<uint32_t>(m);
     p.over = ws.take<uint32_t>(m);
     p.tidx = ws.take<uint32_t>(m * kRowCap);
     p.tdist = dist ? ws.take<float>(m * kRowCap) : nullptr;
     return p;
 }
 
+// Temp rows hold 16-bit ids relative to the batch item's first point when no
+// batch item has more than 65,536 points (host copy of the point row splits).
+#ifndef O3DML_FRS_REL16
+#define O3DML_FRS_REL16 1
+#endif
+static bool rel16_rows(int64_t n_batch, const int64_t* prs_host) {
+    if (!prs_host || !O3DML_FRS_REL16) return false;
+    for (int64_t b = 0; b < n_batch; ++b)
+        if (prs_host[b + 1] - prs_host[b] > 65536) return false;
+    return true;
+}
+
 static size_t plan_bytes(int64_t n, int64_t m) {
     return ws_bytes<int64_t>(4) + ws_bytes<float4>(n + 1) + 2 * ws_bytes<float4>(m) + 3 * ws_bytes<uint32_t>(m) +
-           ws_bytes<int64_t>(m) + ws_bytes<uint32_t>(m) + 2 * ws_bytes<uint32_t>(m * kRowCap);
+           2 * ws_bytes<uint32_t>(m) + 2 * ws_bytes<uint32_t>(m * kRowCap);
 }
 
 }  // namespace o3dml
@@ -667,9 +718,6 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
                                               int64_t* neighbors_row_splits, void* workspace,
                                               size_t workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
-    (void)points_row_splits;
-    (void)points_row_splits_host;
-    (void)self_search;
     O3DML_REQUIRE(metric >= 0 && metric <= 2, "metric must be L1(0), L2(1) or Linf(2)");
     O3DML_REQUIRE(radius > 0.f, "radius must be > 0");
     O3DML_REQUIRE(n_queries < (int64_t(1) << 31) && n_points < (int64_t(1) << 31), "too many points");
@@ -723,14 +771,15 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     }
     {
         TimedRegion tr("frs_group_search", st);
-        launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0, st, group_grid(n_queries),
-                                 pl.pts, static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts, qkeys,
-                                 bshift, n_queries, nullptr, radius, inv, thr,
-                                 (int)n_batch, queries_row_splits, hash_table_splits, pl.counts, pl.tidx, pl.tdist,
-                                 pl.over, pl.scalars, nullptr, nullptr, nullptr);
+        launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0,
+                                 rel16_rows(n_batch, points_row_splits_host), st, group_grid(n_queries), pl.pts,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts, qkeys, bshift,
+                                 n_queries, nullptr, radius, inv, thr, (int)n_batch, queries_row_splits,
+                                 hash_table_splits, points_row_splits, pl.counts, pl.tidx, pl.tdist, pl.over,
+                                 pl.scalars, nullptr, nullptr, nullptr);
     }
     Workspace sws = ws;
-    prim::scan<int64_t, int64_t>(pl.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
+    prim::scan<uint32_t, int64_t>(pl.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
     O3DML_GUARD_END
 }
 
@@ -746,8 +795,6 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
                                              size_t workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
     (void)points;
-    (void)points_row_splits;
-    (void)points_row_splits_host;
     (void)hash_table_index;
     (void)self_search;
     O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
@@ -763,17 +810,22 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
     {
         TimedRegion tr("frs_group_rows", st);
         const unsigned gc = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_queries, 256), 1 << 16)));
-#define O3DML_GCOPY(T)                                                                                        \
-    do {                                                                                                      \
-        if (dist)                                                                                             \
-            group_rows_copy_kernel<true, T><<<gc, 256, 0, st>>>(n_queries, pl.counts, rs, pl.tidx, pl.tdist,  \
-                                                                static_cast<T*>(neighbors_index), dist);      \
-        else                                                                                                  \
-            group_rows_copy_kernel<false, T><<<gc, 256, 0, st>>>(n_queries, pl.counts, rs, pl.tidx, nullptr,  \
-                                                                 static_cast<T*>(neighbors_index), nullptr);  \
+        const bool rel16 = rel16_rows(n_batch, points_row_splits_host);
+#define O3DML_GCOPY3(D, R, T)                                                                                   \
+    group_rows_copy_kernel<D, R, T><<<gc, 256, 0, st>>>(n_queries, pl.counts, rs, queries_row_splits,          \
+                                                        points_row_splits, (int)n_batch, pl.tidx, pl.tdist,    \
+                                                        static_cast<T*>(neighbors_index), dist)
+#define O3DML_GCOPY(T)                                                                                          \
+    do {                                                                                                        \
+        if (dist) {                                                                                             \
+            if (rel16) O3DML_GCOPY3(true, true, T); else O3DML_GCOPY3(true, false, T);                         \
+        } else {                                                                                                \
+            if (rel16) O3DML_GCOPY3(false, true, T); else O3DML_GCOPY3(false, false, T);                       \
+        }                                                                                                       \
     } while (0)
         if (index_bits == 32) O3DML_GCOPY(int32_t); else O3DML_GCOPY(int64_t);
 #undef O3DML_GCOPY
+#undef O3DML_GCOPY3
         O3DML_LAUNCH_CHECK();
     }
     // rows longer than kRowCap: re-run those queries straight into the final
@@ -784,14 +836,16 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
             queries, pl.over, pl.scalars, pl.pts_over);
     O3DML_LAUNCH_CHECK();
     if (index_bits == 32)
-        launch_group<1, int32_t>(metric, ignore_query_point != 0, dist != nullptr, st, go, pl.pts,
-                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.pts_over, nullptr, 32, 0, pl.scalars, radius, inv, thr,
-                                 (int)n_batch, queries_row_splits, hash_table_splits, nullptr, nullptr, nullptr,
-                                 nullptr, nullptr, rs, static_cast<int32_t*>(neighbors_index), dist);
+        launch_group<1, int32_t>(metric, ignore_query_point != 0, dist != nullptr, false, st, go, pl.pts,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.pts_over, nullptr, 32, 0,
+                                 pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
+                                 points_row_splits, nullptr, nullptr, nullptr, nullptr, nullptr, rs,
+                                 static_cast<int32_t*>(neighbors_index), dist);
     else
-        launch_group<1, int64_t>(metric, ignore_query_point != 0, dist != nullptr, st, go, pl.pts,
-                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.pts_over, nullptr, 32, 0, pl.scalars, radius, inv, thr,
-                                 (int)n_batch, queries_row_splits, hash_table_splits, nullptr, nullptr, nullptr,
-                                 nullptr, nullptr, rs, static_cast<int64_t*>(neighbors_index), dist);
+        launch_group<1, int64_t>(metric, ignore_query_point != 0, dist != nullptr, false, st, go, pl.pts,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.pts_over, nullptr, 32, 0,
+                                 pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
+                                 points_row_splits, nullptr, nullptr, nullptr, nullptr, nullptr, rs,
+                                 static_cast<int64_t*>(neighbors_index), dist);
     O3DML_GUARD_END
 }

@@ -146,3 +146,25 @@ def test_frs_dense_cluster_overflow_rows(cuda):
     assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
     assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
     assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
+
+
+@pytest.mark.parametrize("sizes", [[65536, 1000], [70000, 3000], [1, 65536, 0, 40000]])
+def test_frs_temp_row_widths(cuda, sizes):
+    """Temp rows carry 16-bit ids relative to the batch item's first point when
+    no item exceeds 65,536 points (the last id of a full item is 65,535) and
+    32-bit ids otherwise; both must reproduce the oracle, with and without
+    distances and for int64 output."""
+    from o3dml_amd import layers
+    rs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    pts = np.concatenate([_cloud(max(n, 0), 10 + i) for i, n in enumerate(sizes)]) if rs[-1] else \
+        np.zeros((0, 3), np.float32)
+    t = torch.from_numpy(pts).to(cuda)
+    for dist, dt in ((False, torch.int32), (True, torch.int64)):
+        nns = layers.FixedRadiusSearch(return_distances=dist, index_dtype=dt)
+        res = nns(t, t, 0.04, torch.from_numpy(rs), torch.from_numpy(rs))
+        oi, ors, od = O.fixed_radius_search(pts, pts, 0.04, rs, rs, return_distances=dist,
+                                            index_dtype=np.int64 if dt == torch.int64 else np.int32)
+        assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+        assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+        if dist:
+            assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
