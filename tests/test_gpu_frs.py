@@ -168,3 +168,25 @@ def test_frs_temp_row_widths(cuda, sizes):
         assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
         if dist:
             assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
+
+
+@pytest.mark.parametrize("n,rs_mid", [(300000, None), (90000, [5, 5, 40000])])
+def test_hash_table_paths(cuda, n, rs_mid):
+    """Both hash-table builders against the oracle: tables of > 4,096 bins in a
+    batch item take the radix-sort path (300,000 points -> 4,687 bins), smaller
+    ones the chunked counting sort (several 4,096-point chunks per item, empty
+    and one-point items), each bit-exact; the FRS on top stays exact."""
+    from o3dml_amd import ops
+    pts = _cloud(n, 21)
+    rs = np.array([0] + (rs_mid or []) + [n], np.int64)
+    t = torch.from_numpy(pts).to(cuda)
+    ht = ops.build_spatial_hash_table(t, 0.02, torch.from_numpy(rs))
+    oi, oc, osp = O.build_spatial_hash_table(pts, 0.02, rs)
+    assert np.array_equal(ht.hash_table_splits.numpy().astype(np.uint32), osp)
+    assert np.array_equal(ht.hash_table_cell_splits.cpu().numpy().astype(np.uint32), oc)
+    assert np.array_equal(ht.hash_table_index.cpu().numpy().astype(np.uint32), oi)
+    res = ops.fixed_radius_search(t, t, 0.02, torch.from_numpy(rs), torch.from_numpy(rs), ht.hash_table_splits,
+                                  ht.hash_table_index, ht.hash_table_cell_splits)
+    ri, rr, _ = O.fixed_radius_search(pts, pts, 0.02, rs, rs, hash_table=(oi, oc, osp))
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), rr)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), ri)
