@@ -40,7 +40,9 @@ namespace o3dml {
 // a time), so the random reads inside a batch item stay in that XCD's L2.
 __global__ void __launch_bounds__(256) gather_sorted_points_kernel(const float* __restrict__ points,
                                                                    const uint32_t* __restrict__ index, int64_t n,
-                                                                   float4* __restrict__ out, int sentinel) {
+                                                                   float4* __restrict__ out, int sentinel,
+                                                                   int64_t* __restrict__ zero_a, int n_zero_a,
+                                                                   int64_t* __restrict__ zero_b) {
     const int64_t per = ceil_div(n, static_cast<int64_t>(gridDim.x));
     const int64_t blk = xcd_block();
     const int64_t e = min(n, (blk + 1) * per);
@@ -65,9 +67,14 @@ __global__ void __launch_bounds__(256) gather_sorted_points_kernel(const float* 
             if (j < e) out[j] = make_float4(x[u], y[u], z[u], __uint_as_float(id[u]));
         }
     }
-    if (sentinel && blockIdx.x == 0 && threadIdx.x == 0) {  // out[n]: beyond every radius
-        const float inf = __builtin_huge_valf();
-        out[n] = make_float4(inf, inf, inf, 0.f);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (sentinel) {  // out[n]: beyond every radius
+            const float inf = __builtin_huge_valf();
+            out[n] = make_float4(inf, inf, inf, 0.f);
+        }
+        // zeroed words of the caller (instead of memset launches)
+        for (int j = 0; j < n_zero_a; ++j) zero_a[j] = 0;
+        if (zero_b) *zero_b = 0;
     }
 }
 
@@ -725,22 +732,19 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
     FrsPlan pl = take_plan(ws, n_points, n_queries, with_distances != 0);
-    O3DML_CHECK_HIP(hipMemsetAsync(pl.scalars, 0, sizeof(int64_t) * 4, st));
-    if (n_queries == 0) {
-        O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
-        return 0;
-    }
-    if (n_points == 0) {
+    if (n_queries == 0 || n_points == 0) {
+        O3DML_CHECK_HIP(hipMemsetAsync(pl.scalars, 0, sizeof(int64_t) * 4, st));
         O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t) * (n_queries + 1), st));
         return 0;
     }
-    O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
     const float thr = metric == kL2 ? radius * radius : radius;
     const float inv = 1.0f / (2.0f * radius);
     const int batch_bits = prim::bits_needed(static_cast<uint64_t>(n_batch - 1));
     const uint32_t* qkeys;
     int bshift;
-    gather_sorted_points_kernel<<<xcd_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points, pl.pts, 1);
+    // also zeroes the plan scalars and neighbors_row_splits[0]
+    gather_sorted_points_kernel<<<xcd_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points, pl.pts, 1,
+                                                                        pl.scalars, 4, neighbors_row_splits);
     O3DML_LAUNCH_CHECK();
     if (self_search && frs_self_order()) {
         // queries = points: Open3D's bucket order, octant groups made adjacent
@@ -764,7 +768,7 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
                                              batch_bits + 3 * cell_bits, sws, st);
         }
         gather_sorted_points_kernel<<<xcd_grid(n_queries, 256), 256, 0, st>>>(queries, pl.qorder, n_queries,
-                                                                             pl.qpts, 0);
+                                                                             pl.qpts, 0, nullptr, 0, nullptr);
         O3DML_LAUNCH_CHECK();
         qkeys = pl.skeys;
         bshift = batch_bits == 0 ? 32 : 3 * cell_bits;

@@ -1,6 +1,8 @@
 """Host-side plumbing shared by the op wrappers: device placement, streams,
 workspaces and row-split handling.  PyTorch is used only for device memory and
 streams; every computation runs in libo3dml_amd.so."""
+from collections import OrderedDict
+
 import numpy as np
 import torch
 
@@ -31,18 +33,39 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
+_SMALL_CACHE = OrderedDict()  # (device, dtype, shape, bytes) -> device tensor
+_SMALL_CACHE_MAX = 64
+_SMALL_NUMEL = 4096
+
+
 def to_dev(t, device, dtype=None):
     """Contiguous copy (or view) of t on device with dtype.  Host data goes
     through a pinned staging copy and a non-blocking transfer on the current
     stream (torch's caching host allocator keeps the staging buffer alive until
     the copy has run), so row splits and other small host arrays do not
-    synchronise the stream with the host."""
+    synchronise the stream with the host.  Small host integer arrays (row
+    splits, table splits: the same few values call after call) are kept on the
+    device in a small LRU cache keyed by their bytes, so a repeated batch
+    layout costs no transfer at all; the ops only ever read these tensors."""
     if not isinstance(t, torch.Tensor):
         t = torch.as_tensor(np.asarray(t))
     if dtype is not None and t.dtype != dtype:
         t = t.to(dtype)
     if t.device.type == "cpu" and torch.device(device).type == "cuda":
-        return t.contiguous().pin_memory().to(device, non_blocking=True)
+        t = t.contiguous()
+        if (t.numel() <= _SMALL_NUMEL and t.dtype in (torch.int32, torch.int64) and not t.requires_grad
+                and not torch.cuda.is_current_stream_capturing()):
+            key = (str(torch.device(device)), t.dtype, tuple(t.shape), t.numpy().tobytes())
+            hit = _SMALL_CACHE.get(key)
+            if hit is not None:
+                _SMALL_CACHE.move_to_end(key)
+                return hit
+            d = t.pin_memory().to(device, non_blocking=True)
+            _SMALL_CACHE[key] = d
+            if len(_SMALL_CACHE) > _SMALL_CACHE_MAX:
+                _SMALL_CACHE.popitem(last=False)
+            return d
+        return t.pin_memory().to(device, non_blocking=True)
     return t.to(device, non_blocking=False).contiguous()
 
 
