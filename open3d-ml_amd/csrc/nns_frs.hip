@@ -158,8 +158,9 @@ __device__ __forceinline__ void bucket_table(const uint32_t* __restrict__ cs, co
 //         neighbours go to temp row qid, the full count to counts[qid]; ids of
 //         queries with more than kRowCap neighbours are listed in `over` for
 //         a MODE 1 re-run.  qkeys >> bshift is the query's batch item.
-// MODE 1: the queries of qpts[0 .. *m_dev) (one per wave) written straight
-//         into the final rows at rs[qid].
+// MODE 1: the listed queries over[0 .. *m_dev) (one per wave; qpts is then
+//         the raw [M, 3] query array) written straight into the final rows
+//         at rs[qid].
 #ifndef O3DML_FRS_NUM_SGPR
 #define O3DML_FRS_NUM_SGPR 80  // <= 80 SGPRs keep 8 waves per SIMD (the 800-entry SGPR file)
 #endif
@@ -210,7 +211,13 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
         int64_t row = 0;  // MODE 1: the query's final row start
         uint32_t pbase = 0;  // REL16: first point id of the query's batch item
         if (valid) {
-            q4 = qpts[t];
+            if constexpr (MODE == 0) {
+                q4 = qpts[t];
+            } else {  // qpts = the raw query array [M, 3], over = the listed query ids
+                const uint32_t id = over[t];
+                const float* qp = reinterpret_cast<const float*>(qpts) + 3 * static_cast<int64_t>(id);
+                q4 = make_float4(qp[0], qp[1], qp[2], __uint_as_float(id));
+            }
             const uint32_t qid = __float_as_uint(q4.w);
             const int b = qkeys ? (bshift >= 32 ? 0 : static_cast<int>(qkeys[t] >> bshift)) : batch_of(qid, qrs, nb);
             if constexpr (REL16) pbase = static_cast<uint32_t>(prs[b]);
@@ -459,17 +466,6 @@ __global__ void __launch_bounds__(256) group_rows_copy_kernel(int64_t m, const u
     }
 }
 
-// Overflow re-run input: the listed queries (ids) as (x, y, z, id).
-__global__ void gather_over_kernel(const float* __restrict__ queries, const uint32_t* __restrict__ over,
-                                   const int64_t* __restrict__ n_over, float4* __restrict__ out) {
-    const int64_t n = *n_over;
-    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
-         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t q = over[i];
-        out[i] = make_float4(queries[3 * q], queries[3 * q + 1], queries[3 * q + 2], __uint_as_float(over[i]));
-    }
-}
-
 // Query order: (batch, Morton code of the query's r-cell) — the lowest Morton
 // level is the octant of the Open3D 2r-cell, so queries with identical visit
 // lists (one group) are adjacent, and consecutive chunks are spatial
@@ -662,7 +658,6 @@ struct FrsPlan {
     int64_t* scalars;  // [0] overflow count
     float4* pts;       // [N + 1] points in Open3D bucket order + a far sentinel
     float4* qpts;      // [M] queries in (batch, Morton) order
-    float4* pts_over;  // [M] overflow queries
     uint32_t* keys;    // [M]
     uint32_t* skeys;   // [M]
     uint32_t* qorder;  // [M]
@@ -677,7 +672,6 @@ static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m, bool dist) {
     p.scalars = ws.take<int64_t>(4);
     p.pts = ws.take<float4>(n + 1);  // + far sentinel
     p.qpts = ws.take<float4>(m);
-    p.pts_over = ws.take<float4>(m);
     p.keys = ws.take<uint32_t>(m);
     p.skeys = ws.take<uint32_t>(m);
     p.qorder = ws.take<uint32_t>(m);
@@ -701,7 +695,7 @@ static bool rel16_rows(int64_t n_batch, const int64_t* prs_host) {
 }
 
 static size_t plan_bytes(int64_t n, int64_t m) {
-    return ws_bytes<int64_t>(4) + ws_bytes<float4>(n + 1) + 2 * ws_bytes<float4>(m) + 3 * ws_bytes<uint32_t>(m) +
+    return ws_bytes<int64_t>(4) + ws_bytes<float4>(n + 1) + ws_bytes<float4>(m) + 3 * ws_bytes<uint32_t>(m) +
            2 * ws_bytes<uint32_t>(m) + 2 * ws_bytes<uint32_t>(m * kRowCap);
 }
 
@@ -835,21 +829,19 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
     // rows longer than kRowCap: re-run those queries straight into the final
     // rows; the overflow count stays on the device (no host round trip), so a
     // fixed grid strides over however many there are (usually none)
-    const unsigned go = static_cast<unsigned>(std::min<int64_t>(n_queries, 1024));
-    gather_over_kernel<<<stream_grid(std::min<int64_t>(n_queries, 1 << 16), 256), 256, 0, st>>>(
-            queries, pl.over, pl.scalars, pl.pts_over);
-    O3DML_LAUNCH_CHECK();
+    const unsigned go = static_cast<unsigned>(std::min<int64_t>(n_queries, 256));
+    const float4* qraw = reinterpret_cast<const float4*>(queries);  // MODE 1 reads [M, 3] via the over list
     if (index_bits == 32)
         launch_group<1, int32_t>(metric, ignore_query_point != 0, dist != nullptr, false, st, go, pl.pts,
-                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.pts_over, nullptr, 32, 0,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, 32, 0,
                                  pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
-                                 points_row_splits, nullptr, nullptr, nullptr, nullptr, nullptr, rs,
+                                 points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
                                  static_cast<int32_t*>(neighbors_index), dist);
     else
         launch_group<1, int64_t>(metric, ignore_query_point != 0, dist != nullptr, false, st, go, pl.pts,
-                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.pts_over, nullptr, 32, 0,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, 32, 0,
                                  pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
-                                 points_row_splits, nullptr, nullptr, nullptr, nullptr, nullptr, rs,
+                                 points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
                                  static_cast<int64_t*>(neighbors_index), dist);
     O3DML_GUARD_END
 }
