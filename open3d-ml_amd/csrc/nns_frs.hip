@@ -135,6 +135,13 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
 }
 
+// popcount(x) + acc in one v_bcnt_u32_b32 (its second operand is added)
+__device__ __forceinline__ uint32_t bcnt_add(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t rdlane(int v, uint32_t lane) {
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(v, static_cast<int>(lane)));
 }
@@ -329,7 +336,10 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                     for (int u = 0; u < kStreamU; ++u) {
                         const bool keep = box_dist<METRIC>(c[u], lx, ly, lz, hx, hy, hz) <= thr;
                         const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
-                        if (keep) cand[nc + mbcnt64(km)] = c[u];
+                        if (keep)
+                            cand[__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(km >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(km),
+                                                                                     static_cast<uint32_t>(nc)))] = c[u];
                         nc += __popcll(km);
                     }
                     f0 += 64 * kStreamU;
@@ -349,7 +359,8 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                     const uint32_t mlo = static_cast<uint32_t>(bal) & gm_lo;
                     const uint32_t mhi = static_cast<uint32_t>(bal >> 32) & gm_hi;
                     if (hit) {
-                        const uint32_t pos = cnt + __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, 0u));
+                        // mbcnt's accumulator operand adds the running count for free
+                        const uint32_t pos = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cnt));
                         if constexpr (MODE == 0) {
                             // rows longer than kRowCap are re-run (MODE 1), so their
                             // temp row may take anything in its last slot
@@ -365,7 +376,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                             if constexpr (DIST) out_dist[mrow + pos] = d;
                         }
                     }
-                    cnt += __popc(mlo) + __popc(mhi);
+                    cnt = bcnt_add(mhi, bcnt_add(mlo, cnt));
                 };
                 int e0 = 0;
                 for (; e0 + 4 * S <= ncp; e0 += 4 * S) {
