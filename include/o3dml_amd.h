@@ -85,6 +85,22 @@ int o3dml_fixed_radius_search_fill(const float* points, int64_t n_points, const 
                                    int metric, int ignore_query_point, int self_search, int with_distances,
                                    const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
                                    float* neighbors_distance, void* workspace, size_t workspace_bytes, void* stream);
+/* _fill into caller buffers of `capacity` entries allocated before the total
+ * is known (capacity < 0: unbounded = _fill).  When neighbors_row_splits[M] >
+ * capacity nothing is written; the caller reads the total and re-runs _fill.
+ * Lets the host queue the fill before its read of the total (no idle GPU
+ * while the host waits).  Extension: Open3D's op (outside this repository's
+ * reference tree) reads the total before it allocates the outputs. */
+int o3dml_fixed_radius_search_fill_bounded(const float* points, int64_t n_points, const float* queries,
+                                           int64_t n_queries, float radius, int64_t n_batch,
+                                           const int64_t* points_row_splits, const int64_t* queries_row_splits,
+                                           const int64_t* points_row_splits_host,
+                                           const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
+                                           const uint32_t* hash_table_cell_splits, int metric,
+                                           int ignore_query_point, int self_search, int with_distances,
+                                           const int64_t* neighbors_row_splits, int index_bits,
+                                           void* neighbors_index, float* neighbors_distance, int64_t capacity,
+                                           void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- kNN: replaces open3d.ml.torch.ops.knn_search / layers.KNNSearch
  * (ml3d/torch/models/point_transformer.py:724-729) and

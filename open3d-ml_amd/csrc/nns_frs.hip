@@ -188,14 +188,17 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                  const uint32_t* __restrict__ hts, const int64_t* __restrict__ prs,
                  uint32_t* __restrict__ counts, uint32_t* __restrict__ tidx,
                  float* __restrict__ tdist, uint32_t* __restrict__ over, int64_t* __restrict__ n_over,
-                 const int64_t* __restrict__ rs, TIdx* __restrict__ out_idx, float* __restrict__ out_dist) {
+                 const int64_t* __restrict__ rs, TIdx* __restrict__ out_idx, float* __restrict__ out_dist,
+                 const int64_t* __restrict__ total, int64_t cap) {
     __shared__ float4 cand[kCandCap];
     __shared__ float4 qsh[64];
     __shared__ int64_t qrow[MODE == 0 ? 1 : 64];  // MODE 0: the row is the query id (qsh .w)
     const int lane = threadIdx.x;
     const float inf = __builtin_huge_valf();
     const float4 far = make_float4(inf, inf, inf, 0.f);  // never within any radius of a finite query
-    const int64_t m = m_dev ? *m_dev : m_host;
+    // MODE 1 of a bounded fill whose rows do not fit the caller's capacity:
+    // nothing is written (the caller re-runs the fill with exact buffers)
+    const int64_t m = MODE == 1 && cap >= 0 && *total > cap ? 0 : (m_dev ? *m_dev : m_host);
     const int64_t nchunks = MODE == 0 ? (m + 63) >> 6 : m;  // MODE 1: one query per wave
     // buffer resource over pts[0 .. n_pts] when its byte size fits the 32-bit range
     const bool pts_rsrc_ok = n_pts < 0x0FFFFFFFu;
@@ -425,7 +428,9 @@ __global__ void __launch_bounds__(256) group_rows_copy_kernel(int64_t m, const u
                                                               const int64_t* __restrict__ prs, int nb,
                                                               const uint32_t* __restrict__ tidx,
                                                               const float* __restrict__ tdist,
-                                                              TIdx* __restrict__ idx, float* __restrict__ dist) {
+                                                              TIdx* __restrict__ idx, float* __restrict__ dist,
+                                                              int64_t cap) {
+    if (cap >= 0 && rs[m] > cap) return;  // bounded fill, rows do not fit: write nothing
     const int lane = threadIdx.x & 63;
     const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
@@ -632,11 +637,12 @@ static void launch_group(int metric, bool ignore, bool with_dist, bool rel16, hi
                          const uint32_t* qkeys, int bshift, int64_t m, const int64_t* m_dev, float r, float inv,
                          float thr, int nb, const int64_t* qrs, const uint32_t* hts, const int64_t* prs,
                          uint32_t* counts, uint32_t* tidx, float* tdist, uint32_t* over, int64_t* n_over,
-                         const int64_t* rs, TIdx* idx, float* dist) {
+                         const int64_t* rs, TIdx* idx, float* dist, const int64_t* total = nullptr,
+                         int64_t cap = -1) {
 #define O3DML_GRP(M, I, D, R)                                                                                   \
     frs_group_kernel<M, I, D, MODE, TIdx, R><<<grid, 64, 0, st>>>(pts, n_pts, cs, qpts, qkeys, bshift, m, m_dev,  \
                                                                    r, inv, thr, nb, qrs, hts, prs, counts, tidx,  \
-                                                                   tdist, over, n_over, rs, idx, dist)
+                                                                   tdist, over, n_over, rs, idx, dist, total, cap)
 #define O3DML_GRP_R(M, I, D)                                  \
     do {                                                      \
         if (MODE == 0 && rel16)                               \
@@ -802,6 +808,20 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
                                              const int64_t* neighbors_row_splits, int index_bits,
                                              void* neighbors_index, float* neighbors_distance, void* workspace,
                                              size_t workspace_bytes, void* stream) {
+    return o3dml_fixed_radius_search_fill_bounded(
+            points, n_points, queries, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
+            points_row_splits_host, hash_table_splits, hash_table_index, hash_table_cell_splits, metric,
+            ignore_query_point, self_search, with_distances, neighbors_row_splits, index_bits, neighbors_index,
+            neighbors_distance, -1, workspace, workspace_bytes, stream);
+}
+
+O3DML_API int o3dml_fixed_radius_search_fill_bounded(
+        const float* points, int64_t n_points, const float* queries, int64_t n_queries, float radius,
+        int64_t n_batch, const int64_t* points_row_splits, const int64_t* queries_row_splits,
+        const int64_t* points_row_splits_host, const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
+        const uint32_t* hash_table_cell_splits, int metric, int ignore_query_point, int self_search,
+        int with_distances, const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
+        float* neighbors_distance, int64_t capacity, void* workspace, size_t workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
     (void)points;
     (void)hash_table_index;
@@ -823,7 +843,7 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
 #define O3DML_GCOPY3(D, R, T)                                                                                   \
     group_rows_copy_kernel<D, R, T><<<gc, 256, 0, st>>>(n_queries, pl.counts, rs, queries_row_splits,          \
                                                         points_row_splits, (int)n_batch, pl.tidx, pl.tdist,    \
-                                                        static_cast<T*>(neighbors_index), dist)
+                                                        static_cast<T*>(neighbors_index), dist, capacity)
 #define O3DML_GCOPY(T)                                                                                          \
     do {                                                                                                        \
         if (dist) {                                                                                             \
@@ -847,12 +867,12 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
                                  static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, 32, 0,
                                  pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
                                  points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
-                                 static_cast<int32_t*>(neighbors_index), dist);
+                                 static_cast<int32_t*>(neighbors_index), dist, rs + n_queries, capacity);
     else
         launch_group<1, int64_t>(metric, ignore_query_point != 0, dist != nullptr, false, st, go, pl.pts,
                                  static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, 32, 0,
                                  pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
                                  points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
-                                 static_cast<int64_t*>(neighbors_index), dist);
+                                 static_cast<int64_t*>(neighbors_index), dist, rs + n_queries, capacity);
     O3DML_GUARD_END
 }

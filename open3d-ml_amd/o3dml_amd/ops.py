@@ -106,14 +106,62 @@ def _frs_count(points, queries, radius, points_row_splits, queries_row_splits, h
     return rs, (common, ws, st, dev, (pts, qry, prs_d, qrs_d, hts_d, hti_d, hcs_d), prs, bool(return_distances))
 
 
-def _frs_fill(rs, state, total, index_dtype):
+def _frs_fill(rs, state, total, index_dtype, bounded=False):
+    """Phase 2.  bounded: `total` is only a capacity guess made before the
+    real total is read — the library writes nothing when the rows do not fit
+    (o3dml_fixed_radius_search_fill_bounded)."""
     common, ws, st, dev, _keep, _prs, with_dist = state
     bits = index_bits(index_dtype)
     idx = torch.empty(total, dtype=torch.int32 if bits == 32 else torch.int64, device=dev)
     dist = torch.empty(total if with_dist else 0, dtype=torch.float32, device=dev)
-    _lib.call("o3dml_fixed_radius_search_fill", *common, ptr(rs), bits, ptr(idx), ptr(dist) if with_dist else None,
-              ptr(ws), ws.numel(), st)
+    if bounded:
+        _lib.call("o3dml_fixed_radius_search_fill_bounded", *common, ptr(rs), bits, ptr(idx),
+                  ptr(dist) if with_dist else None, total, ptr(ws), ws.numel(), st)
+    else:
+        _lib.call("o3dml_fixed_radius_search_fill", *common, ptr(rs), bits, ptr(idx),
+                  ptr(dist) if with_dist else None, ptr(ws), ws.numel(), st)
     return idx, dist
+
+
+# Neighbours per query of the last search per (radius, metric): the capacity
+# guess that lets the fill be queued before the host reads the total, so the
+# GPU does not idle through that read.  A guess that proves too small costs
+# one more (exact) fill; the rows are always the exact ones.
+_FRS_DENSITY = {}
+
+
+def _frs_count_fill(rs, state, key, m, index_dtype, extra=None):
+    """Fill with the total read after the (bounded, speculative) fill when a
+    density guess exists, else read first.  extra: more device scalars read
+    in the same host transfer.  Returns (idx, dist, host values)."""
+    guess = _FRS_DENSITY.get(key)
+    # the totals go to pinned host memory right behind the count; the host
+    # waits for that copy only, not for the fill queued after it
+    vals_dev = torch.stack([rs[-1]] + list(extra)) if extra else rs[-1:]
+    host = torch.empty(vals_dev.shape, dtype=vals_dev.dtype, pin_memory=True)
+    host.copy_(vals_dev, non_blocking=True)
+    ready = torch.cuda.Event()
+    ready.record(torch.cuda.current_stream(rs.device))
+    if guess is None or m == 0:
+        ready.synchronize()
+        vals = host.tolist()
+        idx, dist = _frs_fill(rs, state, int(vals[0]), index_dtype)
+    else:
+        cap = int(m * guess * 1.0625) + 1024
+        idx, dist = _frs_fill(rs, state, cap, index_dtype, bounded=True)
+        ready.synchronize()
+        vals = host.tolist()
+        total = int(vals[0])
+        if total <= cap:
+            idx = idx[:total]
+            dist = dist[:total] if dist.numel() else dist
+        else:
+            idx, dist = _frs_fill(rs, state, total, index_dtype)
+    if m > 0:
+        _FRS_DENSITY[key] = int(vals[0]) / m
+        if len(_FRS_DENSITY) > 64:
+            _FRS_DENSITY.pop(next(iter(_FRS_DENSITY)))
+    return idx, dist, vals
 
 
 def fixed_radius_search(points, queries, radius, points_row_splits=None, queries_row_splits=None,
@@ -129,7 +177,7 @@ def fixed_radius_search(points, queries, radius, points_row_splits=None, queries
     index_bits(index_dtype)
     rs, state = _frs_count(points, queries, radius, points_row_splits, queries_row_splits, hash_table_splits,
                            hash_table_index, hash_table_cell_splits, metric, ignore_query_point, return_distances)
-    idx, dist = _frs_fill(rs, state, int(rs[-1].item()), index_dtype)
+    idx, dist, _ = _frs_count_fill(rs, state, (scalar(radius), metric_code(metric)), queries.shape[0], index_dtype)
     return FixedRadiusSearchResult(back_to(idx, points), back_to(rs, points), back_to(dist, points))
 
 
@@ -146,9 +194,10 @@ def fixed_radius_search_dense(points, queries, radius, points_row_splits, querie
     m = queries.shape[0]
     if m == 0:
         return torch.zeros((0, 0), dtype=torch.int32, device=rs.device)
-    tw = torch.stack([rs[-1], (rs[1:] - rs[:-1]).max()]).cpu()
-    total, width = int(tw[0]), int(tw[1])
-    idx, _ = _frs_fill(rs, state, total, torch.int32)
+    # the total and the width in one host read, after the fill is queued
+    idx, _, (_total, width) = _frs_count_fill(rs, state, (scalar(radius), -1), m, torch.int32,
+                                              extra=[(rs[1:] - rs[:-1]).max()])
+    width = int(width)
     return ragged_to_dense(idx.reshape(-1, 1), rs, width,
                            torch.tensor([points.shape[0]], dtype=torch.int32)).squeeze(2)
 

@@ -170,6 +170,35 @@ def test_frs_temp_row_widths(cuda, sizes):
             assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
 
 
+@pytest.mark.parametrize("guess", [None, 0.0, 1e3])
+def test_frs_speculative_capacity(cuda, guess):
+    """The fill is queued into buffers sized from the last search's density
+    before the host reads the total: no guess (read first), a guess far too
+    small (bounded fill writes nothing, exact re-run) and far too large
+    (sliced rows) all give the oracle's rows, plain and dense."""
+    from o3dml_amd import ops
+    pts = _cloud(20000, 31)
+    rs = np.array([0, 12000, 20000], np.int64)
+    t = torch.from_numpy(pts).to(cuda)
+    r = 0.05
+    for key in ((float(r), 1), (float(r), -1)):
+        ops._FRS_DENSITY.pop(key, None)
+        if guess is not None:
+            ops._FRS_DENSITY[key] = guess
+    res = ops.fixed_radius_search(t, t, r, torch.from_numpy(rs), torch.from_numpy(rs), return_distances=True)
+    oi, ors, od = O.fixed_radius_search(pts, pts, r, rs, rs, return_distances=True)
+    assert res.neighbors_index.numel() == len(oi)
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+    assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
+    dense = ops.fixed_radius_search_dense(t, t, r, torch.from_numpy(rs), torch.from_numpy(rs)).cpu().numpy()
+    width = int(np.diff(ors).max())
+    assert dense.shape == (len(pts), width)
+    for q in (0, 777, 12000, 19999):
+        row = oi[ors[q]:ors[q + 1]]
+        assert np.array_equal(dense[q, :len(row)], row) and (dense[q, len(row):] == len(pts)).all()
+
+
 @pytest.mark.parametrize("n,rs_mid", [(300000, None), (90000, [5, 5, 40000])])
 def test_hash_table_paths(cuda, n, rs_mid):
     """Both hash-table builders against the oracle: tables of > 4,096 bins in a
