@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--pointpillars-steps", type=int, default=5,
                     help="C5 PointPillars DDP training steps timed on every rank (0: skip)")
     ap.add_argument("--sparse-conv-reps", type=int, default=10, help="C4 sparse-conv forwards timed (0: skip)")
+    ap.add_argument("--sweep-reps", type=int, default=5,
+                    help="C1 size sweep (one scene of N = 2^16 .. 2^24 pts at constant density): calls timed (0: skip)")
     return ap.parse_args()
 
 
@@ -70,6 +72,34 @@ def make_batch(rank, scenes, dev):
 
 
 KERNELS = ("frs_group_search", "frs_group_rows")
+
+
+def c1_sweep(dev, reps):
+    """SURVEY §8(d) C1 sweep: one scene of N U[0,1)^3 points, N = 2^16 .. 2^24,
+    r = 0.05 (65536/N)^(1/3) (constant neighbour density), one
+    layers.FixedRadiusSearch forward per call (hash build + search + fill)."""
+    from o3dml_amd import layers
+    nns = layers.FixedRadiusSearch()
+    out = {}
+    for lg in (16, 18, 20, 22, 24):
+        n = 1 << lg
+        pts = torch.from_numpy(np.random.default_rng(lg).random((n, 3), dtype=np.float32)).to(dev)
+        rs = torch.tensor([0, n], dtype=torch.int64)
+        r = 0.05 * (65536.0 / n) ** (1.0 / 3.0)
+        for _ in range(2):
+            res = nns(pts, pts, r, rs, rs)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            res = nns(pts, pts, r, rs, rs)
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        pairs = int(res.neighbors_row_splits[-1].item())
+        out[str(n)] = {"ms": round(ms, 4), "Mpoints_s": round(n / ms / 1e3, 2), "radius": round(r, 6),
+                       "mean_neighbors": round(pairs / n, 3)}
+        del pts, res
+    torch.cuda.empty_cache()
+    return out
 
 
 def kernel_profile(step, n_queries, pairs, reps):
@@ -491,6 +521,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
+        if world == 1 and args.sweep_reps > 0:
+            out["c1_sweep"] = c1_sweep(dev, args.sweep_reps)
         if world == 1 and args.sparse_conv_reps > 0:
             out["sparse_conv"] = sparse_conv_bench(dev, args.sparse_conv_reps)
         if pp is not None:

@@ -355,7 +355,10 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 if (nc + lane < ncp) cand[nc + lane] = far;
                 __syncthreads();
 #if O3DML_DIAG == 0
-                auto test = [&](const float4& p) {
+                auto test = [&](float4 p) {
+                    // w pinned here: the candidate comes in one ds_read_b128 (4 LDS
+                    // cycles per wave) instead of ds_read_b96 (8) + a b32 for w
+                    asm volatile("" : "+v"(p.w));
                     const float d = dist_metric<METRIC>(p.x, p.y, p.z, mq.x, mq.y, mq.z);
                     const bool hit = d <= thr && !(IGNORE && p.x == mq.x && p.y == mq.y && p.z == mq.z);
                     const uint64_t bal = __builtin_amdgcn_ballot_w64(hit);
@@ -621,9 +624,27 @@ __global__ void __launch_bounds__(256) self_query_order_kernel(const float4* __r
     }
 }
 
-static bool frs_self_order() {
-    const char* e = std::getenv("O3DML_FRS_SELF_ORDER");  // "0": Morton-sort the queries of a self search too (A/B)
-    return !(e && e[0] == '0');
+// Self search queries in Open3D's bucket order (self_query_order_kernel) —
+// unless a batch item is so large that the hash order of its buckets, which
+// is spatially random, costs more in L2 misses than a Morton sort of the
+// queries (>= 2^22 points: search 6.19 -> 4.55 ms at 2^24 points, the sort
+// and query gather 0.9 ms; break-even at 2^22).  Ordering the buckets
+// spatially instead was measured and lost: ~63 % of the cells share their
+// bucket with another cell at Open3D's table size, and those are placed with
+// the bucket's first cell, off their own spatial position.
+#ifndef O3DML_FRS_SELF_ORDER_MAX
+#define O3DML_FRS_SELF_ORDER_MAX (int64_t(1) << 22)
+#endif
+static bool frs_self_order(int64_t n_batch, const int64_t* prs_host, int64_t n_points) {
+    const char* e = std::getenv("O3DML_FRS_SELF_ORDER");  // "0" never, "1" always (A/B)
+    if (e && e[0] == '0') return false;
+    if (e && e[0] == '1') return true;
+    int64_t mx = n_points / std::max<int64_t>(n_batch, 1);
+    if (prs_host) {
+        mx = 0;
+        for (int64_t b = 0; b < n_batch; ++b) mx = std::max(mx, prs_host[b + 1] - prs_host[b]);
+    }
+    return mx < O3DML_FRS_SELF_ORDER_MAX;
 }
 
 static unsigned group_grid(int64_t m, int queries_per_wave = 64) {
@@ -757,7 +778,7 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     gather_sorted_points_kernel<<<xcd_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points, pl.pts, 1,
                                                                         pl.scalars, 4, neighbors_row_splits);
     O3DML_LAUNCH_CHECK();
-    if (self_search && frs_self_order()) {
+    if (self_search && frs_self_order(n_batch, points_row_splits_host, n_points)) {
         // queries = points: Open3D's bucket order, octant groups made adjacent
         // inside each bucket — no sort of the queries at all
         self_query_order_kernel<<<static_cast<unsigned>(std::min<int64_t>(ceil_div(n_points, 64 * 4), 1 << 16)), 256,

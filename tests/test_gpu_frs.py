@@ -199,6 +199,25 @@ def test_frs_speculative_capacity(cuda, guess):
         assert np.array_equal(dense[q, :len(row)], row) and (dense[q, len(row):] == len(pts)).all()
 
 
+@pytest.mark.parametrize("mode", ["1", "0"])
+def test_frs_query_order(cuda, mode, monkeypatch):
+    """Self search with the queries in Open3D's bucket order (the default for
+    items below 2^22 points) and with the Morton-sorted queries of the general
+    path (the default above), each forced on small items with empty and
+    one-point items: the rows stay the oracle's."""
+    from o3dml_amd import ops
+    monkeypatch.setenv("O3DML_FRS_SELF_ORDER", mode)
+    sizes = [30000, 0, 1, 45000]
+    rs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    pts = np.concatenate([_cloud(n, 40 + i) for i, n in enumerate(sizes) if n])
+    t = torch.from_numpy(pts).to(cuda)
+    res = ops.fixed_radius_search(t, t, 0.03, torch.from_numpy(rs), torch.from_numpy(rs), return_distances=True)
+    oi, ors, od = O.fixed_radius_search(pts, pts, 0.03, rs, rs, return_distances=True)
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+    assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
+
+
 @pytest.mark.parametrize("n,rs_mid", [(300000, None), (90000, [5, 5, 40000])])
 def test_hash_table_paths(cuda, n, rs_mid):
     """Both hash-table builders against the oracle: tables of > 4,096 bins in a

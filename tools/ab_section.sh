@@ -10,7 +10,7 @@ case "$sec" in
   pp) A="--pointpillars-steps 10"; K=pointpillars; F=ms_per_step;;
   sc) A="--sparse-conv-reps 20"; K=sparse_conv; F=ms_layer;;
 esac
-B="--steps 1 --warmup 1 --scenes 1 --no-cpu-baseline --randla-frames 0 --sparse-conv-reps 0 --kpconv-steps 0 --pointpillars-steps 0"
+B="--steps 1 --warmup 1 --scenes 1 --no-cpu-baseline --randla-frames 0 --sparse-conv-reps 0 --kpconv-steps 0 --pointpillars-steps 0 --sweep-reps 0"
 for rep in 1 2; do
   for lib in "$@"; do
     O3DML_AMD_LIB=$PWD/open3d-ml_amd/$lib/libo3dml_amd.so timeout -k 10 300 python bench.py $B $A 2>/dev/null | \

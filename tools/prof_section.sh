@@ -6,7 +6,7 @@ R=$(pwd)
 OUT=$R/gpurun_out/${TAG:-sec}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-A="--steps 1 --warmup 1 --scenes 1 --no-cpu-baseline --randla-frames 0 --sparse-conv-reps 0 --kpconv-steps 0 --pointpillars-steps 0"
+A="--steps 1 --warmup 1 --scenes 1 --no-cpu-baseline --randla-frames 0 --sparse-conv-reps 0 --kpconv-steps 0 --pointpillars-steps 0 --sweep-reps 0"
 case "$SECTION" in
   randla) A="$A --randla-frames 3";;
   kpconv) A="$A --kpconv-steps 5";;

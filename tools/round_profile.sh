@@ -8,8 +8,8 @@ ROOTDIR=$(pwd)
 OUT=$ROOTDIR/gpurun_out/${TAG:-prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BARGS_X="--no-cpu-baseline --randla-frames 0 --sparse-conv-reps 0 --kpconv-steps 0 --pointpillars-steps 0"
-BARGS="--steps ${STEPS:-10} --warmup 3 --no-cpu-baseline --randla-frames 0 --sparse-conv-reps 0 --kpconv-steps 0 --pointpillars-steps 0"
+BARGS_X="--no-cpu-baseline --randla-frames 0 --sparse-conv-reps 0 --kpconv-steps 0 --pointpillars-steps 0 --sweep-reps 0"
+BARGS="--steps ${STEPS:-10} --warmup 3 --no-cpu-baseline --randla-frames 0 --sparse-conv-reps 0 --kpconv-steps 0 --pointpillars-steps 0 --sweep-reps 0"
 timeout -k 10 300 python bench.py $BARGS > "$OUT/bench.log" 2>&1 || { echo "bench rc=$?"; exit 1; }
 tail -1 "$OUT/bench.log" | cut -c1-200
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv \
