@@ -117,16 +117,18 @@ __device__ __forceinline__ float wave_max_f(float v) { return -wave_min_f(-v); }
 template <int METRIC>
 __device__ __forceinline__ float box_dist(const float4& p, float lx, float ly, float lz, float hx, float hy,
                                           float hz) {
-    const float gx = fmaxf(fmaxf(lx - p.x, p.x - hx), 0.f);
-    const float gy = fmaxf(fmaxf(ly - p.y, p.y - hy), 0.f);
-    const float gz = fmaxf(fmaxf(lz - p.z, p.z - hz), 0.f);
+    // signed gap to the box: p minus p clamped into [lo, hi] (one v_med3 each)
+    const float gx = p.x - __builtin_amdgcn_fmed3f(p.x, lx, hx);
+    const float gy = p.y - __builtin_amdgcn_fmed3f(p.y, ly, hy);
+    const float gz = p.z - __builtin_amdgcn_fmed3f(p.z, lz, hz);
     if constexpr (METRIC == kL2) {
         return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
     } else if constexpr (METRIC == kL1) {
-        return (gx + gy) + gz;
+        return (fabsf(gx) + fabsf(gy)) + fabsf(gz);
     } else {
-        const float m = gx > gy ? gx : gy;
-        return m > gz ? m : gz;
+        const float ax = fabsf(gx), ay = fabsf(gy), az = fabsf(gz);
+        const float m = ax > ay ? ax : ay;
+        return m > az ? m : az;
     }
 }
 
