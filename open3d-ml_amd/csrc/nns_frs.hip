@@ -148,19 +148,11 @@ __device__ __forceinline__ uint32_t rdlane(int v, uint32_t lane) {
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(v, static_cast<int>(lane)));
 }
 
-// Lanes K..8 of the group's bucket table (see frs_group_kernel): flat start
-// and start - flat start of each deduplicated bucket, written with v_writelane.
+// lb[k] (uniform) into lane k for k = K..8
 template <int K>
-__device__ __forceinline__ void bucket_table(const uint32_t* __restrict__ cs, const uint32_t* lb, int& vpre,
-                                             int& vdel, uint32_t& total) {
-    if constexpr (K < 9) {
-        const uint32_t s0 = cs[lb[K]];
-        const uint32_t len = (K == 0 || lb[K] != lb[K > 0 ? K - 1 : 0]) ? cs[lb[K] + 1] - s0 : 0u;
-        vpre = write_lane<K>(vpre, static_cast<int>(total));
-        vdel = write_lane<K>(vdel, static_cast<int>(s0 - total));
-        total += len;
-        bucket_table<K + 1>(cs, lb, vpre, vdel, total);
-    }
+__device__ __forceinline__ int bin_lanes(int v, const uint32_t* lb) {
+    if constexpr (K < 9) return bin_lanes<K + 1>(write_lane<K>(v, static_cast<int>(lb[K])), lb);
+    return v;
 }
 
 // MODE 0: every query of the (sorted) query array; its first kRowCap
@@ -278,46 +270,72 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
             uint32_t cnt = 0;  // neighbours of query g so far (uniform over its S lanes)
             const uint64_t gmask = ls == 6 ? ~0ull : (((1ull << S) - 1ull) << (g << ls));
             const uint32_t gm_lo = static_cast<uint32_t>(gmask), gm_hi = static_cast<uint32_t>(gmask >> 32);
-            // Bucket table of the group, one bucket per lane: lane k < 9 holds
-            // the flat start pre[k] of bucket k in the concatenated stream and
-            // delta[k] = its start in pts - pre[k]; lane 9 holds the stream
-            // length, lanes > 9 hold UINT_MAX.  Looked up with v_readlane by
-            // the uniform stream cursor.
-            int vpre = -1, vdel = 0;
-            uint32_t total = 0;
-            bucket_table<0>(cs, lb, vpre, vdel, total);
-            vpre = write_lane<9>(vpre, static_cast<int>(total));
+            // Bucket list of the group in visit order, empty and repeated bins
+            // dropped: lane j < nbk holds the start in pts and the length of the
+            // j-th bucket.  Built in parallel (lane k < 9 takes bin k: one pair
+            // of loads) and compacted through the candidate list, free here.
+            uint32_t vst, vlen;
+            int nbk;
+            {
+                const uint32_t vb = static_cast<uint32_t>(bin_lanes<0>(-1, lb));
+                uint32_t s0 = 0, e0 = 0;
+                if (lane < 9) {
+                    s0 = cs[vb];
+                    e0 = cs[vb + 1];
+                }
+                // the bins are sorted: a repeat sits right after its first copy
+                const uint32_t prev = static_cast<uint32_t>(
+                        __builtin_amdgcn_update_dpp(-1, static_cast<int>(vb), 0x111, 0xF, 0xF, false));  // row_shr:1
+                const bool live = lane < 9 && e0 > s0 && prev != vb;
+                const uint64_t km = __builtin_amdgcn_ballot_w64(live);
+                nbk = __popcll(km);
+                uint32_t* tab = reinterpret_cast<uint32_t*>(cand);
+                if (live) {
+                    const uint32_t j = mbcnt64(km);
+                    tab[j] = s0;
+                    tab[16 + j] = e0 - s0;
+                }
+                __syncthreads();
+                vst = lane < nbk ? tab[lane] : 0u;
+                vlen = lane < nbk ? tab[16 + lane] : 0u;
+                __syncthreads();
+            }
 #if O3DML_DIAG == 2
-            total = 0;  // diagnostics: grouping and bucket tables only, no streaming
+            nbk = 0;  // diagnostics: grouping and bucket tables only, no streaming
 #endif
             // stop filling while the next round (and the test padding) might not fit
             const int fill_lim = kCandCap - 64 * kStreamU - (S - 1);
-            // stream cursor: source index of this lane's point in the round of
-            // 64 starting at flat position fb (rounds are requested in order;
-            // lanes past the stream read the far sentinel pts[n_pts])
-            uint32_t kcur = 0;
-            auto round_src = [&](uint32_t fb) -> uint32_t {
-                uint32_t p1 = rdlane(vpre, kcur + 1);
-                while (p1 <= fb) p1 = rdlane(vpre, ++kcur + 1);  // kcur: bucket holding fb
-                const uint32_t f = fb + lane;
-                uint32_t dl = rdlane(vdel, kcur);
-                const uint32_t d1 = rdlane(vdel, kcur + 1);
-                dl = f >= p1 ? d1 : dl;  // no lane matches when p1 lies past the round
-                if (p1 < fb + 64) {      // p1 inside the round: later boundaries may be too (rare)
-                    for (uint32_t kk = kcur + 2;; ++kk) {
-                        const uint32_t pk = rdlane(vpre, kk);
-                        if (pk >= fb + 64) break;
-                        const uint32_t dk = rdlane(vdel, kk);
-                        dl = f >= pk ? dk : dl;
-                    }
+            // Stream cursor (uniform): bucket bk, boff of its entries consumed.  A
+            // round of 64 lanes takes the rest of bucket bk (lanes < t) and the
+            // head of bucket bk + 1, never more than two buckets; lanes past the
+            // group's buckets (or past bucket bk + 1) read the far sentinel.
+            int bk = 0;
+            uint32_t boff = 0;
+            auto round_src = [&]() -> uint32_t {
+                if (bk >= nbk) return n_pts;
+                const uint32_t st0 = rdlane(static_cast<int>(vst), bk) + boff;
+                const uint32_t t = rdlane(static_cast<int>(vlen), bk) - boff;
+                if (t > 64) {
+                    boff += 64;
+                    return st0 + lane;
                 }
-                return f < total ? f + dl : n_pts;
+                const uint32_t n1 = rdlane(static_cast<int>(vlen), bk + 1);  // 0 past the list
+                const uint32_t d1 = rdlane(static_cast<int>(vst), bk + 1) - t;
+                const uint32_t src = static_cast<uint32_t>(lane) < t ? st0 + lane : d1 + lane;
+                if (t + n1 <= 64) {
+                    bk += 2;
+                    boff = 0;
+                } else {
+                    bk += 1;
+                    boff = 64 - t;
+                }
+                return static_cast<uint32_t>(lane) < t + n1 ? src : n_pts;
             };
             // all addresses of a step first, then all its loads (in flight together)
-            auto load_step = [&](uint32_t fb, float4* c) {
+            auto load_step = [&](float4* c) {
                 uint32_t src[kStreamU];
 #pragma unroll
-                for (int u = 0; u < kStreamU; ++u) src[u] = round_src(fb + u * 64);
+                for (int u = 0; u < kStreamU; ++u) src[u] = round_src();
                 if (pts_rsrc_ok) {  // 16-B buffer loads: 32-bit offsets, never split by the compiler
 #pragma unroll
                     for (int u = 0; u < kStreamU; ++u)
@@ -328,15 +346,14 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                     for (int u = 0; u < kStreamU; ++u) c[u] = pts[src[u]];
                 }
             };
-            uint32_t f0 = 0;
             int nc = 0;
             while (true) {
                 // 1. fill the LDS list: steps of kStreamU x 64 loads, all in flight
                 //    (a software-pipelined variant that issued the next step before
                 //    filtering this one measured 8 % slower: more VGPRs, fewer waves)
-                while (f0 < total && nc <= fill_lim) {
+                while (bk < nbk && nc <= fill_lim) {
                     float4 c[kStreamU];
-                    load_step(f0, c);
+                    load_step(c);
 #pragma unroll
                     for (int u = 0; u < kStreamU; ++u) {
                         const bool keep = box_dist<METRIC>(c[u], lx, ly, lz, hx, hy, hz) <= thr;
@@ -347,7 +364,6 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                                                                                      static_cast<uint32_t>(nc)))] = c[u];
                         nc += __popcll(km);
                     }
-                    f0 += 64 * kStreamU;
                 }
                 // 2. pad to whole S-entry slices with the far point, then test the
                 //    list against the group's queries, in order (4 slices per
@@ -398,7 +414,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
 #endif
                 __syncthreads();
                 nc = 0;
-                if (f0 >= total) break;
+                if (bk >= nbk) break;
             }
             if constexpr (MODE == 0) {
                 if (g < ng && sl == 0) {
