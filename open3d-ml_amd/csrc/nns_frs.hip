@@ -80,6 +80,20 @@ __global__ void __launch_bounds__(256) gather_sorted_points_kernel(const float* 
 
 constexpr int kRowCap = 64;  // neighbours kept per query in the temp rows
 
+// Lane split of a group of ng queries: S = floor(64 / ng) in bits 0-7 and
+// M = ceil(65536 / S) in bits 8-31 (g = lane * M >> 16 = floor(lane / S)).
+struct LaneSplitTab {
+    uint32_t v[65];
+    constexpr LaneSplitTab() : v() {
+        for (int ng = 0; ng <= 64; ++ng) {
+            const uint32_t S = ng == 0 ? 64u : 64u / static_cast<uint32_t>(ng);
+            v[ng] = S | (((65536u + S - 1u) / S) << 8);
+        }
+    }
+};
+__constant__ constexpr LaneSplitTab kLaneSplitTab{};
+#define kLaneSplit kLaneSplitTab.v
+
 #ifndef O3DML_DIAG
 #define O3DML_DIAG 0  // 1: skip the candidate test loop, 2: also skip streaming (cost-split diagnostics)
 #endif
@@ -165,14 +179,14 @@ __device__ __forceinline__ int bin_lanes(int v, const uint32_t* lb) {
 #ifndef O3DML_FRS_NUM_SGPR
 #define O3DML_FRS_NUM_SGPR 80  // <= 80 SGPRs keep 8 waves per SIMD (the 800-entry SGPR file)
 #endif
+// 8 waves per SIMD asked of the register allocator (<= 64 VGPRs): the
+// search is VALU-issue bound and needs every wave (65 VGPRs -> 7 waves: +3 %).
+// Not with distances (those builds would spill VGPRs to scratch).
 #ifndef O3DML_FRS_WAVES
-#define O3DML_FRS_WAVES 0
+#define O3DML_FRS_WAVES 8
 #endif
-#if O3DML_FRS_WAVES > 0
-#define O3DML_FRS_ATTR __attribute__((amdgpu_num_sgpr(O3DML_FRS_NUM_SGPR), amdgpu_waves_per_eu(O3DML_FRS_WAVES, 8)))
-#else
-#define O3DML_FRS_ATTR __attribute__((amdgpu_num_sgpr(O3DML_FRS_NUM_SGPR)))
-#endif
+#define O3DML_FRS_ATTR \
+    __attribute__((amdgpu_num_sgpr(O3DML_FRS_NUM_SGPR), amdgpu_waves_per_eu(DIST ? 1 : O3DML_FRS_WAVES, 8)))
 template <int METRIC, bool IGNORE, bool DIST, int MODE, class TIdx, bool REL16>
 __global__ void __launch_bounds__(64) O3DML_FRS_ATTR
 frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t* __restrict__ cs,
@@ -256,10 +270,13 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
             const float hx = wave_max_f(same ? q4.x : -inf), hy = wave_max_f(same ? q4.y : -inf),
                         hz = wave_max_f(same ? q4.z : -inf);
             // lane -> (query g, slice s)
-            const int lg = ng <= 1 ? 0 : 32 - __builtin_clz(static_cast<uint32_t>(ng - 1));  // log2 G
-            const int ls = 6 - lg;                                                         // log2 S
-            const int S = 1 << ls;
-            const int g = lane >> ls, sl = lane & (S - 1);
+            // S = floor(64 / ng) lanes per query (not a power of two: 9 queries
+            // take 63 lanes, not 9 of 16 slots x 4); g = lane / S by the
+            // multiply-shift of the table, exact for lane < 64
+            const uint32_t split = kLaneSplit[ng];
+            const int S = static_cast<int>(split & 0xffu);
+            const int g = static_cast<int>((static_cast<uint32_t>(lane) * (split >> 8)) >> 16);
+            const int sl = lane - g * S;
             __syncthreads();
             float4 mq = far;  // lanes past the group test the far point: never a hit
             int64_t mrow = 0;
@@ -268,7 +285,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 mrow = MODE == 0 ? static_cast<int64_t>(__float_as_uint(mq.w)) : qrow[g];
             }
             uint32_t cnt = 0;  // neighbours of query g so far (uniform over its S lanes)
-            const uint64_t gmask = ls == 6 ? ~0ull : (((1ull << S) - 1ull) << (g << ls));
+            const uint64_t gmask = S == 64 ? ~0ull : (g < ng ? ((1ull << S) - 1ull) << (g * S) : 0ull);
             const uint32_t gm_lo = static_cast<uint32_t>(gmask), gm_hi = static_cast<uint32_t>(gmask >> 32);
             // Bucket list of the group in visit order, empty and repeated bins
             // dropped: lane j < nbk holds the start in pts and the length of the
@@ -369,7 +386,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 //    list against the group's queries, in order (4 slices per
                 //    step, then single slices); hits are ranked by ballot so every
                 //    row is written in canonical order
-                const int ncp = (nc + S - 1) & ~(S - 1);
+                const int ncp = nc + (S - 1 - (nc + S - 1) % S);  // nc rounded up to whole slices
                 if (nc + lane < ncp) cand[nc + lane] = far;
                 __syncthreads();
 #if O3DML_DIAG == 0

@@ -199,6 +199,31 @@ def test_frs_speculative_capacity(cuda, guess):
         assert np.array_equal(dense[q, :len(row)], row) and (dense[q, len(row):] == len(pts)).all()
 
 
+@pytest.mark.parametrize("metric", ["L2", "L1", "Linf"])
+def test_frs_group_sizes(cuda, metric):
+    """Tight clusters of 1..64 points (each one query group of that size:
+    floor(64 / size) lanes per query, sizes that are not powers of two
+    included) among uniform points, with ignore_query_point and distances:
+    rows equal the oracle's."""
+    from o3dml_amd import ops
+    rng = np.random.default_rng(7)
+    parts = [_cloud(5000, 8)]
+    for k in range(1, 65):
+        c = rng.random(3, dtype=np.float32) * 0.9 + 0.05
+        parts.append((c + rng.random((k, 3), dtype=np.float32) * 0.004).astype(np.float32))
+    pts = np.concatenate(parts)
+    rs = np.array([0, len(pts)], np.int64)
+    t = torch.from_numpy(pts).to(cuda)
+    for ignore in (False, True):
+        res = ops.fixed_radius_search(t, t, 0.06, torch.from_numpy(rs), torch.from_numpy(rs), metric=metric,
+                                      ignore_query_point=ignore, return_distances=True)
+        oi, ors, od = O.fixed_radius_search(pts, pts, 0.06, rs, rs, metric=metric, ignore_query_point=ignore,
+                                            return_distances=True)
+        assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+        assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+        assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
+
+
 @pytest.mark.parametrize("mode", ["1", "0"])
 def test_frs_query_order(cuda, mode, monkeypatch):
     """Self search with the queries in Open3D's bucket order (the default for
