@@ -210,6 +210,10 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
     const int64_t nchunks = MODE == 0 ? (m + 63) >> 6 : m;  // MODE 1: one query per wave
     // buffer resource over pts[0 .. n_pts] when its byte size fits the 32-bit range
     const bool pts_rsrc_ok = n_pts < 0x0FFFFFFFu;
+    // REL16 temp rows (2 B x kRowCap per query; REL16 implies they fit 2^31 B,
+    // rel16_rows) through a buffer resource: one VALU per hit for the address
+    const __amdgpu_buffer_rsrc_t rows_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            tidx, static_cast<short>(0), REL16 ? static_cast<int>(m * 2 * kRowCap) : 0, kBufferFlags);
     const __amdgpu_buffer_rsrc_t pts_rsrc = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float4*>(pts), static_cast<short>(0), static_cast<int>((n_pts + 1u) * 16u), kBufferFlags);
     // XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so with a grid
@@ -285,6 +289,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 mrow = MODE == 0 ? static_cast<int64_t>(__float_as_uint(mq.w)) : qrow[g];
             }
             uint32_t cnt = 0;  // neighbours of query g so far (uniform over its S lanes)
+            const uint32_t row_b = static_cast<uint32_t>(mrow) * (2u * kRowCap);  // REL16: byte offset of the row
             const uint64_t gmask = S == 64 ? ~0ull : (g < ng ? ((1ull << S) - 1ull) << (g * S) : 0ull);
             const uint32_t gm_lo = static_cast<uint32_t>(gmask), gm_hi = static_cast<uint32_t>(gmask >> 32);
             // Bucket list of the group in visit order, empty and repeated bins
@@ -375,6 +380,8 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                     for (int u = 0; u < kStreamU; ++u) {
                         const bool keep = box_dist<METRIC>(c[u], lx, ly, lz, hx, hy, hz) <= thr;
                         const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
+                        if constexpr (REL16)  // ids relative to the batch item, as the temp rows store them
+                            c[u].w = __uint_as_float(__float_as_uint(c[u].w) - gbase);
                         if (keep)
                             cand[__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(km >> 32),
                                                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(km),
@@ -407,8 +414,9 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                             // temp row may take anything in its last slot
                             const uint32_t ps = min(pos, static_cast<uint32_t>(kRowCap - 1));
                             if constexpr (REL16)  // 16-bit ids relative to the batch item: 128-B rows
-                                reinterpret_cast<uint16_t*>(tidx)[mrow * kRowCap + ps] =
-                                        static_cast<uint16_t>(__float_as_uint(p.w) - gbase);
+                                __builtin_amdgcn_raw_buffer_store_b16(
+                                        static_cast<unsigned short>(__float_as_uint(p.w)), rows_rsrc,
+                                        row_b + (ps << 1), 0, 0);
                             else
                                 tidx[mrow * kRowCap + ps] = __float_as_uint(p.w);
                             if constexpr (DIST) tdist[mrow * kRowCap + ps] = d;
@@ -760,8 +768,9 @@ static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m, bool dist) {
 #ifndef O3DML_FRS_REL16
 #define O3DML_FRS_REL16 1
 #endif
-static bool rel16_rows(int64_t n_batch, const int64_t* prs_host) {
+static bool rel16_rows(int64_t n_batch, const int64_t* prs_host, int64_t n_queries) {
     if (!prs_host || !O3DML_FRS_REL16) return false;
+    if (n_queries > 0x7FFFFFFF / (2 * kRowCap)) return false;  // the rows' buffer resource covers < 2^31 B
     for (int64_t b = 0; b < n_batch; ++b)
         if (prs_host[b + 1] - prs_host[b] > 65536) return false;
     return true;
@@ -843,7 +852,7 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     {
         TimedRegion tr("frs_group_search", st);
         launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0,
-                                 rel16_rows(n_batch, points_row_splits_host), st, group_grid(n_queries), pl.pts,
+                                 rel16_rows(n_batch, points_row_splits_host, n_queries), st, group_grid(n_queries), pl.pts,
                                  static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts, qkeys, bshift,
                                  n_queries, nullptr, radius, inv, thr, (int)n_batch, queries_row_splits,
                                  hash_table_splits, points_row_splits, pl.counts, pl.tidx, pl.tdist, pl.over,
@@ -895,7 +904,7 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
     {
         TimedRegion tr("frs_group_rows", st);
         const unsigned gc = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_queries, 256), 1 << 16)));
-        const bool rel16 = rel16_rows(n_batch, points_row_splits_host);
+        const bool rel16 = rel16_rows(n_batch, points_row_splits_host, n_queries);
 #define O3DML_GCOPY3(D, R, T)                                                                                   \
     group_rows_copy_kernel<D, R, T><<<gc, 256, 0, st>>>(n_queries, pl.counts, rs, queries_row_splits,          \
                                                         points_row_splits, (int)n_batch, pl.tidx, pl.tdist,    \
