@@ -354,11 +354,11 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 return static_cast<uint32_t>(lane) < t + n1 ? src : n_pts;
             };
             // all addresses of a step first, then all its loads (in flight together)
-            auto load_step = [&](float4* c) {
+            auto load_step = [&](float4* c, auto buf) {
                 uint32_t src[kStreamU];
 #pragma unroll
                 for (int u = 0; u < kStreamU; ++u) src[u] = round_src();
-                if (pts_rsrc_ok) {  // 16-B buffer loads: 32-bit offsets, never split by the compiler
+                if constexpr (decltype(buf)::value) {  // 16-B buffer loads: 32-bit offsets, never split
 #pragma unroll
                     for (int u = 0; u < kStreamU; ++u)
                         c[u] = __builtin_bit_cast(float4,
@@ -368,6 +368,9 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                     for (int u = 0; u < kStreamU; ++u) c[u] = pts[src[u]];
                 }
             };
+            // the stream + test loop, instantiated for buffer loads and (huge
+            // point sets) plain 64-bit loads: no per-step branch between them
+            auto stream_and_test = [&](auto buf) {
             int nc = 0;
             while (true) {
                 // 1. fill the LDS list: steps of kStreamU x 64 loads, all in flight
@@ -375,7 +378,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 //    filtering this one measured 8 % slower: more VGPRs, fewer waves)
                 while (bk < nbk && nc <= fill_lim) {
                     float4 c[kStreamU];
-                    load_step(c);
+                    load_step(c, buf);
 #pragma unroll
                     for (int u = 0; u < kStreamU; ++u) {
                         const bool keep = box_dist<METRIC>(c[u], lx, ly, lz, hx, hy, hz) <= thr;
@@ -441,6 +444,11 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 nc = 0;
                 if (bk >= nbk) break;
             }
+            };
+            if (pts_rsrc_ok)
+                stream_and_test(std::true_type{});
+            else
+                stream_and_test(std::false_type{});
             if constexpr (MODE == 0) {
                 if (g < ng && sl == 0) {
                     counts[__float_as_uint(mq.w)] = cnt;
