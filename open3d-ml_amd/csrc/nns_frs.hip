@@ -124,6 +124,14 @@ __device__ __forceinline__ float wave_min_f(float v) {
     return fminf(fminf(a, b), fminf(c, d));
 }
 __device__ __forceinline__ float wave_max_f(float v) { return -wave_min_f(-v); }
+// min over lanes 0-15 (DPP within row 0), read from lane 0
+__device__ __forceinline__ float row0_min_f(float v) {
+    v = fminf(v, dpp_f<0xB1>(v));   // quad_perm(1,0,3,2)
+    v = fminf(v, dpp_f<0x4E>(v));   // quad_perm(2,3,0,1)
+    v = fminf(v, dpp_f<0x141>(v));  // row_half_mirror
+    v = fminf(v, dpp_f<0x140>(v));  // row_mirror
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+}
 
 // Distance of p to the box [lo, hi] with the metric's own operation order;
 // every operand is <= the corresponding one of dist_metric(p, q) for any q in
@@ -268,11 +276,21 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 qsh[slot] = q4;
                 if constexpr (MODE == 1) qrow[slot] = row;
             }
-            // group bounding box
-            const float lx = wave_min_f(same ? q4.x : inf), ly = wave_min_f(same ? q4.y : inf),
-                        lz = wave_min_f(same ? q4.z : inf);
-            const float hx = wave_max_f(same ? q4.x : -inf), hy = wave_max_f(same ? q4.y : -inf),
-                        hz = wave_max_f(same ? q4.z : -inf);
+            // group bounding box: groups of <= 16 (nearly all) reduce the member
+            // slots qsh[0, ng) within one 16-lane DPP row, larger ones the whole wave
+            float lx, ly, lz, hx, hy, hz;
+            if (ng <= 16) {
+                __syncthreads();
+                const float4 v = lane < ng ? qsh[lane & 15] : far;
+                const float4 w = lane < ng ? v : make_float4(-inf, -inf, -inf, 0.f);
+                lx = row0_min_f(v.x), ly = row0_min_f(v.y), lz = row0_min_f(v.z);
+                hx = -row0_min_f(-w.x), hy = -row0_min_f(-w.y), hz = -row0_min_f(-w.z);
+            } else {
+                lx = wave_min_f(same ? q4.x : inf), ly = wave_min_f(same ? q4.y : inf),
+                lz = wave_min_f(same ? q4.z : inf);
+                hx = wave_max_f(same ? q4.x : -inf), hy = wave_max_f(same ? q4.y : -inf),
+                hz = wave_max_f(same ? q4.z : -inf);
+            }
             // lane -> (query g, slice s)
             // S = floor(64 / ng) lanes per query (not a power of two: 9 queries
             // take 63 lanes, not 9 of 16 slots x 4); g = lane / S by the
@@ -396,7 +414,10 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 //    list against the group's queries, in order (4 slices per
                 //    step, then single slices); hits are ranked by ballot so every
                 //    row is written in canonical order
-                const int ncp = nc + (S - 1 - (nc + S - 1) % S);  // nc rounded up to whole slices
+                // nc rounded up to whole slices: ceil(nc / S) by the table's
+                // multiply-shift (exact for nc + S - 1 < 65536 / S; nc <= kCandCap)
+                const int ncp = static_cast<int>(((static_cast<uint32_t>(nc + S - 1) * (split >> 8)) >> 16) *
+                                                 static_cast<uint32_t>(S));
                 if (nc + lane < ncp) cand[nc + lane] = far;
                 __syncthreads();
 #if O3DML_DIAG == 0
