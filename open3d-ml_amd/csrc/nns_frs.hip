@@ -634,10 +634,16 @@ __global__ void __launch_bounds__(256) self_query_order_kernel(const float4* __r
         }
         for (uint32_t c0 = s; c0 < e; c0 += kSelfChunk) {
             const uint32_t len = min(e - c0, static_cast<uint32_t>(kSelfChunk));
+            const int rows = static_cast<int>((len + 63) >> 6);  // rows past it are skipped (uniform)
             float4 p[E];
             uint32_t hc[E], oct[E];
 #pragma unroll
             for (int h = 0; h < E; ++h) {
+                if (h >= rows) {
+                    hc[h] = 0u;
+                    oct[h] = 0u;
+                    continue;
+                }
                 const uint32_t i = lane + 64 * h;
                 p[h] = i < len ? pts[c0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
                 const int32_t x = static_cast<int32_t>(floorf(p[h].x * inv2)),
@@ -652,6 +658,7 @@ __global__ void __launch_bounds__(256) self_query_order_kernel(const float4* __r
             uint32_t c2 = c1;
 #pragma unroll
             for (int h = E - 1; h >= 0; --h) {  // first entry in another cell (lowest row wins)
+                if (h >= rows) continue;
                 const uint64_t other = __builtin_amdgcn_ballot_w64(lane + 64 * h < len && hc[h] != c1);
                 if (other) c2 = rdlane(static_cast<int>(hc[h]), __builtin_ctzll(other));
             }
@@ -660,6 +667,7 @@ __global__ void __launch_bounds__(256) self_query_order_kernel(const float4* __r
             uint32_t dig[E], loff[E];
 #pragma unroll
             for (int h = 0; h < E; ++h) {  // rows in order: stable within a class
+                if (h >= rows) break;
                 const bool valid = lane + 64 * h < len;
                 const uint32_t cls = hc[h] == c1 ? 0u : (hc[h] == c2 ? 1u : 2u);
                 const uint32_t d = (cls << 3) | oct[h];
@@ -681,6 +689,7 @@ __global__ void __launch_bounds__(256) self_query_order_kernel(const float4* __r
             const uint32_t base = wave_inclusive_scan(cnt) - cnt;  // class bases
 #pragma unroll
             for (int h = 0; h < E; ++h) {
+                if (h >= rows) break;
                 const uint32_t i = lane + 64 * h;
                 const uint32_t pos =
                         static_cast<uint32_t>(__shfl(static_cast<int>(base), static_cast<int>(dig[h]), 64)) + loff[h];
