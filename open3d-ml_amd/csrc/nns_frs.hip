@@ -79,6 +79,9 @@ __global__ void __launch_bounds__(256) gather_sorted_points_kernel(const float* 
 }
 
 constexpr int kRowCap = 64;  // neighbours kept per query in the temp rows
+// voxel-class directory per bucket (bucket_classes_kernel): sizes of classes
+// 0 and 1, 2 spare words, then per class 0-2 the box min x, y, z, max x, y, z
+constexpr int kDirWords = 24;
 
 // Lane split of a group of ng queries: S = floor(64 / ng) in bits 0-7 and
 // M = ceil(65536 / S) in bits 8-31 (g = lane * M >> 16 = floor(lane / S)).
@@ -154,6 +157,26 @@ __device__ __forceinline__ float box_dist(const float4& p, float lx, float ly, f
     }
 }
 
+// Distance bound between two boxes, [al, ah] and [bl, bh], with the metric's
+// operation order: each gap is <= the |difference| of any two points of the
+// boxes and every step is monotone, so the bound is <= dist_metric(p, q) for
+// every p in one box and q in the other.
+template <int METRIC>
+__device__ __forceinline__ float box_box_dist(float alx, float aly, float alz, float ahx, float ahy, float ahz,
+                                              float blx, float bly, float blz, float bhx, float bhy, float bhz) {
+    const float gx = fmaxf(fmaxf(alx - bhx, blx - ahx), 0.f);
+    const float gy = fmaxf(fmaxf(aly - bhy, bly - ahy), 0.f);
+    const float gz = fmaxf(fmaxf(alz - bhz, blz - ahz), 0.f);
+    if constexpr (METRIC == kL2) {
+        return __builtin_fmaf(gz, gz, __builtin_fmaf(gy, gy, gx * gx));
+    } else if constexpr (METRIC == kL1) {
+        return (gx + gy) + gz;
+    } else {
+        const float m = gx > gy ? gx : gy;
+        return m > gz ? m : gz;
+    }
+}
+
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
@@ -205,7 +228,8 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                  uint32_t* __restrict__ counts, uint32_t* __restrict__ tidx,
                  float* __restrict__ tdist, uint32_t* __restrict__ over, int64_t* __restrict__ n_over,
                  const int64_t* __restrict__ rs, TIdx* __restrict__ out_idx, float* __restrict__ out_dist,
-                 const int64_t* __restrict__ total, int64_t cap) {
+                 const int64_t* __restrict__ total, int64_t cap, const uint32_t* __restrict__ dir,
+                 int64_t dir_cap) {
     __shared__ float4 cand[kCandCap];
     __shared__ float4 qsh[64];
     __shared__ int64_t qrow[MODE == 0 ? 1 : 64];  // MODE 0: the row is the query id (qsh .w)
@@ -216,14 +240,17 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
     // nothing is written (the caller re-runs the fill with exact buffers)
     const int64_t m = MODE == 1 && cap >= 0 && *total > cap ? 0 : (m_dev ? *m_dev : m_host);
     const int64_t nchunks = MODE == 0 ? (m + 63) >> 6 : m;  // MODE 1: one query per wave
-    // buffer resource over pts[0 .. n_pts] when its byte size fits the 32-bit range
-    const bool pts_rsrc_ok = n_pts < 0x0FFFFFFFu;
+    // buffer resource over pts[0 .. 2 n_pts + 1] (bucket order, the far
+    // sentinel, the class sub-lists p2) when its byte size fits the 32-bit range
+    const bool pts_rsrc_ok = n_pts < 0x07FFFFFEu;
+    // class directory present for every bin of the table
+    const bool sub = dir != nullptr && static_cast<int64_t>(hts[nb]) <= dir_cap;
     // REL16 temp rows (2 B x kRowCap per query; REL16 implies they fit 2^31 B,
     // rel16_rows) through a buffer resource: one VALU per hit for the address
     const __amdgpu_buffer_rsrc_t rows_rsrc = __builtin_amdgcn_make_buffer_rsrc(
             tidx, static_cast<short>(0), REL16 ? static_cast<int>(m * 2 * kRowCap) : 0, kBufferFlags);
     const __amdgpu_buffer_rsrc_t pts_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float4*>(pts), static_cast<short>(0), static_cast<int>((n_pts + 1u) * 16u), kBufferFlags);
+            const_cast<float4*>(pts), static_cast<short>(0), static_cast<int>((2u * n_pts + 1u) * 16u), kBufferFlags);
     // XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so with a grid
     // of exactly 8 * per blocks, block b takes chunk (b % 8) * per + b / 8 —
     // every XCD sweeps one contiguous, spatially coherent range and its L2
@@ -311,9 +338,13 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
             const uint64_t gmask = S == 64 ? ~0ull : (g < ng ? ((1ull << S) - 1ull) << (g * S) : 0ull);
             const uint32_t gm_lo = static_cast<uint32_t>(gmask), gm_hi = static_cast<uint32_t>(gmask >> 32);
             // Bucket list of the group in visit order, empty and repeated bins
-            // dropped: lane j < nbk holds the start in pts and the length of the
-            // j-th bucket.  Built in parallel (lane k < 9 takes bin k: one pair
-            // of loads) and compacted through the candidate list, free here.
+            // dropped: lane j < nbk holds the start (in pts, or in the class
+            // sub-lists p2) and the length of the j-th stream segment.  Built in
+            // parallel (lane k < 9 takes bin k) and compacted through the
+            // candidate list, free here.  With the class directory, a bucket's
+            // classes whose box is out of reach of the group's box are skipped
+            // (box_box_dist: exact, see bucket_classes_kernel); one class left
+            // streams its sub-list, none skips the bucket, more stream it whole.
             uint32_t vst, vlen;
             int nbk;
             {
@@ -326,14 +357,36 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 // the bins are sorted: a repeat sits right after its first copy
                 const uint32_t prev = static_cast<uint32_t>(
                         __builtin_amdgcn_update_dpp(-1, static_cast<int>(vb), 0x111, 0xF, 0xF, false));  // row_shr:1
-                const bool live = lane < 9 && e0 > s0 && prev != vb;
+                const bool first = lane < 9 && e0 > s0 && prev != vb;
+                uint32_t st = s0, ln = e0 - s0;
+                if (first && sub) {
+                    const uint4* dp = reinterpret_cast<const uint4*>(dir + static_cast<size_t>(vb) * kDirWords);
+                    const uint4 w0 = dp[0], w1 = dp[1], w2 = dp[2], w3 = dp[3], w4 = dp[4], w5 = dp[5];
+                    const uint32_t n0 = w0.x, n1 = w0.y, n2 = ln - n0 - n1;
+                    auto f = [](uint32_t u) { return __uint_as_float(u); };
+                    const bool r0 = n0 > 0 && box_box_dist<METRIC>(f(w1.x), f(w1.y), f(w1.z), f(w1.w), f(w2.x),
+                                                                   f(w2.y), lx, ly, lz, hx, hy, hz) <= thr;
+                    const bool r1 = n1 > 0 && box_box_dist<METRIC>(f(w2.z), f(w2.w), f(w3.x), f(w3.y), f(w3.z),
+                                                                   f(w3.w), lx, ly, lz, hx, hy, hz) <= thr;
+                    const bool r2 = n2 > 0 && box_box_dist<METRIC>(f(w4.x), f(w4.y), f(w4.z), f(w4.w), f(w5.x),
+                                                                   f(w5.y), lx, ly, lz, hx, hy, hz) <= thr;
+                    const int nr = static_cast<int>(r0) + static_cast<int>(r1) + static_cast<int>(r2);
+                    const uint32_t base = n_pts + 1 + s0;  // the bucket's classes in p2
+                    if (nr == 0) {
+                        ln = 0;
+                    } else if (nr == 1) {
+                        st = base + (r0 ? 0u : (r1 ? n0 : n0 + n1));
+                        ln = r0 ? n0 : (r1 ? n1 : n2);
+                    }
+                }
+                const bool live = first && ln > 0;
                 const uint64_t km = __builtin_amdgcn_ballot_w64(live);
                 nbk = __popcll(km);
                 uint32_t* tab = reinterpret_cast<uint32_t*>(cand);
                 if (live) {
                     const uint32_t j = mbcnt64(km);
-                    tab[j] = s0;
-                    tab[16 + j] = e0 - s0;
+                    tab[j] = st;
+                    tab[16 + j] = ln;
                 }
                 __syncthreads();
                 vst = lane < nbk ? tab[lane] : 0u;
@@ -590,25 +643,44 @@ __global__ void __launch_bounds__(256) group_query_keys_kernel(const float* __re
     }
 }
 
-// Self search (queries = points): the queries in Open3D's bucket order (the
-// gathered pts array) with each bucket's entries reordered by (cell, octant),
-// so the queries of one group — same cell, same octant, hence the same 9
-// visited buckets — are adjacent and 64 consecutive queries form few groups,
-// like the Morton order of the general path but with no sort of the queries.
-// One wave per bucket, 128 entries at a time (longer buckets are ordered
-// chunk by chunk: any order is correct, grouping compares the full bucket
-// lists).  qbatch[t] = batch item of query t.
-constexpr int kSelfChunk = 256;  // bucket entries ordered at once (longer buckets: chunk by chunk)
+// Voxel classes of the buckets.  Open3D's table has about one bucket per
+// occupied 2r-voxel, so a bucket a query group visits holds ~2 voxels and the
+// group usually reaches one of them.  bucket_classes_kernel splits every
+// bucket into three classes — the voxel of its first entry, the first other
+// voxel seen, the rest — and writes a second copy of the points,
+// p2 = pts[n + 1 ..], ordered by (bucket, class, id), plus a directory entry
+// per bucket: the sizes of classes 0 and 1 and the exact float bounding box
+// of each class.  The search skips a class when the distance bound between
+// its box and the group's box exceeds the radius (monotone float ops in the
+// metric's order, as box_dist: every skipped point would fail the exact test
+// for every member), and streams one class's sub-list when it is the only one
+// left (ids ascending: Open3D's order), the whole bucket otherwise.
+//
+// Self search (queries = points) also takes the query order from here: each
+// bucket's entries by (class, octant), so the queries of one group — same
+// voxel, same octant, hence the same 9 visited bins — are adjacent and 64
+// consecutive queries form few groups, with no sort of the queries (qpts,
+// qbatch[t] = batch item of query t; 256 entries at a time: longer buckets
+// are ordered chunk by chunk, any order is correct).
+constexpr int kSelfChunk = 256;  // bucket entries ordered at once
 
-// The chunk's entries get a 5-bit class: the octant (3 bits) and which of the
-// bucket's cells holds the point (first cell seen, second cell seen, any
-// other: 2 bits); a stable counting sort by class (ballot ranking, per-class
-// counts in LDS) makes every (cell, octant) group contiguous.
-__global__ void __launch_bounds__(256) self_query_order_kernel(const float4* __restrict__ pts,
-                                                               const uint32_t* __restrict__ cs,
-                                                               const uint32_t* __restrict__ hts, int nb, float inv2,
-                                                               float4* __restrict__ qpts,
-                                                               uint32_t* __restrict__ qbatch) {
+__device__ __forceinline__ int32_t wave_min_i(int32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int32_t wave_max_i(int32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __restrict__ pts, int64_t n_pts,
+                                                             const uint32_t* __restrict__ cs,
+                                                             const uint32_t* __restrict__ hts, int nb, float inv,
+                                                             float cell, uint32_t* __restrict__ dir, int64_t dir_cap,
+                                                             float4* __restrict__ qpts,
+                                                             uint32_t* __restrict__ qbatch) {
     constexpr int E = kSelfChunk / 64;
     __shared__ uint32_t s_hts[kLdsSplits];
     __shared__ uint32_t wcnt[4][32];
@@ -619,6 +691,9 @@ __global__ void __launch_bounds__(256) self_query_order_kernel(const float4* __r
     __syncthreads();
     const uint32_t* H = lds_hts ? s_hts : hts;
     const int64_t nbins = H[nb];
+    const bool with_dir = dir != nullptr && nbins <= dir_cap;  // else the search streams whole buckets
+    float4* p2 = const_cast<float4*>(pts) + n_pts + 1;
+    const float inf = __builtin_huge_valf();
     const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
     const uint64_t lt = lanemask_lt();
     int64_t bin = static_cast<int64_t>(blockIdx.x) * 4 + wv;
@@ -627,85 +702,181 @@ __global__ void __launch_bounds__(256) self_query_order_kernel(const float4* __r
         // next bucket's bounds in flight while this one is ordered
         const int64_t nbin = bin + nwaves;
         const uint32_t ns = nbin < nbins ? cs[nbin] : 0u, ne = nbin < nbins ? cs[nbin + 1] : 0u;
-        int lo = 0, hi = nb - 1;  // batch item of the bucket (uniform)
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (H[mid] <= bin) lo = mid; else hi = mid - 1;
-        }
-        for (uint32_t c0 = s; c0 < e; c0 += kSelfChunk) {
-            const uint32_t len = min(e - c0, static_cast<uint32_t>(kSelfChunk));
-            const int rows = static_cast<int>((len + 63) >> 6);  // rows past it are skipped (uniform)
+        if (s < e) {
+            int lo = 0, hi = nb - 1;  // batch item of the bucket (uniform)
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (H[mid] <= bin) lo = mid; else hi = mid - 1;
+            }
             float4 p[E];
-            uint32_t hc[E], oct[E];
+            int32_t vx[E], vy[E], vz[E];
+            uint32_t oct[E];
+            int rows = 0;
+            auto load_chunk = [&](uint32_t c0, uint32_t len) {
+                rows = static_cast<int>((len + 63) >> 6);  // rows past it are skipped (uniform)
 #pragma unroll
-            for (int h = 0; h < E; ++h) {
-                if (h >= rows) {
-                    hc[h] = 0u;
-                    oct[h] = 0u;
-                    continue;
+                for (int h = 0; h < E; ++h) {
+                    if (h >= rows) {
+                        vx[h] = vy[h] = vz[h] = 0;
+                        oct[h] = 0u;
+                        continue;
+                    }
+                    const uint32_t i = lane + 64 * h;
+                    p[h] = i < len ? pts[c0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    // the 2r-voxel as the hash build computes it; the octant
+                    // (query order only) from the fractional part
+                    const float fx = p[h].x * inv, fy = p[h].y * inv, fz = p[h].z * inv;
+                    const float gx = floorf(fx), gy = floorf(fy), gz = floorf(fz);
+                    vx[h] = static_cast<int32_t>(gx);
+                    vy[h] = static_cast<int32_t>(gy);
+                    vz[h] = static_cast<int32_t>(gz);
+                    oct[h] = (fx - gx >= 0.5f ? 1u : 0u) | (fy - gy >= 0.5f ? 2u : 0u) | (fz - gz >= 0.5f ? 4u : 0u);
                 }
-                const uint32_t i = lane + 64 * h;
-                p[h] = i < len ? pts[c0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
-                const int32_t x = static_cast<int32_t>(floorf(p[h].x * inv2)),
-                              y = static_cast<int32_t>(floorf(p[h].y * inv2)),
-                              z = static_cast<int32_t>(floorf(p[h].z * inv2));
-                // 2r-cell = half-cell >> 1, octant = the half-cell parities
-                hc[h] = (static_cast<uint32_t>(x >> 1) * 0x9E3779B1u) ^ (static_cast<uint32_t>(y >> 1) * 0x85EBCA77u) ^
-                        (static_cast<uint32_t>(z >> 1) * 0xC2B2AE3Du);
-                oct[h] = (x & 1) | ((y & 1) << 1) | ((z & 1) << 2);
-            }
-            const uint32_t c1 = rdlane(static_cast<int>(hc[0]), 0);
-            uint32_t c2 = c1;
-#pragma unroll
-            for (int h = E - 1; h >= 0; --h) {  // first entry in another cell (lowest row wins)
-                if (h >= rows) continue;
-                const uint64_t other = __builtin_amdgcn_ballot_w64(lane + 64 * h < len && hc[h] != c1);
-                if (other) c2 = rdlane(static_cast<int>(hc[h]), __builtin_ctzll(other));
-            }
-            if (lane < 32) wcnt[wv][lane] = 0;
-            __builtin_amdgcn_wave_barrier();
-            uint32_t dig[E], loff[E];
-#pragma unroll
-            for (int h = 0; h < E; ++h) {  // rows in order: stable within a class
-                if (h >= rows) break;
-                const bool valid = lane + 64 * h < len;
-                const uint32_t cls = hc[h] == c1 ? 0u : (hc[h] == c2 ? 1u : 2u);
-                const uint32_t d = (cls << 3) | oct[h];
-                dig[h] = d;
-                uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
-#pragma unroll
-                for (int b = 0; b < 5; ++b) {
-                    const bool bit = (d >> b) & 1u;
-                    const uint64_t m = __builtin_amdgcn_ballot_w64(bit);
-                    peers &= bit ? m : ~m;
+            };
+            // pass 1: the class voxels and sizes, and the voxel range of class 2
+            int32_t ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;
+            bool have1 = false;
+            uint32_t n0 = 0, n1 = 0;
+            int32_t rlx = INT32_MAX, rly = INT32_MAX, rlz = INT32_MAX, rhx = INT32_MIN, rhy = INT32_MIN,
+                    rhz = INT32_MIN;  // lane-partial voxel range of class 2
+            auto classify = [&](int h) {
+                const bool is0 = vx[h] == ax && vy[h] == ay && vz[h] == az;
+                const bool is1 = have1 && !is0 && vx[h] == bx && vy[h] == by && vz[h] == bz;
+                return is0 ? 0 : (is1 ? 1 : 2);
+            };
+            const bool one_chunk = e - s <= static_cast<uint32_t>(kSelfChunk);
+            for (uint32_t c0 = s; c0 < e; c0 += kSelfChunk) {
+                const uint32_t len = min(e - c0, static_cast<uint32_t>(kSelfChunk));
+                load_chunk(c0, len);
+                if (c0 == s) {
+                    ax = rdlane(vx[0], 0);
+                    ay = rdlane(vy[0], 0);
+                    az = rdlane(vz[0], 0);
                 }
-                const uint32_t rank = __popcll(peers & lt);
-                const uint32_t before = valid ? wcnt[wv][d] : 0u;
-                loff[h] = before + rank;
-                if (valid && rank == 0) wcnt[wv][d] = before + static_cast<uint32_t>(__popcll(peers));
-            }
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t cnt = lane < 32 ? wcnt[wv][lane] : 0u;
-            const uint32_t base = wave_inclusive_scan(cnt) - cnt;  // class bases
 #pragma unroll
-            for (int h = 0; h < E; ++h) {
-                if (h >= rows) break;
-                const uint32_t i = lane + 64 * h;
-                const uint32_t pos =
-                        static_cast<uint32_t>(__shfl(static_cast<int>(base), static_cast<int>(dig[h]), 64)) + loff[h];
-                if (i < len) {
-                    qpts[c0 + pos] = p[h];
-                    qbatch[c0 + pos] = static_cast<uint32_t>(lo);
+                for (int h = 0; h < E; ++h) {
+                    if (h >= rows) break;
+                    const bool valid = lane + 64 * h < len;
+                    if (!have1) {  // first entry of another voxel (entry order)
+                        const uint64_t other = __builtin_amdgcn_ballot_w64(
+                                valid && !(vx[h] == ax && vy[h] == ay && vz[h] == az));
+                        if (other) {
+                            const int l = __builtin_ctzll(other);
+                            bx = rdlane(vx[h], l);
+                            by = rdlane(vy[h], l);
+                            bz = rdlane(vz[h], l);
+                            have1 = true;
+                        }
+                    }
+                    const int c = classify(h);
+                    n0 += __popcll(__builtin_amdgcn_ballot_w64(valid && c == 0));
+                    n1 += __popcll(__builtin_amdgcn_ballot_w64(valid && c == 1));
+                    if (valid && c == 2) {
+                        rlx = min(rlx, vx[h]), rly = min(rly, vy[h]), rlz = min(rlz, vz[h]);
+                        rhx = max(rhx, vx[h]), rhy = max(rhy, vy[h]), rhz = max(rhz, vz[h]);
+                    }
                 }
             }
-            __builtin_amdgcn_wave_barrier();
+            if (with_dir) {
+                // class boxes from the voxel ranges: a point p of voxel W has
+                // floor(fl(p inv)) = W, so p inv lies in [W - 1/16, W + 1 + 1/8]
+                // while |W| < 2^20 (relative rounding 2^-24 of the product); the
+                // box [(W - 0.5) 2r, (W + 1.5) 2r] in float holds it with >= 1/4
+                // voxel to spare for the rounding of the box edges and of
+                // 1 / inv vs 2r (within 2^16 voxels: 1/32-voxel margins, the
+                // rounding being < 1/128 voxel).  Beyond 2^20: no box.
+                const uint32_t n2 = (e - s) - n0 - n1;
+                if (n2 > 0) {
+                    rlx = wave_min_i(rlx), rly = wave_min_i(rly), rlz = wave_min_i(rlz);
+                    rhx = wave_max_i(rhx), rhy = wave_max_i(rhy), rhz = wave_max_i(rhz);
+                }
+                // lane 4 + 6 k + d: class k, value d (min x y z, max x y z)
+                const int j = lane - 4, k = j / 6, d = j % 6;
+                const int32_t vlo[3][3] = {{ax, ay, az}, {bx, by, bz}, {rlx, rly, rlz}};
+                const int32_t vhi[3][3] = {{ax, ay, az}, {bx, by, bz}, {rhx, rhy, rhz}};
+                uint32_t w = lane == 0 ? n0 : (lane == 1 ? n1 : 0u);
+                if (j >= 0 && j < 18) {
+                    int32_t vl = 0, vh = 0;
+#pragma unroll
+                    for (int kk = 0; kk < 3; ++kk)
+#pragma unroll
+                        for (int dd = 0; dd < 3; ++dd)
+                            if (kk == k && dd == d % 3) vl = vlo[kk][dd], vh = vhi[kk][dd];
+                    const bool ok = vl > -(1 << 20) && vh < (1 << 20);
+                    // within 2^16 voxels of the origin the rounding is < 1/128 voxel:
+                    // a 1/32-voxel margin suffices
+                    const bool near0 = vl > -(1 << 16) && vh < (1 << 16);
+                    const float mg = near0 ? 0.03125f : 0.5f;
+                    const float edge = d < 3 ? (static_cast<float>(vl) - mg) * cell
+                                             : (static_cast<float>(vh) + (1.0f + mg)) * cell;
+                    w = __float_as_uint(ok ? edge : (d < 3 ? -__builtin_huge_valf() : __builtin_huge_valf()));
+                }
+                if (lane < kDirWords) dir[bin * kDirWords + lane] = w;
+            }
+            // pass 2: p2 by (class, id); queries by (class, octant) per chunk
+            uint32_t run0 = 0, run1 = n0, run2 = n0 + n1;
+            for (uint32_t c0 = s; c0 < e; c0 += kSelfChunk) {
+                const uint32_t len = min(e - c0, static_cast<uint32_t>(kSelfChunk));
+                if (!one_chunk) load_chunk(c0, len);
+                if (qpts && lane < 32) wcnt[wv][lane] = 0;
+                __builtin_amdgcn_wave_barrier();
+                uint32_t dig[E], loff[E];
+#pragma unroll
+                for (int h = 0; h < E; ++h) {  // rows in order: stable within a class
+                    if (h >= rows) break;
+                    const bool valid = lane + 64 * h < len;
+                    const int c = classify(h);
+                    const uint64_t m0 = __builtin_amdgcn_ballot_w64(valid && c == 0);
+                    const uint64_t m1 = __builtin_amdgcn_ballot_w64(valid && c == 1);
+                    const uint64_t m2 = __builtin_amdgcn_ballot_w64(valid && c == 2);
+                    const uint64_t mine = c == 0 ? m0 : (c == 1 ? m1 : m2);
+                    const uint32_t run = c == 0 ? run0 : (c == 1 ? run1 : run2);
+                    if (valid) p2[s + run + __popcll(mine & lt)] = p[h];
+                    run0 += __popcll(m0);
+                    run1 += __popcll(m1);
+                    run2 += __popcll(m2);
+                    if (qpts) {
+                        const uint32_t d = (static_cast<uint32_t>(c) << 3) | oct[h];
+                        dig[h] = d;
+                        uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
+#pragma unroll
+                        for (int bb = 0; bb < 5; ++bb) {
+                            const bool bit = (d >> bb) & 1u;
+                            const uint64_t mm = __builtin_amdgcn_ballot_w64(bit);
+                            peers &= bit ? mm : ~mm;
+                        }
+                        const uint32_t rank = __popcll(peers & lt);
+                        const uint32_t before = valid ? wcnt[wv][d] : 0u;
+                        loff[h] = before + rank;
+                        if (valid && rank == 0) wcnt[wv][d] = before + static_cast<uint32_t>(__popcll(peers));
+                    }
+                }
+                if (qpts) {
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t cnt = lane < 32 ? wcnt[wv][lane] : 0u;
+                    const uint32_t base = wave_inclusive_scan(cnt) - cnt;  // class bases
+#pragma unroll
+                    for (int h = 0; h < E; ++h) {
+                        if (h >= rows) break;
+                        const uint32_t i = lane + 64 * h;
+                        const uint32_t pos = static_cast<uint32_t>(
+                                                     __shfl(static_cast<int>(base), static_cast<int>(dig[h]), 64)) +
+                                             loff[h];
+                        if (i < len) {
+                            qpts[c0 + pos] = p[h];
+                            qbatch[c0 + pos] = static_cast<uint32_t>(lo);
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
         }
         s = ns;
         e = ne;
     }
 }
 
-// Self search queries in Open3D's bucket order (self_query_order_kernel) —
+// Self search queries in Open3D's bucket order (bucket_classes_kernel) —
 // unless a batch item is so large that the hash order of its buckets, which
 // is spatially random, costs more in L2 misses than a Morton sort of the
 // queries (>= 2^22 points: search 6.19 -> 4.55 ms at 2^24 points, the sort
@@ -739,12 +910,12 @@ static void launch_group(int metric, bool ignore, bool with_dist, bool rel16, hi
                          const uint32_t* qkeys, int bshift, int64_t m, const int64_t* m_dev, float r, float inv,
                          float thr, int nb, const int64_t* qrs, const uint32_t* hts, const int64_t* prs,
                          uint32_t* counts, uint32_t* tidx, float* tdist, uint32_t* over, int64_t* n_over,
-                         const int64_t* rs, TIdx* idx, float* dist, const int64_t* total = nullptr,
-                         int64_t cap = -1) {
+                         const int64_t* rs, TIdx* idx, float* dist, const uint32_t* dir, int64_t dir_cap,
+                         const int64_t* total = nullptr, int64_t cap = -1) {
 #define O3DML_GRP(M, I, D, R)                                                                                   \
     frs_group_kernel<M, I, D, MODE, TIdx, R><<<grid, 64, 0, st>>>(pts, n_pts, cs, qpts, qkeys, bshift, m, m_dev,  \
                                                                    r, inv, thr, nb, qrs, hts, prs, counts, tidx,  \
-                                                                   tdist, over, n_over, rs, idx, dist, total, cap)
+                                                                   tdist, over, n_over, rs, idx, dist, total, cap, dir, dir_cap)
 #define O3DML_GRP_R(M, I, D)                                  \
     do {                                                      \
         if (MODE == 0 && rel16)                               \
@@ -775,7 +946,7 @@ static void launch_group(int metric, bool ignore, bool with_dist, bool rel16, hi
 // Workspace kept between _count and _fill (same layout in both entries).
 struct FrsPlan {
     int64_t* scalars;  // [0] overflow count
-    float4* pts;       // [N + 1] points in Open3D bucket order + a far sentinel
+    float4* pts;       // [2 (N + 1)] points in Open3D bucket order, a far sentinel, the class sub-lists p2
     float4* qpts;      // [M] queries in (batch, Morton) order
     uint32_t* keys;    // [M]
     uint32_t* skeys;   // [M]
@@ -784,12 +955,18 @@ struct FrsPlan {
     uint32_t* over;    // [M]
     uint32_t* tidx;    // [M * kRowCap]
     float* tdist;      // [M * kRowCap] (with distances)
+    uint32_t* dir;     // [dir_cap * kDirWords] voxel-class directory per bucket
+    int64_t dir_cap;   // bins the directory holds (dir_bins)
 };
 
-static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m, bool dist) {
+// Bins the class directory holds: twice Open3D's default table (N_b / 64
+// bins per item); a table with more bins streams whole buckets
+static int64_t dir_bins(int64_t n, int64_t nb) { return n / 32 + 2 * nb + 64; }
+
+static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m, int64_t nb, bool dist) {
     FrsPlan p;
     p.scalars = ws.take<int64_t>(4);
-    p.pts = ws.take<float4>(n + 1);  // + far sentinel
+    p.pts = ws.take<float4>(2 * (n + 1));  // + far sentinel + p2
     p.qpts = ws.take<float4>(m);
     p.keys = ws.take<uint32_t>(m);
     p.skeys = ws.take<uint32_t>(m);
@@ -798,6 +975,8 @@ static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m, bool dist) {
     p.over = ws.take<uint32_t>(m);
     p.tidx = ws.take<uint32_t>(m * kRowCap);
     p.tdist = dist ? ws.take<float>(m * kRowCap) : nullptr;
+    p.dir_cap = dir_bins(n, nb);
+    p.dir = ws.take<uint32_t>(p.dir_cap * kDirWords);
     return p;
 }
 
@@ -814,9 +993,10 @@ static bool rel16_rows(int64_t n_batch, const int64_t* prs_host, int64_t n_queri
     return true;
 }
 
-static size_t plan_bytes(int64_t n, int64_t m) {
-    return ws_bytes<int64_t>(4) + ws_bytes<float4>(n + 1) + ws_bytes<float4>(m) + 3 * ws_bytes<uint32_t>(m) +
-           2 * ws_bytes<uint32_t>(m) + 2 * ws_bytes<uint32_t>(m * kRowCap);
+static size_t plan_bytes(int64_t n, int64_t m, int64_t nb) {
+    return ws_bytes<int64_t>(4) + ws_bytes<float4>(2 * (n + 1)) + ws_bytes<float4>(m) + 3 * ws_bytes<uint32_t>(m) +
+           2 * ws_bytes<uint32_t>(m) + 2 * ws_bytes<uint32_t>(m * kRowCap) +
+           ws_bytes<uint32_t>(dir_bins(n, nb) * kDirWords);
 }
 
 }  // namespace o3dml
@@ -824,8 +1004,7 @@ static size_t plan_bytes(int64_t n, int64_t m) {
 using namespace o3dml;
 
 O3DML_API size_t o3dml_fixed_radius_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t n_batch) {
-    (void)n_batch;
-    return plan_bytes(n_points, n_queries) +
+    return plan_bytes(n_points, n_queries, n_batch) +
            std::max(prim::scan_workspace_bytes(n_queries), prim::radix_sort_workspace_bytes<uint32_t>(n_queries));
 }
 
@@ -845,7 +1024,7 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     O3DML_REQUIRE(n_batch >= 1, "need at least one batch item");
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
-    FrsPlan pl = take_plan(ws, n_points, n_queries, with_distances != 0);
+    FrsPlan pl = take_plan(ws, n_points, n_queries, n_batch, with_distances != 0);
     if (n_queries == 0 || n_points == 0) {
         O3DML_CHECK_HIP(hipMemsetAsync(pl.scalars, 0, sizeof(int64_t) * 4, st));
         O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t) * (n_queries + 1), st));
@@ -860,13 +1039,15 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     gather_sorted_points_kernel<<<xcd_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points, pl.pts, 1,
                                                                         pl.scalars, 4, neighbors_row_splits);
     O3DML_LAUNCH_CHECK();
-    if (self_search && frs_self_order(n_batch, points_row_splits_host, n_points)) {
-        // queries = points: Open3D's bucket order, octant groups made adjacent
-        // inside each bucket — no sort of the queries at all
-        self_query_order_kernel<<<static_cast<unsigned>(std::min<int64_t>(ceil_div(n_points, 64 * 4), 1 << 16)), 256,
-                                  0, st>>>(pl.pts, hash_table_cell_splits, hash_table_splits, (int)n_batch,
-                                           2.0f * inv, pl.qpts, pl.keys);
-        O3DML_LAUNCH_CHECK();
+    const bool self_order = self_search && frs_self_order(n_batch, points_row_splits_host, n_points);
+    // class sub-lists + directory; for a self search also the query order:
+    // Open3D's bucket order with the (voxel, octant) groups made adjacent
+    // inside each bucket — no sort of the queries at all
+    bucket_classes_kernel<<<static_cast<unsigned>(std::min<int64_t>(ceil_div(n_points, 64 * 4), 1 << 16)), 256, 0,
+                            st>>>(pl.pts, n_points, hash_table_cell_splits, hash_table_splits, (int)n_batch, inv,
+                                  2.0f * radius, pl.dir, pl.dir_cap, self_order ? pl.qpts : nullptr, self_order ? pl.keys : nullptr);
+    O3DML_LAUNCH_CHECK();
+    if (self_order) {
         qkeys = pl.keys;
         bshift = 0;
     } else {
@@ -894,7 +1075,7 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
                                  static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts, qkeys, bshift,
                                  n_queries, nullptr, radius, inv, thr, (int)n_batch, queries_row_splits,
                                  hash_table_splits, points_row_splits, pl.counts, pl.tidx, pl.tdist, pl.over,
-                                 pl.scalars, nullptr, nullptr, nullptr);
+                                 pl.scalars, nullptr, nullptr, nullptr, pl.dir, pl.dir_cap);
     }
     Workspace sws = ws;
     prim::scan<uint32_t, int64_t>(pl.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
@@ -934,7 +1115,7 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
     if (n_queries == 0 || n_points == 0) return 0;
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
-    FrsPlan pl = take_plan(ws, n_points, n_queries, with_distances != 0);  // built by _count (same workspace)
+    FrsPlan pl = take_plan(ws, n_points, n_queries, n_batch, with_distances != 0);  // built by _count (same workspace)
     const float thr = metric == kL2 ? radius * radius : radius;
     const float inv = 1.0f / (2.0f * radius);
     int64_t* rs = const_cast<int64_t*>(neighbors_row_splits);
@@ -970,12 +1151,14 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
                                  static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, 32, 0,
                                  pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
                                  points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
-                                 static_cast<int32_t*>(neighbors_index), dist, rs + n_queries, capacity);
+                                 static_cast<int32_t*>(neighbors_index), dist, pl.dir, pl.dir_cap, rs + n_queries,
+                                 capacity);
     else
         launch_group<1, int64_t>(metric, ignore_query_point != 0, dist != nullptr, false, st, go, pl.pts,
                                  static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, 32, 0,
                                  pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
                                  points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
-                                 static_cast<int64_t*>(neighbors_index), dist, rs + n_queries, capacity);
+                                 static_cast<int64_t*>(neighbors_index), dist, pl.dir, pl.dir_cap, rs + n_queries,
+                                 capacity);
     O3DML_GUARD_END
 }

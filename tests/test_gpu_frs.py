@@ -224,6 +224,31 @@ def test_frs_group_sizes(cuda, metric):
         assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
 
 
+@pytest.mark.parametrize("factor,offset", [(1 / 512, 0.0), (1 / 64, 2700.0), (1 / 16, -3.0e5), (2.0, 0.0)])
+def test_frs_voxel_classes(cuda, factor, offset):
+    """The voxel-class sub-lists of the buckets: tables of 1/512 (many voxels
+    per bucket: class 2 boxes), 1/16 and 2 bins per point (more bins than the
+    class directory holds: whole buckets), coordinates ~2^17 voxels out
+    (0.5-voxel box margins) and ~10^7 voxels out (no boxes): rows equal the
+    oracle's on the same table, with distances, L2 and Linf."""
+    from o3dml_amd import ops
+    pts = (_cloud(30000, 51) + np.float32(offset)).astype(np.float32)
+    rs = np.array([0, 12000, 30000], np.int64)
+    r = 0.01
+    t = torch.from_numpy(pts).to(cuda)
+    ht = ops.build_spatial_hash_table(t, r, torch.from_numpy(rs), hash_table_size_factor=factor)
+    oi_h, oc_h, osp_h = O.build_spatial_hash_table(pts, r, rs, hash_table_size_factor=factor)
+    for metric in ("L2", "Linf"):
+        res = ops.fixed_radius_search(t, t, r, torch.from_numpy(rs), torch.from_numpy(rs), ht.hash_table_splits,
+                                      ht.hash_table_index, ht.hash_table_cell_splits, metric=metric,
+                                      return_distances=True)
+        ri, rr, rd = O.fixed_radius_search(pts, pts, r, rs, rs, hash_table=(oi_h, oc_h, osp_h), metric=metric,
+                                           return_distances=True)
+        assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), rr)
+        assert np.array_equal(res.neighbors_index.cpu().numpy(), ri)
+        assert np.array_equal(res.neighbors_distance.cpu().numpy(), rd)
+
+
 @pytest.mark.parametrize("mode", ["1", "0"])
 def test_frs_query_order(cuda, mode, monkeypatch):
     """Self search with the queries in Open3D's bucket order (the default for
