@@ -375,7 +375,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                     if (nr == 0) {
                         ln = 0;
                     } else if (nr == 1) {
-                        st = base + (r0 ? 0u : (r1 ? n0 : n0 + n1));
+                        st = r0 && n0 == ln ? s0 : base + (r0 ? 0u : (r1 ? n0 : n0 + n1));  // one voxel: pts
                         ln = r0 ? n0 : (r1 ? n1 : n2);
                     }
                 }
@@ -664,16 +664,19 @@ __global__ void __launch_bounds__(256) group_query_keys_kernel(const float* __re
 // are ordered chunk by chunk, any order is correct).
 constexpr int kSelfChunk = 256;  // bucket entries ordered at once
 
-__device__ __forceinline__ int32_t wave_min_i(int32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
+// wave-wide int min / max: DPP within the 16-lane rows, then the 4 row results
+template <bool MAX>
+__device__ __forceinline__ int32_t wave_ext_i(int32_t v) {
+    auto op = [](int32_t a, int32_t b) { return MAX ? max(a, b) : min(a, b); };
+    v = op(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));   // quad_perm(1,0,3,2)
+    v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));   // quad_perm(2,3,0,1)
+    v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));  // row_mirror
+    return op(op(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+              op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
-__device__ __forceinline__ int32_t wave_max_i(int32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
-}
+__device__ __forceinline__ int32_t wave_min_i(int32_t v) { return wave_ext_i<false>(v); }
+__device__ __forceinline__ int32_t wave_max_i(int32_t v) { return wave_ext_i<true>(v); }
 
 __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __restrict__ pts, int64_t n_pts,
                                                              const uint32_t* __restrict__ cs,
@@ -813,7 +816,10 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
                 }
                 if (lane < kDirWords) dir[bin * kDirWords + lane] = w;
             }
-            // pass 2: p2 by (class, id); queries by (class, octant) per chunk
+            // pass 2: p2 by (class, id) — not for a one-voxel bucket, whose only
+            // class is the bucket itself (the search streams it from pts);
+            // queries by (class, octant) per chunk
+            const bool single = n0 == e - s;
             uint32_t run0 = 0, run1 = n0, run2 = n0 + n1;
             for (uint32_t c0 = s; c0 < e; c0 += kSelfChunk) {
                 const uint32_t len = min(e - c0, static_cast<uint32_t>(kSelfChunk));
@@ -831,7 +837,7 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
                     const uint64_t m2 = __builtin_amdgcn_ballot_w64(valid && c == 2);
                     const uint64_t mine = c == 0 ? m0 : (c == 1 ? m1 : m2);
                     const uint32_t run = c == 0 ? run0 : (c == 1 ? run1 : run2);
-                    if (valid) p2[s + run + __popcll(mine & lt)] = p[h];
+                    if (valid && !single) p2[s + run + __popcll(mine & lt)] = p[h];
                     run0 += __popcll(m0);
                     run1 += __popcll(m1);
                     run2 += __popcll(m2);
