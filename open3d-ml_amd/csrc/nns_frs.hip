@@ -221,7 +221,7 @@ __device__ __forceinline__ int bin_lanes(int v, const uint32_t* lb) {
 template <int METRIC, bool IGNORE, bool DIST, int MODE, class TIdx, bool REL16>
 __global__ void __launch_bounds__(64) O3DML_FRS_ATTR
 frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t* __restrict__ cs,
-                 const float4* __restrict__ qpts,
+                 const float4* __restrict__ qpts, const uint32_t* __restrict__ qsel,
                  const uint32_t* __restrict__ qkeys, int bshift, int64_t m_host, const int64_t* __restrict__ m_dev,
                  float r, float inv, float thr, int nb, const int64_t* __restrict__ qrs,
                  const uint32_t* __restrict__ hts, const int64_t* __restrict__ prs,
@@ -269,7 +269,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
         uint32_t pbase = 0;  // REL16: first point id of the query's batch item
         if (valid) {
             if constexpr (MODE == 0) {
-                q4 = qpts[t];
+                q4 = qsel ? pts[qsel[t]] : qpts[t];  // self search: the queries are points
             } else {  // qpts = the raw query array [M, 3], over = the listed query ids
                 const uint32_t id = over[t];
                 const float* qp = reinterpret_cast<const float*>(qpts) + 3 * static_cast<int64_t>(id);
@@ -682,7 +682,7 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
                                                              const uint32_t* __restrict__ cs,
                                                              const uint32_t* __restrict__ hts, int nb, float inv,
                                                              float cell, uint32_t* __restrict__ dir, int64_t dir_cap,
-                                                             float4* __restrict__ qpts,
+                                                             uint32_t* __restrict__ qsel,
                                                              uint32_t* __restrict__ qbatch) {
     constexpr int E = kSelfChunk / 64;
     __shared__ uint32_t s_hts[kLdsSplits];
@@ -824,7 +824,7 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
             for (uint32_t c0 = s; c0 < e; c0 += kSelfChunk) {
                 const uint32_t len = min(e - c0, static_cast<uint32_t>(kSelfChunk));
                 if (!one_chunk) load_chunk(c0, len);
-                if (qpts && lane < 32) wcnt[wv][lane] = 0;
+                if (qsel && lane < 32) wcnt[wv][lane] = 0;
                 __builtin_amdgcn_wave_barrier();
                 uint32_t dig[E], loff[E];
 #pragma unroll
@@ -841,7 +841,7 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
                     run0 += __popcll(m0);
                     run1 += __popcll(m1);
                     run2 += __popcll(m2);
-                    if (qpts) {
+                    if (qsel) {
                         const uint32_t d = (static_cast<uint32_t>(c) << 3) | oct[h];
                         dig[h] = d;
                         uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
@@ -857,7 +857,7 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
                         if (valid && rank == 0) wcnt[wv][d] = before + static_cast<uint32_t>(__popcll(peers));
                     }
                 }
-                if (qpts) {
+                if (qsel) {
                     __builtin_amdgcn_wave_barrier();
                     const uint32_t cnt = lane < 32 ? wcnt[wv][lane] : 0u;
                     const uint32_t base = wave_inclusive_scan(cnt) - cnt;  // class bases
@@ -869,7 +869,7 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
                                                      __shfl(static_cast<int>(base), static_cast<int>(dig[h]), 64)) +
                                              loff[h];
                         if (i < len) {
-                            qpts[c0 + pos] = p[h];
+                            qsel[c0 + pos] = c0 + i;
                             qbatch[c0 + pos] = static_cast<uint32_t>(lo);
                         }
                     }
@@ -913,13 +913,14 @@ static unsigned group_grid(int64_t m, int queries_per_wave = 64) {
 template <int MODE, class TIdx>
 static void launch_group(int metric, bool ignore, bool with_dist, bool rel16, hipStream_t st, unsigned grid,
                          const float4* pts, uint32_t n_pts, const uint32_t* cs, const float4* qpts,
+                         const uint32_t* qsel,
                          const uint32_t* qkeys, int bshift, int64_t m, const int64_t* m_dev, float r, float inv,
                          float thr, int nb, const int64_t* qrs, const uint32_t* hts, const int64_t* prs,
                          uint32_t* counts, uint32_t* tidx, float* tdist, uint32_t* over, int64_t* n_over,
                          const int64_t* rs, TIdx* idx, float* dist, const uint32_t* dir, int64_t dir_cap,
                          const int64_t* total = nullptr, int64_t cap = -1) {
 #define O3DML_GRP(M, I, D, R)                                                                                   \
-    frs_group_kernel<M, I, D, MODE, TIdx, R><<<grid, 64, 0, st>>>(pts, n_pts, cs, qpts, qkeys, bshift, m, m_dev,  \
+    frs_group_kernel<M, I, D, MODE, TIdx, R><<<grid, 64, 0, st>>>(pts, n_pts, cs, qpts, qsel, qkeys, bshift, m, m_dev, \
                                                                    r, inv, thr, nb, qrs, hts, prs, counts, tidx,  \
                                                                    tdist, over, n_over, rs, idx, dist, total, cap, dir, dir_cap)
 #define O3DML_GRP_R(M, I, D)                                  \
@@ -1051,7 +1052,8 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     // inside each bucket — no sort of the queries at all
     bucket_classes_kernel<<<static_cast<unsigned>(std::min<int64_t>(ceil_div(n_points, 64 * 4), 1 << 16)), 256, 0,
                             st>>>(pl.pts, n_points, hash_table_cell_splits, hash_table_splits, (int)n_batch, inv,
-                                  2.0f * radius, pl.dir, pl.dir_cap, self_order ? pl.qpts : nullptr, self_order ? pl.keys : nullptr);
+                                  2.0f * radius, pl.dir, pl.dir_cap, self_order ? pl.qorder : nullptr,
+                                  self_order ? pl.keys : nullptr);
     O3DML_LAUNCH_CHECK();
     if (self_order) {
         qkeys = pl.keys;
@@ -1078,7 +1080,8 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
         TimedRegion tr("frs_group_search", st);
         launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0,
                                  rel16_rows(n_batch, points_row_splits_host, n_queries), st, group_grid(n_queries), pl.pts,
-                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts, qkeys, bshift,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts,
+                                 self_order ? pl.qorder : nullptr, qkeys, bshift,
                                  n_queries, nullptr, radius, inv, thr, (int)n_batch, queries_row_splits,
                                  hash_table_splits, points_row_splits, pl.counts, pl.tidx, pl.tdist, pl.over,
                                  pl.scalars, nullptr, nullptr, nullptr, pl.dir, pl.dir_cap);
@@ -1154,14 +1157,16 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
     const float4* qraw = reinterpret_cast<const float4*>(queries);  // MODE 1 reads [M, 3] via the over list
     if (index_bits == 32)
         launch_group<1, int32_t>(metric, ignore_query_point != 0, dist != nullptr, false, st, go, pl.pts,
-                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, 32, 0,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, nullptr, 32,
+                                 0,
                                  pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
                                  points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
                                  static_cast<int32_t*>(neighbors_index), dist, pl.dir, pl.dir_cap, rs + n_queries,
                                  capacity);
     else
         launch_group<1, int64_t>(metric, ignore_query_point != 0, dist != nullptr, false, st, go, pl.pts,
-                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, 32, 0,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, nullptr, 32,
+                                 0,
                                  pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
                                  points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
                                  static_cast<int64_t*>(neighbors_index), dist, pl.dir, pl.dir_cap, rs + n_queries,
