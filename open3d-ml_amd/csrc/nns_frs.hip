@@ -699,7 +699,9 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
     const float inf = __builtin_huge_valf();
     const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
     const uint64_t lt = lanemask_lt();
-    int64_t bin = static_cast<int64_t>(blockIdx.x) * 4 + wv;
+    // XCD-contiguous (xcd_block): each XCD orders the buckets whose points its
+    // L2 received from the XCD-contiguous gather
+    int64_t bin = xcd_block() * 4 + wv;
     uint32_t s = bin < nbins ? cs[bin] : 0u, e = bin < nbins ? cs[bin + 1] : 0u;
     for (; bin < nbins; bin += nwaves) {
         // next bucket's bounds in flight while this one is ordered
