@@ -88,6 +88,9 @@ int o3dml_fixed_radius_search_fill(const float* points, int64_t n_points, const 
 /* _fill into caller buffers of `capacity` entries allocated before the total
  * is known (capacity < 0: unbounded = _fill).  When neighbors_row_splits[M] >
  * capacity nothing is written; the caller reads the total and re-runs _fill.
+ * parts: 1 = the row copy, 2 = the re-run of rows longer than 64 (3 = both,
+ * as _fill); a caller that read the overflow count (the first int64 of the
+ * workspace, see o3dml_fixed_radius_search_count) as zero may omit 2.
  * Lets the host queue the fill before its read of the total (no idle GPU
  * while the host waits).  Extension: Open3D's op (outside this repository's
  * reference tree) reads the total before it allocates the outputs. */
@@ -100,7 +103,7 @@ int o3dml_fixed_radius_search_fill_bounded(const float* points, int64_t n_points
                                            int ignore_query_point, int self_search, int with_distances,
                                            const int64_t* neighbors_row_splits, int index_bits,
                                            void* neighbors_index, float* neighbors_distance, int64_t capacity,
-                                           void* workspace, size_t workspace_bytes, void* stream);
+                                           int parts, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- kNN: replaces open3d.ml.torch.ops.knn_search / layers.KNNSearch
  * (ml3d/torch/models/point_transformer.py:724-729) and

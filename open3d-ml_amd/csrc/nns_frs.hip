@@ -1107,7 +1107,7 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
             points, n_points, queries, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
             points_row_splits_host, hash_table_splits, hash_table_index, hash_table_cell_splits, metric,
             ignore_query_point, self_search, with_distances, neighbors_row_splits, index_bits, neighbors_index,
-            neighbors_distance, -1, workspace, workspace_bytes, stream);
+            neighbors_distance, -1, 3, workspace, workspace_bytes, stream);
 }
 
 O3DML_API int o3dml_fixed_radius_search_fill_bounded(
@@ -1116,7 +1116,8 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
         const int64_t* points_row_splits_host, const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
         const uint32_t* hash_table_cell_splits, int metric, int ignore_query_point, int self_search,
         int with_distances, const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
-        float* neighbors_distance, int64_t capacity, void* workspace, size_t workspace_bytes, void* stream) {
+        float* neighbors_distance, int64_t capacity, int parts, void* workspace, size_t workspace_bytes,
+        void* stream) {
     O3DML_GUARD_BEGIN
     (void)points;
     (void)hash_table_index;
@@ -1131,7 +1132,7 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
     const float inv = 1.0f / (2.0f * radius);
     int64_t* rs = const_cast<int64_t*>(neighbors_row_splits);
     float* dist = with_distances ? neighbors_distance : nullptr;
-    {
+    if (parts & 1) {
         TimedRegion tr("frs_group_rows", st);
         const unsigned gc = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_queries, 256), 1 << 16)));
         const bool rel16 = rel16_rows(n_batch, points_row_splits_host, n_queries);
@@ -1155,6 +1156,7 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
     // rows longer than kRowCap: re-run those queries straight into the final
     // rows; the overflow count stays on the device (no host round trip), so a
     // fixed grid strides over however many there are (usually none)
+    if (!(parts & 2)) return 0;  // the caller read a zero overflow count
     const unsigned go = static_cast<unsigned>(std::min<int64_t>(n_queries, 256));
     const float4* qraw = reinterpret_cast<const float4*>(queries);  // MODE 1 reads [M, 3] via the over list
     if (index_bits == 32)

@@ -43,7 +43,7 @@ SIGNATURES = {
                                                c_p, c_sz, c_p]),
     "o3dml_fixed_radius_search_fill_bounded": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p, c_p,
                                                        c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_p,
-                                                       c_i64, c_p, c_sz, c_p]),
+                                                       c_i64, c_i32, c_p, c_sz, c_p]),
     # nns_knn.hip
     "o3dml_knn_search_workspace_size": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
     "o3dml_knn_search_count": (c_i32, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i32, c_i32,

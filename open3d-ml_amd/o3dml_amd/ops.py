@@ -106,21 +106,22 @@ def _frs_count(points, queries, radius, points_row_splits, queries_row_splits, h
     return rs, (common, ws, st, dev, (pts, qry, prs_d, qrs_d, hts_d, hti_d, hcs_d), prs, bool(return_distances))
 
 
-def _frs_fill(rs, state, total, index_dtype, bounded=False):
-    """Phase 2.  bounded: `total` is only a capacity guess made before the
-    real total is read — the library writes nothing when the rows do not fit
-    (o3dml_fixed_radius_search_fill_bounded)."""
-    common, ws, st, dev, _keep, _prs, with_dist = state
+def _frs_alloc(state, total, index_dtype):
+    dev, with_dist = state[3], state[6]
     bits = index_bits(index_dtype)
     idx = torch.empty(total, dtype=torch.int32 if bits == 32 else torch.int64, device=dev)
     dist = torch.empty(total if with_dist else 0, dtype=torch.float32, device=dev)
-    if bounded:
-        _lib.call("o3dml_fixed_radius_search_fill_bounded", *common, ptr(rs), bits, ptr(idx),
-                  ptr(dist) if with_dist else None, total, ptr(ws), ws.numel(), st)
-    else:
-        _lib.call("o3dml_fixed_radius_search_fill", *common, ptr(rs), bits, ptr(idx),
-                  ptr(dist) if with_dist else None, ptr(ws), ws.numel(), st)
     return idx, dist
+
+
+def _frs_launch_fill(rs, state, idx, dist, capacity, parts):
+    """Phase 2 (o3dml_fixed_radius_search_fill_bounded): parts 1 = row copy,
+    2 = the re-run of rows longer than 64; capacity < 0: exact buffers,
+    else a guess made before the total was read (nothing written if short)."""
+    common, ws, st, _dev, _keep, _prs, with_dist = state
+    bits = 32 if idx.dtype == torch.int32 else 64
+    _lib.call("o3dml_fixed_radius_search_fill_bounded", *common, ptr(rs), bits, ptr(idx),
+              ptr(dist) if with_dist else None, capacity, parts, ptr(ws), ws.numel(), st)
 
 
 # Neighbours per query of the last search per (radius, metric): the capacity
@@ -131,13 +132,17 @@ _FRS_DENSITY = {}
 
 
 def _frs_count_fill(rs, state, key, m, index_dtype, extra=None):
-    """Fill with the total read after the (bounded, speculative) fill when a
-    density guess exists, else read first.  extra: more device scalars read
-    in the same host transfer.  Returns (idx, dist, host values)."""
+    """Fill with the total read after the (bounded, speculative) row copy when a
+    density guess exists, else read first.  The overflow count (the plan's
+    first int64) comes in the same host transfer, so the re-run of rows longer
+    than 64 is launched only when there are any.  extra: more device scalars
+    read in that transfer.  Returns (idx, dist, [total] + extra values)."""
     guess = _FRS_DENSITY.get(key)
+    ws = state[1]
+    n_over_dev = ws[:8].view(torch.int64)
     # the totals go to pinned host memory right behind the count; the host
     # waits for that copy only, not for the fill queued after it
-    vals_dev = torch.stack([rs[-1]] + list(extra)) if extra else rs[-1:]
+    vals_dev = torch.stack([rs[-1], n_over_dev[0]] + list(extra or ()))
     host = torch.empty(vals_dev.shape, dtype=vals_dev.dtype, pin_memory=True)
     host.copy_(vals_dev, non_blocking=True)
     ready = torch.cuda.Event()
@@ -145,23 +150,28 @@ def _frs_count_fill(rs, state, key, m, index_dtype, extra=None):
     if guess is None or m == 0:
         ready.synchronize()
         vals = host.tolist()
-        idx, dist = _frs_fill(rs, state, int(vals[0]), index_dtype)
+        idx, dist = _frs_alloc(state, int(vals[0]), index_dtype)
+        _frs_launch_fill(rs, state, idx, dist, -1, 1 | (2 if vals[1] else 0))
     else:
         cap = int(m * guess * 1.0625) + 1024
-        idx, dist = _frs_fill(rs, state, cap, index_dtype, bounded=True)
+        idx, dist = _frs_alloc(state, cap, index_dtype)
+        _frs_launch_fill(rs, state, idx, dist, cap, 1)
         ready.synchronize()
         vals = host.tolist()
         total = int(vals[0])
         if total <= cap:
+            if vals[1]:
+                _frs_launch_fill(rs, state, idx, dist, cap, 2)
             idx = idx[:total]
             dist = dist[:total] if dist.numel() else dist
         else:
-            idx, dist = _frs_fill(rs, state, total, index_dtype)
+            idx, dist = _frs_alloc(state, total, index_dtype)
+            _frs_launch_fill(rs, state, idx, dist, -1, 1 | (2 if vals[1] else 0))
     if m > 0:
         _FRS_DENSITY[key] = int(vals[0]) / m
         if len(_FRS_DENSITY) > 64:
             _FRS_DENSITY.pop(next(iter(_FRS_DENSITY)))
-    return idx, dist, vals
+    return idx, dist, [vals[0]] + vals[2:]
 
 
 def fixed_radius_search(points, queries, radius, points_row_splits=None, queries_row_splits=None,

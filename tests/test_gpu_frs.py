@@ -178,6 +178,7 @@ def test_frs_speculative_capacity(cuda, guess):
     (sliced rows) all give the oracle's rows, plain and dense."""
     from o3dml_amd import ops
     pts = _cloud(20000, 31)
+    pts[:300] = (0.5 + _cloud(300, 32) * 0.01).astype(np.float32)  # rows > 64: the overflow re-run (parts 2)
     rs = np.array([0, 12000, 20000], np.int64)
     t = torch.from_numpy(pts).to(cuda)
     r = 0.05
