@@ -124,6 +124,21 @@ def _frs_launch_fill(rs, state, idx, dist, capacity, parts):
               ptr(dist) if with_dist else None, capacity, parts, ptr(ws), ws.numel(), st)
 
 
+# One pinned host buffer per device for the totals read (a fresh pinned
+# allocation per call can block the host until the device is idle, which
+# would delay the fill launch behind the search); the host reads it before
+# the next call writes it.
+_PINNED = {}
+
+
+def _pinned_slot(device, n):
+    buf = _PINNED.get(device)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(max(n, 8), dtype=torch.int64, pin_memory=True)
+        _PINNED[device] = buf
+    return buf[:n]
+
+
 # Neighbours per query of the last search per (radius, metric): the capacity
 # guess that lets the fill be queued before the host reads the total, so the
 # GPU does not idle through that read.  A guess that proves too small costs
@@ -143,7 +158,7 @@ def _frs_count_fill(rs, state, key, m, index_dtype, extra=None):
     # the totals go to pinned host memory right behind the count; the host
     # waits for that copy only, not for the fill queued after it
     vals_dev = torch.stack([rs[-1], n_over_dev[0]] + list(extra or ()))
-    host = torch.empty(vals_dev.shape, dtype=vals_dev.dtype, pin_memory=True)
+    host = _pinned_slot(rs.device, vals_dev.numel())
     host.copy_(vals_dev, non_blocking=True)
     ready = torch.cuda.Event()
     ready.record(torch.cuda.current_stream(rs.device))
