@@ -76,6 +76,12 @@ int o3dml_fixed_radius_search_count(const float* points, int64_t n_points, const
                                     int metric, int ignore_query_point, int self_search, int with_distances,
                                     int64_t* neighbors_row_splits, void* workspace, size_t workspace_bytes,
                                     void* stream);
+/* totals[0] = neighbors_row_splits[M], totals[1] = the count of rows longer
+ * than 64 (the workspace's first int64), written by one small kernel on the
+ * stream — totals may be pinned host memory, so the host reads both after an
+ * event without a separate device-to-host copy. */
+int o3dml_fixed_radius_search_totals(const int64_t* neighbors_row_splits, int64_t n_queries, void* workspace,
+                                     int64_t* totals, void* stream);
 /* index_bits 32 or 64 (index_dtype); neighbors_distance nullable (squared for L2). */
 int o3dml_fixed_radius_search_fill(const float* points, int64_t n_points, const float* queries,
                                    int64_t n_queries, float radius, int64_t n_batch,

@@ -28,6 +28,7 @@
 // into the final CSR and re-runs the rare longer rows straight into place.
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 
 #include "primitives.hpp"
 #include "spatial_hash.hpp"
@@ -994,6 +995,38 @@ static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m, int64_t nb, bool d
 #ifndef O3DML_FRS_REL16
 #define O3DML_FRS_REL16 1
 #endif
+// Side stream per device for the re-run of rows longer than kRowCap: it
+// needs only the count's outputs and writes rows the row copy skips, so it
+// runs beside the copy (fork: recorded on the caller's stream at the end of
+// _count; join: the caller's stream waits for it).  Created once, never freed.
+struct FrsSide {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+static FrsSide& frs_side() {
+    static std::mutex mu;
+    static FrsSide side[64];
+    int dev = 0;
+    O3DML_CHECK_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(mu);
+    FrsSide& x = side[dev & 63];
+    if (!x.s) {
+        O3DML_CHECK_HIP(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking));
+        O3DML_CHECK_HIP(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming));
+        O3DML_CHECK_HIP(hipEventCreateWithFlags(&x.join, hipEventDisableTiming));
+    }
+    return x;
+}
+
+// [total, overflow count] straight into the caller's pinned host buffer
+__global__ void frs_totals_kernel(const int64_t* __restrict__ rs, int64_t m, const int64_t* __restrict__ scalars,
+                                  int64_t* __restrict__ out) {
+    if (threadIdx.x == 0) {
+        out[0] = rs[m];
+        out[1] = scalars[0];
+    }
+}
+
 static bool rel16_rows(int64_t n_batch, const int64_t* prs_host, int64_t n_queries) {
     if (!prs_host || !O3DML_FRS_REL16) return false;
     if (n_queries > 0x7FFFFFFF / (2 * kRowCap)) return false;  // the rows' buffer resource covers < 2^31 B
@@ -1090,6 +1123,17 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     }
     Workspace sws = ws;
     prim::scan<uint32_t, int64_t>(pl.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
+    O3DML_CHECK_HIP(hipEventRecord(frs_side().fork, st));  // the overflow re-run may start here
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_fixed_radius_search_totals(const int64_t* neighbors_row_splits, int64_t n_queries,
+                                               void* workspace, int64_t* totals, void* stream) {
+    O3DML_GUARD_BEGIN
+    hipStream_t st = as_stream(stream);
+    frs_totals_kernel<<<1, 64, 0, st>>>(neighbors_row_splits, n_queries, static_cast<const int64_t*>(workspace),
+                                        totals);
+    O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }
 
@@ -1157,6 +1201,10 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
     // rows; the overflow count stays on the device (no host round trip), so a
     // fixed grid strides over however many there are (usually none)
     if (!(parts & 2)) return 0;  // the caller read a zero overflow count
+    FrsSide& side = frs_side();
+    O3DML_CHECK_HIP(hipStreamWaitEvent(side.s, side.fork, 0));
+    const hipStream_t st_main = st;
+    st = side.s;
     const unsigned go = static_cast<unsigned>(std::min<int64_t>(n_queries, 256));
     const float4* qraw = reinterpret_cast<const float4*>(queries);  // MODE 1 reads [M, 3] via the over list
     if (index_bits == 32)
@@ -1175,5 +1223,7 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
                                  points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
                                  static_cast<int64_t*>(neighbors_index), dist, pl.dir, pl.dir_cap, rs + n_queries,
                                  capacity);
+    O3DML_CHECK_HIP(hipEventRecord(side.join, st));
+    O3DML_CHECK_HIP(hipStreamWaitEvent(st_main, side.join, 0));
     O3DML_GUARD_END
 }

@@ -153,13 +153,17 @@ def _frs_count_fill(rs, state, key, m, index_dtype, extra=None):
     than 64 is launched only when there are any.  extra: more device scalars
     read in that transfer.  Returns (idx, dist, [total] + extra values)."""
     guess = _FRS_DENSITY.get(key)
-    ws = state[1]
-    n_over_dev = ws[:8].view(torch.int64)
+    ws, st = state[1], state[2]
     # the totals go to pinned host memory right behind the count; the host
-    # waits for that copy only, not for the fill queued after it
-    vals_dev = torch.stack([rs[-1], n_over_dev[0]] + list(extra or ()))
-    host = _pinned_slot(rs.device, vals_dev.numel())
-    host.copy_(vals_dev, non_blocking=True)
+    # waits for them only, not for the fill queued after them
+    if extra:
+        n_over_dev = ws[:8].view(torch.int64)
+        vals_dev = torch.stack([rs[-1], n_over_dev[0]] + list(extra))
+        host = _pinned_slot(rs.device, vals_dev.numel())
+        host.copy_(vals_dev, non_blocking=True)
+    else:  # one small kernel writes both into the pinned buffer
+        host = _pinned_slot(rs.device, 2)
+        _lib.call("o3dml_fixed_radius_search_totals", ptr(rs), m, ptr(ws), host.data_ptr(), st)
     ready = torch.cuda.Event()
     ready.record(torch.cuda.current_stream(rs.device))
     if guess is None or m == 0:
