@@ -679,13 +679,23 @@ __device__ __forceinline__ int32_t wave_ext_i(int32_t v) {
 __device__ __forceinline__ int32_t wave_min_i(int32_t v) { return wave_ext_i<false>(v); }
 __device__ __forceinline__ int32_t wave_max_i(int32_t v) { return wave_ext_i<true>(v); }
 
-__global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __restrict__ pts, int64_t n_pts,
+__global__ void __launch_bounds__(256) bucket_classes_kernel(const float* __restrict__ points,
+                                                             const uint32_t* __restrict__ hti,
+                                                             float4* __restrict__ pts, int64_t n_pts,
                                                              const uint32_t* __restrict__ cs,
                                                              const uint32_t* __restrict__ hts, int nb, float inv,
                                                              float cell, uint32_t* __restrict__ dir, int64_t dir_cap,
                                                              uint32_t* __restrict__ qsel,
-                                                             uint32_t* __restrict__ qbatch) {
+                                                             uint32_t* __restrict__ qbatch,
+                                                             int64_t* __restrict__ zero_a, int n_zero_a,
+                                                             int64_t* __restrict__ zero_b) {
     constexpr int E = kSelfChunk / 64;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const float inf = __builtin_huge_valf();
+        pts[n_pts] = make_float4(inf, inf, inf, 0.f);  // the far sentinel: beyond every radius
+        for (int j = 0; j < n_zero_a; ++j) zero_a[j] = 0;  // zeroed words of the caller
+        if (zero_b) *zero_b = 0;
+    }
     __shared__ uint32_t s_hts[kLdsSplits];
     __shared__ uint32_t wcnt[4][32];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -696,7 +706,7 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
     const uint32_t* H = lds_hts ? s_hts : hts;
     const int64_t nbins = H[nb];
     const bool with_dir = dir != nullptr && nbins <= dir_cap;  // else the search streams whole buckets
-    float4* p2 = const_cast<float4*>(pts) + n_pts + 1;
+    float4* p2 = pts + n_pts + 1;
     const float inf = __builtin_huge_valf();
     const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
     const uint64_t lt = lanemask_lt();
@@ -718,8 +728,17 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
             int32_t vx[E], vy[E], vz[E];
             uint32_t oct[E];
             int rows = 0;
-            auto load_chunk = [&](uint32_t c0, uint32_t len) {
+            // the bucket's points gathered through Open3D's hash_table_index;
+            // the first pass also writes them to pts in that order (one
+            // bucket = one contiguous 16-B-per-point stream for the search)
+            auto load_chunk = [&](uint32_t c0, uint32_t len, bool store) {
                 rows = static_cast<int>((len + 63) >> 6);  // rows past it are skipped (uniform)
+                uint32_t id[E];
+#pragma unroll
+                for (int h = 0; h < E; ++h) {
+                    const uint32_t i = lane + 64 * h;
+                    id[h] = h < rows && i < len ? hti[c0 + i] : 0u;
+                }
 #pragma unroll
                 for (int h = 0; h < E; ++h) {
                     if (h >= rows) {
@@ -728,7 +747,9 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
                         continue;
                     }
                     const uint32_t i = lane + 64 * h;
-                    p[h] = i < len ? pts[c0 + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const float* q = points + 3 * static_cast<int64_t>(id[h]);
+                    p[h] = i < len ? make_float4(q[0], q[1], q[2], __uint_as_float(id[h])) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (store && i < len) pts[c0 + i] = p[h];
                     // the 2r-voxel as the hash build computes it; the octant
                     // (query order only) from the fractional part
                     const float fx = p[h].x * inv, fy = p[h].y * inv, fz = p[h].z * inv;
@@ -753,7 +774,7 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
             const bool one_chunk = e - s <= static_cast<uint32_t>(kSelfChunk);
             for (uint32_t c0 = s; c0 < e; c0 += kSelfChunk) {
                 const uint32_t len = min(e - c0, static_cast<uint32_t>(kSelfChunk));
-                load_chunk(c0, len);
+                load_chunk(c0, len, true);
                 if (c0 == s) {
                     ax = rdlane(vx[0], 0);
                     ay = rdlane(vy[0], 0);
@@ -826,7 +847,7 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float4* __res
             uint32_t run0 = 0, run1 = n0, run2 = n0 + n1;
             for (uint32_t c0 = s; c0 < e; c0 += kSelfChunk) {
                 const uint32_t len = min(e - c0, static_cast<uint32_t>(kSelfChunk));
-                if (!one_chunk) load_chunk(c0, len);
+                if (!one_chunk) load_chunk(c0, len, false);
                 if (qsel && lane < 32) wcnt[wv][lane] = 0;
                 __builtin_amdgcn_wave_barrier();
                 uint32_t dig[E], loff[E];
@@ -1077,18 +1098,16 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     const int batch_bits = prim::bits_needed(static_cast<uint64_t>(n_batch - 1));
     const uint32_t* qkeys;
     int bshift;
-    // also zeroes the plan scalars and neighbors_row_splits[0]
-    gather_sorted_points_kernel<<<xcd_grid(n_points, 256), 256, 0, st>>>(points, hash_table_index, n_points, pl.pts, 1,
-                                                                        pl.scalars, 4, neighbors_row_splits);
-    O3DML_LAUNCH_CHECK();
     const bool self_order = self_search && frs_self_order(n_batch, points_row_splits_host, n_points);
-    // class sub-lists + directory; for a self search also the query order:
-    // Open3D's bucket order with the (voxel, octant) groups made adjacent
-    // inside each bucket — no sort of the queries at all
+    // the points in Open3D bucket order, class sub-lists + directory; for a
+    // self search also the query order: Open3D's bucket order with the
+    // (voxel, octant) groups made adjacent inside each bucket — no sort of the
+    // queries at all.  Also zeroes the plan scalars and neighbors_row_splits[0].
     bucket_classes_kernel<<<static_cast<unsigned>(std::min<int64_t>(ceil_div(n_points, 64 * 4), 1 << 16)), 256, 0,
-                            st>>>(pl.pts, n_points, hash_table_cell_splits, hash_table_splits, (int)n_batch, inv,
-                                  2.0f * radius, pl.dir, pl.dir_cap, self_order ? pl.qorder : nullptr,
-                                  self_order ? pl.keys : nullptr);
+                            st>>>(points, hash_table_index, pl.pts, n_points, hash_table_cell_splits,
+                                  hash_table_splits, (int)n_batch, inv, 2.0f * radius, pl.dir, pl.dir_cap,
+                                  self_order ? pl.qorder : nullptr, self_order ? pl.keys : nullptr, pl.scalars, 4,
+                                  neighbors_row_splits);
     O3DML_LAUNCH_CHECK();
     if (self_order) {
         qkeys = pl.keys;
