@@ -36,7 +36,7 @@ def _close(a, b, rtol=RTOL):
     assert np.abs(a - b).max() <= rtol * scale, f"max err {np.abs(a - b).max() / scale:.3e} (rel to max)"
 
 
-@pytest.mark.parametrize("cin,cout", [(32, 32), (3, 16), (64, 96), (96, 224)])
+@pytest.mark.parametrize("cin,cout", [(32, 32), (3, 16), (64, 96), (96, 224), (64, 128)])
 def test_submanifold_conv_forward(cuda, cin, cout):
     from o3dml_amd import layers
     pos = _voxels(4000, 24, cin)
