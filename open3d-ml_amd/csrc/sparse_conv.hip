@@ -34,7 +34,10 @@ namespace o3dml {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kGemmThreads = 256; // 4 waves
+#ifndef O3DML_GEMM_THREADS
+#define O3DML_GEMM_THREADS 256
+#endif
+constexpr int kGemmThreads = O3DML_GEMM_THREADS;  // 4 waves
 
 // --------------------------------------------------------------------------
 // kernel maps
@@ -409,6 +412,9 @@ __device__ __forceinline__ void glds16(const float* g, float* lds_wave_base) {
 
 // DMA of one stage (offset k, channels [c0, c0+32)) into abuf / bbuf, plus the
 // row factors of lane (i, h)'s row i into st.
+// BREG: B (the filters, L2-resident) as fragment-shaped 16-B loads straight
+// into st.b instead of through LDS — half the LDS per wave, so more waves.
+template <bool BREG>
 __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_t* mtile, int K, int k, int c0,
                                           int lane, int64_t o, int i, int col0, const float* __restrict__ src,
                                           const float* __restrict__ sscale, const float* __restrict__ pscale,
@@ -426,10 +432,27 @@ __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_
         const int32_t m = mq[q];
         const float* ga = (m >= 0 && c < cin) ? src + static_cast<int64_t>(m) * cin + c : g_zero_page;
         glds16(ga, abuf + 256 * q);
-        const int cc = col0 + r;
-        const float* gb = (live && cc < cout && c < cin) ? Wt + (static_cast<int64_t>(k) * cout + cc) * cin + c
-                                                          : g_zero_page;
-        glds16(gb, bbuf + 256 * q);
+        if constexpr (!BREG) {
+            const int cc = col0 + r;
+            const float* gb = (live && cc < cout && c < cin) ? Wt + (static_cast<int64_t>(k) * cout + cc) * cin + c
+                                                              : g_zero_page;
+            glds16(gb, bbuf + 256 * q);
+        }
+    }
+    if constexpr (BREG) {  // lane (i, h): channels [c0 + 16h, +16) of column col0 + i
+        const int cb = c0 + 16 * (lane >> 5);
+        const int col = col0 + i;
+        const bool colv = live && col < cout;
+        const float* wr = Wt + (static_cast<int64_t>(k) * cout + (colv ? col : 0)) * cin;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = cb + 4 * q;
+            const float4 v = *reinterpret_cast<const float4*>((colv && c < cin) ? wr + c : g_zero_page);
+            st.b[4 * q] = v.x;
+            st.b[4 * q + 1] = v.y;
+            st.b[4 * q + 2] = v.z;
+            st.b[4 * q + 3] = v.w;
+        }
     }
     const bool valid = mi >= 0;
     st.s1 = *(sscale ? sscale + (valid ? mi : 0) : g_one_page);
@@ -437,24 +460,27 @@ __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_
     st.v = valid ? 1.f : 0.f;
 }
 
+template <bool BREG>
 __device__ __forceinline__ void lds_read(const float* abuf, const float* bbuf, int i, int h, GemmStage& st) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int slot = (4 * h + q) ^ (i & 7);
         const float4 va = *reinterpret_cast<const float4*>(abuf + 32 * i + 4 * slot);
-        const float4 vb = *reinterpret_cast<const float4*>(bbuf + 32 * i + 4 * slot);
         st.a[4 * q] = va.x;
         st.a[4 * q + 1] = va.y;
         st.a[4 * q + 2] = va.z;
         st.a[4 * q + 3] = va.w;
-        st.b[4 * q] = vb.x;
-        st.b[4 * q + 1] = vb.y;
-        st.b[4 * q + 2] = vb.z;
-        st.b[4 * q + 3] = vb.w;
+        if constexpr (!BREG) {
+            const float4 vb = *reinterpret_cast<const float4*>(bbuf + 32 * i + 4 * slot);
+            st.b[4 * q] = vb.x;
+            st.b[4 * q + 1] = vb.y;
+            st.b[4 * q + 2] = vb.z;
+            st.b[4 * q + 3] = vb.w;
+        }
     }
 }
 
-template <bool PRE>
+template <bool PRE, bool BREG>
 __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order,
                          const int* order_flag, int K, int64_t n_out,
@@ -464,7 +490,7 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
                          float* __restrict__ out, int nsplit, float* __restrict__ part, GemmPrologue pre,
                          const float* __restrict__ residual) {
     __shared__ float lpre[PRE ? 2 * (kPreMax + 32) : 1];
-    __shared__ __attribute__((aligned(16))) float stage_all[kGemmThreads / 64][2][32 * 32];
+    __shared__ __attribute__((aligned(16))) float stage_all[kGemmThreads / 64][BREG ? 1 : 2][32 * 32];
     __shared__ int32_t mtile_all[kGemmThreads / 64][32 * 32];
     __shared__ int32_t orow_all[kGemmThreads / 64][32];
     float* lps = lpre;
@@ -486,7 +512,7 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     int32_t* mtile = mtile_all[w];
     int32_t* orow = orow_all[w];
     float* abuf = stage_all[w][0];
-    float* bbuf = stage_all[w][1];
+    float* bbuf = stage_all[w][BREG ? 0 : 1];  // unused with BREG
     if (order && *order_flag == 0) order = nullptr;  // map built without a tile order
     if (lane < 32) {
         const int64_t oo = o0 + lane;
@@ -522,10 +548,14 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
         int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
         GemmStage nx, cu;
-        lds_issue(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout, true, nx);
+        lds_issue<BREG>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout, true, nx);
         for (int j = j0; j < j1; ++j) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage j in LDS, its row factors in nx
-            lds_read(abuf, bbuf, i, h, cu);
+            lds_read<BREG>(abuf, bbuf, i, h, cu);
+            if constexpr (BREG) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) cu.b[r] = nx.b[r];
+            }
             cu.s1 = nx.s1;
             cu.s2 = nx.s2;
             cu.v = nx.v;
@@ -537,8 +567,8 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
                 k = u ? __builtin_ctz(u) : 0;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffer read out before the next DMA
-            lds_issue(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout, j + 1 < j1,
-                      nx);
+            lds_issue<BREG>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout,
+                            j + 1 < j1, nx);
             __builtin_amdgcn_sched_barrier(0);
             (void)kj;
             gemm_finish<PRE>(cu, cj, h, lps, lpb);
@@ -795,15 +825,21 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
         return e ? std::atoi(e) != 0 : true;
     }();
     TimedRegion tr("sparse_conv_gemm", st);  // the GEMM kernel alone (bench roofline)
+    static const bool breg = [] {
+        const char* e = std::getenv("O3DML_GEMM_BREG");
+        return e ? std::atoi(e) != 0 : true;
+    }();
     if (vec4 && lds_path) {
-        if (pre.scale)
-            implicit_gemm_lds_kernel<true><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, pscale, Wt,
-                                                                      cin, cout, oscale, bias, out, ns, part, pre,
-                                                                      residual);
-        else
-            implicit_gemm_lds_kernel<false><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, pscale, Wt,
-                                                                       cin, cout, oscale, bias, out, ns, part, pre,
-                                                                       residual);
+#define O3DML_GEMM_LDS(P, BR)                                                                                  \
+    implicit_gemm_lds_kernel<P, BR><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
+                                                                pscale, Wt, cin, cout, oscale, bias, out, ns,  \
+                                                                part, pre, residual)
+        if (pre.scale) {
+            if (breg) O3DML_GEMM_LDS(true, true); else O3DML_GEMM_LDS(true, false);
+        } else {
+            if (breg) O3DML_GEMM_LDS(false, true); else O3DML_GEMM_LDS(false, false);
+        }
+#undef O3DML_GEMM_LDS
     } else if (pre.scale) {
         if (vec4) O3DML_GEMM_LAUNCH(true, true); else O3DML_GEMM_LAUNCH(false, true);
     } else {
