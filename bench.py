@@ -385,20 +385,37 @@ def sparse_conv_bench(dev, reps):
     return {"voxels": int(n), "pairs": pairs, "mvoxels_per_s_layer": round(n / t_layer / 1e6, 2),
             "ms_layer": round(t_layer * 1e3, 4), "ms_gemm": round(t_gemm * 1e3, 4),
             "tflops_gemm": round(flops / t_gemm / 1e12, 3),
-            "mfma_roofline": [gemm_roofline(dev, pos, nb, kidx, pairs, c, reps) for c in (32, 128)],
-            "config": "C4: ~80k 2 cm room voxels, SparseConv 3^3 32->32 fp32, rulebook rebuilt per call",
+            "mfma_roofline": [gemm_roofline(dev, pos, nb, kidx, pairs, c, reps, mode)
+                              for mode in (0, 1) for c in (32, 128)],
+            "config": "C4: ~80k 2 cm room voxels, SparseConv 3^3 32->32 fp32 (bf16x6 MFMA products), rulebook rebuilt per call",
             "unet": scn_bench(dev, pos, reps)}
 
 
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32-input MFMA (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz
+# bf16-split products: useful f32 flop peak = bf16 peak / MFMAs per product
+MFMA_SPLIT_PEAK_TFLOPS = {6: round(MFMA_BF16_PEAK_TFLOPS / 6, 1), 3: round(MFMA_BF16_PEAK_TFLOPS / 3, 1)}
 
 
-def gemm_roofline(dev, pos, nb, kidx, pairs, ch, reps):
+def gemm_roofline(dev, pos, nb, kidx, pairs, ch, reps, mode=0):
     """MFMA roofline of the sparse-conv GEMM kernel alone (HIP events around the
     launch inside the library, o3dml_timing_*) on the C4 3^3 map (lattice
     rulebook, cached and tile-ordered as in SparseConvUnet) at ch -> ch
     channels: useful flops 2 * pairs * ch^2 per launch over the kernel time,
-    against the fp32 MFMA peak."""
+    against the MFMA peak of the product precision in use — bf16x6 (mode 0,
+    the default: each f32 operand as hi + mid + lo bf16 terms, six bf16 MFMAs
+    per f32 product, peak = bf16 peak / 6), exact f32-input MFMA (mode 1) or
+    bf16x3 (mode 2, peak = bf16 / 3)."""
+    from o3dml_amd import _lib, layers, sparse_conv as sc
+    lib = _lib.load()
+    prev = lib.o3dml_sparse_conv_set_exact(int(mode))
+    try:
+        return _gemm_roofline(dev, pos, nb, kidx, pairs, ch, reps, mode)
+    finally:
+        lib.o3dml_sparse_conv_set_exact(prev)
+
+
+def _gemm_roofline(dev, pos, nb, kidx, pairs, ch, reps, mode):
     from o3dml_amd import _lib, layers, sparse_conv as sc
     torch.manual_seed(0)
     conv = layers.SparseConv(ch, ch, [3, 3, 3], use_bias=False).to(dev)
@@ -416,9 +433,11 @@ def gemm_roofline(dev, pos, nb, kidx, pairs, ch, reps):
         lib.o3dml_timing_enable(0)
     t = ms / max(cnt, 1) / 1e3
     tf = 2.0 * pairs * ch * ch / t / 1e12 if t > 0 else 0.0
-    return {"channels": ch, "kernel": "implicit_gemm_lds_kernel", "kernel_us": round(t * 1e6, 2),
-            "bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4)}
+    peak = MFMA_F32_PEAK_TFLOPS if mode == 1 else MFMA_SPLIT_PEAK_TFLOPS[6 if mode == 0 else 3]
+    return {"channels": ch, "kernel": "implicit_gemm_lds_kernel",
+            "products": {0: "bf16x6", 1: "f32", 2: "bf16x3"}[mode],
+            "kernel_us": round(t * 1e6, 2), "bound": "mfma", "achieved": round(tf, 2), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(tf / peak, 4)}
 
 
 def scn_bench(dev, pos, reps):
@@ -440,7 +459,7 @@ def scn_bench(dev, pos, reps):
         torch.cuda.synchronize(dev)
         dt = (time.perf_counter() - t) / reps
     return {"ms_per_frame": round(dt * 1e3, 3), "mvoxels_per_s": round(pos.shape[0] / dt / 1e6, 3),
-            "config": "SparseConvUnet m=32 residual reps=1 (sparseconvunet_scannet.yml), fp32, eval"}
+            "config": "SparseConvUnet m=32 residual reps=1 (sparseconvunet_scannet.yml), fp32 (bf16x6 MFMA products), eval"}
 
 
 def timed_run(step, steps, warmup, world, sync):

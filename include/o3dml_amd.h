@@ -246,6 +246,17 @@ int o3dml_sparse_conv_backward(const float* filters, int K, int cin, int cout, c
                                const float* grad_out, int64_t n_out, float* grad_inp, float* grad_filters,
                                void* map_workspace, size_t map_workspace_bytes, void* workspace,
                                size_t workspace_bytes, void* stream);
+/* Product precision of the sparse-conv gather-GEMMs (forward, input
+ * gradient and filter gradient), all accumulating in f32:
+ *   0 (default) "bf16x6": each f32 operand split into three bf16 terms
+ *     (hi + mid + lo holds all 24 mantissa bits) and the six products down to
+ *     2^-16 relative taken on the bf16 MFMA pipe — the dropped terms are below
+ *     the f32 rounding level;
+ *   1 exact f32-input MFMA (v_mfma_f32_32x32x2_f32, bitwise an fmaf chain);
+ *   2 "bf16x3": hi + mid only, three products (~2^-17 relative per product).
+ * Env O3DML_SPARSE_CONV_EXACT sets the initial mode.  Returns the previous
+ * mode (-1 for a mode > 2, nothing changed); exact < 0 only queries. */
+int o3dml_sparse_conv_set_exact(int exact);
 int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* query_positions,
                                    const int32_t* neighbors_index, const int64_t* neighbors_row_splits,
                                    int64_t n_query, const int32_t* ksize_host, float voxel_size, int mirror,

@@ -33,6 +33,7 @@
 namespace o3dml {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #ifndef O3DML_GEMM_THREADS
 #define O3DML_GEMM_THREADS 256
@@ -480,7 +481,62 @@ __device__ __forceinline__ void lds_read(const float* abuf, const float* bbuf, i
     }
 }
 
-template <bool PRE, bool BREG>
+// f32 products on the bf16 MFMA pipe.  x = hi + mid + lo with hi =
+// rne_bf16(x), mid = rne_bf16(x - hi), lo = rne_bf16(x - hi - mid): each
+// rounding keeps 8 more significant bits, so the three terms hold all 24 bits
+// of an f32 (exact up to the last rounding, <= 2^-25 |x|).  Each bf16 x bf16
+// product is exact in the f32 accumulator.
+//  * NT = 6 (default, "bf16x6"): a*b = hh + hm + mh + hl + lh + mm, dropping
+//    terms <= 2^-24 |a*b| — the f32 rounding level, so the sums agree with the
+//    exact f32-input MFMA to within its own rounding.  Six
+//    v_mfma_f32_32x32x16_bf16 (32 cycles each) per 16 reduction steps instead
+//    of eight v_mfma_f32_32x32x2_f32 (64 cycles each): 2.7x fewer MFMA cycles.
+//  * NT = 3 ("bf16x3"): hh + hm + mh with x = hi + mid only (<= 2^-17
+//    relative per product), 5.3x fewer MFMA cycles.
+// Fragment of MFMA t (t = 0, 1) on lane (i, h): element j = stage register
+// 8t + j (channel c0 + 16h + 8t + j in the forward GEMM) — the same map on A
+// (row i) and B (column i), so any consistent permutation of the reduction.
+template <int NT>
+__device__ __forceinline__ void split_bf16x8(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        hi[j] = static_cast<__bf16>(v[j]);
+        const float r1 = v[j] - static_cast<float>(hi[j]);
+        mid[j] = static_cast<__bf16>(r1);
+        if constexpr (NT == 6) lo[j] = static_cast<__bf16>(r1 - static_cast<float>(mid[j]));
+    }
+}
+
+template <int NT, class Stage>
+__device__ __forceinline__ void mfma_stage_split(const Stage& cu, f32x16& acc) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        bf16x8 ah, am, al, bh, bm, bl;
+        split_bf16x8<NT>(cu.a + 8 * t, ah, am, al);
+        split_bf16x8<NT>(cu.b + 8 * t, bh, bm, bl);
+        if constexpr (NT == 6) {  // smallest terms first
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+    }
+}
+
+// product precision of a GEMM instantiation: 0 = exact f32 MFMA, 3 / 6 = bf16 split
+template <int NT, class Stage>
+__device__ __forceinline__ void mfma_stage(const Stage& cu, f32x16& acc) {
+    if constexpr (NT == 0) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cu.a[r], cu.b[r], acc, 0, 0, 0);
+    } else {
+        mfma_stage_split<NT>(cu, acc);
+    }
+}
+
+template <bool PRE, bool BREG, int NT = 0>
 __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order,
                          const int* order_flag, int K, int64_t n_out,
@@ -572,8 +628,7 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
             __builtin_amdgcn_sched_barrier(0);
             (void)kj;
             gemm_finish<PRE>(cu, cj, h, lps, lpb);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cu.a[r], cu.b[r], acc, 0, 0, 0);
+            mfma_stage<NT>(cu, acc);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead DMA has landed before the wave exits
     }
@@ -662,6 +717,7 @@ __device__ __forceinline__ void dw_finish(DwStage& st, int base, int h, const fl
     }
 }
 
+template <int NT>
 __global__ void __launch_bounds__(64)
 dweight_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ po, const int64_t* __restrict__ kstart, int K,
                int nchunk, const float* __restrict__ src, const float* __restrict__ sscale,
@@ -706,8 +762,7 @@ dweight_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ po, 
             const bool more = j + 1 < nst;
             if (more) dw_load(nxt, 32 * (j + 1), h, lo, lm, lra, lrb, src, g, cin, cout, ci0 + i, co0 + i);
             dw_finish(cur, 32 * j, h, lra, lrb);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.a[r], cur.b[r], acc, 0, 0, 0);
+            mfma_stage<NT>(cur, acc);  // split forms: element j of MFMA t = pair 2(8t + j) + h
             if (!more) break;
             cur = nxt;
         }
@@ -786,6 +841,23 @@ constexpr int64_t kGemmTargetWaves = 4096;
 constexpr int kGemmMinStages = 4;
 constexpr int64_t kGemmSplitBytes = int64_t(64) << 20;
 
+// Product precision of the gather-GEMMs (mfma_stage_split): 0 = bf16x6
+// (default, f32-accurate), 1 = exact f32-input MFMA, 2 = bf16x3.  Env
+// O3DML_SPARSE_CONV_EXACT sets the initial mode; o3dml_sparse_conv_set_exact.
+static int g_gemm_mode = -1;
+static int gemm_mode() {
+    if (g_gemm_mode < 0) {
+        const char* e = std::getenv("O3DML_SPARSE_CONV_EXACT");
+        const int v = e ? std::atoi(e) : 0;
+        g_gemm_mode = (v == 1 || v == 2) ? v : 0;
+    }
+    return g_gemm_mode;
+}
+static int gemm_nt() {  // template argument of the kernels: 0 exact, 3, 6 splits
+    const int m = gemm_mode();
+    return m == 1 ? 0 : (m == 2 ? 3 : 6);
+}
+
 static int gemm_splits(int64_t n_out, int K, int cin, int cout) {
     if (n_out <= 0 || cout <= 0) return 1;
     static const int64_t target = [] {
@@ -830,14 +902,19 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
         return e ? std::atoi(e) != 0 : true;
     }();
     if (vec4 && lds_path) {
-#define O3DML_GEMM_LDS(P, BR)                                                                                  \
-    implicit_gemm_lds_kernel<P, BR><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
-                                                                pscale, Wt, cin, cout, oscale, bias, out, ns,  \
-                                                                part, pre, residual)
-        if (pre.scale) {
-            if (breg) O3DML_GEMM_LDS(true, true); else O3DML_GEMM_LDS(true, false);
+#define O3DML_GEMM_LDS(P, BR, X)                                                                                  \
+    implicit_gemm_lds_kernel<P, BR, X><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
+                                                                   pscale, Wt, cin, cout, oscale, bias, out, ns,  \
+                                                                   part, pre, residual)
+        const int nt = gemm_nt();
+        if (nt == 6) {
+            if (pre.scale) O3DML_GEMM_LDS(true, true, 6); else O3DML_GEMM_LDS(false, true, 6);
+        } else if (nt == 3) {
+            if (pre.scale) O3DML_GEMM_LDS(true, true, 3); else O3DML_GEMM_LDS(false, true, 3);
+        } else if (pre.scale) {
+            if (breg) O3DML_GEMM_LDS(true, true, 0); else O3DML_GEMM_LDS(true, false, 0);
         } else {
-            if (breg) O3DML_GEMM_LDS(false, true); else O3DML_GEMM_LDS(false, false);
+            if (breg) O3DML_GEMM_LDS(false, true, 0); else O3DML_GEMM_LDS(false, false, 0);
         }
 #undef O3DML_GEMM_LDS
     } else if (pre.scale) {
@@ -1405,9 +1482,16 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
         O3DML_LAUNCH_CHECK();
         dim3 gg(static_cast<unsigned>(ceil_div(cin, 32) * ceil_div(cout, 32)), static_cast<unsigned>(K),
                 static_cast<unsigned>(nchunk));
-        dweight_kernel<<<gg, 64, 0, st>>>(map, po, kstart, K, nchunk, inp_features, inp_importance,
-                                                    has_neighbors_importance ? pscale : nullptr, grad_out, os, cin,
-                                                    cout, part);
+#define O3DML_DW(NT)                                                                                      \
+    dweight_kernel<NT><<<gg, 64, 0, st>>>(map, po, kstart, K, nchunk, inp_features, inp_importance,        \
+                                          has_neighbors_importance ? pscale : nullptr, grad_out, os, cin, \
+                                          cout, part)
+        switch (gemm_nt()) {
+            case 0: O3DML_DW(0); break;
+            case 3: O3DML_DW(3); break;
+            default: O3DML_DW(6); break;
+        }
+#undef O3DML_DW
         O3DML_LAUNCH_CHECK();
         if (nchunk > 1) {
             reduce_slabs_kernel<<<stream_grid(KC, 256), 256, 0, st>>>(part, K, nchunk,
@@ -1419,6 +1503,15 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
 }
 
 // ksize_host[3] = filter dims (k0,k1,k2) = (z,y,x) extents.
+O3DML_API int o3dml_sparse_conv_set_exact(int exact) {
+    const int prev = gemm_mode();
+    if (exact >= 0) {
+        if (exact > 2) return -1;
+        g_gemm_mode = exact;
+    }
+    return prev;
+}
+
 O3DML_API int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* query_positions,
                                              const int32_t* neighbors_index, const int64_t* neighbors_row_splits,
                                              int64_t n_query, const int32_t* ksize_host, float voxel_size,

@@ -104,6 +104,7 @@ SIGNATURES = {
     "o3dml_sparse_conv_backward_workspace_size": (c_sz, [c_i64, c_i64, c_i32, c_i32, c_i32]),
     "o3dml_sparse_conv_backward": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i64, c_p,
                                            c_p, c_p, c_sz, c_p, c_sz, c_p]),
+    "o3dml_sparse_conv_set_exact": (c_i32, [c_i32]),
     "o3dml_sparse_conv_kernel_index": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_i32, c_p, c_p]),
     # ragged.hip
     "o3dml_ragged_to_dense": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p]),

@@ -184,3 +184,47 @@ def test_lattice_rulebook_falls_back_off_lattice(cuda):
     ok = O.kernel_index(jitter, jitter, oi, ors, [3, 3, 3], 1.0)
     ref = O.sparse_conv(conv.kernel.detach().cpu().numpy(), feat.cpu().numpy(), oi, ok, ors)
     _close(out.cpu().numpy(), ref + conv.bias.detach().cpu().numpy())
+
+
+@pytest.mark.parametrize("cin,cout", [(32, 32), (64, 128), (3, 48)])
+def test_bf16_split_products_match_exact_f32(cuda, cin, cout):
+    """Product precisions of the gather-GEMMs against a float64 reference:
+    the default bf16x6 (each f32 operand as hi + mid + lo bf16, six products)
+    must be as accurate as the exact f32-input MFMA kernel (within a few times
+    its own f32 rounding error); bf16x3 (two terms, three products) within the
+    north-star 1e-4.  Forward, input gradient and filter gradient; features
+    span six decades of magnitude across channels."""
+    from o3dml_amd import _lib, ops
+    lib = _lib.load()
+    pos = _voxels(3000, 20, 11 + cin)
+    oi, ors, _ = O.fixed_radius_search(pos, pos, 1.5, metric="Linf")
+    ok = O.kernel_index(pos, pos, oi, ors, [3, 3, 3], 1.0)
+    gen = torch.Generator().manual_seed(cin + cout)
+    W = torch.randn(3, 3, 3, cin, cout, dtype=torch.float64, generator=gen) * 0.1
+    x = torch.randn(len(pos), cin, dtype=torch.float64, generator=gen) * \
+        10.0 ** torch.randint(-3, 4, (1, cin), generator=gen).double()
+    g = torch.randn(len(pos), cout, dtype=torch.float64, generator=gen)
+    W64, x64 = W.clone().requires_grad_(), x.clone().requires_grad_()
+    ref = _csr_conv64(W64, x64, torch.from_numpy(oi), torch.from_numpy(ok), torch.from_numpy(ors))
+    ref.backward(g)
+    refs = [ref.detach().numpy(), x64.grad.numpy(), W64.grad.numpy()]
+    errs = {}
+    prev = lib.o3dml_sparse_conv_set_exact(-1)
+    assert prev in (0, 1, 2)
+    assert lib.o3dml_sparse_conv_set_exact(3) == -1 and lib.o3dml_sparse_conv_set_exact(-1) == prev
+    try:
+        for mode in (0, 1, 2):
+            lib.o3dml_sparse_conv_set_exact(mode)
+            Wd = W.float().to(cuda).requires_grad_()
+            xd = x.float().to(cuda).requires_grad_()
+            out = ops.sparse_conv(Wd, xd, torch.empty(0), torch.from_numpy(oi), torch.from_numpy(ok),
+                                  torch.empty(0), torch.from_numpy(ors))
+            out.backward(g.float().to(cuda))
+            got = [out.detach().cpu().numpy(), xd.grad.cpu().numpy(), Wd.grad.cpu().numpy()]
+            errs[mode] = [np.abs(a - b).max() / (np.abs(b).max() + 1e-30) for a, b in zip(got, refs)]
+            for a, b in zip(got, refs):
+                _close(a, b)
+    finally:
+        lib.o3dml_sparse_conv_set_exact(prev)
+    for e6, e1 in zip(errs[0], errs[1]):
+        assert e6 <= 3 * e1 + 1e-7, (errs[0], errs[1])
