@@ -687,7 +687,7 @@ __global__ void pair_lists_kernel(const int32_t* __restrict__ map, int64_t n_out
 // pair records (out row, in row, scales) are staged in LDS kDwSub at a time,
 // so a stage's gathers depend on LDS reads only and the next stage's gathers
 // are in flight while the current 16 MFMAs run.  No barriers beyond the wave.
-// part[(k*nchunk + ch)][cin][cout].
+// part[chunk][cin][cout] (dw_plan_kernel).
 constexpr int kDwSub = 512;
 
 struct DwStage {
@@ -696,9 +696,11 @@ struct DwStage {
 
 __device__ __forceinline__ void dw_load(DwStage& st, int base, int h, const int32_t* lo, const int32_t* lm,
                                         const float* lra, const float* lrb, const float* __restrict__ src,
-                                        const float* __restrict__ g, int cin, int cout, int ci, int co) {
-    // unconditional loads, absent data read from the zero page (see gemm_load)
-    const bool cv = ci < cin, ov = co < cout;
+                                        const float* __restrict__ g, int cin, int cout, int ci, int co,
+                                        bool live = true) {
+    // unconditional loads, absent data read from the zero page (see gemm_load);
+    // a dead stage (past the sub-chunk) reads only the zero page
+    const bool cv = live && ci < cin, ov = live && co < cout;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
         const int pp = base + 2 * s + h;
@@ -717,22 +719,46 @@ __device__ __forceinline__ void dw_finish(DwStage& st, int base, int h, const fl
     }
 }
 
+// Chunk plan of the dW pair lists (one thread): chunks of one length L over
+// every offset's list, so the waves get equal pair counts however unevenly the
+// offsets are used (the centre offset of a submanifold conv has every output,
+// corner offsets a fraction: per-offset chunk counts left the centre's waves
+// 3x longer than the average).  plan[k] = first chunk (= partial slab) of
+// offset k, plan[K] = number of chunks, plan[K + 1] = L.  direct: one chunk
+// per offset (slab k = grad_filters[k], no reduce).
+__global__ void dw_plan_kernel(const int64_t* __restrict__ kstart, int K, int64_t max_chunks, int direct,
+                               int64_t* __restrict__ plan) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int64_t P = kstart[K];
+    // smallest L with sum_k ceil(n_k / L) <= max_chunks: L = ceil(P / (max_chunks - K)) suffices
+    const int64_t L = direct ? (int64_t(1) << 62)
+                             : max<int64_t>(1, (P + (max_chunks - K) - 1) / max<int64_t>(1, max_chunks - K));
+    int64_t c = 0;
+    for (int k = 0; k < K; ++k) {
+        plan[k] = c;
+        c += direct ? 1 : (kstart[k + 1] - kstart[k] + L - 1) / L;
+    }
+    plan[K] = c;
+    plan[K + 1] = L;
+}
+
 template <int NT>
 __global__ void __launch_bounds__(64)
 dweight_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ po, const int64_t* __restrict__ kstart, int K,
-               int nchunk, const float* __restrict__ src, const float* __restrict__ sscale,
+               const int64_t* __restrict__ plan, const float* __restrict__ src, const float* __restrict__ sscale,
                const float* __restrict__ pscale, const float* __restrict__ g, const float* __restrict__ oscale, int cin,
                int cout, float* __restrict__ part) {
     __shared__ int32_t lo[kDwSub], lm[kDwSub];
     __shared__ float lra[kDwSub], lrb[kDwSub];
     const int ncot = (cout + 31) >> 5;
     const int ci0 = (blockIdx.x / ncot) * 32, co0 = (blockIdx.x % ncot) * 32;
-    const int k = blockIdx.y, ch = blockIdx.z;
+    const int64_t w = blockIdx.y;  // chunk = partial slab
+    if (w >= plan[K]) return;      // whole wave (grid sized for the worst case)
+    int k = 0;
+    while (plan[k + 1] <= w) ++k;  // uniform scan; empty offsets own no chunk
     const int lane = threadIdx.x, i = lane & 31, h = lane >> 5;
-    const int64_t s0 = kstart[k], e0 = kstart[k + 1];
-    const int64_t len = (e0 - s0 + nchunk - 1) / nchunk;
-    const int64_t js = s0 + ch * len;
-    const int64_t je = min(e0, js + len);
+    const int64_t js = kstart[k] + (w - plan[k]) * plan[K + 1];
+    const int64_t je = min(kstart[k + 1], js + plan[K + 1]);
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -756,21 +782,31 @@ dweight_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ po, 
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int nst = (n + 31) >> 5;
-        DwStage cur, nxt;
-        dw_load(cur, 0, h, lo, lm, lra, lrb, src, g, cin, cout, ci0 + i, co0 + i);
-        for (int j = 0;; ++j) {
-            const bool more = j + 1 < nst;
-            if (more) dw_load(nxt, 32 * (j + 1), h, lo, lm, lra, lrb, src, g, cin, cout, ci0 + i, co0 + i);
-            dw_finish(cur, 32 * j, h, lra, lrb);
-            mfma_stage<NT>(cur, acc);  // split forms: element j of MFMA t = pair 2(8t + j) + h
-            if (!more) break;
-            cur = nxt;
+        // two stage buffers in ping-pong, loads issued unconditionally (a dead
+        // stage reads the zero page): no register copy and no branch around the
+        // loads, so the next stage's loads stay in flight under these MFMAs
+        // (a `cur = nxt` copy made every stage wait for the loads just issued)
+        DwStage sa, sb;
+        dw_load(sa, 0, h, lo, lm, lra, lrb, src, g, cin, cout, ci0 + i, co0 + i);
+        for (int j = 0;; j += 2) {
+            const bool lb = j + 1 < nst;
+            dw_load(sb, lb ? 32 * (j + 1) : 0, h, lo, lm, lra, lrb, src, g, cin, cout, ci0 + i, co0 + i, lb);
+            __builtin_amdgcn_sched_barrier(0);
+            dw_finish(sa, 32 * j, h, lra, lrb);
+            mfma_stage<NT>(sa, acc);  // split forms: element j of MFMA t = pair 2(8t + j) + h
+            if (!lb) break;
+            const bool la = j + 2 < nst;
+            dw_load(sa, la ? 32 * (j + 2) : 0, h, lo, lm, lra, lrb, src, g, cin, cout, ci0 + i, co0 + i, la);
+            __builtin_amdgcn_sched_barrier(0);
+            dw_finish(sb, 32 * (j + 1), h, lra, lrb);
+            mfma_stage<NT>(sb, acc);
+            if (!la) break;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // LDS records are rewritten by the next sub-chunk
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    float* P = part + (static_cast<int64_t>(k) * nchunk + ch) * cin * cout;
+    float* P = part + w * cin * cout;
     const int col = co0 + i;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -779,14 +815,24 @@ dweight_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ po, 
     }
 }
 
-__global__ void reduce_slabs_kernel(const float* __restrict__ part, int K, int nchunk, int64_t slab,
-                                    float* __restrict__ dw) {
+__global__ void reduce_slabs_kernel(const float* __restrict__ part, int K, const int64_t* __restrict__ plan,
+                                    int64_t slab, float* __restrict__ dw) {
     const int64_t total = static_cast<int64_t>(K) * slab;
     for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int64_t k = e / slab, r = e - k * slab;
-        float s = 0.f;
-        for (int c = 0; c < nchunk; ++c) s += part[(k * nchunk + c) * slab + r];
+        // fixed order (0 for an unused offset): 8 interleaved partial sums over
+        // the offset's chunks ascending, combined pairwise — 8 independent loads
+        // in flight per thread instead of one serial chain
+        const int64_t c0 = plan[k], c1 = plan[k + 1];
+        float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int64_t c = c0;
+        for (; c + 8 <= c1; c += 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) p[u] += part[(c + u) * slab + r];
+        }
+        for (int u = 0; c < c1; ++c, ++u) p[u] += part[c * slab + r];
+        const float s = ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
         dw[e] = s;
     }
 }
@@ -1425,7 +1471,8 @@ O3DML_API size_t o3dml_sparse_conv_backward_workspace_size(int64_t n_out, int64_
     const int nchunk = dw_chunks(n_out, K, cin, cout);
     return ws_bytes<float>(static_cast<int64_t>(K) * cin * cout) + ws_bytes<float>(n_out * cout) +
            gemm_split_bytes(n_in, K, cout, cin) + ws_bytes<int64_t>(n_out * K) * 2 + ws_bytes<int32_t>(n_out * K) +
-           ws_bytes<int64_t>(K + 1) + ws_bytes<float>(static_cast<int64_t>(K) * nchunk * cin * cout) +
+           ws_bytes<int64_t>(K + 1) + ws_bytes<int64_t>(K + 2) +
+           (nchunk > 1 ? ws_bytes<float>(static_cast<int64_t>(K) * (nchunk + 1) * cin * cout) : 0) +
            prim::scan_workspace_bytes(n_out * K);
 }
 
@@ -1472,18 +1519,21 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
         int64_t* incl = ws.take<int64_t>(n_out * K);
         int32_t* po = ws.take<int32_t>(n_out * K);
         int64_t* kstart = ws.take<int64_t>(K + 1);
+        int64_t* plan = ws.take<int64_t>(K + 2);
         const int nchunk = dw_chunks(n_out, K, cin, cout);
-        float* part = nchunk > 1 ? ws.take<float>(static_cast<int64_t>(K) * nchunk * cin * cout) : grad_filters;
+        const int64_t max_chunks = nchunk > 1 ? static_cast<int64_t>(K) * (nchunk + 1) : K;
+        float* part = nchunk > 1 ? ws.take<float>(max_chunks * cin * cout) : grad_filters;
         pair_flags_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, n_out, K, flags);
         O3DML_LAUNCH_CHECK();
         Workspace sws = ws;
         prim::scan<int64_t, int64_t>(flags, incl, n_out * K, true, sws, st);
         pair_lists_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, n_out, K, incl, po, kstart);
         O3DML_LAUNCH_CHECK();
-        dim3 gg(static_cast<unsigned>(ceil_div(cin, 32) * ceil_div(cout, 32)), static_cast<unsigned>(K),
-                static_cast<unsigned>(nchunk));
+        dw_plan_kernel<<<1, 64, 0, st>>>(kstart, K, max_chunks, nchunk > 1 ? 0 : 1, plan);
+        O3DML_LAUNCH_CHECK();
+        dim3 gg(static_cast<unsigned>(ceil_div(cin, 32) * ceil_div(cout, 32)), static_cast<unsigned>(max_chunks));
 #define O3DML_DW(NT)                                                                                      \
-    dweight_kernel<NT><<<gg, 64, 0, st>>>(map, po, kstart, K, nchunk, inp_features, inp_importance,        \
+    dweight_kernel<NT><<<gg, 64, 0, st>>>(map, po, kstart, K, plan, inp_features, inp_importance,          \
                                           has_neighbors_importance ? pscale : nullptr, grad_out, os, cin, \
                                           cout, part)
         switch (gemm_nt()) {
@@ -1494,7 +1544,7 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
 #undef O3DML_DW
         O3DML_LAUNCH_CHECK();
         if (nchunk > 1) {
-            reduce_slabs_kernel<<<stream_grid(KC, 256), 256, 0, st>>>(part, K, nchunk,
+            reduce_slabs_kernel<<<stream_grid(KC, 256), 256, 0, st>>>(part, K, plan,
                                                                       static_cast<int64_t>(cin) * cout, grad_filters);
             O3DML_LAUNCH_CHECK();
         }
