@@ -655,6 +655,167 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
 }
 
 // --------------------------------------------------------------------------
+// implicit GEMM, A tile shared by the workgroup (cout >= 64): NW waves own the
+// same 32 output rows and NW adjacent 32-column blocks, so the gathered rows
+// of a stage (32 rows x 32 channels, the bytes that bound the per-wave kernel
+// once its products run on the bf16 pipe) are fetched once per workgroup
+// instead of once per column block: each wave DMAs 4/NW of the 4 row groups
+// into a double-buffered LDS image, a barrier per stage publishes it, and
+// every wave reads the whole tile in the MFMA layout.  B (filters) stays in
+// registers per wave; stage order, split-K partition and reduction order per
+// output are those of implicit_gemm_lds_kernel (same sums).
+// --------------------------------------------------------------------------
+template <int NW>
+__device__ __forceinline__ void shared_issue(float* abuf, const int32_t* mtile, int K, int k, int c0, int lane, int w,
+                                             const float* __restrict__ src, int cin, bool live) {
+    const int sl = lane & 7;
+    int32_t mq[4 / NW];
+#pragma unroll
+    for (int t = 0; t < 4 / NW; ++t) mq[t] = live ? mtile[(8 * (w + NW * t) + (lane >> 3)) * K + k] : -1;
+#pragma unroll
+    for (int t = 0; t < 4 / NW; ++t) {
+        const int q = w + NW * t;
+        const int r = 8 * q + (lane >> 3);
+        const int c = c0 + 4 * (sl ^ (r & 7));
+        const float* ga = (mq[t] >= 0 && c < cin) ? src + static_cast<int64_t>(mq[t]) * cin + c : g_zero_page;
+        glds16(ga, abuf + 256 * q);
+    }
+}
+
+__device__ __forceinline__ void shared_regs(const int32_t* mtile, int K, int k, int c0, int lane, int64_t o, int i,
+                                            int col, const float* __restrict__ sscale,
+                                            const float* __restrict__ pscale, const float* __restrict__ Wt, int cin,
+                                            int cout, bool live, GemmStage& st) {
+    const int32_t mi = live ? mtile[i * K + k] : -1;
+    const int cb = c0 + 16 * (lane >> 5);
+    const bool colv = live && col < cout;
+    const float* wr = Wt + (static_cast<int64_t>(k) * cout + (colv ? col : 0)) * cin;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int c = cb + 4 * q;
+        const float4 v = *reinterpret_cast<const float4*>((colv && c < cin) ? wr + c : g_zero_page);
+        st.b[4 * q] = v.x;
+        st.b[4 * q + 1] = v.y;
+        st.b[4 * q + 2] = v.z;
+        st.b[4 * q + 3] = v.w;
+    }
+    const bool valid = mi >= 0;
+    st.s1 = *(sscale ? sscale + (valid ? mi : 0) : g_one_page);
+    st.s2 = *(pscale ? pscale + (valid ? o : 0) * K + k : g_one_page);
+    st.v = valid ? 1.f : 0.f;
+}
+
+template <bool PRE, int NT, int NW>
+__global__ void __launch_bounds__(NW * 64)
+implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order,
+                            const int* order_flag, int K, int64_t n_out,
+                            const float* __restrict__ src, const float* __restrict__ sscale,
+                            const float* __restrict__ pscale, const float* __restrict__ Wt /*[K][cout][cin]*/,
+                            int cin, int cout, const float* __restrict__ oscale, const float* __restrict__ bias,
+                            float* __restrict__ out, int nsplit, float* __restrict__ part, GemmPrologue pre,
+                            const float* __restrict__ residual) {
+    __shared__ float lpre[PRE ? 2 * (kPreMax + 32) : 1];
+    __shared__ __attribute__((aligned(16))) float abuf[2][32 * 32];
+    __shared__ int32_t mtile[32 * 32];
+    __shared__ int32_t orow[32];
+    const int64_t o0 = static_cast<int64_t>(blockIdx.x) * 32;
+    if (o0 >= n_out) return;  // whole workgroup, before any barrier
+    float* lps = lpre;
+    float* lpb = lpre + (PRE ? kPreMax + 32 : 0);
+    if (PRE) {
+        for (int c = threadIdx.x; c < kPreMax + 32; c += NW * 64) {
+            lps[c] = c < cin ? pre.scale[c] : 0.f;
+            lpb[c] = c < cin ? pre.shift[c] : 0.f;
+        }
+    }
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int i = lane & 31, h = lane >> 5;
+    const int col = (blockIdx.y * NW + w) * 32 + i;
+    if (order && *order_flag == 0) order = nullptr;
+    if (threadIdx.x < 32) {
+        const int64_t oo = o0 + threadIdx.x;
+        orow[threadIdx.x] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 32 * K; e += NW * 64) {
+        const int rr = e / K;
+        const int32_t orr = orow[rr];
+        mtile[e] = orr >= 0 ? map[static_cast<int64_t>(orr) * K + (e - rr * K)] : -1;
+    }
+    __syncthreads();
+    unsigned used = 0u;  // identical in every wave (same rows)
+    for (int k = h; k < K; k += 2) {
+        const uint64_t b = __ballot(mtile[i * K + k] >= 0);
+        used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
+    }
+    used = __builtin_amdgcn_readlane(used, 32) | __builtin_amdgcn_readlane(used, 0);
+    const int64_t o = orow[i] >= 0 ? orow[i] : 0;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int nch = (cin + 31) >> 5;
+    const int s = blockIdx.z;
+    const int j0 = split_stage(used, nch, K, s, nsplit);
+    const int j1 = split_stage(used, nch, K, s + 1, nsplit);
+    if (j0 < j1) {  // uniform over the workgroup
+        unsigned u = used;
+        for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
+        int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
+        GemmStage nx, cu;
+        shared_issue<NW>(abuf[0], mtile, K, k, c0, lane, w, src, cin, true);
+        shared_regs(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, true, nx);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int j = j0; j < j1; ++j) {
+            const int b = (j - j0) & 1;
+            lds_read<true>(abuf[b], nullptr, i, h, cu);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cu.b[r] = nx.b[r];
+            cu.s1 = nx.s1;
+            cu.s2 = nx.s2;
+            cu.v = nx.v;
+            const int cj = c0;
+            c0 += 32;
+            if (c0 >= cin) {
+                c0 = 0;
+                u &= u - 1u;
+                k = u ? __builtin_ctz(u) : 0;
+            }
+            const bool live = j + 1 < j1;
+            // the other buffer was last read in stage j-1, before that stage's barrier
+            shared_issue<NW>(abuf[b ^ 1], mtile, K, k, c0, lane, w, src, cin, live);
+            shared_regs(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, live, nx);
+            __builtin_amdgcn_sched_barrier(0);
+            gemm_finish<PRE>(cu, cj, h, lps, lpb);
+            mfma_stage<NT>(cu, acc);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own share of stage j+1 landed
+            __syncthreads();  // every share landed; stage j's buffer free
+        }
+    }
+    if (nsplit > 1) {
+        float* P = part + static_cast<int64_t>(s) * n_out * cout;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t orr = orow[(r & 3) + 8 * (r >> 2) + 4 * h];
+            if (orr >= 0 && col < cout) P[orr * cout + col] = acc[r];
+        }
+        return;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t orr = orow[(r & 3) + 8 * (r >> 2) + 4 * h];
+        if (orr >= 0 && col < cout) {
+            float v = acc[r];
+            if (oscale) v *= oscale[orr];
+            if (bias) v += bias[col];
+            if (residual) v += residual[orr * cout + col];
+            out[orr * cout + col] = v;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
 // dW: per offset pair lists, split-K slabs
 // --------------------------------------------------------------------------
 // k-major flags: flag[k*n_out + o] = map[o*K+k] >= 0
@@ -947,7 +1108,33 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
         const char* e = std::getenv("O3DML_GEMM_BREG");
         return e ? std::atoi(e) != 0 : true;
     }();
-    if (vec4 && lds_path) {
+    static const bool shared_path = [] {
+        const char* e = std::getenv("O3DML_GEMM_SHARED");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    if (vec4 && lds_path && shared_path && cout >= 64) {
+        // A tile shared by NW column-block waves (implicit_gemm_shared_kernel)
+        const int nw = (cout % 128 == 0) ? 4 : 2;
+        const dim3 gs(static_cast<unsigned>(ceil_div(n_out, 32)), static_cast<unsigned>(ceil_div(cout, 32 * nw)),
+                      static_cast<unsigned>(ns));
+#define O3DML_GEMM_SH(P, X, W)                                                                               \
+    implicit_gemm_shared_kernel<P, X, W><<<gs, W * 64, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
+                                                                pscale, Wt, cin, cout, oscale, bias, out, ns,  \
+                                                                part, pre, residual)
+#define O3DML_GEMM_SH_NT(P, W)                          \
+    switch (gemm_nt()) {                                \
+        case 0: O3DML_GEMM_SH(P, 0, W); break;          \
+        case 3: O3DML_GEMM_SH(P, 3, W); break;          \
+        default: O3DML_GEMM_SH(P, 6, W); break;         \
+    }
+        if (nw == 4) {
+            if (pre.scale) { O3DML_GEMM_SH_NT(true, 4) } else { O3DML_GEMM_SH_NT(false, 4) }
+        } else {
+            if (pre.scale) { O3DML_GEMM_SH_NT(true, 2) } else { O3DML_GEMM_SH_NT(false, 2) }
+        }
+#undef O3DML_GEMM_SH_NT
+#undef O3DML_GEMM_SH
+    } else if (vec4 && lds_path) {
 #define O3DML_GEMM_LDS(P, BR, X)                                                                                  \
     implicit_gemm_lds_kernel<P, BR, X><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
                                                                    pscale, Wt, cin, cout, oscale, bias, out, ns,  \
