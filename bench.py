@@ -434,7 +434,7 @@ def _gemm_roofline(dev, pos, nb, kidx, pairs, ch, reps, mode):
     t = ms / max(cnt, 1) / 1e3
     tf = 2.0 * pairs * ch * ch / t / 1e12 if t > 0 else 0.0
     peak = MFMA_F32_PEAK_TFLOPS if mode == 1 else MFMA_SPLIT_PEAK_TFLOPS[6 if mode == 0 else 3]
-    return {"channels": ch, "kernel": "implicit_gemm_lds_kernel",
+    return {"channels": ch, "kernel": "implicit_gemm_shared_kernel" if ch >= 64 else "implicit_gemm_lds_kernel",
             "products": {0: "bf16x6", 1: "f32", 2: "bf16x3"}[mode],
             "kernel_us": round(t * 1e6, 2), "bound": "mfma", "achieved": round(tf, 2), "peak": peak,
             "unit": "TFLOP/s", "frac": round(tf / peak, 4)}

@@ -665,15 +665,19 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
 // registers per wave; stage order, split-K partition and reduction order per
 // output are those of implicit_gemm_lds_kernel (same sums).
 // --------------------------------------------------------------------------
-template <int NW>
+// DMA of this wave's share of one stage: row groups q = w, w + NW, ... of the
+// tile's 4*RB groups of 8 rows (lane-linear LDS destination, swizzled source
+// as in lds_issue)
+template <int NW, int RB>
 __device__ __forceinline__ void shared_issue(float* abuf, const int32_t* mtile, int K, int k, int c0, int lane, int w,
                                              const float* __restrict__ src, int cin, bool live) {
+    constexpr int NQ = 4 * RB / NW;
     const int sl = lane & 7;
-    int32_t mq[4 / NW];
+    int32_t mq[NQ];
 #pragma unroll
-    for (int t = 0; t < 4 / NW; ++t) mq[t] = live ? mtile[(8 * (w + NW * t) + (lane >> 3)) * K + k] : -1;
+    for (int t = 0; t < NQ; ++t) mq[t] = live ? mtile[(8 * (w + NW * t) + (lane >> 3)) * K + k] : -1;
 #pragma unroll
-    for (int t = 0; t < 4 / NW; ++t) {
+    for (int t = 0; t < NQ; ++t) {
         const int q = w + NW * t;
         const int r = 8 * q + (lane >> 3);
         const int c = c0 + 4 * (sl ^ (r & 7));
@@ -682,30 +686,76 @@ __device__ __forceinline__ void shared_issue(float* abuf, const int32_t* mtile, 
     }
 }
 
-__device__ __forceinline__ void shared_regs(const int32_t* mtile, int K, int k, int c0, int lane, int64_t o, int i,
-                                            int col, const float* __restrict__ sscale,
+template <int RB>
+struct SharedStage {
+    float a[RB][16], b[16];
+    float sc[RB];  // row factor (importance x pair scale, 0 for a missing row)
+};
+
+template <int RB>
+__device__ __forceinline__ void shared_regs(const int32_t* mtile, int K, int k, int c0, int lane, const int64_t* o,
+                                            int i, int col, const float* __restrict__ sscale,
                                             const float* __restrict__ pscale, const float* __restrict__ Wt, int cin,
-                                            int cout, bool live, GemmStage& st) {
-    const int32_t mi = live ? mtile[i * K + k] : -1;
+                                            int cout, bool live, SharedStage<RB>& st, float (&s1)[RB],
+                                            float (&s2)[RB], bool (&v)[RB]) {
     const int cb = c0 + 16 * (lane >> 5);
     const bool colv = live && col < cout;
     const float* wr = Wt + (static_cast<int64_t>(k) * cout + (colv ? col : 0)) * cin;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int c = cb + 4 * q;
-        const float4 v = *reinterpret_cast<const float4*>((colv && c < cin) ? wr + c : g_zero_page);
-        st.b[4 * q] = v.x;
-        st.b[4 * q + 1] = v.y;
-        st.b[4 * q + 2] = v.z;
-        st.b[4 * q + 3] = v.w;
+        const float4 x = *reinterpret_cast<const float4*>((colv && c < cin) ? wr + c : g_zero_page);
+        st.b[4 * q] = x.x;
+        st.b[4 * q + 1] = x.y;
+        st.b[4 * q + 2] = x.z;
+        st.b[4 * q + 3] = x.w;
     }
-    const bool valid = mi >= 0;
-    st.s1 = *(sscale ? sscale + (valid ? mi : 0) : g_one_page);
-    st.s2 = *(pscale ? pscale + (valid ? o : 0) * K + k : g_one_page);
-    st.v = valid ? 1.f : 0.f;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+        const int32_t mi = live ? mtile[(32 * rb + i) * K + k] : -1;
+        v[rb] = mi >= 0;
+        s1[rb] = *(sscale ? sscale + (v[rb] ? mi : 0) : g_one_page);
+        s2[rb] = *(pscale ? pscale + (v[rb] ? o[rb] : 0) * K + k : g_one_page);
+    }
 }
 
-template <bool PRE, int NT, int NW>
+// RB row blocks against one column block: B split once, each row block's A
+// split and multiplied into its accumulator (same per-output sums as
+// mfma_stage: the reduction order of one accumulator does not change)
+template <int NT, int RB>
+__device__ __forceinline__ void mfma_stage_rb(const SharedStage<RB>& cu, f32x16 (&acc)[RB]) {
+    if constexpr (NT == 0) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                acc[rb] = __builtin_amdgcn_mfma_f32_32x32x2f32(cu.a[rb][r], cu.b[r], acc[rb], 0, 0, 0);
+    } else {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            bf16x8 bh, bm, bl;
+            split_bf16x8<NT>(cu.b + 8 * t, bh, bm, bl);
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) {
+                bf16x8 ah, am, al;
+                split_bf16x8<NT>(cu.a[rb] + 8 * t, ah, am, al);
+                if constexpr (NT == 6) {
+                    acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc[rb], 0, 0, 0);
+                    acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[rb], 0, 0, 0);
+                    acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[rb], 0, 0, 0);
+                }
+                acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[rb], 0, 0, 0);
+                acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[rb], 0, 0, 0);
+                acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[rb], 0, 0, 0);
+            }
+        }
+    }
+}
+
+// The tile: 32*RB output rows (RB row blocks) x NW column blocks; wave w owns
+// column block w for all RB row blocks, so each stage's B fragment (the
+// filters, read by every wave of every tile) feeds RB accumulators.
+template <bool PRE, int NT, int NW, int RB>
 __global__ void __launch_bounds__(NW * 64)
 implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order,
                             const int* order_flag, int K, int64_t n_out,
@@ -714,11 +764,12 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
                             int cin, int cout, const float* __restrict__ oscale, const float* __restrict__ bias,
                             float* __restrict__ out, int nsplit, float* __restrict__ part, GemmPrologue pre,
                             const float* __restrict__ residual) {
+    constexpr int R = 32 * RB;
     __shared__ float lpre[PRE ? 2 * (kPreMax + 32) : 1];
-    __shared__ __attribute__((aligned(16))) float abuf[2][32 * 32];
-    __shared__ int32_t mtile[32 * 32];
-    __shared__ int32_t orow[32];
-    const int64_t o0 = static_cast<int64_t>(blockIdx.x) * 32;
+    __shared__ __attribute__((aligned(16))) float abuf[2][R * 32];
+    __shared__ int32_t mtile[R * 32];
+    __shared__ int32_t orow[R];
+    const int64_t o0 = static_cast<int64_t>(blockIdx.x) * R;
     if (o0 >= n_out) return;  // whole workgroup, before any barrier
     float* lps = lpre;
     float* lpb = lpre + (PRE ? kPreMax + 32 : 0);
@@ -733,12 +784,12 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
     const int i = lane & 31, h = lane >> 5;
     const int col = (blockIdx.y * NW + w) * 32 + i;
     if (order && *order_flag == 0) order = nullptr;
-    if (threadIdx.x < 32) {
-        const int64_t oo = o0 + threadIdx.x;
-        orow[threadIdx.x] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
+    for (int t = threadIdx.x; t < R; t += NW * 64) {
+        const int64_t oo = o0 + t;
+        orow[t] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < 32 * K; e += NW * 64) {
+    for (int e = threadIdx.x; e < R * K; e += NW * 64) {
         const int rr = e / K;
         const int32_t orr = orow[rr];
         mtile[e] = orr >= 0 ? map[static_cast<int64_t>(orr) * K + (e - rr * K)] : -1;
@@ -746,14 +797,21 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
     __syncthreads();
     unsigned used = 0u;  // identical in every wave (same rows)
     for (int k = h; k < K; k += 2) {
-        const uint64_t b = __ballot(mtile[i * K + k] >= 0);
+        bool any = false;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) any |= mtile[(32 * rb + i) * K + k] >= 0;
+        const uint64_t b = __ballot(any);
         used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
     }
     used = __builtin_amdgcn_readlane(used, 32) | __builtin_amdgcn_readlane(used, 0);
-    const int64_t o = orow[i] >= 0 ? orow[i] : 0;
-    f32x16 acc;
+    int64_t o[RB];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int rb = 0; rb < RB; ++rb) o[rb] = orow[32 * rb + i] >= 0 ? orow[32 * rb + i] : 0;
+    f32x16 acc[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[rb][r] = 0.f;
     const int nch = (cin + 31) >> 5;
     const int s = blockIdx.z;
     const int j0 = split_stage(used, nch, K, s, nsplit);
@@ -762,19 +820,25 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
         unsigned u = used;
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
         int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
-        GemmStage nx, cu;
-        shared_issue<NW>(abuf[0], mtile, K, k, c0, lane, w, src, cin, true);
-        shared_regs(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, true, nx);
+        SharedStage<RB> nx, cu;
+        float s1[RB], s2[RB];
+        bool vv[RB];
+        shared_issue<NW, RB>(abuf[0], mtile, K, k, c0, lane, w, src, cin, true);
+        shared_regs<RB>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, true, nx, s1, s2, vv);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         for (int j = j0; j < j1; ++j) {
             const int b = (j - j0) & 1;
-            lds_read<true>(abuf[b], nullptr, i, h, cu);
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) {
+                GemmStage ta;
+                lds_read<true>(abuf[b] + 32 * 32 * rb, nullptr, i, h, ta);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) cu.a[rb][r] = ta.a[r];
+                cu.sc[rb] = vv[rb] ? s1[rb] * s2[rb] : 0.f;
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) cu.b[r] = nx.b[r];
-            cu.s1 = nx.s1;
-            cu.s2 = nx.s2;
-            cu.v = nx.v;
             const int cj = c0;
             c0 += 32;
             if (c0 >= cin) {
@@ -784,33 +848,41 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
             }
             const bool live = j + 1 < j1;
             // the other buffer was last read in stage j-1, before that stage's barrier
-            shared_issue<NW>(abuf[b ^ 1], mtile, K, k, c0, lane, w, src, cin, live);
-            shared_regs(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, live, nx);
+            shared_issue<NW, RB>(abuf[b ^ 1], mtile, K, k, c0, lane, w, src, cin, live);
+            shared_regs<RB>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, live, nx, s1, s2, vv);
             __builtin_amdgcn_sched_barrier(0);
-            gemm_finish<PRE>(cu, cj, h, lps, lpb);
-            mfma_stage<NT>(cu, acc);
+            const int cbb = cj + 16 * h;
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    cu.a[rb][r] = (PRE ? pre_act(cu.a[rb][r], lps[cbb + r], lpb[cbb + r]) : cu.a[rb][r]) * cu.sc[rb];
+            mfma_stage_rb<NT, RB>(cu, acc);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own share of stage j+1 landed
             __syncthreads();  // every share landed; stage j's buffer free
         }
     }
-    if (nsplit > 1) {
-        float* P = part + static_cast<int64_t>(s) * n_out * cout;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+        if (nsplit > 1) {
+            float* P = part + static_cast<int64_t>(s) * n_out * cout;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t orr = orow[32 * rb + (r & 3) + 8 * (r >> 2) + 4 * h];
+                if (orr >= 0 && col < cout) P[orr * cout + col] = acc[rb][r];
+            }
+            continue;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int64_t orr = orow[(r & 3) + 8 * (r >> 2) + 4 * h];
-            if (orr >= 0 && col < cout) P[orr * cout + col] = acc[r];
-        }
-        return;
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int64_t orr = orow[(r & 3) + 8 * (r >> 2) + 4 * h];
-        if (orr >= 0 && col < cout) {
-            float v = acc[r];
-            if (oscale) v *= oscale[orr];
-            if (bias) v += bias[col];
-            if (residual) v += residual[orr * cout + col];
-            out[orr * cout + col] = v;
+            const int64_t orr = orow[32 * rb + (r & 3) + 8 * (r >> 2) + 4 * h];
+            if (orr >= 0 && col < cout) {
+                float v = acc[rb][r];
+                if (oscale) v *= oscale[orr];
+                if (bias) v += bias[col];
+                if (residual) v += residual[orr * cout + col];
+                out[orr * cout + col] = v;
+            }
         }
     }
 }
@@ -1115,23 +1187,30 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
     if (vec4 && lds_path && shared_path && cout >= 64) {
         // A tile shared by NW column-block waves (implicit_gemm_shared_kernel)
         const int nw = (cout % 128 == 0) ? 4 : 2;
-        const dim3 gs(static_cast<unsigned>(ceil_div(n_out, 32)), static_cast<unsigned>(ceil_div(cout, 32 * nw)),
+        static const int rb = [] {
+            const char* e = std::getenv("O3DML_GEMM_RB");  // 2 row blocks per wave: measured slower
+            return (e && std::atoi(e) == 2) ? 2 : 1;
+        }();
+        const dim3 gs(static_cast<unsigned>(ceil_div(n_out, 32 * rb)), static_cast<unsigned>(ceil_div(cout, 32 * nw)),
                       static_cast<unsigned>(ns));
-#define O3DML_GEMM_SH(P, X, W)                                                                               \
-    implicit_gemm_shared_kernel<P, X, W><<<gs, W * 64, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
-                                                                pscale, Wt, cin, cout, oscale, bias, out, ns,  \
-                                                                part, pre, residual)
+#define O3DML_GEMM_SH(P, X, W, B)                                                                               \
+    implicit_gemm_shared_kernel<P, X, W, B><<<gs, W * 64, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
+                                                                   pscale, Wt, cin, cout, oscale, bias, out, ns,  \
+                                                                   part, pre, residual)
+#define O3DML_GEMM_SH_RB(P, X, W) \
+    if (rb == 2) O3DML_GEMM_SH(P, X, W, 2); else O3DML_GEMM_SH(P, X, W, 1);
 #define O3DML_GEMM_SH_NT(P, W)                          \
     switch (gemm_nt()) {                                \
-        case 0: O3DML_GEMM_SH(P, 0, W); break;          \
-        case 3: O3DML_GEMM_SH(P, 3, W); break;          \
-        default: O3DML_GEMM_SH(P, 6, W); break;         \
+        case 0: O3DML_GEMM_SH_RB(P, 0, W) break;        \
+        case 3: O3DML_GEMM_SH_RB(P, 3, W) break;        \
+        default: O3DML_GEMM_SH_RB(P, 6, W) break;       \
     }
         if (nw == 4) {
             if (pre.scale) { O3DML_GEMM_SH_NT(true, 4) } else { O3DML_GEMM_SH_NT(false, 4) }
         } else {
             if (pre.scale) { O3DML_GEMM_SH_NT(true, 2) } else { O3DML_GEMM_SH_NT(false, 2) }
         }
+#undef O3DML_GEMM_SH_RB
 #undef O3DML_GEMM_SH_NT
 #undef O3DML_GEMM_SH
     } else if (vec4 && lds_path) {
