@@ -1048,6 +1048,108 @@ dweight_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ po, 
     }
 }
 
+// dW with the stage's rows staged through LDS (cin, cout % 4 == 0, 16-B
+// aligned rows): the 32 pairs' x segments (32 channels = one 128-B line per
+// pair) and g segments arrive by global_load_lds_dwordx4, 4 instructions per
+// operand (8 lanes per line) instead of 16 single-dword gathers each, and are
+// read back in the MFMA layout with conflict-free ds_read_b32 (lanes = the 32
+// consecutive channels of one pair's row).  One buffer per operand: stage j
+// is read into registers, then stage j+1's DMA goes into the same buffers and
+// runs under stage j's MFMAs.  Same element -> pair map as dweight_kernel
+// (element s = pair 2s + h), so the same sums.
+constexpr int kDwSubL = 256;
+
+template <int NT>
+__global__ void __launch_bounds__(64)
+dweight_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ po,
+                   const int64_t* __restrict__ kstart, int K, const int64_t* __restrict__ plan,
+                   const float* __restrict__ src, const float* __restrict__ sscale, const float* __restrict__ pscale,
+                   const float* __restrict__ g, const float* __restrict__ oscale, int cin, int cout,
+                   float* __restrict__ part) {
+    __shared__ int32_t lo[kDwSubL], lm[kDwSubL];
+    __shared__ float lra[kDwSubL], lrb[kDwSubL];
+    __shared__ __attribute__((aligned(16))) float xbuf[32 * 32], gbuf[32 * 32];
+    const int ncot = (cout + 31) >> 5;
+    const int ci0 = (blockIdx.x / ncot) * 32, co0 = (blockIdx.x % ncot) * 32;
+    const int64_t w = blockIdx.y;
+    if (w >= plan[K]) return;
+    int k = 0;
+    while (plan[k + 1] <= w) ++k;
+    const int lane = threadIdx.x, i = lane & 31, h = lane >> 5, sl = lane & 7;
+    const int64_t js = kstart[k] + (w - plan[k]) * plan[K + 1];
+    const int64_t je = min(kstart[k + 1], js + plan[K + 1]);
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    // DMA of the 32 pairs at base: pair base + 8q + (lane >> 3), 16-B piece sl
+    auto issue = [&](int base, bool live) {
+        int32_t mq[4], oq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int pp = base + 8 * q + (lane >> 3);
+            mq[q] = live ? lm[pp] : -1;
+            oq[q] = live ? lo[pp] : -1;
+        }
+        const int ci = ci0 + 4 * sl, co = co0 + 4 * sl;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float* ga = (mq[q] >= 0 && ci < cin) ? src + static_cast<int64_t>(mq[q]) * cin + ci : g_zero_page;
+            const float* gb = (oq[q] >= 0 && co < cout) ? g + static_cast<int64_t>(oq[q]) * cout + co : g_zero_page;
+            glds16(ga, xbuf + 256 * q);
+            glds16(gb, gbuf + 256 * q);
+        }
+    };
+    for (int64_t sub = js; sub < je; sub += kDwSubL) {
+        const int n = static_cast<int>(min(static_cast<int64_t>(kDwSubL), je - sub));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA in flight over the record rewrite
+        for (int t = lane; t < kDwSubL; t += 64) {
+            int32_t o = -1, m = -1;
+            float ra = 0.f, rb = 0.f;
+            if (t < n) {
+                o = po[sub + t];
+                m = map[static_cast<int64_t>(o) * K + k];
+                ra = (sscale ? sscale[m] : 1.f) * (pscale ? pscale[static_cast<int64_t>(o) * K + k] : 1.f);
+                rb = oscale ? oscale[o] : 1.f;
+            }
+            lo[t] = o;
+            lm[t] = m;
+            lra[t] = ra;
+            lrb[t] = rb;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int nst = (n + 31) >> 5;
+        issue(0, true);
+        for (int j = 0; j < nst; ++j) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage j in LDS
+            DwStage cu;
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) {
+                const int pp = 2 * s2 + h;
+                cu.a[s2] = xbuf[pp * 32 + i];
+                cu.b[s2] = gbuf[pp * 32 + i];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffers read out before the next DMA
+            issue(32 * (j + 1) < kDwSubL ? 32 * (j + 1) : 0, j + 1 < nst);
+            __builtin_amdgcn_sched_barrier(0);
+            dw_finish(cu, 32 * j, h, lra, lrb);
+            mfma_stage<NT>(cu, acc);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead DMA has landed before the wave exits
+    float* P = part + w * cin * cout;
+    const int col = co0 + i;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int row = ci0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < cin && col < cout) P[static_cast<int64_t>(row) * cout + col] = acc[r];
+    }
+}
+
 __global__ void reduce_slabs_kernel(const float* __restrict__ part, int K, const int64_t* __restrict__ plan,
                                     int64_t slab, float* __restrict__ dw) {
     const int64_t total = static_cast<int64_t>(K) * slab;
@@ -1802,11 +1904,31 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
     dweight_kernel<NT><<<gg, 64, 0, st>>>(map, po, kstart, K, plan, inp_features, inp_importance,          \
                                           has_neighbors_importance ? pscale : nullptr, grad_out, os, cin, \
                                           cout, part)
-        switch (gemm_nt()) {
-            case 0: O3DML_DW(0); break;
-            case 3: O3DML_DW(3); break;
-            default: O3DML_DW(6); break;
+#define O3DML_DWL(NT)                                                                                     \
+    dweight_lds_kernel<NT><<<gg, 64, 0, st>>>(map, po, kstart, K, plan, inp_features, inp_importance,      \
+                                              has_neighbors_importance ? pscale : nullptr, grad_out, os, cin, \
+                                              cout, part)
+        static const bool dw_lds = [] {
+            const char* e = std::getenv("O3DML_DW_LDS");
+            return e ? std::atoi(e) != 0 : true;
+        }();
+        const bool lds_ok = dw_lds && cin % 4 == 0 && cout % 4 == 0 &&
+                            reinterpret_cast<uintptr_t>(inp_features) % 16 == 0 &&
+                            reinterpret_cast<uintptr_t>(grad_out) % 16 == 0;
+        if (lds_ok) {
+            switch (gemm_nt()) {
+                case 0: O3DML_DWL(0); break;
+                case 3: O3DML_DWL(3); break;
+                default: O3DML_DWL(6); break;
+            }
+        } else {
+            switch (gemm_nt()) {
+                case 0: O3DML_DW(0); break;
+                case 3: O3DML_DW(3); break;
+                default: O3DML_DW(6); break;
+            }
         }
+#undef O3DML_DWL
 #undef O3DML_DW
         O3DML_LAUNCH_CHECK();
         if (nchunk > 1) {
