@@ -1390,8 +1390,13 @@ __device__ __forceinline__ int lat_stat_merge(int j, int a, int b) { return (j &
 
 __global__ void __launch_bounds__(256) lattice_stats_kernel(const float* __restrict__ inp_pos, int64_t n_in,
                                                             const float* __restrict__ qpos, int64_t n_q,
-                                                            float inv_vs, int* __restrict__ part) {
+                                                            float inv_vs, int* __restrict__ part,
+                                                            uint64_t* __restrict__ keys, int64_t cap) {
     __shared__ int red[12][256];
+    // the voxel hash's empty keys (lattice_insert_kernel runs after finalize)
+    for (int64_t e = (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+         e < cap; e += static_cast<int64_t>(gridDim.x) * gridDim.y * blockDim.x)
+        keys[e] = kLatEmpty;
     const float* pos = blockIdx.y ? qpos : inp_pos;
     const int64_t n = blockIdx.y ? n_q : n_in;
     int v[12];
@@ -1441,8 +1446,15 @@ __global__ void __launch_bounds__(64) lattice_finalize_kernel(const int* __restr
     const int t = threadIdx.x;
     if (t < 24) {
         const int set = t / 12, j = t % 12;
-        int v = (j & 1) ? ((j & 2) ? static_cast<int>(0x80000000u) : 0) : 0x7fffffff;
-        for (int b = 0; b < nblk; ++b) v = lat_stat_merge(j, v, part[(set * nblk + b) * 12 + j]);
+        const int init = (j & 1) ? ((j & 2) ? static_cast<int>(0x80000000u) : 0) : 0x7fffffff;
+        int v = init;
+        for (int b0 = 0; b0 < nblk; b0 += 16) {  // 16 independent loads in flight
+            int tmp[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) tmp[u] = b0 + u < nblk ? part[(set * nblk + b0 + u) * 12 + j] : init;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v = lat_stat_merge(j, v, tmp[u]);
+        }
         st[t] = v;
     }
     __syncthreads();
@@ -1686,12 +1698,11 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     const float inv_vs = 1.0f / voxel_size;
     // ---- 1. lattice check + offsets, on the device (no host round trip)
     const int nblk = static_cast<int>(std::min<int64_t>(kLatStatBlocks, ceil_div(std::max(n_in, n_out), 256)));
-    lattice_stats_kernel<<<dim3(nblk, 2), 256, 0, st>>>(inp_pos, n_in, query_pos, n_out, inv_vs, part);
+    lattice_stats_kernel<<<dim3(nblk, 2), 256, 0, st>>>(inp_pos, n_in, query_pos, n_out, inv_vs, part, keys, cap);
     O3DML_LAUNCH_CHECK();
     lattice_finalize_kernel<<<1, 64, 0, st>>>(part, nblk, ksize, mirror, lo, status);
     O3DML_LAUNCH_CHECK();
-    // ---- 2. hash the input voxels, 3. K lookups per output
-    O3DML_CHECK_HIP(hipMemsetAsync(keys, 0xff, sizeof(uint64_t) * cap, st));
+    // ---- 2. hash the input voxels (keys emptied by lattice_stats_kernel), 3. K lookups per output
     lattice_insert_kernel<<<stream_grid(n_in, 256), 256, 0, st>>>(inp_pos, n_in, inv_vs, keys, vals,
                                                                  static_cast<uint32_t>(cap - 1), status);
     O3DML_LAUNCH_CHECK();

@@ -221,12 +221,17 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
         key = (ks, bool(mirror), bool(normalize), bool(want_grad), float(voxel_size)) + tuple(cache_key[2:])
         key = key + (id(cache_key[0]), cache_key[0]._version, id(cache_key[1]), cache_key[1]._version)
     hit = scope.maps.get(key) if key is not None else None
+    late = None  # status word read after the GEMM (standalone call, no scope)
     if hit is not None:
         mws, status0 = hit[0], hit[1]
     else:
         if lazy_q:
             qp = to_dev(query_positions(), dev, torch.float32)
-        defer = scope is not None and scope.defer and n_in > 0 and n_out > 0
+        # the lattice test stays on the device in a deferring scope and in a
+        # standalone call; the latter reads it once after the GEMM (a failed
+        # test leaves an all-empty, safe map, and the caller recomputes with the
+        # search rulebook), so no host round trip sits between map and GEMM
+        defer = (scope is None or scope.defer) and n_in > 0 and n_out > 0
         mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
         lws = workspace(lib.o3dml_sparse_conv_lattice_workspace_size(n_in), dev)
         status = np.zeros(1, np.int32)
@@ -241,7 +246,10 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
                       stream_handle(dev))
         if defer:
             off = lib.o3dml_sparse_conv_map_status_offset(n_out, n_in, K)
-            scope.pending.append(mws[off:off + 4].view(torch.int32))
+            if scope is None:
+                late = mws[off:off + 4].view(torch.int32)
+            else:
+                scope.pending.append(mws[off:off + 4].view(torch.int32))
         if key is not None:
             scope.maps[key] = (mws, status0, cache_key[0], cache_key[1])
     if status0 & 4:
@@ -264,11 +272,25 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
                   ptr(x.detach().contiguous()), n_in, ptr(ps), ptr(pb), ptr(res),
                   ptr(None if b is None else b.detach().contiguous()), n_out, ptr(out), ptr(mws), mws.numel(),
                   ptr(fws), fws.numel(), stream_handle(dev))
-        return out
+        return out if _late_ok(late) else None
     empty = torch.empty(0, dtype=torch.int64, device=dev)
     out = _ConvFn.apply(f, x, b, empty, empty, None, empty, _opt(inp_importance, dev), bool(normalize), oimp,
                         want_grad, (mws, n_out))
+    if not _late_ok(late):
+        return None
     return out if inp_features.is_cuda else out.cpu()
+
+
+def _late_ok(status):
+    """Lattice status word read after the GEMM: True when the map was a
+    lattice map (the result stands), False when the caller must recompute with
+    the search rulebook; duplicate kernel indices raise."""
+    if status is None:
+        return True
+    st = int(status.item())
+    if st & 1:
+        raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index")
+    return not st & 4
 
 
 def _transposed_filters(f):
