@@ -121,17 +121,40 @@ def kernel_profile(step, n_queries, pairs, reps):
     return dominant, avg, alg_bytes, mean_nbrs
 
 
-def load_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary
-    (profiles/*/pmc_<kernel>.json written by tools/pmc_traffic.py), newest round first."""
+def load_pmc(kernel):
+    """Committed PMC summary of `kernel` (profiles/*/pmc_<kernel>.json written by
+    tools/pmc_traffic.py), newest round first; {} when there is none."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_{kernel}.json")), reverse=True):
         try:
             with open(path) as f:
-                return json.load(f).get("hbm_bytes_per_launch")
+                return json.load(f)
         except Exception:
             continue
-    return None
+    return {}
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary."""
+    return load_pmc(kernel).get("hbm_bytes_per_launch")
+
+
+SIMDS, CLOCK_GHZ = 1024, 2.4  # MI355X: 256 CUs x 4 SIMDs
+
+
+def issue_bound(kernel):
+    """The bound the search kernel actually sits on: VALU issue.
+    From the committed PMC counters: wave64 VALU instructions x 2 cycles each
+    over SIMD-cycles of the measured launch duration, and the same for the one
+    scalar unit per CU (SALU, 1 cycle each).  None without a PMC summary."""
+    c = load_pmc(kernel).get("counters_per_launch") or {}
+    if not c.get("SQ_INSTS_VALU") or not c.get("dur_us_mean"):
+        return None
+    cyc = c["dur_us_mean"] * 1e3 * CLOCK_GHZ
+    return {"valu_instr": int(c["SQ_INSTS_VALU"]), "salu_instr": int(c.get("SQ_INSTS_SALU", 0)),
+            "valu_issue_frac": round(2 * c["SQ_INSTS_VALU"] / (SIMDS * cyc), 4),
+            "salu_issue_frac": round(c.get("SQ_INSTS_SALU", 0) / (SIMDS / 4 * cyc), 4),
+            "source": "profiles/*/pmc_%s.json (PMC pass duration %.1f us)" % (kernel, c["dur_us_mean"])}
 
 
 def cpu_baseline():
@@ -535,7 +558,8 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic(dominant), "kernel_ms": round(ms, 5),
                          "kernel_ms_all": {k: round(v, 5) for k, v in avg.items()},
-                         "alg_bytes_per_launch": int(alg_bytes), "mean_neighbors": round(mean_nbrs, 3)},
+                         "alg_bytes_per_launch": int(alg_bytes), "mean_neighbors": round(mean_nbrs, 3),
+                         "issue": issue_bound(dominant)},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
