@@ -79,9 +79,9 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
                 }
             }
         };
-        auto visit = [&](int x, int y, int z) {
-            const uint32_t c = g.offset + static_cast<uint32_t>(x + g.dx * (y + g.dy * z));
-            const uint32_t s = splits[c], e = splits[c + 1];
+        auto visit = [&](int xa, int xb, int y, int z) {  // cells xa..xb of a row: one contiguous run
+            const uint32_t c = g.offset + static_cast<uint32_t>(g.dx * (y + g.dy * z));
+            const uint32_t s = splits[c + xa], e = splits[c + xb + 1];
             uint32_t j = s;
             for (; j + 8 <= e; j += 8) {  // 8 loads in flight per lane
                 float4 p[8];
@@ -100,10 +100,10 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
             for (int z = za; z <= zb; ++z) {
                 for (int y = ya; y <= yb; ++y) {
                     if (z == z0 || z == z1 || y == y0 || y == y1) {
-                        for (int x = xa; x <= xb; ++x) visit(x, y, z);
+                        visit(xa, xb, y, z);
                     } else {
-                        if (x0 >= 0) visit(x0, y, z);
-                        if (x1 < g.dx) visit(x1, y, z);
+                        if (x0 >= 0) visit(x0, x0, y, z);
+                        if (x1 < g.dx) visit(x1, x1, y, z);
                     }
                 }
             }
@@ -243,9 +243,13 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
                 }
             }
         };
-        auto visit = [&](int x, int y, int z) {
-            const uint32_t c = g.offset + static_cast<uint32_t>(x + g.dx * (y + g.dy * z));
-            const uint32_t s = splits[c], e = splits[c + 1];
+        // cells xa..xb of one (y, z) row are adjacent in the cell order (x
+        // fastest), so their points are one contiguous run of `sorted`: one
+        // pair of split loads and one stream per run instead of per cell (the
+        // chain of dependent split -> point loads per cell bounded this kernel)
+        auto visit = [&](int xa, int xb, int y, int z) {
+            const uint32_t c = g.offset + static_cast<uint32_t>(g.dx * (y + g.dy * z));
+            const uint32_t s = splits[c + xa], e = splits[c + xb + 1];
             uint32_t j = s + gl;
             for (; j + kKnnG < e; j += 2 * kKnnG) {  // two loads in flight per lane
                 const float4 p0 = sorted[j], p1 = sorted[j + kKnnG];
@@ -262,10 +266,10 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
             for (int z = za; z <= zb; ++z) {
                 for (int y = ya; y <= yb; ++y) {
                     if (z == z0 || z == z1 || y == y0 || y == y1) {
-                        for (int x = xa; x <= xb; ++x) visit(x, y, z);
+                        visit(xa, xb, y, z);
                     } else {
-                        if (x0 >= 0) visit(x0, y, z);
-                        if (x1 < g.dx) visit(x1, y, z);
+                        if (x0 >= 0) visit(x0, x0, y, z);
+                        if (x1 < g.dx) visit(x1, x1, y, z);
                     }
                 }
             }
