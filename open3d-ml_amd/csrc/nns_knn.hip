@@ -157,41 +157,44 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
 // ---------------------------------------------------------------------------
 constexpr int kKnnG = 8;
 
+// (distance, index) as one 64-bit key: distances are >= +0 (squared L2, L1,
+// Linf of fabsf terms), whose float bits order as unsigned ints, so the
+// lexicographic (distance, index) order is the unsigned order of
+// (bits(d) << 32 | index) — one 64-bit compare instead of three float/int
+// compares, one 64-bit select per move.  NaN distances (bits above +inf) sort
+// after every finite one and after the empty entry's +inf, as lex_less never
+// admits them either.
+__device__ __forceinline__ uint64_t knn_key(float d, uint32_t id) {
+    return (static_cast<uint64_t>(__float_as_uint(d)) << 32) | id;
+}
+constexpr uint64_t kKnnEmpty = (static_cast<uint64_t>(0x7f800000u) << 32) | 0xffffffffull;  // (+inf, ~0)
+
 template <int K>
-__device__ __forceinline__ void cas_lex(float (&d)[K], uint32_t (&id)[K], int i, int j) {
-    if (lex_less(d[j], id[j], d[i], id[i])) {
-        const float td = d[i];
-        const uint32_t ti = id[i];
-        d[i] = d[j];
-        id[i] = id[j];
-        d[j] = td;
-        id[j] = ti;
-    }
+__device__ __forceinline__ void cas_key(uint64_t (&a)[K], int i, int j) {
+    const uint64_t lo = a[j] < a[i] ? a[j] : a[i];
+    const uint64_t hi = a[j] < a[i] ? a[i] : a[j];
+    a[i] = lo;
+    a[j] = hi;
 }
 
 template <int K>
-__device__ __forceinline__ void group_merge(float (&d)[K], uint32_t (&id)[K]) {
+__device__ __forceinline__ void group_merge(uint64_t (&a)[K]) {
 #pragma unroll
     for (int mask = 1; mask < kKnnG; mask <<= 1) {
-        float od[K];
-        uint32_t oi[K];
+        uint64_t o[K];
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            od[i] = __shfl_xor(d[i], mask, 64);
-            oi[i] = __shfl_xor(id[i], mask, 64);
+            const uint32_t lo = __shfl_xor(static_cast<uint32_t>(a[i]), mask, 64);
+            const uint32_t hi = __shfl_xor(static_cast<uint32_t>(a[i] >> 32), mask, 64);
+            o[i] = (static_cast<uint64_t>(hi) << 32) | lo;
         }
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
-            if (lex_less(od[K - 1 - i], oi[K - 1 - i], d[i], id[i])) {
-                d[i] = od[K - 1 - i];
-                id[i] = oi[K - 1 - i];
-            }
-        }
+        for (int i = 0; i < K; ++i) a[i] = o[K - 1 - i] < a[i] ? o[K - 1 - i] : a[i];
 #pragma unroll
         for (int st = K / 2; st >= 1; st >>= 1) {
 #pragma unroll
             for (int i = 0; i < K; ++i)
-                if ((i & st) == 0) cas_lex<K>(d, id, i, i + st);
+                if ((i & st) == 0) cas_key<K>(a, i, i + st);
         }
     }
 }
@@ -215,32 +218,21 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
         const int cx = grid_axis(qx, g.ox, g.inv_h, g.dx);
         const int cy = grid_axis(qy, g.oy, g.inv_h, g.dy);
         const int cz = grid_axis(qz, g.oz, g.inv_h, g.dz);
-        float bd[K];
-        uint32_t bi[K];
+        uint64_t bk[K];  // this lane's sorted top-K keys (knn_key)
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            bd[j] = INFINITY;
-            bi[j] = 0xffffffffu;
-        }
-        float kd = INFINITY;  // group k-th best after the last merge (pruning bound)
-        uint32_t ki = 0xffffffffu;
+        for (int j = 0; j < K; ++j) bk[j] = kKnnEmpty;
+        uint64_t kk = kKnnEmpty;  // group k-th best after the last merge (pruning bound)
         bool full = false;
         auto consider = [&](const float4& p) {
             if (IGNORE && p.x == qx && p.y == qy && p.z == qz) return;
             const float d = dist_metric<METRIC>(p.x, p.y, p.z, qx, qy, qz);
-            const uint32_t id = __float_as_uint(p.w);
-            if (!lex_less(d, id, kd, ki) || !lex_less(d, id, bd[K - 1], bi[K - 1])) return;
+            const uint64_t key = knn_key(d, __float_as_uint(p.w));
+            if (!(key < kk) || !(key < bk[K - 1])) return;
 #pragma unroll
-            for (int r = K - 1; r >= 0; --r) {
-                const bool lt_prev = r > 0 && lex_less(d, id, bd[r > 0 ? r - 1 : 0], bi[r > 0 ? r - 1 : 0]);
-                const bool lt_cur = lex_less(d, id, bd[r], bi[r]);
-                if (lt_prev) {
-                    bd[r] = bd[r - 1];
-                    bi[r] = bi[r - 1];
-                } else if (lt_cur) {
-                    bd[r] = d;
-                    bi[r] = id;
-                }
+            for (int r = K - 1; r >= 0; --r) {  // insertion: shift the larger entries up
+                const bool lt_prev = r > 0 && key < bk[r > 0 ? r - 1 : 0];
+                const bool lt_cur = key < bk[r];
+                bk[r] = lt_prev ? bk[r > 0 ? r - 1 : 0] : (lt_cur ? key : bk[r]);
             }
         };
         // cells xa..xb of one (y, z) row are adjacent in the cell order (x
@@ -277,20 +269,18 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
             // prune and terminate); before that the lists keep accumulating
             int have = 0;
 #pragma unroll
-            for (int r = 0; r < K; ++r) have += bi[r] != 0xffffffffu ? 1 : 0;
+            for (int r = 0; r < K; ++r) have += static_cast<uint32_t>(bk[r]) != 0xffffffffu ? 1 : 0;
 #pragma unroll
             for (int mask = 1; mask < kKnnG; mask <<= 1) have += __shfl_xor(have, mask, 64);
             const bool last_ring = x0 <= 0 && x1 >= g.dx - 1 && y0 <= 0 && y1 >= g.dy - 1 && z0 <= 0 &&
                                    z1 >= g.dz - 1;
             if (have < k && !last_ring) continue;
-            group_merge<K>(bd, bi);
+            group_merge<K>(bk);
 #pragma unroll
             for (int r = 0; r < K; ++r)
-                if (r == k - 1) {
-                    kd = bd[r];
-                    ki = bi[r];
-                }
-            full = ki != 0xffffffffu;
+                if (r == k - 1) kk = bk[r];
+            full = static_cast<uint32_t>(kk) != 0xffffffffu;
+            const float kd = __uint_as_float(static_cast<uint32_t>(kk >> 32));
             const bool lo_x = x0 <= 0, hi_x = x1 >= g.dx - 1, lo_y = y0 <= 0, hi_y = y1 >= g.dy - 1;
             const bool lo_z = z0 <= 0, hi_z = z1 >= g.dz - 1;
             if (lo_x && hi_x && lo_y && hi_y && lo_z && hi_z) break;  // every cell visited
@@ -310,23 +300,20 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
             }
             if (gl != 0) {  // lane 0 carries the merged list into the next ring
 #pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    bd[j] = INFINITY;
-                    bi[j] = 0xffffffffu;
-                }
+                for (int j = 0; j < K; ++j) bk[j] = kKnnEmpty;
             }
         }
         int c = 0;
 #pragma unroll
-        for (int r = 0; r < K; ++r) c += (r < k && bi[r] != 0xffffffffu) ? 1 : 0;
+        for (int r = 0; r < K; ++r) c += (r < k && static_cast<uint32_t>(bk[r]) != 0xffffffffu) ? 1 : 0;
         if (gl == 0) counts[q] = c;
         int32_t* oi = out_idx + q * static_cast<int64_t>(k);
         float* od = out_dist + q * static_cast<int64_t>(k);
 #pragma unroll
         for (int r = 0; r < K; ++r) {
             if (r < c && (r & (kKnnG - 1)) == gl) {
-                oi[r] = static_cast<int32_t>(bi[r]);
-                od[r] = bd[r];
+                oi[r] = static_cast<int32_t>(static_cast<uint32_t>(bk[r]));
+                od[r] = __uint_as_float(static_cast<uint32_t>(bk[r] >> 32));
             }
         }
     }
