@@ -25,6 +25,18 @@ __device__ __forceinline__ bool lex_less(float da, uint32_t ia, float db, uint32
     return da < db || (da == db && ia < ib);
 }
 
+// (distance, index) as one 64-bit key: distances are >= +0 (squared L2, L1,
+// Linf of fabsf terms), whose float bits order as unsigned ints, so the
+// lexicographic (distance, index) order is the unsigned order of
+// (bits(d) << 32 | index) — one 64-bit compare instead of three float/int
+// compares, one 64-bit select per move.  NaN distances (bits above +inf) sort
+// after every finite one and after the empty entry's +inf, as lex_less never
+// admits them either.
+__device__ __forceinline__ uint64_t knn_key(float d, uint32_t id) {
+    return (static_cast<uint64_t>(__float_as_uint(d)) << 32) | id;
+}
+constexpr uint64_t kKnnEmpty = (static_cast<uint64_t>(0x7f800000u) << 32) | 0xffffffffull;  // (+inf, ~0)
+
 template <int K, int METRIC, bool IGNORE>
 __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict__ sorted, const uint32_t* __restrict__ splits,
                                                        const GridBatch* __restrict__ grids, const float* __restrict__ queries,
@@ -40,43 +52,27 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
         const int cx = grid_axis(qx, g.ox, g.inv_h, g.dx);
         const int cy = grid_axis(qy, g.oy, g.inv_h, g.dy);
         const int cz = grid_axis(qz, g.oz, g.inv_h, g.dz);
-        float bd[K];
-        uint32_t bi[K];
+        uint64_t bk[K];  // sorted top-K keys (knn_key)
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            bd[j] = INFINITY;
-            bi[j] = 0xffffffffu;
-        }
-        float kd = INFINITY;
-        uint32_t ki = 0xffffffffu;
+        for (int j = 0; j < K; ++j) bk[j] = kKnnEmpty;
+        uint64_t kk = kKnnEmpty;
         int cnt = 0;
         auto consider = [&](const float4& p) {
-            {
-                if (IGNORE && p.x == qx && p.y == qy && p.z == qz) return;
-                const float d = dist_metric<METRIC>(p.x, p.y, p.z, qx, qy, qz);
-                const uint32_t id = __float_as_uint(p.w);
-                if (!lex_less(d, id, kd, ki)) return;
-                ++cnt;
+            if (IGNORE && p.x == qx && p.y == qy && p.z == qz) return;
+            const float d = dist_metric<METRIC>(p.x, p.y, p.z, qx, qy, qz);
+            const uint64_t key = knn_key(d, __float_as_uint(p.w));
+            if (!(key < kk)) return;
+            ++cnt;
 #pragma unroll
-                for (int r = K - 1; r >= 0; --r) {
-                    const bool lt_prev = r > 0 && lex_less(d, id, bd[r > 0 ? r - 1 : 0], bi[r > 0 ? r - 1 : 0]);
-                    const bool lt_cur = lex_less(d, id, bd[r], bi[r]);
-                    if (lt_prev) {
-                        bd[r] = bd[r - 1];
-                        bi[r] = bi[r - 1];
-                    } else if (lt_cur) {
-                        bd[r] = d;
-                        bi[r] = id;
-                    }
-                }
-                if (cnt >= k) {
+            for (int r = K - 1; r >= 0; --r) {
+                const bool lt_prev = r > 0 && key < bk[r > 0 ? r - 1 : 0];
+                const bool lt_cur = key < bk[r];
+                bk[r] = lt_prev ? bk[r > 0 ? r - 1 : 0] : (lt_cur ? key : bk[r]);
+            }
+            if (cnt >= k) {
 #pragma unroll
-                    for (int r = 0; r < K; ++r)
-                        if (r == k - 1) {
-                            kd = bd[r];
-                            ki = bi[r];
-                        }
-                }
+                for (int r = 0; r < K; ++r)
+                    if (r == k - 1) kk = bk[r];
             }
         };
         auto visit = [&](int xa, int xb, int y, int z) {  // cells xa..xb of a row: one contiguous run
@@ -123,7 +119,7 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
                 lb = lb - 1e-3f * g.h - 1e-6f * (fabsf(qx) + fabsf(qy) + fabsf(qz));
                 if (lb > 0.f) {
                     const float bound = METRIC == kL2 ? lb * lb : lb;
-                    if (kd < bound) break;
+                    if (__uint_as_float(static_cast<uint32_t>(kk >> 32)) < bound) break;
                 }
             }
         }
@@ -134,8 +130,8 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
 #pragma unroll
         for (int r = 0; r < K; ++r) {
             if (r < c) {
-                oi[r] = static_cast<int32_t>(bi[r]);
-                od[r] = bd[r];
+                oi[r] = static_cast<int32_t>(static_cast<uint32_t>(bk[r]));
+                od[r] = __uint_as_float(static_cast<uint32_t>(bk[r] >> 32));
             }
         }
     }
@@ -156,18 +152,6 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
 // empty, so no entry is counted twice.  Order: (distance, index) ascending.
 // ---------------------------------------------------------------------------
 constexpr int kKnnG = 8;
-
-// (distance, index) as one 64-bit key: distances are >= +0 (squared L2, L1,
-// Linf of fabsf terms), whose float bits order as unsigned ints, so the
-// lexicographic (distance, index) order is the unsigned order of
-// (bits(d) << 32 | index) — one 64-bit compare instead of three float/int
-// compares, one 64-bit select per move.  NaN distances (bits above +inf) sort
-// after every finite one and after the empty entry's +inf, as lex_less never
-// admits them either.
-__device__ __forceinline__ uint64_t knn_key(float d, uint32_t id) {
-    return (static_cast<uint64_t>(__float_as_uint(d)) << 32) | id;
-}
-constexpr uint64_t kKnnEmpty = (static_cast<uint64_t>(0x7f800000u) << 32) | 0xffffffffull;  // (+inf, ~0)
 
 template <int K>
 __device__ __forceinline__ void cas_key(uint64_t (&a)[K], int i, int j) {
