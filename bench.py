@@ -9,9 +9,16 @@ r = 0.05, L2, int32 indices.  One step = the full Open3D
 scan + host read of the total + fill.  Inputs are resident in HBM before the
 timed region.  value = queries processed by all ranks / wall time (Mpoints/s).
 
-Multi-GPU: one process per GPU (torchrun), scenes are independent, so there is
-no data-path collective ("scaling": "weak"); the only collectives are the
-timing barrier and the max-over-ranks of the elapsed time.
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) every rank
+is one of its processes; `python bench.py --gpus N` without torchrun spawns
+the N processes itself (torch.multiprocessing, 'spawn' start method, before
+any GPU call in the parent; rendezvous on 127.0.0.1), mirroring the
+reference's mp.spawn + init_process_group (scripts/run_pipeline.py:194-206,
+213-251).  Scenes are independent, so there is no data-path collective
+("scaling": "weak"); the only collectives are the timing barrier, the
+max-over-ranks of the elapsed time and the gather of each rank's processed
+units (value = their sum / that time).  The C5 PointPillars leg runs DDP over
+RCCL on every rank (its gradient all-reduce is the one real exchange).
 
 roofline: per-kernel HIP-event timing inside the library (events recorded on
 the stream each kernel is launched on, o3dml_timing_*); the dominant kernel's
@@ -60,6 +67,9 @@ def parse():
     ap.add_argument("--sparse-conv-reps", type=int, default=10, help="C4 sparse-conv forwards timed (0: skip)")
     ap.add_argument("--sweep-reps", type=int, default=5,
                     help="C1 size sweep (one scene of N = 2^16 .. 2^24 pts at constant density): calls timed (0: skip)")
+    ap.add_argument("--plumbing-test", action="store_true",
+                    help="launcher test only (CPU, gloo): spawn/rendezvous/timing/aggregation with a trivial step "
+                         "in place of the GPU workload; reports no metric")
     return ap.parse_args()
 
 
@@ -511,11 +521,62 @@ def timed_run(step, steps, warmup, world, sync):
     return elapsed, res
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _spawned(rank, world, port, args):
+    """One process per GPU started by `bench.py --gpus N` (no torchrun)."""
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run(args)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        import torch.multiprocessing as mp
+        mp.spawn(_spawned, args=(args.gpus, _free_port(), args), nprocs=args.gpus, join=True)
+        return
+    run(args)
+
+
+def gather_units(units, world):
+    """Every rank's processed units (queries) -> list on every rank."""
+    if world == 1:
+        return [units]
+    out = [None] * world
+    dist.all_gather_object(out, units)
+    return out
+
+
+def plumbing_test(args, world, rank):
+    """Launcher check on CPU (gloo): the same spawn / rendezvous / barrier /
+    max-over-ranks / aggregation path as the GPU run, with a trivial CPU step
+    in place of the workload.  Reports plumbing fields only, no metric."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    x = torch.ones(1 << 14)
+    elapsed, _ = timed_run(lambda: x.sum(), args.steps, args.warmup, world, lambda: None)
+    units = gather_units(args.scenes * N_POINTS * args.steps, world)
+    if rank == 0:
+        print(json.dumps({"plumbing_test": True, "n_gpus": world, "ranks_reported": len(units),
+                          "units_per_rank": units, "value": sum(units) / elapsed / 1e6,
+                          "elapsed_max_s": elapsed, "steps": args.steps}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plumbing_test:
+        return plumbing_test(args, world, rank)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
@@ -527,15 +588,18 @@ def main():
     step = lambda: nns(pts, pts, RADIUS, rs, rs)  # noqa: E731
     elapsed, res = timed_run(step, args.steps, args.warmup, world, lambda: torch.cuda.synchronize(dev))
     pairs = int(res.neighbors_row_splits[-1].item())
+    units = gather_units(args.scenes * N_POINTS * args.steps, world)
 
     pp = pointpillars_bench(dev, world, rank, args.pointpillars_steps) if args.pointpillars_steps > 0 else None
     out = None
     if rank == 0:
-        queries_total = world * args.scenes * N_POINTS * args.steps
+        queries_total = sum(units)
         value = queries_total / elapsed / 1e6
+        ms_step = elapsed / args.steps * 1e3
         dominant, avg, alg_bytes, mean_nbrs = kernel_profile(step, args.scenes * N_POINTS, pairs, args.kernel_reps)
         ms = avg[dominant]
         achieved = alg_bytes / (ms * 1e-3) / 1e9
+        step_achieved = alg_bytes / (ms_step * 1e-3) / 1e9
         out = {
             "metric": "Mpoints/s neighbor-search + sparse-conv fwd; RandLA-Net frames/s",
             "value": round(value, 2),
@@ -543,7 +607,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -553,13 +617,17 @@ def main():
                 "workload": "C1 fixed_radius_search: layers.FixedRadiusSearch forward (hash build + search) "
                             f"over {args.scenes} scenes/GPU x 65,536 U[0,1)^3 pts, r=0.05, L2, int32 idx",
                 "scenes_per_gpu": args.scenes, "points_per_scene": N_POINTS, "radius": RADIUS,
-                "pairs_per_step_rank0": pairs, "parallelism": f"scene-dp{world}"},
+                "pairs_per_step_rank0": pairs, "parallelism": f"scene-dp{world}",
+                "queries_per_rank": units},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic(dominant), "kernel_ms": round(ms, 5),
                          "kernel_ms_all": {k: round(v, 5) for k, v in avg.items()},
                          "alg_bytes_per_launch": int(alg_bytes), "mean_neighbors": round(mean_nbrs, 3),
-                         "issue": issue_bound(dominant)},
+                         "issue": issue_bound(dominant),
+                         "step": {"achieved": round(step_achieved, 2), "frac": round(step_achieved / HBM_PEAK_GBS, 4),
+                                  "note": "same algorithmic bytes / ms_per_step (hash build, search, "
+                                          "row copy and host gaps included)"}},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

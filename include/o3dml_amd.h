@@ -117,7 +117,11 @@ int o3dml_fixed_radius_search_fill_bounded(const float* points, int64_t n_points
  * (ml3d/datasets/utils/dataprocessing.py:99-101 <- randlanet.py:218-229).
  * Per query the min(k, N_b) nearest points of its batch item, ascending
  * (distance, index); distances squared for L2.  k <= 64: grid ring search;
- * k > 64: per-query full sort (few queries, e.g. the patch crop).
+ * 64 < k <= 2048: batched, one workgroup per query over the cell cube that
+ * holds its k nearest, LDS bitonic sort (nns_many.hip); larger k (few
+ * queries, e.g. the 45,056-point patch crop) and queries whose candidates
+ * overflow the LDS list: per-query full sort.  ignore_query_point drops every
+ * point at the query's exact position, for every k.
  * The *_host row splits are host copies (grid planning); self_search = 1
  * when queries are the points themselves (same splits). ------------------- */
 size_t o3dml_knn_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t k, int64_t n_batch);
@@ -127,10 +131,38 @@ int o3dml_knn_search_count(const float* points, int64_t n_points, const float* q
                            int ignore_query_point, int self_search, int64_t* neighbors_row_splits, void* workspace,
                            size_t workspace_bytes, void* stream);
 int o3dml_knn_search_fill(const float* points, int64_t n_points, const float* queries, int64_t n_queries, int64_t k,
-                          int64_t n_batch, const int64_t* points_row_splits_host,
-                          const int64_t* queries_row_splits_host, int metric, const int64_t* neighbors_row_splits,
-                          int index_bits, void* neighbors_index, float* neighbors_distance, void* workspace,
-                          size_t workspace_bytes, void* stream);
+                          int64_t n_batch, const int64_t* queries_row_splits, const int64_t* points_row_splits_host,
+                          const int64_t* queries_row_splits_host, int metric, int ignore_query_point,
+                          const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
+                          float* neighbors_distance, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- radius search: replaces open3d.ml.torch.ops.radius_search /
+ * layers.RadiusSearch (Open3D ml ops API; SURVEY.md §2.2, no reference model
+ * calls it).  Per query q every point of its batch item with
+ * dist <= radii[q] (L2: squared distance <= radii[q]^2; L1; Linf), ascending
+ * (distance, index); ignore_query_point drops points at the query's exact
+ * position; normalize_distances divides each distance by radii[q] (L2:
+ * radii[q]^2).  Phases: _count (grid build + counts -> neighbors_row_splits,
+ * device), _totals ([total, longest row] into a host buffer), _fill (rows up
+ * to 8192 sorted in LDS; longer rows written unsorted WITH distances), then,
+ * only if the longest row exceeds 8192, _sort_long_rows with the host copy of
+ * the row splits.  radii: device f32 [M]. -------------------------------- */
+size_t o3dml_radius_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t n_batch);
+int o3dml_radius_search_count(const float* points, int64_t n_points, const float* queries, int64_t n_queries,
+                              const float* radii, int64_t n_batch, const int64_t* points_row_splits,
+                              const int64_t* queries_row_splits, int metric, int ignore_query_point,
+                              int64_t* neighbors_row_splits, void* workspace, size_t workspace_bytes, void* stream);
+int o3dml_radius_search_totals(const int64_t* neighbors_row_splits, int64_t n_queries, void* workspace,
+                               int64_t* totals, void* stream);
+int o3dml_radius_search_fill(const float* points, int64_t n_points, const float* queries, int64_t n_queries,
+                             const float* radii, int64_t n_batch, const int64_t* queries_row_splits, int metric,
+                             int ignore_query_point, int normalize_distances, const int64_t* neighbors_row_splits,
+                             int64_t max_row, int index_bits, void* neighbors_index, float* neighbors_distance,
+                             void* workspace, size_t workspace_bytes, void* stream);
+int o3dml_radius_search_sort_long_rows(int64_t n_points, int64_t n_queries, int64_t n_batch,
+                                       const int64_t* rows_host, int index_bits, void* neighbors_index,
+                                       float* neighbors_distance, void* workspace, size_t workspace_bytes,
+                                       void* stream);
 
 /* ---- voxelize: replaces open3d.ml.torch.ops.voxelize
  * (ml3d/torch/models/point_pillars.py:352-357, sparseconvnet.py:293-298).

@@ -1016,28 +1016,59 @@ static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m, int64_t nb, bool d
 #ifndef O3DML_FRS_REL16
 #define O3DML_FRS_REL16 1
 #endif
-// Side stream per device for the re-run of rows longer than kRowCap: it
-// needs only the count's outputs and writes rows the row copy skips, so it
-// runs beside the copy (fork: recorded on the caller's stream at the end of
-// _count; join: the caller's stream waits for it).  Created once, never freed.
+// Side stream for the re-run of rows longer than kRowCap, one per device of
+// the CALLER'S stream (not the current device: the tensors may live on
+// another GPU).  The re-run needs only the count's outputs and writes rows the
+// row copy skips, so it runs beside the copy: fork = an event recorded on the
+// caller's stream when the fill is issued (after the count, before the copy),
+// join = the caller's stream waits for the side stream.  The fork/launch/join
+// sequence holds the device's lock, so concurrent searches on other streams
+// or threads can neither re-record the fork nor the join in between (an event
+// wait binds the event's state at the time of the wait call).  Created once,
+// never freed.
 struct FrsSide {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    std::mutex mu;
 };
-static FrsSide& frs_side() {
+static int stream_device(hipStream_t st) {
+    int dev = 0;
+    if (st) {
+        hipDevice_t d = 0;
+        O3DML_CHECK_HIP(hipStreamGetDevice(st, &d));
+        dev = static_cast<int>(d);
+    } else {
+        O3DML_CHECK_HIP(hipGetDevice(&dev));
+    }
+    return dev;
+}
+static FrsSide& frs_side(int dev) {
     static std::mutex mu;
     static FrsSide side[64];
-    int dev = 0;
-    O3DML_CHECK_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lock(mu);
     FrsSide& x = side[dev & 63];
     if (!x.s) {
+        int cur = 0;
+        O3DML_CHECK_HIP(hipGetDevice(&cur));
+        O3DML_CHECK_HIP(hipSetDevice(dev));  // the stream and events belong to the caller's device
         O3DML_CHECK_HIP(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking));
         O3DML_CHECK_HIP(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming));
         O3DML_CHECK_HIP(hipEventCreateWithFlags(&x.join, hipEventDisableTiming));
+        O3DML_CHECK_HIP(hipSetDevice(cur));
     }
     return x;
 }
+// Restores the current device on scope exit (launches follow the stream's device).
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        O3DML_CHECK_HIP(hipGetDevice(&prev));
+        if (prev != dev) O3DML_CHECK_HIP(hipSetDevice(dev)); else prev = -1;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
 
 // [total, overflow count] straight into the caller's pinned host buffer
 __global__ void frs_totals_kernel(const int64_t* __restrict__ rs, int64_t m, const int64_t* __restrict__ scalars,
@@ -1142,7 +1173,6 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     }
     Workspace sws = ws;
     prim::scan<uint32_t, int64_t>(pl.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
-    O3DML_CHECK_HIP(hipEventRecord(frs_side().fork, st));  // the overflow re-run may start here
     O3DML_GUARD_END
 }
 
@@ -1195,6 +1225,15 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
     const float inv = 1.0f / (2.0f * radius);
     int64_t* rs = const_cast<int64_t*>(neighbors_row_splits);
     float* dist = with_distances ? neighbors_distance : nullptr;
+    const int dev = stream_device(st);
+    DeviceScope dscope(dev);
+    FrsSide* side = nullptr;
+    std::unique_lock<std::mutex> side_lock;
+    if (parts & 2) {  // fork before the row copy is queued: the re-run runs beside it
+        side = &frs_side(dev);
+        side_lock = std::unique_lock<std::mutex>(side->mu);
+        O3DML_CHECK_HIP(hipEventRecord(side->fork, st));
+    }
     if (parts & 1) {
         TimedRegion tr("frs_group_rows", st);
         const unsigned gc = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_queries, 256), 1 << 16)));
@@ -1220,10 +1259,9 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
     // rows; the overflow count stays on the device (no host round trip), so a
     // fixed grid strides over however many there are (usually none)
     if (!(parts & 2)) return 0;  // the caller read a zero overflow count
-    FrsSide& side = frs_side();
-    O3DML_CHECK_HIP(hipStreamWaitEvent(side.s, side.fork, 0));
+    O3DML_CHECK_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
     const hipStream_t st_main = st;
-    st = side.s;
+    st = side->s;
     const unsigned go = static_cast<unsigned>(std::min<int64_t>(n_queries, 256));
     const float4* qraw = reinterpret_cast<const float4*>(queries);  // MODE 1 reads [M, 3] via the over list
     if (index_bits == 32)
@@ -1242,7 +1280,7 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
                                  points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
                                  static_cast<int64_t*>(neighbors_index), dist, pl.dir, pl.dir_cap, rs + n_queries,
                                  capacity);
-    O3DML_CHECK_HIP(hipEventRecord(side.join, st));
-    O3DML_CHECK_HIP(hipStreamWaitEvent(st_main, side.join, 0));
+    O3DML_CHECK_HIP(hipEventRecord(side->join, st));
+    O3DML_CHECK_HIP(hipStreamWaitEvent(st_main, side->join, 0));
     O3DML_GUARD_END
 }

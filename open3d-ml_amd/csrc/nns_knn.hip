@@ -346,7 +346,8 @@ __global__ void compact_rows_kernel(const int32_t* __restrict__ si, const float*
     }
 }
 
-// ---- k > 64: one query at a time, full sort of its batch item's distances ----
+// ---- k > kManyKnnMaxK (and the overflow queries of nns_many.hip): one query
+// at a time, every distance of its batch item + a stable radix sort ----
 __global__ void bigk_counts_kernel(const int64_t* __restrict__ prs, const int64_t* __restrict__ qrs, int nb,
                                    int64_t m, int64_t k, int64_t* __restrict__ counts) {
     for (int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; q < m;
@@ -357,20 +358,54 @@ __global__ void bigk_counts_kernel(const int64_t* __restrict__ prs, const int64_
     }
 }
 
+// ignore_query_point: min(k, N_b - points at the query's exact position), one
+// workgroup per query over its batch item
+__global__ void __launch_bounds__(256) bigk_counts_ignore_kernel(const float* __restrict__ pts,
+                                                                 const float* __restrict__ queries,
+                                                                 const int64_t* __restrict__ prs,
+                                                                 const int64_t* __restrict__ qrs, int nb, int64_t m,
+                                                                 int64_t k, int64_t* __restrict__ counts) {
+    __shared__ uint32_t s_same;
+    for (int64_t q = blockIdx.x; q < m; q += gridDim.x) {
+        if (threadIdx.x == 0) s_same = 0;
+        __syncthreads();
+        const int b = batch_of(q, qrs, nb);
+        const float qx = queries[3 * q], qy = queries[3 * q + 1], qz = queries[3 * q + 2];
+        uint32_t same = 0;
+        for (int64_t i = prs[b] + threadIdx.x; i < prs[b + 1]; i += blockDim.x)
+            same += (pts[3 * i] == qx && pts[3 * i + 1] == qy && pts[3 * i + 2] == qz) ? 1u : 0u;
+        same = wave_sum(same);
+        if ((threadIdx.x & 63) == 0 && same) atomicAdd(&s_same, same);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int64_t n = prs[b + 1] - prs[b] - s_same;
+            counts[q] = n < k ? n : k;
+        }
+        __syncthreads();
+    }
+}
+
+// distance bits of every point of the query's batch item; with ignore, the
+// points at the query's position get the largest key (sorted past the row)
 template <int METRIC>
 __global__ void dist_keys_kernel(const float* __restrict__ pts, int64_t s, int64_t n, const float* __restrict__ q,
-                                 uint32_t* __restrict__ keys) {
+                                 int ignore, uint32_t* __restrict__ keys) {
     const float qx = q[0], qy = q[1], qz = q[2];
     for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
          j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int64_t i = s + j;
-        keys[j] = __float_as_uint(dist_metric<METRIC>(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], qx, qy, qz));
+        const float px = pts[3 * i], py = pts[3 * i + 1], pz = pts[3 * i + 2];
+        keys[j] = ignore && px == qx && py == qy && pz == qz
+                          ? 0xffffffffu
+                          : __float_as_uint(dist_metric<METRIC>(px, py, pz, qx, qy, qz));
     }
 }
 
-__global__ void write_bigk_kernel(const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sidx, int64_t cnt,
-                                  int64_t base_id, int64_t out_off, int bits, void* __restrict__ out_idx,
-                                  float* __restrict__ out_dist) {
+// the first rs[q+1] - rs[q] sorted entries into the row at rs[q]
+__global__ void write_bigk_kernel(const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sidx,
+                                  const int64_t* __restrict__ rs, int64_t q, int64_t base_id, int bits,
+                                  void* __restrict__ out_idx, float* __restrict__ out_dist) {
+    const int64_t out_off = rs[q], cnt = rs[q + 1] - out_off;
     for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < cnt;
          j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int64_t id = base_id + sidx[j];
@@ -381,6 +416,33 @@ __global__ void write_bigk_kernel(const uint32_t* __restrict__ skeys, const uint
         if (out_dist) out_dist[out_off + j] = __uint_as_float(skeys[j]);
     }
 }
+
+// One query of the per-query path (host-side loop driver).
+static void bigk_one(const float* points, const float* queries, int64_t q, int64_t ps, int64_t pn, int64_t k,
+                     int metric, int ignore, const int64_t* rs, int bits, void* oi, float* od, uint32_t* keys,
+                     uint32_t* skeys, uint32_t* sidx, Workspace ws, hipStream_t st) {
+    if (pn == 0) return;
+    const unsigned g = stream_grid(pn, 256);
+    if (metric == kL2)
+        dist_keys_kernel<kL2><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, ignore, keys);
+    else if (metric == kL1)
+        dist_keys_kernel<kL1><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, ignore, keys);
+    else
+        dist_keys_kernel<kLinf><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, ignore, keys);
+    O3DML_LAUNCH_CHECK();
+    prim::radix_sort_pairs<uint32_t>(keys, nullptr, skeys, sidx, pn, 32, ws, st);
+    write_bigk_kernel<<<stream_grid(std::min(k, pn), 256), 256, 0, st>>>(skeys, sidx, rs, q, ps, bits, oi, od);
+    O3DML_LAUNCH_CHECK();
+}
+
+// nns_many.hip: batched 64 < k <= kManyKnnMaxK
+constexpr int64_t kManyKnnMaxK = 2048;
+size_t knn_many_workspace_bytes(int64_t n, int64_t m, int64_t k, int64_t nb);
+void knn_many_count(const float* pts, int64_t n, const float* queries, int64_t m, int64_t k, int nb,
+                    const int64_t* prs, const int64_t* qrs, int ignore, int64_t* rs, Workspace ws, hipStream_t st);
+void knn_many_fill(const float* pts, int64_t n, const float* queries, int64_t m, int64_t k, int nb,
+                   const int64_t* qrs, int metric, int ignore, const int64_t* rs, int bits, void* oi, float* od,
+                   Workspace ws, hipStream_t st, uint32_t** over, int64_t** n_over);
 
 }  // namespace o3dml
 
@@ -409,9 +471,9 @@ static double knn_min_target() {
 
 O3DML_API size_t o3dml_knn_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t k, int64_t n_batch) {
     if (knn_bucket(k) == 0) {
-        int64_t maxn = n_points;
-        return std::max(3 * ws_bytes<uint32_t>(maxn) + prim::radix_sort_workspace_bytes<uint32_t>(maxn),
-                        ws_bytes<int64_t>(n_queries) + prim::scan_workspace_bytes(n_queries));
+        const size_t one = 3 * ws_bytes<uint32_t>(n_points) + prim::radix_sort_workspace_bytes<uint32_t>(n_points);
+        if (k <= kManyKnnMaxK) return knn_many_workspace_bytes(n_points, n_queries, k, n_batch) + one;
+        return std::max(one, ws_bytes<int64_t>(n_queries) + prim::scan_workspace_bytes(n_queries));
     }
     return grid_workspace_bytes(n_points, static_cast<int>(n_batch), kKnnCapFactor) +
            3 * ws_bytes<uint32_t>(n_queries) + prim::radix_sort_workspace_bytes<uint32_t>(n_queries) +
@@ -437,15 +499,23 @@ O3DML_API int o3dml_knn_search_count(const float* points, int64_t n_points, cons
     const int nb = static_cast<int>(n_batch);
     const int K = knn_bucket(k);
     if (K == 0) {
-        O3DML_REQUIRE(!ignore_query_point, "ignore_query_point is not supported for k > 64");
-        // rows: min(k, N_b) per query, on the device (no host round trip)
+        // rows: min(k, eligible points) per query, on the device (no host round trip)
         (void)points_row_splits_host;
         (void)queries_row_splits_host;
+        if (k <= kManyKnnMaxK) {  // batched (nns_many.hip): grid + eligible counts
+            knn_many_count(points, n_points, queries, n_queries, k, nb, points_row_splits, queries_row_splits,
+                           ignore_query_point, neighbors_row_splits, ws, st);
+            return 0;
+        }
         O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
         if (n_queries == 0) return 0;
         int64_t* cnt = ws.take<int64_t>(n_queries);
-        bigk_counts_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(points_row_splits, queries_row_splits, nb,
-                                                                       n_queries, k, cnt);
+        if (ignore_query_point)
+            bigk_counts_ignore_kernel<<<static_cast<unsigned>(std::min<int64_t>(n_queries, 1 << 16)), 256, 0, st>>>(
+                    points, queries, points_row_splits, queries_row_splits, nb, n_queries, k, cnt);
+        else
+            bigk_counts_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(points_row_splits, queries_row_splits,
+                                                                           nb, n_queries, k, cnt);
         O3DML_LAUNCH_CHECK();
         prim::scan<int64_t, int64_t>(cnt, neighbors_row_splits + 1, n_queries, true, ws, st);
         return 0;
@@ -490,9 +560,9 @@ O3DML_API int o3dml_knn_search_count(const float* points, int64_t n_points, cons
 }
 
 O3DML_API int o3dml_knn_search_fill(const float* points, int64_t n_points, const float* queries, int64_t n_queries,
-                                    int64_t k, int64_t n_batch, const int64_t* points_row_splits_host,
-                                    const int64_t* queries_row_splits_host, int metric,
-                                    const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
+                                    int64_t k, int64_t n_batch, const int64_t* queries_row_splits,
+                                    const int64_t* points_row_splits_host, const int64_t* queries_row_splits_host,
+                                    int metric, int ignore_query_point, const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
                                     float* neighbors_distance, void* workspace, size_t workspace_bytes,
                                     void* stream) {
     O3DML_GUARD_BEGIN
@@ -503,30 +573,39 @@ O3DML_API int o3dml_knn_search_fill(const float* points, int64_t n_points, const
     const int K = knn_bucket(k);
     if (n_queries == 0) return 0;
     if (K == 0) {
+        const bool many = k <= kManyKnnMaxK;
+        std::vector<uint32_t> qlist;
+        if (many) {  // batched; queries whose candidates overflow the LDS list come back listed
+            uint32_t* over = nullptr;
+            int64_t* n_over = nullptr;
+            knn_many_fill(points, n_points, queries, n_queries, k, nb, queries_row_splits, metric,
+                          ignore_query_point, neighbors_row_splits, index_bits, neighbors_index, neighbors_distance,
+                          ws, st, &over, &n_over);
+            int64_t nov = 0;
+            O3DML_CHECK_HIP(hipMemcpyAsync(&nov, n_over, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+            O3DML_CHECK_HIP(hipStreamSynchronize(st));
+            if (nov > 0) {
+                qlist.resize(static_cast<size_t>(nov));
+                O3DML_CHECK_HIP(hipMemcpyAsync(qlist.data(), over, sizeof(uint32_t) * nov, hipMemcpyDeviceToHost, st));
+                O3DML_CHECK_HIP(hipStreamSynchronize(st));
+                std::sort(qlist.begin(), qlist.end());
+            }
+            ws.take<uint8_t>(static_cast<int64_t>(knn_many_workspace_bytes(n_points, n_queries, k, n_batch)));
+        }
         uint32_t* keys = ws.take<uint32_t>(n_points);
         uint32_t* skeys = ws.take<uint32_t>(n_points);
         uint32_t* sidx = ws.take<uint32_t>(n_points);
-        int64_t off = 0;
-        for (int b = 0; b < nb; ++b) {
+        auto run = [&](int64_t q) {
+            int b = 0;
+            while (b + 1 < nb && queries_row_splits_host[b + 1] <= q) ++b;
             const int64_t ps = points_row_splits_host[b], pn = points_row_splits_host[b + 1] - ps;
-            const int64_t cnt = std::min<int64_t>(k, pn);
-            for (int64_t q = queries_row_splits_host[b]; q < queries_row_splits_host[b + 1]; ++q) {
-                if (cnt == 0) continue;
-                const unsigned g = stream_grid(pn, 256);
-                if (metric == kL2)
-                    dist_keys_kernel<kL2><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, keys);
-                else if (metric == kL1)
-                    dist_keys_kernel<kL1><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, keys);
-                else
-                    dist_keys_kernel<kLinf><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, keys);
-                O3DML_LAUNCH_CHECK();
-                Workspace sws = ws;
-                prim::radix_sort_pairs<uint32_t>(keys, nullptr, skeys, sidx, pn, 32, sws, st);
-                write_bigk_kernel<<<stream_grid(cnt, 256), 256, 0, st>>>(skeys, sidx, cnt, ps, off, index_bits,
-                                                                        neighbors_index, neighbors_distance);
-                O3DML_LAUNCH_CHECK();
-                off += cnt;
-            }
+            bigk_one(points, queries, q, ps, pn, k, metric, ignore_query_point, neighbors_row_splits, index_bits,
+                     neighbors_index, neighbors_distance, keys, skeys, sidx, ws, st);
+        };
+        if (many) {
+            for (uint32_t q : qlist) run(q);
+        } else {
+            for (int64_t q = 0; q < n_queries; ++q) run(q);
         }
         return 0;
     }

@@ -26,6 +26,14 @@ def gpu_device(*tensors):
 
 
 def stream_handle(device):
+    """The current torch stream of `device`.  The op's device is made the
+    current one first: the library's launches, scratch streams and events then
+    belong to the device that holds the tensors even when the caller's current
+    device is another GPU (and torch's default stream handle, the null stream,
+    resolves to that device)."""
+    device = torch.device(device)
+    if device.index is not None and torch.cuda.current_device() != device.index:
+        torch.cuda.set_device(device)
     return torch.cuda.current_stream(device).cuda_stream
 
 
@@ -33,7 +41,7 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
-_SMALL_CACHE = OrderedDict()  # (device, dtype, shape, bytes) -> device tensor
+_SMALL_CACHE = OrderedDict()  # (device, stream, dtype, shape, bytes) -> device tensor
 _SMALL_CACHE_MAX = 64
 _SMALL_NUMEL = 4096
 
@@ -46,7 +54,11 @@ def to_dev(t, device, dtype=None):
     synchronise the stream with the host.  Small host integer arrays (row
     splits, table splits: the same few values call after call) are kept on the
     device in a small LRU cache keyed by their bytes, so a repeated batch
-    layout costs no transfer at all; the ops only ever read these tensors."""
+    layout costs no transfer at all; the ops only ever read these tensors.
+    The cache key holds the current stream: an entry is only handed out on
+    the stream its upload was queued on (so every use is ordered after the
+    copy), and an evicted block returns to that stream's pool, the only one
+    that ever used it."""
     if not isinstance(t, torch.Tensor):
         t = torch.as_tensor(np.asarray(t))
     if dtype is not None and t.dtype != dtype:
@@ -55,7 +67,8 @@ def to_dev(t, device, dtype=None):
         t = t.contiguous()
         if (t.numel() <= _SMALL_NUMEL and t.dtype in (torch.int32, torch.int64) and not t.requires_grad
                 and not torch.cuda.is_current_stream_capturing()):
-            key = (str(torch.device(device)), t.dtype, tuple(t.shape), t.numpy().tobytes())
+            key = (str(torch.device(device)), torch.cuda.current_stream(device).cuda_stream, t.dtype,
+                   tuple(t.shape), t.numpy().tobytes())
             hit = _SMALL_CACHE.get(key)
             if hit is not None:
                 _SMALL_CACHE.move_to_end(key)

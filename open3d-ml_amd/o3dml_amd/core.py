@@ -104,12 +104,21 @@ class NearestNeighborSearch:
         return Tensor(idx.cpu()), Tensor(dist.cpu())
 
     def fixed_radius_search(self, query_points, radius=None, sort=True):
-        """-> (indices Int64 [P], squared distances Float32 [P], row splits Int64 [Nq+1])."""
+        """-> (indices Int64 [P], squared distances Float32 [P], row splits Int64 [Nq+1]).
+        sort=True (Open3D's default) orders every row by ascending distance,
+        ties in the canonical (bucket, id) order; sort=False keeps that order."""
         r = self._radius if radius is None else radius
         q = _as_torch(query_points).float().to(self._dev).contiguous()
         res = ops.fixed_radius_search(self._pts, q, float(r), index_dtype=torch.int64, return_distances=True)
-        return (Tensor(res.neighbors_index.cpu()), Tensor(res.neighbors_distance.cpu()),
-                Tensor(res.neighbors_row_splits.cpu()))
+        idx, dist, rs = res.neighbors_index, res.neighbors_distance, res.neighbors_row_splits
+        if sort and idx.numel():
+            # rows by ascending distance: a stable sort by distance, then a
+            # stable sort by row keeps each row's distance order (and ties)
+            row = torch.repeat_interleave(torch.arange(rs.numel() - 1, device=rs.device), rs[1:] - rs[:-1])
+            o = torch.sort(dist, stable=True).indices
+            o = o[torch.sort(row[o], stable=True).indices]
+            idx, dist = idx[o], dist[o]
+        return Tensor(idx.cpu()), Tensor(dist.cpu()), Tensor(rs.cpu())
 
 
 nns = types.SimpleNamespace(NearestNeighborSearch=NearestNeighborSearch)

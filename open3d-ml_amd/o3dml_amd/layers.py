@@ -61,6 +61,31 @@ class KNNSearch(torch.nn.Module):
                               return_distances=self.return_distances)
 
 
+class RadiusSearch(torch.nn.Module):
+    """Open3D ``layers.RadiusSearch`` (per-query radii; Open3D ml API,
+    SURVEY §2.2): ops.radius_search with the layer's options."""
+
+    def __init__(self, metric="L2", ignore_query_point=False, return_distances=False,
+                 normalize_distances=False, index_dtype=torch.int32, **kwargs):
+        super().__init__()
+        self.metric = metric
+        self.ignore_query_point = ignore_query_point
+        self.return_distances = return_distances
+        self.normalize_distances = normalize_distances
+        self.index_dtype = index_dtype
+
+    def forward(self, points, queries, radii, points_row_splits=None, queries_row_splits=None):
+        if points_row_splits is None:
+            points_row_splits = torch.LongTensor([0, points.shape[0]])
+        if queries_row_splits is None:
+            queries_row_splits = torch.LongTensor([0, queries.shape[0]])
+        return ops.radius_search(points, queries, radii, points_row_splits, queries_row_splits,
+                                 index_dtype=self.index_dtype, metric=self.metric,
+                                 ignore_query_point=self.ignore_query_point,
+                                 return_distances=self.return_distances,
+                                 normalize_distances=self.normalize_distances)
+
+
 def _voxel_size_scalar(voxel_size, like):
     if isinstance(voxel_size, torch.Tensor):
         if voxel_size.dim() != 0 and voxel_size.numel() != 1:

@@ -139,11 +139,17 @@ def _pinned_slot(device, n):
     return buf[:n]
 
 
-# Neighbours per query of the last search per (radius, metric): the capacity
-# guess that lets the fill be queued before the host reads the total, so the
-# GPU does not idle through that read.  A guess that proves too small costs
-# one more (exact) fill; the rows are always the exact ones.
+# Neighbours per query of the last search per (radius, metric, points,
+# queries): the capacity guess that lets the fill be queued before the host
+# reads the total, so the GPU does not idle through that read.  A guess that
+# proves too small costs one more (exact) fill; the rows are always the exact
+# ones.  The key holds the cloud sizes, so a dense cloud's density is never
+# applied to another call shape; a guess above _FRS_GUESS_MAX_BYTES reads the
+# total first instead, and a result far below its capacity is returned as a
+# compact copy (a view would keep the whole speculative buffer alive).
 _FRS_DENSITY = {}
+_FRS_GUESS_MAX_BYTES = 1 << 30
+_FRS_SLACK = 1.25
 
 
 def _frs_count_fill(rs, state, key, m, index_dtype, extra=None):
@@ -166,13 +172,14 @@ def _frs_count_fill(rs, state, key, m, index_dtype, extra=None):
         _lib.call("o3dml_fixed_radius_search_totals", ptr(rs), m, ptr(ws), host.data_ptr(), st)
     ready = torch.cuda.Event()
     ready.record(torch.cuda.current_stream(rs.device))
-    if guess is None or m == 0:
+    cap = 0 if guess is None else int(m * guess * 1.0625) + 1024
+    elem = (4 if index_bits(index_dtype) == 32 else 8) + (4 if state[6] else 0)
+    if guess is None or m == 0 or cap * elem > _FRS_GUESS_MAX_BYTES:
         ready.synchronize()
         vals = host.tolist()
         idx, dist = _frs_alloc(state, int(vals[0]), index_dtype)
         _frs_launch_fill(rs, state, idx, dist, -1, 1 | (2 if vals[1] else 0))
     else:
-        cap = int(m * guess * 1.0625) + 1024
         idx, dist = _frs_alloc(state, cap, index_dtype)
         _frs_launch_fill(rs, state, idx, dist, cap, 1)
         ready.synchronize()
@@ -181,8 +188,9 @@ def _frs_count_fill(rs, state, key, m, index_dtype, extra=None):
         if total <= cap:
             if vals[1]:
                 _frs_launch_fill(rs, state, idx, dist, cap, 2)
-            idx = idx[:total]
-            dist = dist[:total] if dist.numel() else dist
+            compact = cap > _FRS_SLACK * total + 1024
+            idx = idx[:total].clone() if compact else idx[:total]
+            dist = (dist[:total].clone() if compact else dist[:total]) if dist.numel() else dist
         else:
             idx, dist = _frs_alloc(state, total, index_dtype)
             _frs_launch_fill(rs, state, idx, dist, -1, 1 | (2 if vals[1] else 0))
@@ -206,7 +214,8 @@ def fixed_radius_search(points, queries, radius, points_row_splits=None, queries
     index_bits(index_dtype)
     rs, state = _frs_count(points, queries, radius, points_row_splits, queries_row_splits, hash_table_splits,
                            hash_table_index, hash_table_cell_splits, metric, ignore_query_point, return_distances)
-    idx, dist, _ = _frs_count_fill(rs, state, (scalar(radius), metric_code(metric)), queries.shape[0], index_dtype)
+    idx, dist, _ = _frs_count_fill(rs, state, (scalar(radius), metric_code(metric), points.shape[0], queries.shape[0]),
+                                   queries.shape[0], index_dtype)
     return FixedRadiusSearchResult(back_to(idx, points), back_to(rs, points), back_to(dist, points))
 
 
@@ -224,7 +233,7 @@ def fixed_radius_search_dense(points, queries, radius, points_row_splits, querie
     if m == 0:
         return torch.zeros((0, 0), dtype=torch.int32, device=rs.device)
     # the total and the width in one host read, after the fill is queued
-    idx, _, (_total, width) = _frs_count_fill(rs, state, (scalar(radius), -1), m, torch.int32,
+    idx, _, (_total, width) = _frs_count_fill(rs, state, (scalar(radius), -1, points.shape[0], m), m, torch.int32,
                                               extra=[(rs[1:] - rs[:-1]).max()])
     width = int(width)
     return ragged_to_dense(idx.reshape(-1, 1), rs, width,
@@ -272,9 +281,62 @@ def knn_search(points, queries, k, points_row_splits=None, queries_row_splits=No
         total = int(sum((qrs[b + 1] - qrs[b]) * min(k, prs[b + 1] - prs[b]) for b in range(B)))
     idx = torch.empty(total, dtype=torch.int32 if bits == 32 else torch.int64, device=dev)
     dist = torch.empty(total if return_distances else 0, dtype=torch.float32, device=dev)
-    _lib.call("o3dml_knn_search_fill", ptr(pts), n, ptr(qry), m, k, B, prs.ctypes.data, qrs.ctypes.data, mcode,
-              ptr(rs), bits, ptr(idx), ptr(dist) if return_distances else None, ptr(ws), ws.numel(), st)
+    _lib.call("o3dml_knn_search_fill", ptr(pts), n, ptr(qry), m, k, B, ptr(qrs_d), prs.ctypes.data,
+              qrs.ctypes.data, mcode, int(bool(ignore_query_point)), ptr(rs), bits, ptr(idx),
+              ptr(dist) if return_distances else None, ptr(ws), ws.numel(), st)
     return KnnSearchResult(back_to(idx, points), back_to(rs, points), back_to(dist, points))
+
+
+def radius_search(points, queries, radii, points_row_splits=None, queries_row_splits=None,
+                  index_dtype=torch.int32, metric="L2", ignore_query_point=False, return_distances=False,
+                  normalize_distances=False):
+    """Open3D ``ops.radius_search`` (per-query radius; Open3D ml ops API,
+    SURVEY §2.2 — no reference model calls it): per query q every point of its
+    batch item with dist <= radii[q] (L2 squared against radii[q]^2), rows in
+    ascending (distance, index) order; normalize_distances divides by radii[q]
+    (L2: radii[q]^2).  Returns (neighbors_index [P], neighbors_row_splits int64
+    [M+1], neighbors_distance [P] or [0])."""
+    dev = gpu_device(points, queries, radii)
+    check_points("points", points)
+    check_points("queries", queries)
+    bits = index_bits(index_dtype)
+    mcode = metric_code(metric)
+    lib = _lib.load()
+    n, m = points.shape[0], queries.shape[0]
+    rad = to_dev(torch.as_tensor(radii), dev, torch.float32).reshape(-1)
+    if rad.numel() != m:
+        raise RuntimeError(f"radii must have one entry per query ({m}), got {rad.numel()}")
+    prs = row_splits_host(points_row_splits, n)
+    qrs = row_splits_host(queries_row_splits, m)
+    if len(prs) != len(qrs):
+        raise RuntimeError("points_row_splits and queries_row_splits must have the same length")
+    pts = to_dev(points, dev)
+    qry = to_dev(queries, dev)
+    prs_d = to_dev(prs, dev)
+    qrs_d = to_dev(qrs, dev)
+    B = len(prs) - 1
+    st = stream_handle(dev)
+    rs = torch.empty(m + 1, dtype=torch.int64, device=dev)
+    ws = workspace(lib.o3dml_radius_search_workspace_size(n, m, B), dev)
+    _lib.call("o3dml_radius_search_count", ptr(pts), n, ptr(qry), m, ptr(rad), B, ptr(prs_d), ptr(qrs_d), mcode,
+              int(bool(ignore_query_point)), ptr(rs), ptr(ws), ws.numel(), st)
+    host = _pinned_slot(rs.device, 2)
+    _lib.call("o3dml_radius_search_totals", ptr(rs), m, ptr(ws), host.data_ptr(), st)
+    torch.cuda.current_stream(dev).synchronize()
+    total, max_row = (int(v) for v in host.tolist())
+    long_rows = max_row > 8192
+    idx = torch.empty(total, dtype=torch.int32 if bits == 32 else torch.int64, device=dev)
+    dist = torch.empty(total if (return_distances or long_rows) else 0, dtype=torch.float32, device=dev)
+    _lib.call("o3dml_radius_search_fill", ptr(pts), n, ptr(qry), m, ptr(rad), B, ptr(qrs_d), mcode,
+              int(bool(ignore_query_point)), int(bool(normalize_distances)), ptr(rs), max_row, bits, ptr(idx),
+              ptr(dist) if dist.numel() else None, ptr(ws), ws.numel(), st)
+    if long_rows:  # rows past the LDS list were written unsorted
+        rows = rs.cpu().numpy()
+        _lib.call("o3dml_radius_search_sort_long_rows", n, m, B, rows.ctypes.data, bits, ptr(idx), ptr(dist),
+                  ptr(ws), ws.numel(), st)
+    if not return_distances:
+        dist = torch.empty(0, dtype=torch.float32, device=dev)
+    return RadiusSearchResult(back_to(idx, points), back_to(rs, points), back_to(dist, points))
 
 
 # ---------------------------------------------------------------------------
@@ -533,7 +595,7 @@ def nms(boxes, scores, nms_overlap_thresh):
 from .sparse_conv import sparse_conv, sparse_conv_transpose  # noqa: E402,F401
 
 
-__all__ = ["build_spatial_hash_table", "fixed_radius_search", "knn_search", "ragged_to_dense",
+__all__ = ["build_spatial_hash_table", "fixed_radius_search", "knn_search", "radius_search", "ragged_to_dense",
            "reduce_subarrays_sum", "voxelize", "grid_subsample", "calculate_grid", "furthest_point_sampling",
            "ball_query", "three_nn", "three_interpolate", "three_interpolate_grad", "nms", "sparse_conv",
            "sparse_conv_transpose"]

@@ -25,6 +25,41 @@ def _opt(t, dev, dtype=torch.float32):
 # GEMM is wide enough that the saved MFMA work beats the sort's few launches.
 TILE_ORDER_MIN_CHANNELS = 64 * 64
 
+def _build_map(nidx, kidx, nimp, rs, n_in, K, normalize, out_importance, want_inv, tile_order, dev, st):
+    """Dense kernel map of the CSR pairs (o3dml_sparse_conv_build_map)."""
+    lib = _lib.load()
+    n_out = rs.shape[0] - 1
+    mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
+    status = np.zeros(1, np.int32)
+    _lib.call("o3dml_sparse_conv_build_map", ptr(nidx), ptr(kidx), ptr(nimp), ptr(rs), n_out, n_in, K,
+              int(bool(normalize)), ptr(out_importance), int(bool(want_inv)), status.ctypes.data, ptr(mws),
+              mws.numel(), st)
+    if status[0] & 2:
+        raise RuntimeError("sparse_conv: neighbors_kernel_index out of range for the filter")
+    if status[0] & 1:
+        raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index "
+                           "(non-lattice neighbourhood); not representable by the dense kernel map")
+    if tile_order:
+        _lib.call("o3dml_sparse_conv_tile_order", ptr(mws), mws.numel(), n_out, n_in, K, int(bool(want_inv)), st)
+    return mws, n_out
+
+
+def _backward(W, x, mws, sscale, meta, grad_out, need_w, need_x):
+    """(dW, dIn) through o3dml_sparse_conv_backward on a map built with the
+    inverse map (want_inv)."""
+    K, cin, cout, n_in, n_out, has_nimp, use_os, has_ss = meta[:8]
+    dev = grad_out.device
+    lib = _lib.load()
+    g = grad_out.contiguous().float()
+    gx = torch.empty((n_in, cin), dtype=torch.float32, device=dev) if need_x else None
+    gw = torch.empty(W.shape, dtype=torch.float32, device=dev) if need_w else None
+    ws = workspace(lib.o3dml_sparse_conv_backward_workspace_size(n_out, n_in, K, cin, cout), dev)
+    _lib.call("o3dml_sparse_conv_backward", ptr(W), K, cin, cout, ptr(x), n_in, ptr(sscale) if has_ss else None,
+              int(has_nimp), use_os, ptr(g), n_out, ptr(gx), ptr(gw), ptr(mws), mws.numel(), ptr(ws), ws.numel(),
+              stream_handle(dev))
+    return gw, gx
+
+
 class _ConvFn(torch.autograd.Function):
     """out = oscale * sum_k gather(x * sscale * pscale) @ W[k] (+ bias)."""
 
@@ -41,21 +76,9 @@ class _ConvFn(torch.autograd.Function):
         st = stream_handle(dev)
         if prebuilt is not None:  # dense map already built (lattice rulebook)
             mws, n_out = prebuilt
-        else:
-            n_out = rs.shape[0] - 1
-            mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
-            status = np.zeros(1, np.int32)
-            want_inv = int(bool(want_grad))  # the inverse map serves dIn / dW only
-            _lib.call("o3dml_sparse_conv_build_map", ptr(nidx), ptr(kidx), ptr(nimp), ptr(rs), n_out, n_in, K,
-                      int(bool(normalize)), ptr(out_importance), want_inv, status.ctypes.data, ptr(mws), mws.numel(),
-                      st)
-            if status[0] & 2:
-                raise RuntimeError("sparse_conv: neighbors_kernel_index out of range for the filter")
-            if status[0] & 1:
-                raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index "
-                                   "(non-lattice neighbourhood); not representable by the dense kernel map")
-            if cin * cout >= TILE_ORDER_MIN_CHANNELS:
-                _lib.call("o3dml_sparse_conv_tile_order", ptr(mws), mws.numel(), n_out, n_in, K, want_inv, st)
+        else:  # the inverse map serves dIn / dW only
+            mws, n_out = _build_map(nidx, kidx, nimp, rs, n_in, K, normalize, out_importance, want_grad,
+                                    cin * cout >= TILE_ORDER_MIN_CHANNELS, dev, st)
         W = filters.detach().contiguous()
         x = inp_features.detach().contiguous()
         out = torch.empty((n_out, cout), dtype=torch.float32, device=dev)
@@ -71,19 +94,32 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out):
         W, x, mws, sscale = ctx.saved_tensors
-        K, cin, cout, n_in, n_out, has_nimp, use_os, has_ss, has_bias = ctx.meta
-        dev = grad_out.device
-        lib = _lib.load()
-        g = grad_out.contiguous().float()
-        need_x, need_w = ctx.needs_input_grad[1], ctx.needs_input_grad[0]
-        gx = torch.empty((n_in, cin), dtype=torch.float32, device=dev) if need_x else None
-        gw = torch.empty(W.shape, dtype=torch.float32, device=dev) if need_w else None
-        ws = workspace(lib.o3dml_sparse_conv_backward_workspace_size(n_out, n_in, K, cin, cout), dev)
-        _lib.call("o3dml_sparse_conv_backward", ptr(W), K, cin, cout, ptr(x), n_in, ptr(sscale) if has_ss else None,
-                  int(has_nimp), use_os, ptr(g), n_out, ptr(gx), ptr(gw), ptr(mws), mws.numel(), ptr(ws), ws.numel(),
-                  stream_handle(dev))
-        gb = g.sum(0) if (has_bias and ctx.needs_input_grad[2]) else None
+        gw, gx = _backward(W, x, mws, sscale, ctx.meta, grad_out, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        gb = grad_out.float().sum(0) if (ctx.meta[8] and ctx.needs_input_grad[2]) else None
         return gw, gx, gb, None, None, None, None, None, None, None, None, None
+
+
+def conv_grads(filters, inp_features, grad_out, neighbors_index, neighbors_kernel_index, neighbors_importance,
+               neighbors_row_splits, sscale, normalize, out_importance, need_w=True, need_x=True):
+    """(dW, dIn) of _conv's output given grad_out, without the forward GEMM:
+    the map (with its inverse) is rebuilt and the backward kernels run —
+    the backward of the registered ``torch.ops.open3d.sparse_conv*`` ops."""
+    dev = gpu_device(inp_features, filters)
+    W = filters.to(dev).detach().contiguous()
+    x = inp_features.to(dev).detach().contiguous()
+    nidx = to_dev(neighbors_index, dev, torch.int32)
+    kidx = to_dev(neighbors_kernel_index, dev, torch.int32)
+    rs = to_dev(neighbors_row_splits, dev, torch.int64)
+    nimp = _opt(neighbors_importance, dev)
+    oimp = _opt(out_importance, dev)
+    K = int(np.prod(W.shape[:-2]))
+    cin, cout = int(W.shape[-2]), int(W.shape[-1])
+    mws, n_out = _build_map(nidx, kidx, nimp, rs, x.shape[0], K, normalize, oimp, True,
+                            cin * cout >= TILE_ORDER_MIN_CHANNELS, dev, stream_handle(dev))
+    use_os = int(bool(normalize) or oimp is not None)
+    meta = (K, cin, cout, x.shape[0], n_out, nimp is not None, use_os, sscale is not None)
+    ss = sscale if sscale is not None else torch.empty(0, device=dev)
+    return _backward(W, x, mws, ss, meta, grad_out.to(dev), need_w, need_x)
 
 
 def _conv(filters, inp_features, bias, neighbors_index, neighbors_kernel_index, neighbors_importance,
@@ -127,19 +163,25 @@ def sparse_conv_transpose(filters, out_importance, inp_features, inp_neighbors_i
     inp_neighbors_* is the same relation per INPUT point and, with normalize,
     each input's contribution is divided by its importance sum (or neighbour
     count).  out_importance scales the outputs."""
-    dev = gpu_device(inp_features, filters)
-    n_in = inp_features.shape[0]
-    ss = None
-    if normalize:
-        s = _opt(inp_neighbors_importance_sum, dev)
-        if s is None:
-            irs = to_dev(inp_neighbors_row_splits, dev, torch.int64)
-            s = (irs[1:] - irs[:-1]).float()
-        ss = torch.where(s != 0, 1.0 / s, torch.ones_like(s)).contiguous()
-        if ss.numel() != n_in:
-            raise RuntimeError("sparse_conv_transpose: inp_neighbors_* must describe every input point")
+    ss = transpose_scale(inp_features, filters, inp_neighbors_importance_sum, inp_neighbors_row_splits, normalize)
     return _conv(filters, inp_features, None, neighbors_index, neighbors_kernel_index, neighbors_importance,
                  neighbors_row_splits, ss, False, out_importance)
+
+
+def transpose_scale(inp_features, filters, inp_neighbors_importance_sum, inp_neighbors_row_splits, normalize):
+    """Per-input scale of sparse_conv_transpose(normalize=True): 1 / (importance
+    sum or neighbour count), 1 where that is 0; None without normalize."""
+    if not normalize:
+        return None
+    dev = gpu_device(inp_features, filters)
+    s = _opt(inp_neighbors_importance_sum, dev)
+    if s is None:
+        irs = to_dev(inp_neighbors_row_splits, dev, torch.int64)
+        s = (irs[1:] - irs[:-1]).float()
+    ss = torch.where(s != 0, 1.0 / s, torch.ones_like(s)).contiguous()
+    if ss.numel() != inp_features.shape[0]:
+        raise RuntimeError("sparse_conv_transpose: inp_neighbors_* must describe every input point")
+    return ss
 
 
 def conv_with_bias(filters, bias, inp_features, neighbors_index, neighbors_kernel_index, neighbors_row_splits,

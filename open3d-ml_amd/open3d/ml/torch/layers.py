@@ -1,2 +1,2 @@
-"""open3d.ml.torch.layers — FixedRadiusSearch, KNNSearch, SparseConv, SparseConvTranspose."""
-from o3dml_amd.layers import FixedRadiusSearch, KNNSearch, SparseConv, SparseConvTranspose  # noqa: F401
+"""open3d.ml.torch.layers — FixedRadiusSearch, RadiusSearch, KNNSearch, SparseConv, SparseConvTranspose."""
+from o3dml_amd.layers import FixedRadiusSearch, KNNSearch, RadiusSearch, SparseConv, SparseConvTranspose  # noqa: F401

@@ -135,3 +135,26 @@ def test_two_rank_pointpillars_ddp_gradients():
         assert p.exitcode == 0
     for _, err in out:
         assert err < 1e-5
+
+
+def test_bench_spawns_ranks_without_torchrun():
+    """`python bench.py --gpus 2` (no torchrun, WORLD_SIZE unset) starts two
+    ranks itself (mp.spawn + env:// rendezvous on 127.0.0.1, as the reference's
+    run_pipeline.py:194-206 does); rank 0 prints one line whose value
+    aggregates both ranks' units over the max-over-ranks time.  The launcher
+    path only (--plumbing-test: gloo on CPU, trivial step)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing-test",
+                          "--steps", "3", "--warmup", "1", "--scenes", "2"], env=env, capture_output=True,
+                         text=True, timeout=240, check=True).stdout
+    lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out  # rank 0 only
+    rec = lines[0]
+    assert rec["n_gpus"] == 2 and rec["ranks_reported"] == 2
+    assert rec["units_per_rank"] == [2 * 65536 * 3] * 2
+    assert abs(rec["value"] - sum(rec["units_per_rank"]) / rec["elapsed_max_s"] / 1e6) < 1e-6 * rec["value"]

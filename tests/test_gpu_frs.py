@@ -182,7 +182,7 @@ def test_frs_speculative_capacity(cuda, guess):
     rs = np.array([0, 12000, 20000], np.int64)
     t = torch.from_numpy(pts).to(cuda)
     r = 0.05
-    for key in ((float(r), 1), (float(r), -1)):
+    for key in ((float(r), 1, len(pts), len(pts)), (float(r), -1, len(pts), len(pts))):
         ops._FRS_DENSITY.pop(key, None)
         if guess is not None:
             ops._FRS_DENSITY[key] = guess
