@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(kManyThreads) knn_many_kernel(
             for (int i = n + threadIdx.x; i < N; i += kManyThreads) keys[i] = ~0ull;
             __syncthreads();
             block_bitonic(keys, N);
-            bound = keys[min<int64_t>(want, n) - 1];  // n >= want here (whole grid: n == want)
+            bound = keys[static_cast<int>(min<int64_t>(want, static_cast<int64_t>(n))) - 1];  // n >= want here (whole grid: n == want)
             if (whole) {
                 done = true;
                 break;
