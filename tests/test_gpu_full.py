@@ -1,0 +1,205 @@
+"""Parity at the FULL sizes the bench times (tests/golden/full.npz, made by
+tests/golden/make_golden_full.py from the reference imported in the build
+container).
+
+C2 — SemanticKITTI-shaped 120,000-point scan (bench.make_scan(0)):
+  * the GPU grid subsampling reproduces the reference sub-cloud bit for bit
+    (sha256 of the oracle's contrib.subsample);
+  * A2: the k = 45,056 patch crops and the 1-NN projection of every raw point
+    against sklearn's float64 KDTree (randlanet.py:141-152,
+    semseg_spatially_regular.py:94-95): sets / indices equal except entries
+    tagged as float64 near-ties (within 1e-6 relative);
+  * the fused GPU RandLANet on one full 45,056-point patch (GPU kNN levels)
+    against the reference model: logits within 2e-4 abs, column sums within
+    1e-5 per row.
+C3 — KPFCNN (kpconv_s3dis.yml, first_features_dim 128) on bench.make_c3(0),
+  40,000 points: every collate array sha-identical to the reference collate;
+  eval and training mode: logits within 1e-4 of their range, loss within 1e-5
+  relative, every parameter-gradient norm within 1e-4 relative and three full
+  gradients within 1e-4 of their range.
+C4 — SparseConvUnet m=32 on the 88,006-voxel room (bench.make_room(0)):
+  logits within 1e-4 of their range, column sums within 1e-5 per row."""
+import hashlib
+import os
+import sys
+import types
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+sys.path.insert(0, os.path.dirname(HERE))
+import randla_weights  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+F = np.load(os.path.join(HERE, "golden", "full.npz"))
+C2_K = 45056
+C2_CENTERS = (1000, 40000, 77777)
+C2_PERM_SEED = 5
+C3_CFG = dict(lbl_values=list(range(13)), num_classes=13, ignored_label_inds=[], first_subsampling_dl=0.04,
+              in_features_dim=5, first_features_dim=128, batch_norm_momentum=0.98, conv_radius=2.5,
+              KP_extent=1.2, num_kernel_points=15)
+
+
+def sha(a):
+    a = np.ascontiguousarray(a)
+    return hashlib.sha256(a.dtype.str.encode() + str(a.shape).encode() + a.tobytes()).hexdigest()
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-30))
+
+
+@pytest.fixture(scope="module")
+def c2(cuda):
+    import bench
+    from o3dml_amd import ops
+    scan, _ = bench.make_scan(0)
+    scan_t = torch.from_numpy(scan).to(cuda)
+    sub_t = ops.grid_subsample(scan_t, [len(scan)], 0.06).points
+    return scan, scan_t, sub_t
+
+
+def test_c2_grid_subsample_is_reference_subcloud(c2):
+    sub = c2[2].cpu().numpy()
+    assert len(sub) == int(F["c2_sub_n"]) and sha(sub) == str(F["c2_sub_sha"])
+
+
+def test_c2_patch_crops_vs_sklearn(c2):
+    from o3dml_amd import ops
+    sub_t = c2[2]
+    for j, c in enumerate(C2_CENTERS):
+        got = ops.knn_search(sub_t, sub_t[c:c + 1].contiguous(), C2_K).neighbors_index.cpu().numpy()
+        ref = F[f"c2_crop{j}"]
+        amb = set(F[f"c2_crop{j}_amb"].tolist())
+        assert len(got) == len(ref) == C2_K and len(np.unique(got)) == C2_K
+        assert set(got.tolist()) - amb == set(ref.tolist()) - amb, j
+
+
+def test_c2_projection_vs_sklearn(c2):
+    from o3dml_amd import ops
+    scan, scan_t, sub_t = c2
+    proj = ops.knn_search(sub_t, scan_t, 1).neighbors_index.cpu().numpy()
+    keep = np.ones(len(scan), bool)
+    keep[F["c2_proj_amb"]] = False
+    assert keep.sum() > 0.99 * len(scan)
+    assert np.array_equal(proj[keep], F["c2_proj"][keep])
+
+
+def test_c2_randla_full_patch_vs_reference(c2):
+    from o3dml_amd import ops
+    from o3dml_amd.randlanet import RandLANet
+    sub_t = c2[2]
+    c = C2_CENTERS[0]
+    crop = ops.knn_search(sub_t, sub_t[c:c + 1].contiguous(), C2_K).neighbors_index.cpu().numpy()
+    sub = sub_t.cpu().numpy()
+    perm = np.random.default_rng(C2_PERM_SEED).permutation(C2_K)
+    pc = sub[crop.astype(np.int64)][perm].copy()
+    pc[:, :2] -= pc[:, :2].mean(0, dtype=np.float64).astype(np.float32)
+    dev = sub_t.device
+    inputs = {"features": torch.from_numpy(pc)[None].to(dev)}
+    cs, nb, sb, up = [], [], [], []
+    cur = torch.from_numpy(pc).to(dev)
+    for _ in range(4):
+        n = ops.knn_search(cur, cur, 16).neighbors_index.view(-1, 16).long()
+        sub_l = cur[: cur.shape[0] // 4].contiguous()
+        u = ops.knn_search(sub_l, cur, 1).neighbors_index.view(-1, 1).long()
+        cs.append(cur[None])
+        nb.append(n[None])
+        sb.append(n[: cur.shape[0] // 4][None])
+        up.append(u[None])
+        cur = sub_l
+    inputs.update(coords=cs, neighbor_indices=nb, sub_idx=sb, interp_idx=up)
+    m = RandLANet(num_points=C2_K)
+    sd = m.state_dict()
+    m.load_state_dict(randla_weights.state_dict_for([(k, tuple(v.shape)) for k, v in sd.items()]))
+    m = m.to(dev).eval()
+    with torch.no_grad():
+        out = m(inputs)[0].cpu().numpy()
+    np.testing.assert_allclose(out[::11], F["c2_logit_rows"], rtol=0, atol=2e-4)
+    np.testing.assert_allclose(out.astype(np.float64).sum(0), F["c2_logit_colsum"], rtol=0, atol=1e-5 * C2_K)
+
+
+@pytest.fixture(scope="module")
+def c3(cuda):
+    import bench
+    from o3dml_amd.kpfcnn import Config, DEFAULTS, segmentation_inputs
+    pts, feats, labels, lengths = bench.make_c3(0)
+    cfg = Config(DEFAULTS)
+    cfg.update(C3_CFG)
+    b = segmentation_inputs(cfg, torch.from_numpy(pts).to(cuda), torch.from_numpy(feats).to(cuda), labels, lengths,
+                            rotations=list(F["c3_rotations"]))
+    return b
+
+
+def test_c3_collate_matches_reference(c3):
+    b = c3
+    for l in range(5):
+        arrays = {"layer_points": b.points[l].cpu().numpy().astype(np.float32),
+                  "neighbors": b.neighbors[l].cpu().numpy().astype(np.int32),
+                  "pools": b.pools[l].cpu().numpy().astype(np.int32),
+                  "upsamples": b.upsamples[l].cpu().numpy().astype(np.int32),
+                  "layer_lengths": np.asarray(b.lengths[l]).astype(np.int32)}
+        for name, a in arrays.items():
+            shape = tuple(F[f"c3_shape_{name}_{l}"].tolist())
+            if shape[0] == 0:
+                assert a.shape[0] == 0, (name, l)
+                continue
+            assert a.shape == shape, (name, l, a.shape, shape)
+            assert sha(a) == str(F[f"c3_sha_{name}_{l}"]), (name, l)
+
+
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_c3_step_matches_reference(c3, mode):
+    from o3dml_amd.kpfcnn import KPFCNN
+    dev = c3.features.device
+    m = KPFCNN(**C3_CFG)
+    sd = m.state_dict()
+    new = randla_weights.state_dict_for([(k, tuple(v.shape)) for k, v in sd.items()], sd)
+    for k in sd:
+        if k.endswith("kernel_points"):
+            new[k] = torch.from_numpy(F["c3_kp:" + k])
+    m.load_state_dict(new)
+    m = m.to(dev).train(mode == "train")
+    logits = m(c3)
+    loss = torch.nn.functional.cross_entropy(logits, c3.labels)
+    loss.backward()
+    lg = logits.detach().cpu().numpy()
+    ref_rows = F[f"c3_{mode}_logit_rows"]
+    assert _rel(lg[::10], ref_rows) < 1e-4
+    np.testing.assert_allclose(lg.astype(np.float64).sum(0), F[f"c3_{mode}_logit_colsum"], rtol=0,
+                               atol=1e-5 * len(lg) * np.abs(ref_rows).max())
+    ref_loss = float(F[f"c3_{mode}_loss"])
+    assert abs(loss.item() - ref_loss) < 1e-5 * abs(ref_loss)
+    params = dict(m.named_parameters())
+    names = [str(s) for s in F[f"c3_{mode}_grad_names"]]
+    for k, ref_norm in zip(names, F[f"c3_{mode}_grad_norms"]):
+        g = params[k].grad.detach().double().norm().item()
+        assert abs(g - ref_norm) <= 1e-4 * ref_norm + 1e-12, (k, g, ref_norm)
+    for key in F.files:
+        if key.startswith(f"c3_{mode}_grad:"):
+            k = key.split(":", 1)[1]
+            assert _rel(params[k].grad.cpu().numpy(), F[key]) < 1e-4, k
+
+
+def test_c4_scn_full_room_vs_reference(cuda):
+    import bench
+    from o3dml_amd.sparseconvnet import SparseConvUnet
+    pos, _ = bench.make_room(0)
+    assert len(pos) == int(F["c4_n"])
+    feat = np.random.default_rng(3).random((len(pos), 3), dtype=np.float32)
+    m = SparseConvUnet(multiplier=32, residual_blocks=True, conv_block_reps=1, num_classes=20)
+    sd = m.state_dict()
+    m.load_state_dict(randla_weights.state_dict_for([(k, tuple(v.shape)) for k, v in sd.items()], sd))
+    m = m.to(cuda).eval()
+    inp = types.SimpleNamespace(point=[torch.from_numpy(pos).to(cuda)], feat=[torch.from_numpy(feat).to(cuda)],
+                                batch_lengths=[len(pos)])
+    with torch.no_grad():
+        out = m(inp).cpu().numpy()
+    ref = F["c4_logit_rows"]
+    assert _rel(out[::11], ref) < 1e-4
+    np.testing.assert_allclose(out.astype(np.float64).sum(0), F["c4_logit_colsum"], rtol=0,
+                               atol=1e-5 * len(out) * np.abs(ref).max())
