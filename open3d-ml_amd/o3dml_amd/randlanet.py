@@ -343,18 +343,43 @@ class RandLANet(nn.Module):
 # ---------------------------------------------------------------------------
 # inference pipeline (GPU)
 # ---------------------------------------------------------------------------
+def _last_occurrence(idxs, n):
+    """Mask of the entries of idxs that are the LAST occurrence of their value:
+    numpy's ``a[idxs] += v`` / ``a[idxs] = f(a[idxs])`` (the reference's
+    semseg_spatially_regular.py:104 and randlanet.py:462) keep the value of the
+    last duplicate — selected here deterministically instead of a racing
+    scatter."""
+    pos = torch.arange(idxs.shape[0], device=idxs.device)
+    last = torch.full((n,), -1, dtype=torch.int64, device=idxs.device)  # idxs < n
+    last.scatter_reduce_(0, idxs, pos, reduce="amax")
+    return last[idxs] == pos
+
+
 class SemSegInference:
     """GPU ``run_inference`` for RandLA-Net with the spatially-regular patch
     sampler.  ``run(points)`` -> (predicted labels [N] int64, probabilities
-    [N, C] float32), both on the GPU; ``stats`` records patches per frame."""
+    [N, C]), both on the GPU; ``stats`` records patches per frame.
 
-    def __init__(self, model, device=None, seed=0, test_smooth=0.95, use_graph=None):
+    Arithmetic as in the reference (semseg_spatially_regular.py:79-109,
+    randlanet.py:441-465, semantic_segmentation.py:264-299): possibilities in
+    float64 with float32 ``delta = (1 - d / d_max)^2``, centre = first argmin;
+    the per-point probabilities stored in float16 as the reference's
+    ``test_probs`` (update ``f16(f16(0.95) * p16 + f32(0.05) * probs)``;
+    ``probs_dtype=torch.float32`` keeps them in f32); duplicate patch indices
+    (clouds smaller than a patch) take the last duplicate's value, as numpy's
+    fancy-index assignment does.  ``run(points, patch_hook=f,
+    init_possibility=p0)`` replays a recorded patch order: f(patch_number,
+    centre_id) returns the patch's (already shuffled) indices in place of the
+    GPU kNN crop + shuffle (tests/test_gpu_pipeline.py)."""
+
+    def __init__(self, model, device=None, seed=0, test_smooth=0.95, use_graph=None, probs_dtype=torch.float16):
         self.model = model
         if use_graph is None:
             use_graph = os.environ.get("O3DML_RANDLA_GRAPH", "1") != "0"
         self.use_graph = use_graph
         self.device = device or next(model.parameters()).device
         self.test_smooth = test_smooth
+        self.probs_dtype = probs_dtype
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
         self.stats = {}
@@ -366,22 +391,34 @@ class SemSegInference:
         proj = ops.knn_search(sub, points, 1).neighbors_index.long()
         return sub, proj
 
-    def transform(self, sub, possibility):
+    def transform(self, sub, possibility, idxs=None):
         """Patch crop + possibility update + per-layer kNN (randlanet.py:156-239,
-        semseg_spatially_regular.py:82-109)."""
+        semseg_spatially_regular.py:82-109).  idxs: a replayed patch (shuffled
+        indices) instead of the crop."""
         cfg = self.model.cfg
         n_pts = cfg["num_points"]
-        center = sub.index_select(0, torch.argmin(possibility).view(1))  # stays on the device: no host read
-        if sub.shape[0] < n_pts:
+        center_id = torch.argmin(possibility).view(1)  # first minimum, as np.argmin; no host read
+        center = sub.index_select(0, center_id)
+        if idxs is not None:
+            idxs = idxs.to(self.device).long()
+        elif sub.shape[0] < n_pts:
             extra = torch.randint(0, sub.shape[0], (n_pts - sub.shape[0],), generator=self.gen, device=self.device)
             idxs = torch.cat([torch.arange(sub.shape[0], device=self.device), extra])
+            idxs = idxs[torch.randperm(idxs.shape[0], generator=self.gen, device=self.device)]
         else:
             idxs = ops.knn_search(sub, center, n_pts).neighbors_index.long()
-        idxs = idxs[torch.randperm(idxs.shape[0], generator=self.gen, device=self.device)]
+            idxs = idxs[torch.randperm(idxs.shape[0], generator=self.gen, device=self.device)]
         pc = sub[idxs]
-        d = ((pc - center) ** 2).sum(1)
+        # the reference's float32 arithmetic term by term: d = (dx^2 + dy^2) + dz^2
+        dd = pc - center
+        d = dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1] + dd[:, 2] * dd[:, 2]
         delta = (1 - d / d.max()) ** 2
-        possibility.index_add_(0, idxs, delta)
+        if sub.shape[0] < n_pts:  # duplicates: the last one's value, as numpy's a[idxs] += delta
+            keep = _last_occurrence(idxs, sub.shape[0])
+            ui, ud = idxs[keep], delta[keep]
+        else:
+            ui, ud = idxs, delta
+        possibility[ui] = possibility[ui] + ud.to(possibility.dtype)
         pc = pc.clone()
         pc[:, :2] -= pc[:, :2].mean(0)  # augment recenter dim [0, 1]
         # all levels are prefixes of the shuffled patch: one batched self-kNN
@@ -399,6 +436,20 @@ class SemSegInference:
         srs = np.concatenate([[0], np.cumsum(sizes[1:])]).astype(np.int64)
         up_all = ops.knn_search(sup, cat, 1, srs, rs).neighbors_index.long()
         return pc, idxs, nb_all, up_all, (sizes, rs, srs)
+
+    def update_probs(self, test_probs, idxs, probs):
+        """test_probs[idxs] = smooth * test_probs[idxs] + (1 - smooth) * probs
+        (randlanet.py:441-465) with the reference's dtypes: a float16 store
+        multiplies in float16 (numpy casts the Python scalar to the array's
+        dtype), the new term is float32, the sum float32 rounded to the store;
+        duplicate indices keep the last one (numpy semantics)."""
+        if test_probs.shape[0] < idxs.shape[0]:  # a patch larger than the cloud repeats points
+            keep = _last_occurrence(idxs, test_probs.shape[0])
+            idxs, probs = idxs[keep], probs[keep]
+        old = test_probs[idxs]
+        a = old * torch.tensor(self.test_smooth, dtype=test_probs.dtype, device=old.device)
+        b = probs.float() * torch.tensor(1 - self.test_smooth, dtype=torch.float32, device=old.device)
+        test_probs[idxs] = (a.float() + b).to(test_probs.dtype)
 
     def _levels(self, pc, nb_all, up_all, plan):
         """Per-layer (coords, nbrs, subs, ups) views of the batched kNN results."""
@@ -444,23 +495,31 @@ class SemSegInference:
         return out
 
     @torch.no_grad()
-    def run(self, points):
+    def run(self, points, patch_hook=None, init_possibility=None):
         self.model.eval()
         points = points.to(self.device).float().contiguous()
         C = self.model.cfg["num_classes"]
         sub, proj = self.preprocess(points)
         n_sub = sub.shape[0]
-        possibility = torch.rand(n_sub, generator=self.gen, device=self.device) * 1e-3
-        test_probs = torch.zeros((n_sub, C), dtype=torch.float32, device=self.device)
-        patches = 0
+        if init_possibility is not None:
+            possibility = torch.as_tensor(init_possibility, dtype=torch.float64).to(self.device).clone()
+        else:
+            possibility = torch.rand(n_sub, generator=self.gen, device=self.device, dtype=torch.float64) * 1e-3
+        test_probs = torch.zeros((n_sub, C), dtype=self.probs_dtype, device=self.device)
+        patches, centers = 0, []
         while float(possibility.min()) <= 0.5:
-            pc, idxs, nb_all, up_all, plan = self.transform(sub, possibility)
+            idxs = None
+            if patch_hook is not None:
+                cid = int(torch.argmin(possibility))
+                centers.append(cid)
+                idxs = patch_hook(patches, cid)
+            pc, idxs, nb_all, up_all, plan = self.transform(sub, possibility, idxs)
             if self.use_graph and n_sub >= self.model.cfg["num_points"]:
                 probs = self._graph_probs(pc, nb_all, up_all, plan)
             else:
                 probs = self._patch_probs(pc, nb_all, up_all, plan)
-            test_probs[idxs] = self.test_smooth * test_probs[idxs] + (1 - self.test_smooth) * probs
+            self.update_probs(test_probs, idxs, probs)
             patches += 1
-        self.stats = {"patches": patches, "sub_points": n_sub}
+        self.stats = {"patches": patches, "sub_points": n_sub, "centers": centers}
         probs = test_probs[proj]
         return probs.argmax(1), probs

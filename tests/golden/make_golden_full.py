@@ -23,7 +23,9 @@ C3 (bench.make_c3(0), 40,000 points, KPFCNN kpconv_s3dis.yml at
   seeded np.random rotations recorded) as per-array sha256 + shapes, the
   kernel-point dispositions, and in eval and training mode: every 10th logit
   row, the logit column sums, the cross-entropy loss, the float64 L2 norm of
-  every parameter gradient and the full gradient of the smallest tensors.
+  every parameter gradient and the full gradient of the smallest tensors —
+  of the reference in float32 AND of the same reference model run in float64
+  (the truth), with the reference's own float32 error against it.
 C4 (bench.make_room(0), 88,006 voxels, SparseConvUnet m=32 residual, 20
   classes, eval): every 11th logit row and the column sums."""
 import hashlib
@@ -191,28 +193,55 @@ def make_c3(out):
             new[k] = sd[k].clone()
             out["c3_kp:" + k] = sd[k].numpy().astype(np.float32)
     model.load_state_dict(new)
+    import copy
+    model64 = copy.deepcopy(model).double()
+    batch64 = types.SimpleNamespace(**{**batch.__dict__, "points": [p.double() for p in batch.points],
+                                       "features": batch.features.double()})
     for mode in ("eval", "train"):
-        model.zero_grad()
-        model.train(mode == "train")
-        t0 = time.time()
-        logits = model(batch)
-        loss = torch.nn.functional.cross_entropy(logits, batch.labels)
-        loss.backward()
-        print("c3", mode, round(time.time() - t0, 1), "s, loss", float(loss))
-        lg = logits.detach().numpy().astype(np.float32)
-        out[f"c3_{mode}_logit_rows"] = lg[::10]
-        out[f"c3_{mode}_logit_colsum"] = lg.astype(np.float64).sum(0)
-        out[f"c3_{mode}_loss"] = np.float64(loss.item())
-        names_g, norms = [], []
-        for k, p in model.named_parameters():
-            if p.grad is None:
-                continue
-            names_g.append(k)
-            norms.append(float(np.linalg.norm(p.grad.numpy().astype(np.float64))))
-            if k in C3_FULL_GRADS:
-                out[f"c3_{mode}_grad:{k}"] = p.grad.numpy().astype(np.float32)
-        out[f"c3_{mode}_grad_names"] = np.array(names_g)
-        out[f"c3_{mode}_grad_norms"] = np.array(norms, np.float64)
+        res = {}
+        for tag, mdl, b in (("", model, batch), ("64", model64, batch64)):
+            mdl.zero_grad()
+            mdl.train(mode == "train")
+            t0 = time.time()
+            logits = mdl(b)
+            loss = torch.nn.functional.cross_entropy(logits, b.labels)
+            loss.backward()
+            print("c3", mode, tag or "32", round(time.time() - t0, 1), "s, loss", float(loss))
+            lg = logits.detach().double().numpy()
+            res[tag] = {"rows": lg[::10], "colsum": lg.sum(0), "loss": float(loss.item()),
+                        "names": [], "norms": [], "full": {}}
+            for k, p in mdl.named_parameters():
+                if p.grad is None:
+                    continue
+                res[tag]["names"].append(k)
+                res[tag]["norms"].append(float(np.linalg.norm(p.grad.double().numpy())))
+                if k in C3_FULL_GRADS:
+                    res[tag]["full"][k] = p.grad.double().numpy()
+        r32, r64 = res[""], res["64"]
+        assert r32["names"] == r64["names"]
+        out[f"c3_{mode}_logit_rows"] = r32["rows"].astype(np.float32)
+        out[f"c3_{mode}_logit_colsum"] = r32["colsum"]
+        out[f"c3_{mode}_loss"] = np.float64(r32["loss"])
+        out[f"c3_{mode}_grad_names"] = np.array(r32["names"])
+        out[f"c3_{mode}_grad_norms"] = np.array(r32["norms"], np.float64)
+        for k, g in r32["full"].items():
+            out[f"c3_{mode}_grad:{k}"] = g.astype(np.float32)
+        # the float64 run of the same reference model: the truth the fp32
+        # results are held to, and the reference's own fp32 error against it
+        out[f"c3_{mode}_f64_logit_rows"] = r64["rows"]
+        out[f"c3_{mode}_f64_loss"] = np.float64(r64["loss"])
+        out[f"c3_{mode}_f64_grad_norms"] = np.array(r64["norms"], np.float64)
+        for k, g in r64["full"].items():
+            out[f"c3_{mode}_f64_grad:{k}"] = g
+        rel = lambda a, b: float(np.abs(a - b).max() / (np.abs(b).max() + 1e-300))  # noqa: E731
+        out[f"c3_{mode}_ref32_err_rows"] = np.float64(rel(r32["rows"], r64["rows"]))
+        out[f"c3_{mode}_ref32_err_norms"] = np.abs(np.array(r32["norms"]) - np.array(r64["norms"])) / \
+            np.maximum(np.array(r64["norms"]), 1e-300)
+        for k in r32["full"]:
+            out[f"c3_{mode}_ref32_err_grad:{k}"] = np.float64(rel(r32["full"][k], r64["full"][k]))
+        print("c3", mode, "ref fp32 vs fp64: rows", out[f"c3_{mode}_ref32_err_rows"], "norms max",
+              float(out[f"c3_{mode}_ref32_err_norms"].max()),
+              {k: float(out[f"c3_{mode}_ref32_err_grad:{k}"]) for k in r32["full"]})
 
 
 def make_c4(out):

@@ -14,9 +14,12 @@ C2 — SemanticKITTI-shaped 120,000-point scan (bench.make_scan(0)):
     1e-5 per row.
 C3 — KPFCNN (kpconv_s3dis.yml, first_features_dim 128) on bench.make_c3(0),
   40,000 points: every collate array sha-identical to the reference collate;
-  eval and training mode: logits within 1e-4 of their range, loss within 1e-5
-  relative, every parameter-gradient norm within 1e-4 relative and three full
-  gradients within 1e-4 of their range.
+  eval and training mode against the reference model run in float64: logits
+  within 1e-4 of their range (also vs the fp32 reference), loss within 1e-5
+  relative, every parameter-gradient norm and three full gradients within
+  max(1e-4, 2x the reference's own fp32-vs-fp64 error) — at this depth the
+  reference's fp32 first-layer gradient is itself 4e-4 (eval) / 2.7e-3
+  (training) off the fp64 one.
 C4 — SparseConvUnet m=32 on the 88,006-voxel room (bench.make_room(0)):
   logits within 1e-4 of their range, column sums within 1e-5 per row."""
 import hashlib
@@ -168,21 +171,27 @@ def test_c3_step_matches_reference(c3, mode):
     loss = torch.nn.functional.cross_entropy(logits, c3.labels)
     loss.backward()
     lg = logits.detach().cpu().numpy()
+    # against the float64 run of the reference model (the truth): within 1e-4,
+    # or within twice the reference's own float32 error where that is larger
+    # (deep gradients: the reference's fp32 drifts 4e-4 .. 3e-3 from fp64)
+    bound = lambda ref32_err: max(1e-4, 2.0 * float(ref32_err))  # noqa: E731
+    assert _rel(lg[::10], F[f"c3_{mode}_f64_logit_rows"]) < bound(F[f"c3_{mode}_ref32_err_rows"])
+    assert _rel(lg[::10], F[f"c3_{mode}_logit_rows"]) < 1e-4  # and the fp32 reference itself
     ref_rows = F[f"c3_{mode}_logit_rows"]
-    assert _rel(lg[::10], ref_rows) < 1e-4
     np.testing.assert_allclose(lg.astype(np.float64).sum(0), F[f"c3_{mode}_logit_colsum"], rtol=0,
                                atol=1e-5 * len(lg) * np.abs(ref_rows).max())
-    ref_loss = float(F[f"c3_{mode}_loss"])
+    ref_loss = float(F[f"c3_{mode}_f64_loss"])
     assert abs(loss.item() - ref_loss) < 1e-5 * abs(ref_loss)
     params = dict(m.named_parameters())
     names = [str(s) for s in F[f"c3_{mode}_grad_names"]]
-    for k, ref_norm in zip(names, F[f"c3_{mode}_grad_norms"]):
+    for k, ref_norm, err32 in zip(names, F[f"c3_{mode}_f64_grad_norms"], F[f"c3_{mode}_ref32_err_norms"]):
         g = params[k].grad.detach().double().norm().item()
-        assert abs(g - ref_norm) <= 1e-4 * ref_norm + 1e-12, (k, g, ref_norm)
+        assert abs(g - ref_norm) <= bound(err32) * ref_norm + 1e-12, (k, g, ref_norm, err32)
     for key in F.files:
-        if key.startswith(f"c3_{mode}_grad:"):
+        if key.startswith(f"c3_{mode}_f64_grad:"):
             k = key.split(":", 1)[1]
-            assert _rel(params[k].grad.cpu().numpy(), F[key]) < 1e-4, k
+            err = _rel(params[k].grad.cpu().numpy(), F[key])
+            assert err < bound(F[f"c3_{mode}_ref32_err_grad:{k}"]), (k, err)
 
 
 def test_c4_scn_full_room_vs_reference(cuda):

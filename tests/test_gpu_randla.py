@@ -88,7 +88,7 @@ def test_inference_graph_replay_matches_eager(cuda):
     rng = np.random.default_rng(2)
     pts = np.stack([rng.uniform(-20, 20, 20000), rng.uniform(-20, 20, 20000), rng.uniform(-2, 2, 20000)], 1)
     pts = torch.from_numpy(pts.astype(np.float32)).to(cuda)
-    lg, pg = SemSegInference(m, seed=0, use_graph=True).run(pts)
-    le, pe = SemSegInference(m, seed=0, use_graph=False).run(pts)
+    lg, pg = SemSegInference(m, seed=0, use_graph=True, probs_dtype=torch.float32).run(pts)
+    le, pe = SemSegInference(m, seed=0, use_graph=False, probs_dtype=torch.float32).run(pts)
     torch.testing.assert_close(pg, pe, rtol=0, atol=1e-6)
     assert torch.equal(lg, le)
