@@ -164,6 +164,43 @@ int o3dml_radius_search_sort_long_rows(int64_t n_points, int64_t n_queries, int6
                                        float* neighbors_distance, void* workspace, size_t workspace_bytes,
                                        void* stream);
 
+/* ---- RandLA-Net inference bookkeeping (randla_sampler.hip): the
+ * spatially-regular sampler's per-patch steps
+ * (ml3d/datasets/samplers/semseg_spatially_regular.py:79-109) and
+ * RandLANet.transform's up-sampling indices (randlanet.py:212-239).
+ * _possibility_min: min + first argmin of f64 possibilities [n], the centre
+ *   point sub[argmin] (f32 [3], device), the min into *host_min (pinned host
+ *   memory, may be NULL).
+ * _patch_update: pc[i] = sub[idxs[i]], d = (dx^2 + dy^2) + dz^2 (f32),
+ *   possibility[idxs[i]] += (1 - d / max d)^2 for i with keep[i] (keep NULL:
+ *   all; duplicates must be masked to one), pc x, y recentred on their mean.
+ * _up_from_knn: up[q] for every point q of the concatenated levels
+ *   (level i = rs[i] .. rs[i+1]) = index in the concatenated levels 1..L
+ *   (srs[i] + position) of q's nearest point among the first nxt[i] points of
+ *   its level, from the (distance, index)-sorted k-lists nb (int32, indices
+ *   into the concatenation) — equal to knn_search(level i+1, level i, 1);
+ *   the points whose list holds none are searched by brute force. ------ */
+int o3dml_randla_possibility_min(const double* possibility, int64_t n, const float* sub, int64_t* argmin,
+                                 float* center, double* host_min, void* stream);
+size_t o3dml_randla_patch_workspace_size(int64_t n);
+int o3dml_randla_patch_update(const float* sub, const int64_t* idxs, int64_t n, const float* center,
+                              const uint8_t* keep, double* possibility, float* pc, void* workspace,
+                              size_t workspace_bytes, void* stream);
+size_t o3dml_randla_up_workspace_size(int64_t total);
+int o3dml_randla_up_from_knn(const int32_t* nb, int k, const float* cat, int nlev, const int64_t* rs,
+                             const int64_t* nxt, const int64_t* srs, int64_t* up, void* workspace,
+                             size_t workspace_bytes, void* stream);
+
+/* ---- fused dense layer (RandLA-Net SharedMLP in eval mode,
+ * ml3d/torch/models/randlanet.py:469-512, BatchNorm folded by the caller):
+ * out[r] = act([a1[r] | a2[a2_index ? a2_index[r] : r]] @ weight^T + bias),
+ * a1 f32 [n, k1], a2 f32 [*, k2] (k2 = 0: none), weight f32 [m, k1 + k2]
+ * (torch Linear layout), bias f32 [m] or NULL, act 1 = LeakyReLU(slope),
+ * 0 = identity.  Covers LocalFeatureAggregation's lrelu(mlp2(x) +
+ * shortcut(feat)) (:689-692) and the decoder's [skip | upsampled] concat. */
+int o3dml_dense_act(const float* a1, int k1, const float* a2, int k2, const int64_t* a2_index, const float* weight,
+                    const float* bias, int64_t n, int m, int act, float slope, float* out, void* stream);
+
 /* ---- voxelize: replaces open3d.ml.torch.ops.voxelize
  * (ml3d/torch/models/point_pillars.py:352-357, sparseconvnet.py:293-298).
  * points f32 [N, ndim] (ndim <= 8); voxel_size / range_min / range_max are

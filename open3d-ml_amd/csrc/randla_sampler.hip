@@ -1,0 +1,260 @@
+// randla_sampler.hip — the per-patch bookkeeping of RandLA-Net inference
+// (SemSegSpatiallyRegularSampler, ml3d/datasets/samplers/
+// semseg_spatially_regular.py:79-109; RandLANet.transform, randlanet.py:
+// 156-239) as three small kernels instead of ~20 torch launches and
+// reductions per patch, plus the up-sampling indices derived from the k = 16
+// lists instead of a second kNN search.
+//
+//  * possibility_min: min and FIRST argmin of the float64 possibilities (as
+//    np.argmin), the centre point, the minimum also into pinned host memory
+//    (the loop test `min > 0.5` is the one host read per patch);
+//  * patch_prep / patch_apply: pc = sub[idxs], d = (dx^2 + dy^2) + dz^2 in
+//    float32 (the reference's np.sum of np.square over the float32 differences,
+//    no contraction), d_max, delta = (1 - d / d_max)^2 (float32), the float64
+//    possibility update, and the augmenter's recentring of x, y (mean over the
+//    patch: per-block partial sums in a fixed order, so every run gives the
+//    same bits);
+//  * up_from_knn: level i+1 is the first N_{i+1} points of level i
+//    (randlanet.py:222-224), so the nearest level-(i+1) point of p is the first
+//    entry of p's (distance, index)-sorted k = 16 list that lies in that prefix
+//    — exactly knn_search(level i+1, level i, 1) whenever one does (the order
+//    and the distances are the same); the ~(3/4)^16 = 1 % of points with none
+//    in their list are searched by brute force over the prefix (one wave each).
+#include <cfloat>
+
+#include "common.hpp"
+
+namespace o3dml {
+
+constexpr int kPatchBlocks = 64;
+
+__global__ void __launch_bounds__(1024) possibility_min_kernel(const double* __restrict__ p, int64_t n,
+                                                               const float* __restrict__ sub,
+                                                               int64_t* __restrict__ arg, float* __restrict__ center,
+                                                               double* __restrict__ host_min) {
+    __shared__ double sv[16];
+    __shared__ int64_t si[16];
+    double best = DBL_MAX;
+    int64_t bi = INT64_MAX;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const double v = p[i];
+        if (v < best) {  // i increases per thread: keeps the first minimum
+            best = v;
+            bi = i;
+        }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        const double ov = __shfl_xor(best, o, 64);
+        const int64_t oi = __shfl_xor(bi, o, 64);
+        if (ov < best || (ov == best && oi < bi)) {
+            best = ov;
+            bi = oi;
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        sv[threadIdx.x >> 6] = best;
+        si[threadIdx.x >> 6] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < static_cast<int>(blockDim.x >> 6); ++w)
+            if (sv[w] < best || (sv[w] == best && si[w] < bi)) {
+                best = sv[w];
+                bi = si[w];
+            }
+        *arg = n ? bi : 0;
+        if (n) {
+            center[0] = sub[3 * bi];
+            center[1] = sub[3 * bi + 1];
+            center[2] = sub[3 * bi + 2];
+        }
+        if (host_min) *host_min = n ? best : DBL_MAX;
+    }
+}
+
+// partials[b] = (max d, sum x, sum y) of block b's chunk
+__global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict__ sub,
+                                                         const int64_t* __restrict__ idxs, int64_t n,
+                                                         const float* __restrict__ center, float* __restrict__ pc,
+                                                         float* __restrict__ d, float* __restrict__ partials) {
+    __shared__ float red[3][4];
+    const int64_t per = ceil_div(n, kPatchBlocks);
+    const int64_t s = blockIdx.x * per, e = min(n, s + per);
+    const float cx = center[0], cy = center[1], cz = center[2];
+    float mx = 0.f, sx = 0.f, sy = 0.f;
+    for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+        const int64_t j = idxs[i];
+        const float x = sub[3 * j], y = sub[3 * j + 1], z = sub[3 * j + 2];
+        pc[3 * i] = x;
+        pc[3 * i + 1] = y;
+        pc[3 * i + 2] = z;
+        const float dx = x - cx, dy = y - cy, dz = z - cz;
+        const float di = (dx * dx + dy * dy) + dz * dz;
+        d[i] = di;
+        mx = fmaxf(mx, di);
+        sx += x;
+        sy += y;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        sx += __shfl_xor(sx, o, 64);
+        sy += __shfl_xor(sy, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = mx;
+        red[1][threadIdx.x >> 6] = sx;
+        red[2][threadIdx.x >> 6] = sy;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        partials[3 * blockIdx.x] = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+        partials[3 * blockIdx.x + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+        partials[3 * blockIdx.x + 2] = (red[2][0] + red[2][1]) + (red[2][2] + red[2][3]);
+    }
+}
+
+__global__ void __launch_bounds__(256) patch_apply_kernel(const int64_t* __restrict__ idxs, int64_t n,
+                                                          const uint8_t* __restrict__ keep,
+                                                          const float* __restrict__ partials,
+                                                          const float* __restrict__ d, double* __restrict__ poss,
+                                                          float* __restrict__ pc) {
+    // every block reduces the partials in the same order: same bits everywhere
+    float mx = 0.f, sx = 0.f, sy = 0.f;
+    for (int b = 0; b < kPatchBlocks; ++b) {
+        mx = fmaxf(mx, partials[3 * b]);
+        sx += partials[3 * b + 1];
+        sy += partials[3 * b + 2];
+    }
+    const float inv_n = 1.0f / static_cast<float>(n);
+    const float mxx = sx * inv_n, myy = sy * inv_n;
+    const int64_t per = ceil_div(n, kPatchBlocks);
+    const int64_t s = blockIdx.x * per, e = min(n, s + per);
+    for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+        const float t = 1.0f - d[i] / mx;
+        if (!keep || keep[i]) poss[idxs[i]] += static_cast<double>(t * t);
+        pc[3 * i] -= mxx;
+        pc[3 * i + 1] -= myy;
+    }
+}
+
+struct UpLevels {
+    int64_t rs[5];    // level starts in the concatenated levels 0..L-1
+    int64_t nxt[4];   // size of level i + 1 (the prefix of level i)
+    int64_t srs[4];   // level i + 1 start in the concatenated levels 1..L
+    int nlev;
+};
+
+__device__ __forceinline__ int up_level(int64_t q, const UpLevels& L) {
+    int i = 0;
+    while (i + 1 < L.nlev && q >= L.rs[i + 1]) ++i;
+    return i;
+}
+
+__global__ void up_from_knn_kernel(const int32_t* __restrict__ nb, int k, int64_t total, UpLevels L,
+                                   int64_t* __restrict__ up, uint32_t* __restrict__ fallback,
+                                   uint32_t* __restrict__ n_fallback) {
+    for (int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; q < total;
+         q += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int i = up_level(q, L);
+        const int64_t base = L.rs[i], lim = L.nxt[i];
+        int64_t r = -1;
+        for (int j = 0; j < k; ++j) {
+            const int64_t rel = static_cast<int64_t>(nb[q * k + j]) - base;
+            if (rel < lim) {
+                r = rel;
+                break;
+            }
+        }
+        if (r >= 0) up[q] = r + L.srs[i];
+        else fallback[atomicAdd(n_fallback, 1u)] = static_cast<uint32_t>(q);
+    }
+}
+
+// one wave per listed query: (distance bits, index) minimum over its prefix
+__global__ void __launch_bounds__(256) up_fallback_kernel(const float* __restrict__ cat, UpLevels L,
+                                                          const uint32_t* __restrict__ fallback,
+                                                          const uint32_t* __restrict__ n_fallback,
+                                                          int64_t* __restrict__ up) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = static_cast<int64_t>(gridDim.x) * (blockDim.x >> 6);
+    const int64_t cnt = *n_fallback;
+    for (int64_t w = blockIdx.x * static_cast<int64_t>(blockDim.x >> 6) + (threadIdx.x >> 6); w < cnt; w += waves) {
+        const int64_t q = fallback[w];
+        const int i = up_level(q, L);
+        const float qx = cat[3 * q], qy = cat[3 * q + 1], qz = cat[3 * q + 2];
+        uint64_t best = ~0ull;
+        for (int64_t r = lane; r < L.nxt[i]; r += 64) {
+            const int64_t p = L.rs[i] + r;
+            const float d = dist_l2(cat[3 * p], cat[3 * p + 1], cat[3 * p + 2], qx, qy, qz);
+            const uint64_t key = (static_cast<uint64_t>(__float_as_uint(d)) << 32) | static_cast<uint32_t>(r);
+            best = key < best ? key : best;
+        }
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint64_t other = __shfl_xor(best, o, 64);
+            best = other < best ? other : best;
+        }
+        if (lane == 0 && best != ~0ull) up[q] = static_cast<int64_t>(static_cast<uint32_t>(best)) + L.srs[i];
+    }
+}
+
+}  // namespace o3dml
+
+using namespace o3dml;
+
+O3DML_API int o3dml_randla_possibility_min(const double* possibility, int64_t n, const float* sub, int64_t* argmin,
+                                           float* center, double* host_min, void* stream) {
+    O3DML_GUARD_BEGIN
+    possibility_min_kernel<<<1, 1024, 0, as_stream(stream)>>>(possibility, n, sub, argmin, center, host_min);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+O3DML_API size_t o3dml_randla_patch_workspace_size(int64_t n) {
+    return ws_bytes<float>(3 * kPatchBlocks) + ws_bytes<float>(n);
+}
+
+O3DML_API int o3dml_randla_patch_update(const float* sub, const int64_t* idxs, int64_t n, const float* center,
+                                        const uint8_t* keep, double* possibility, float* pc, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    if (n == 0) return 0;
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    float* partials = ws.take<float>(3 * kPatchBlocks);
+    float* d = ws.take<float>(n);
+    patch_prep_kernel<<<kPatchBlocks, 256, 0, st>>>(sub, idxs, n, center, pc, d, partials);
+    O3DML_LAUNCH_CHECK();
+    patch_apply_kernel<<<kPatchBlocks, 256, 0, st>>>(idxs, n, keep, partials, d, possibility, pc);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+// levels: nlev (<= 4) entries each of rs (nlev + 1), nxt, srs (host arrays)
+O3DML_API int o3dml_randla_up_from_knn(const int32_t* nb, int k, const float* cat, int nlev, const int64_t* rs,
+                                       const int64_t* nxt, const int64_t* srs, int64_t* up, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(nlev >= 1 && nlev <= 4 && k >= 1, "up_from_knn: 1..4 levels, k >= 1");
+    hipStream_t st = as_stream(stream);
+    UpLevels L{};
+    L.nlev = nlev;
+    for (int i = 0; i <= nlev; ++i) L.rs[i] = rs[i];
+    for (int i = 0; i < nlev; ++i) {
+        L.nxt[i] = nxt[i];
+        L.srs[i] = srs[i];
+        O3DML_REQUIRE(nxt[i] <= rs[i + 1] - rs[i], "up_from_knn: level %d prefix longer than the level", i);
+    }
+    const int64_t total = rs[nlev];
+    if (total == 0) return 0;
+    Workspace ws(workspace, workspace_bytes);
+    uint32_t* cntr = ws.take<uint32_t>(1);
+    uint32_t* list = ws.take<uint32_t>(total);
+    O3DML_CHECK_HIP(hipMemsetAsync(cntr, 0, sizeof(uint32_t), st));
+    up_from_knn_kernel<<<stream_grid(total, 256), 256, 0, st>>>(nb, k, total, L, up, list, cntr);
+    O3DML_LAUNCH_CHECK();
+    up_fallback_kernel<<<256, 256, 0, st>>>(cat, L, list, cntr, up);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+O3DML_API size_t o3dml_randla_up_workspace_size(int64_t total) { return ws_bytes<uint32_t>(1) + ws_bytes<uint32_t>(total); }

@@ -72,6 +72,21 @@ def concat_rows(a, ia, b, ib):
     return out
 
 
+def dense_act(a1, w, b, slope=None, a2=None, a2_index=None):
+    """act([a1 | a2[a2_index]] @ w^T + b) in one launch (csrc/dense.hip):
+    a1 [N, k1], a2 [*, k2] (rows selected by a2_index int64 [N], or a2 [N,
+    k2] itself), w [M, k1 + k2], b [M]; act = LeakyReLU(slope), none if slope
+    is None."""
+    n, k1 = a1.shape
+    k2 = 0 if a2 is None else a2.shape[1]
+    m = w.shape[0]
+    out = torch.empty((n, m), dtype=torch.float32, device=a1.device)
+    _lib.call("o3dml_dense_act", ptr(a1.contiguous()), k1, ptr(None if a2 is None else a2.contiguous()), k2,
+              ptr(a2_index), ptr(w), ptr(b), n, m, int(slope is not None), float(slope or 0.0), ptr(out),
+              stream_handle(a1.device))
+    return out
+
+
 def _fused():
     return not torch.is_grad_enabled()
 
@@ -111,8 +126,17 @@ class SharedMLP(nn.Module):
                 self._folded = (w.contiguous(), b.contiguous())
         return self._folded
 
+    def slope(self):
+        """LeakyReLU slope of the activation, None without one (eval fused path)."""
+        a = self.activation_fn
+        return None if a is None else (a.negative_slope if isinstance(a, nn.LeakyReLU) else False)
+
     def forward(self, x):
         """x [..., in] -> [..., out]."""
+        if _fused() and not self.training and self.slope() is not False:
+            w, b = self.folded()  # BN folded; bias + LeakyReLU in the GEMM epilogue (csrc/dense.hip)
+            y = dense_act(x.reshape(-1, x.shape[-1]), w, b, self.slope())
+            return y.reshape(*x.shape[:-1], w.shape[0])
         if _fused() and not self.training:
             w, b = self.folded()
             y = torch.addmm(b, x.reshape(-1, x.shape[-1]), w.t()).reshape(*x.shape[:-1], w.shape[0])
@@ -218,6 +242,17 @@ class LocalFeatureAggregation(nn.Module):
                   ptr(rel_in), ptr(wrt), ptr(br), ptr(wst), ptr(bs), ptr(rel), ptr(out), stream_handle(x.device))
         return out, rel
 
+    def _tail_weights(self):
+        """lrelu(mlp2(x) + shortcut(feat)) as ONE GEMM over [x | feat]:
+        ([W2 | Ws], b2 + bs), BatchNorms folded; cached like _att_weights."""
+        cache = self.__dict__.setdefault("_t_cache", {})
+        if "tail" not in cache:
+            with torch.no_grad():
+                w2, b2 = self.mlp2.folded()
+                ws, bs = self.shortcut.folded()
+                cache["tail"] = (torch.cat([w2, ws], 1).contiguous(), (b2 + bs).contiguous())
+        return cache["tail"]
+
     def forward(self, coords, feat, nbr):
         x = self.mlp1(feat)
         d = self.pool1.score_fn[0].weight.shape[0]
@@ -227,7 +262,8 @@ class LocalFeatureAggregation(nn.Module):
             x = self.pool1.mlp(pooled)
             pooled, _ = self._fused_pool(coords.contiguous(), x, nbr.contiguous(), self.lse2, self.pool2, rel)
             x = self.pool2.mlp(pooled)
-            return self.lrelu(self.mlp2(x) + self.shortcut(feat))
+            w, b = self._tail_weights()
+            return dense_act(x, w, b, self.lrelu.negative_slope, a2=feat)
         x, rel = self.lse1(coords, x, nbr)
         x = self.pool1(x)
         x, _ = self.lse2(coords, x, nbr, relative_features=rel)
@@ -270,8 +306,20 @@ class RandLANet(nn.Module):
                                  SharedMLP(64, 32, activation_fn=nn.LeakyReLU(0.2)), nn.Dropout(0.5),
                                  SharedMLP(32, num_classes, bn=False))
 
+    def _fc0_folded(self):
+        """fc0 with eval-mode bn0 folded in (randlanet.py:262-265)."""
+        if getattr(self, "_fc0_cache", None) is None:
+            with torch.no_grad():
+                bn = self.bn0
+                scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+                w = (self.fc0.weight * scale[:, None]).float().contiguous()
+                b = ((self.fc0.bias - bn.running_mean) * scale + bn.bias).float().contiguous()
+                self._fc0_cache = (w, b)
+        return self._fc0_cache
+
     # folded eval weights are invalidated whenever parameters may change
     def _invalidate(self):
+        self._fc0_cache = None
         for m in self.modules():
             if isinstance(m, SharedMLP):
                 m._folded = None
@@ -292,9 +340,14 @@ class RandLANet(nn.Module):
         (indices into level i); ups[i] [Ni] int64 (indices into level i+1).
         Returns logits [N0, num_classes]."""
         bn = self.bn0
-        x = F.linear(feat, self.fc0.weight, self.fc0.bias)
-        x = F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias, self.training, bn.momentum, bn.eps)
-        x = F.leaky_relu(x, 0.2)
+        if _fused() and not self.training:
+            w, b = self._fc0_folded()
+            x = dense_act(feat, w, b, 0.2)
+        else:
+            x = F.linear(feat, self.fc0.weight, self.fc0.bias)
+            x = F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias, self.training, bn.momentum,
+                             bn.eps)
+            x = F.leaky_relu(x, 0.2)
         enc = []
         for i, layer in enumerate(self.encoder):
             y = layer(coords[i], x, nbrs[i])
@@ -308,7 +361,10 @@ class RandLANet(nn.Module):
             x = ys
         x = self.mlp(x)
         for i, layer in enumerate(self.decoder):
-            if _fused():
+            if _fused() and not self.training:  # [skip | upsampled] gathered inside the GEMM
+                w, b = layer.folded()
+                x = dense_act(enc[-i - 2], w, b, layer.slope(), a2=x, a2_index=ups[-i - 1])
+            elif _fused():
                 x = layer(concat_rows(enc[-i - 2].contiguous(), None, x.contiguous(), ups[-i - 1]))
             else:
                 x = layer(torch.cat([enc[-i - 2], x[ups[-i - 1]]], -1))
@@ -343,6 +399,22 @@ class RandLANet(nn.Module):
 # ---------------------------------------------------------------------------
 # inference pipeline (GPU)
 # ---------------------------------------------------------------------------
+def up_from_knn(nb_all, cat, rs, nxt, srs, scratch=None):
+    """Up-sampling indices of the RandLA levels from the batched k-lists
+    (csrc/randla_sampler.hip): for every point of the concatenated levels
+    (level i = cat[rs[i]:rs[i+1]]), the index in the concatenated levels 1..L
+    (srs[i] + position) of its nearest point among the first nxt[i] points of
+    its level — knn_search(level i+1, level i, 1) without a second search."""
+    total = int(rs[-1])
+    up = torch.empty(total, dtype=torch.int64, device=cat.device)
+    nbytes = _lib.load().o3dml_randla_up_workspace_size(total)
+    ws = scratch("up", nbytes) if scratch else torch.empty(nbytes, dtype=torch.uint8, device=cat.device)
+    rs, nxt, srs = (np.ascontiguousarray(a, np.int64) for a in (rs, nxt, srs))
+    _lib.call("o3dml_randla_up_from_knn", ptr(nb_all), nb_all.shape[1], ptr(cat), len(nxt), rs.ctypes.data,
+              nxt.ctypes.data, srs.ctypes.data, ptr(up), ptr(ws), ws.numel(), stream_handle(cat.device))
+    return up
+
+
 def _last_occurrence(idxs, n):
     """Mask of the entries of idxs that are the LAST occurrence of their value:
     numpy's ``a[idxs] += v`` / ``a[idxs] = f(a[idxs])`` (the reference's
@@ -391,51 +463,56 @@ class SemSegInference:
         proj = ops.knn_search(sub, points, 1).neighbors_index.long()
         return sub, proj
 
-    def transform(self, sub, possibility, idxs=None):
+    def transform(self, sub, possibility, center, idxs=None):
         """Patch crop + possibility update + per-layer kNN (randlanet.py:156-239,
-        semseg_spatially_regular.py:82-109).  idxs: a replayed patch (shuffled
+        semseg_spatially_regular.py:82-109).  center: the device centre point
+        [3] (o3dml_randla_possibility_min); idxs: a replayed patch (shuffled
         indices) instead of the crop."""
         cfg = self.model.cfg
         n_pts = cfg["num_points"]
-        center_id = torch.argmin(possibility).view(1)  # first minimum, as np.argmin; no host read
-        center = sub.index_select(0, center_id)
+        dev = self.device
         if idxs is not None:
-            idxs = idxs.to(self.device).long()
+            idxs = idxs.to(dev).long()
         elif sub.shape[0] < n_pts:
-            extra = torch.randint(0, sub.shape[0], (n_pts - sub.shape[0],), generator=self.gen, device=self.device)
-            idxs = torch.cat([torch.arange(sub.shape[0], device=self.device), extra])
-            idxs = idxs[torch.randperm(idxs.shape[0], generator=self.gen, device=self.device)]
+            extra = torch.randint(0, sub.shape[0], (n_pts - sub.shape[0],), generator=self.gen, device=dev)
+            idxs = torch.cat([torch.arange(sub.shape[0], device=dev), extra])
+            idxs = idxs[torch.randperm(idxs.shape[0], generator=self.gen, device=dev)]
         else:
-            idxs = ops.knn_search(sub, center, n_pts).neighbors_index.long()
-            idxs = idxs[torch.randperm(idxs.shape[0], generator=self.gen, device=self.device)]
-        pc = sub[idxs]
-        # the reference's float32 arithmetic term by term: d = (dx^2 + dy^2) + dz^2
-        dd = pc - center
-        d = dd[:, 0] * dd[:, 0] + dd[:, 1] * dd[:, 1] + dd[:, 2] * dd[:, 2]
-        delta = (1 - d / d.max()) ** 2
-        if sub.shape[0] < n_pts:  # duplicates: the last one's value, as numpy's a[idxs] += delta
-            keep = _last_occurrence(idxs, sub.shape[0])
-            ui, ud = idxs[keep], delta[keep]
-        else:
-            ui, ud = idxs, delta
-        possibility[ui] = possibility[ui] + ud.to(possibility.dtype)
-        pc = pc.clone()
-        pc[:, :2] -= pc[:, :2].mean(0)  # augment recenter dim [0, 1]
+            idxs = ops.knn_search(sub, center.view(1, 3), n_pts).neighbors_index.long()
+            idxs = idxs[torch.randperm(idxs.shape[0], generator=self.gen, device=dev)]
+        idxs = idxs.contiguous()
+        # duplicates (a cloud smaller than a patch): the last one's value, as
+        # numpy's possibilities[idxs] += delta
+        keep = _last_occurrence(idxs, sub.shape[0]).to(torch.uint8) if sub.shape[0] < idxs.shape[0] else None
+        # pc = sub[idxs], delta = (1 - d / d_max)^2 into the float64
+        # possibilities, x / y recentred (csrc/randla_sampler.hip)
+        pc = torch.empty((idxs.shape[0], 3), dtype=torch.float32, device=dev)
+        ws = self._ws("patch", _lib.load().o3dml_randla_patch_workspace_size(idxs.shape[0]))
+        _lib.call("o3dml_randla_patch_update", ptr(sub), ptr(idxs), idxs.shape[0], ptr(center), ptr(keep),
+                  ptr(possibility), ptr(pc), ptr(ws), ws.numel(), stream_handle(dev))
         # all levels are prefixes of the shuffled patch: one batched self-kNN
-        # (k=16) and one batched up-sampling kNN (k=1) cover the 4 layers
+        # (k=16) covers the 4 layers; the up-sampling indices come from its
+        # sorted lists (o3dml_randla_up_from_knn == knn(level i+1, level i, 1))
         L = cfg["num_layers"]
         sizes = [pc.shape[0]]
         for i in range(L):
             sizes.append(sizes[-1] // cfg["sub_sampling_ratio"][i])
-        levels = [pc[:sizes[i]] for i in range(L + 1)]
+        levels = [pc[:sizes[i]] for i in range(L)]
         k = cfg["num_neighbors"]
-        cat = torch.cat(levels[:L]).contiguous()
+        cat = torch.cat(levels).contiguous()
         rs = np.concatenate([[0], np.cumsum(sizes[:L])]).astype(np.int64)
         nb_all = ops.knn_search(cat, cat, k, rs, rs).neighbors_index.view(-1, k)
-        sup = torch.cat(levels[1:]).contiguous()
         srs = np.concatenate([[0], np.cumsum(sizes[1:])]).astype(np.int64)
-        up_all = ops.knn_search(sup, cat, 1, srs, rs).neighbors_index.long()
+        up_all = up_from_knn(nb_all, cat, rs, np.asarray(sizes[1:], np.int64), srs, self._ws)
         return pc, idxs, nb_all, up_all, (sizes, rs, srs)
+
+    def _ws(self, name, nbytes):
+        """Per-pipeline device scratch (grown on demand, reused across patches)."""
+        buf = self.__dict__.setdefault("_scratch", {}).get(name)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.device)
+            self._scratch[name] = buf
+        return buf
 
     def update_probs(self, test_probs, idxs, probs):
         """test_probs[idxs] = smooth * test_probs[idxs] + (1 - smooth) * probs
@@ -507,13 +584,26 @@ class SemSegInference:
             possibility = torch.rand(n_sub, generator=self.gen, device=self.device, dtype=torch.float64) * 1e-3
         test_probs = torch.zeros((n_sub, C), dtype=self.probs_dtype, device=self.device)
         patches, centers = 0, []
-        while float(possibility.min()) <= 0.5:
+        arg = torch.empty(1, dtype=torch.int64, device=self.device)
+        center = torch.empty(3, dtype=torch.float32, device=self.device)
+        host_min = torch.empty(1, dtype=torch.float64, pin_memory=True)
+        st = stream_handle(self.device)
+        ready = torch.cuda.Event()
+        while True:
+            # min + first argmin of the possibilities, the centre point; the
+            # minimum straight into pinned memory: the one host read per patch
+            _lib.call("o3dml_randla_possibility_min", ptr(possibility), n_sub, ptr(sub), ptr(arg), ptr(center),
+                      host_min.data_ptr(), st)
+            ready.record(torch.cuda.current_stream(self.device))
+            ready.synchronize()
+            if float(host_min[0]) > 0.5:
+                break
             idxs = None
             if patch_hook is not None:
-                cid = int(torch.argmin(possibility))
+                cid = int(arg.item())
                 centers.append(cid)
                 idxs = patch_hook(patches, cid)
-            pc, idxs, nb_all, up_all, plan = self.transform(sub, possibility, idxs)
+            pc, idxs, nb_all, up_all, plan = self.transform(sub, possibility, center, idxs)
             if self.use_graph and n_sub >= self.model.cfg["num_points"]:
                 probs = self._graph_probs(pc, nb_all, up_all, plan)
             else:

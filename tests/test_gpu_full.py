@@ -184,9 +184,13 @@ def test_c3_step_matches_reference(c3, mode):
     assert abs(loss.item() - ref_loss) < 1e-5 * abs(ref_loss)
     params = dict(m.named_parameters())
     names = [str(s) for s in F[f"c3_{mode}_grad_names"]]
+    bad = []
     for k, ref_norm, err32 in zip(names, F[f"c3_{mode}_f64_grad_norms"], F[f"c3_{mode}_ref32_err_norms"]):
         g = params[k].grad.detach().double().norm().item()
-        assert abs(g - ref_norm) <= bound(err32) * ref_norm + 1e-12, (k, g, ref_norm, err32)
+        err = abs(g - ref_norm) / (ref_norm + 1e-30)
+        if err > bound(err32):
+            bad.append((k, err, float(err32)))
+    assert not bad, sorted(bad, key=lambda b: -b[1])[:8]
     for key in F.files:
         if key.startswith(f"c3_{mode}_f64_grad:"):
             k = key.split(":", 1)[1]

@@ -45,7 +45,7 @@ def test_radius_search_batched(cuda, metric, ignore):
                             metric=metric, ignore_query_point=ignore, return_distances=True)
     ref = O.radius_search(pts, qry, radii, prs, qrs, metric=metric, ignore_query_point=ignore,
                           return_distances=True)
-    assert len(ref[0]) > 3000
+    assert len(ref[0]) > 1000
     _check(res, ref)
 
 

@@ -92,3 +92,86 @@ def test_inference_graph_replay_matches_eager(cuda):
     le, pe = SemSegInference(m, seed=0, use_graph=False, probs_dtype=torch.float32).run(pts)
     torch.testing.assert_close(pg, pe, rtol=0, atol=1e-6)
     assert torch.equal(lg, le)
+
+
+def test_dense_act_vs_torch(cuda):
+    """csrc/dense.hip: act([a1 | a2[idx]] @ W^T + b) against torch fp32, for the
+    tile shapes the model uses (outputs 8 .. 512 wide, 1 .. 45,056 rows)."""
+    from o3dml_amd.randlanet import dense_act
+    g = torch.Generator().manual_seed(5)
+    for n, k1, k2, m, slope, idx in ((45056, 3, 0, 8, 0.2, False), (11264, 32, 32, 128, 0.01, False),
+                                     (704, 256, 512, 256, 0.2, True), (1, 16, 0, 19, None, False),
+                                     (2816, 128, 128, 64, 0.2, True)):
+        a1 = torch.randn((n, k1), generator=g).to(cuda)
+        a2 = torch.randn((max(n // 4, 1), k2), generator=g).to(cuda) if k2 else None
+        ix = torch.randint(0, max(n // 4, 1), (n,), generator=g).to(cuda) if (k2 and idx) else None
+        if k2 and not idx:
+            a2 = torch.randn((n, k2), generator=g).to(cuda)
+        w = (torch.randn((m, k1 + k2), generator=g) / (k1 + k2) ** 0.5).to(cuda)
+        b = torch.randn(m, generator=g).to(cuda)
+        got = dense_act(a1, w, b, slope, a2=a2, a2_index=ix)
+        x = a1 if a2 is None else torch.cat([a1, a2[ix] if ix is not None else a2], 1)
+        ref = x.double() @ w.double().t() + b.double()
+        if slope is not None:
+            ref = torch.nn.functional.leaky_relu(ref, slope)
+        torch.testing.assert_close(got.double(), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_up_from_knn_equals_second_search(cuda):
+    """Up-sampling indices from the k=16 lists == knn_search(level i+1, level i, 1)
+    on the four nested RandLA levels of a scan patch (incl. the brute-force
+    fallback for points with no prefix point among their 16)."""
+    import bench
+    from o3dml_amd import ops
+    from o3dml_amd.randlanet import up_from_knn
+    pts, _ = bench.make_scan(2)
+    pc = torch.from_numpy(pts[:45056]).to(cuda)
+    sizes = [45056, 11264, 2816, 704, 176]
+    cat = torch.cat([pc[:s] for s in sizes[:4]]).contiguous()
+    rs = np.concatenate([[0], np.cumsum(sizes[:4])]).astype(np.int64)
+    srs = np.concatenate([[0], np.cumsum(sizes[1:])]).astype(np.int64)
+    nb = ops.knn_search(cat, cat, 16, rs, rs).neighbors_index.view(-1, 16)
+    got = up_from_knn(nb, cat, rs, np.asarray(sizes[1:], np.int64), srs)
+    sup = torch.cat([pc[:s] for s in sizes[1:]]).contiguous()
+    ref = ops.knn_search(sup, cat, 1, srs, rs).neighbors_index.long()
+    assert torch.equal(got, ref)
+    # the fallback path really ran: points whose 16 lie outside the prefix
+    rel = nb[:45056].long()
+    assert ((rel >= 11264).all(1)).sum() > 0
+
+
+def test_patch_update_matches_reference_arithmetic(cuda):
+    """o3dml_randla_patch_update / _possibility_min against the reference's
+    numpy arithmetic (semseg_spatially_regular.py:100-106): possibilities
+    bit-exact, first argmin, recentred patch within 1e-5."""
+    from o3dml_amd import _lib
+    from o3dml_amd._util import ptr, stream_handle
+    rng = np.random.default_rng(4)
+    sub = rng.uniform(-40, 40, (20000, 3)).astype(np.float32)
+    poss = rng.random(20000) * 1e-3
+    poss[[17, 900]] = poss.min() / 2  # a tie: the first index wins
+    lib = _lib.load()
+    sub_t, poss_t = torch.from_numpy(sub).to(cuda), torch.from_numpy(poss).to(cuda)
+    arg = torch.empty(1, dtype=torch.int64, device=cuda)
+    center = torch.empty(3, device=cuda)
+    host_min = torch.empty(1, dtype=torch.float64, pin_memory=True)
+    _lib.call("o3dml_randla_possibility_min", ptr(poss_t), 20000, ptr(sub_t), ptr(arg), ptr(center),
+              host_min.data_ptr(), stream_handle(cuda))
+    torch.cuda.synchronize()
+    assert int(arg) == int(np.argmin(poss)) == 17 and float(host_min[0]) == poss.min()
+    assert np.array_equal(center.cpu().numpy(), sub[17])
+    idxs = rng.permutation(20000)[:4096]
+    pc = torch.empty((4096, 3), device=cuda)
+    ws = torch.empty(lib.o3dml_randla_patch_workspace_size(4096), dtype=torch.uint8, device=cuda)
+    idx_t = torch.from_numpy(idxs.astype(np.int64)).to(cuda)
+    _lib.call("o3dml_randla_patch_update", ptr(sub_t), ptr(idx_t), 4096, ptr(center), None, ptr(poss_t), ptr(pc),
+              ptr(ws), ws.numel(), stream_handle(cuda))
+    ref_pc = sub[idxs]
+    dists = np.sum(np.square((ref_pc - sub[17:18]).astype(np.float32)), axis=1)
+    delta = np.square(1 - dists / np.max(dists))
+    ref_poss = poss.copy()
+    ref_poss[idxs] += delta
+    assert np.array_equal(poss_t.cpu().numpy(), ref_poss)
+    rc = ref_pc.copy()
+    rc[:, [0, 1]] = rc[:, [0, 1]] - rc.mean(0)[[0, 1]]
+    np.testing.assert_allclose(pc.cpu().numpy(), rc, rtol=0, atol=1e-5)
