@@ -175,19 +175,31 @@ int o3dml_radius_search_sort_long_rows(int64_t n_points, int64_t n_queries, int6
  *   possibility[idxs[i]] += (1 - d / max d)^2 for i with keep[i] (keep NULL:
  *   all; duplicates must be masked to one), pc x, y recentred on their mean.
  * _up_from_knn: up[q] for every point q of the concatenated levels
- *   (level i = rs[i] .. rs[i+1]) = index in the concatenated levels 1..L
- *   (srs[i] + position) of q's nearest point among the first nxt[i] points of
- *   its level, from the (distance, index)-sorted k-lists nb (int32, indices
- *   into the concatenation) — equal to knn_search(level i+1, level i, 1);
- *   the points whose list holds none are searched by brute force. ------ */
+ *   (level i = rs[i] .. rs[i+1]) = position (within level i+1) of q's
+ *   nearest point among the first nxt[i] points of its level, from the
+ *   (distance, index)-sorted k-lists nb (int32, indices into the
+ *   concatenation; rewritten IN PLACE relative to each row's own level) —
+ *   equal to knn_search(level i+1, level i, 1) minus srs[i]; the points whose
+ *   list holds none are searched by brute force (srs: unused, kept for the
+ *   caller's bookkeeping). ------------------------------------------------ */
+size_t o3dml_randla_possibility_min_workspace_size(void);
 int o3dml_randla_possibility_min(const double* possibility, int64_t n, const float* sub, int64_t* argmin,
-                                 float* center, double* host_min, void* stream);
+                                 float* center, double* host_min, void* workspace, size_t workspace_bytes,
+                                 void* stream);
+/* dst[i] = src[perm(i)], perm a keyed (seed) bijection of [0, n) (Feistel
+ * network + cycle walking): the patch shuffle. */
+int o3dml_random_permute(const int64_t* src, int64_t n, uint64_t seed, int64_t* dst, void* stream);
+/* test_probs[idxs[i]] = smooth * test_probs[idxs[i]] + (1 - smooth) * probs[i]
+ * (randlanet.py:441-465), probs f32 [n, c]; store f16 (store_half: the
+ * reference's float16 test_probs arithmetic) or f32; keep masks duplicates. */
+int o3dml_randla_update_probs(const float* probs, const int64_t* idxs, const uint8_t* keep, int64_t n, int c,
+                              double smooth, int store_half, void* test_probs, void* stream);
 size_t o3dml_randla_patch_workspace_size(int64_t n);
 int o3dml_randla_patch_update(const float* sub, const int64_t* idxs, int64_t n, const float* center,
                               const uint8_t* keep, double* possibility, float* pc, void* workspace,
                               size_t workspace_bytes, void* stream);
 size_t o3dml_randla_up_workspace_size(int64_t total);
-int o3dml_randla_up_from_knn(const int32_t* nb, int k, const float* cat, int nlev, const int64_t* rs,
+int o3dml_randla_up_from_knn(int32_t* nb, int k, const float* cat, int nlev, const int64_t* rs,
                              const int64_t* nxt, const int64_t* srs, int64_t* up, void* workspace,
                              size_t workspace_bytes, void* stream);
 
@@ -197,9 +209,12 @@ int o3dml_randla_up_from_knn(const int32_t* nb, int k, const float* cat, int nle
  * a1 f32 [n, k1], a2 f32 [*, k2] (k2 = 0: none), weight f32 [m, k1 + k2]
  * (torch Linear layout), bias f32 [m] or NULL, act 1 = LeakyReLU(slope),
  * 0 = identity.  Covers LocalFeatureAggregation's lrelu(mlp2(x) +
- * shortcut(feat)) (:689-692) and the decoder's [skip | upsampled] concat. */
+ * shortcut(feat)) (:689-692) and the decoder's [skip | upsampled] concat.
+ * Workspace: split-K partial slabs when the grid is small (deep levels). */
+size_t o3dml_dense_act_workspace_size(int64_t n, int k, int m);
 int o3dml_dense_act(const float* a1, int k1, const float* a2, int k2, const int64_t* a2_index, const float* weight,
-                    const float* bias, int64_t n, int m, int act, float slope, float* out, void* stream);
+                    const float* bias, int64_t n, int m, int act, float slope, float* out, void* workspace,
+                    size_t workspace_bytes, void* stream);
 
 /* ---- voxelize: replaces open3d.ml.torch.ops.voxelize
  * (ml3d/torch/models/point_pillars.py:352-357, sparseconvnet.py:293-298).

@@ -22,46 +22,58 @@
 //    in their list are searched by brute force over the prefix (one wave each).
 #include <cfloat>
 
+#include <hip/hip_fp16.h>
+
 #include "common.hpp"
 
 namespace o3dml {
 
 constexpr int kPatchBlocks = 64;
 
-__global__ void __launch_bounds__(1024) possibility_min_kernel(const double* __restrict__ p, int64_t n,
-                                                               const float* __restrict__ sub,
-                                                               int64_t* __restrict__ arg, float* __restrict__ center,
-                                                               double* __restrict__ host_min) {
-    __shared__ double sv[16];
-    __shared__ int64_t si[16];
+constexpr int kMinBlocks = 128;
+
+__device__ __forceinline__ void min_pair(double& v, int64_t& i, double ov, int64_t oi) {
+    if (ov < v || (ov == v && oi < i)) {  // the first minimum, as np.argmin
+        v = ov;
+        i = oi;
+    }
+}
+
+// per-block (min, first argmin) of a contiguous chunk
+__global__ void __launch_bounds__(256) possibility_min_partial_kernel(const double* __restrict__ p, int64_t n,
+                                                                      double* __restrict__ pv,
+                                                                      int64_t* __restrict__ pi) {
+    __shared__ double sv[4];
+    __shared__ int64_t si[4];
+    const int64_t per = ceil_div(n, kMinBlocks);
+    const int64_t s = blockIdx.x * per, e = min(n, s + per);
     double best = DBL_MAX;
     int64_t bi = INT64_MAX;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const double v = p[i];
-        if (v < best) {  // i increases per thread: keeps the first minimum
-            best = v;
-            bi = i;
-        }
-    }
-    for (int o = 32; o >= 1; o >>= 1) {
-        const double ov = __shfl_xor(best, o, 64);
-        const int64_t oi = __shfl_xor(bi, o, 64);
-        if (ov < best || (ov == best && oi < bi)) {
-            best = ov;
-            bi = oi;
-        }
-    }
+    for (int64_t i = s + threadIdx.x; i < e; i += blockDim.x) min_pair(best, bi, p[i], i);
+    for (int o = 32; o >= 1; o >>= 1) min_pair(best, bi, __shfl_xor(best, o, 64), __shfl_xor(bi, o, 64));
     if ((threadIdx.x & 63) == 0) {
         sv[threadIdx.x >> 6] = best;
         si[threadIdx.x >> 6] = bi;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < static_cast<int>(blockDim.x >> 6); ++w)
-            if (sv[w] < best || (sv[w] == best && si[w] < bi)) {
-                best = sv[w];
-                bi = si[w];
-            }
+        for (int w = 1; w < 4; ++w) min_pair(best, bi, sv[w], si[w]);
+        pv[blockIdx.x] = best;
+        pi[blockIdx.x] = bi;
+    }
+}
+
+__global__ void __launch_bounds__(64) possibility_min_final_kernel(const double* __restrict__ pv,
+                                                                   const int64_t* __restrict__ pi, int64_t n,
+                                                                   const float* __restrict__ sub,
+                                                                   int64_t* __restrict__ arg,
+                                                                   float* __restrict__ center,
+                                                                   double* __restrict__ host_min) {
+    double best = DBL_MAX;
+    int64_t bi = INT64_MAX;
+    for (int b = threadIdx.x; b < kMinBlocks; b += 64) min_pair(best, bi, pv[b], pi[b]);
+    for (int o = 32; o >= 1; o >>= 1) min_pair(best, bi, __shfl_xor(best, o, 64), __shfl_xor(bi, o, 64));
+    if (threadIdx.x == 0) {
         *arg = n ? bi : 0;
         if (n) {
             center[0] = sub[3 * bi];
@@ -150,7 +162,10 @@ __device__ __forceinline__ int up_level(int64_t q, const UpLevels& L) {
     return i;
 }
 
-__global__ void up_from_knn_kernel(const int32_t* __restrict__ nb, int k, int64_t total, UpLevels L,
+// up[q] = position of q's nearest point in level i + 1 (relative to that
+// level); the k-list row is rewritten relative to q's own level in the same
+// pass (the network consumes level-relative indices)
+__global__ void up_from_knn_kernel(int32_t* __restrict__ nb, int k, int64_t total, UpLevels L,
                                    int64_t* __restrict__ up, uint32_t* __restrict__ fallback,
                                    uint32_t* __restrict__ n_fallback) {
     for (int64_t q = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; q < total;
@@ -160,40 +175,123 @@ __global__ void up_from_knn_kernel(const int32_t* __restrict__ nb, int k, int64_
         int64_t r = -1;
         for (int j = 0; j < k; ++j) {
             const int64_t rel = static_cast<int64_t>(nb[q * k + j]) - base;
-            if (rel < lim) {
-                r = rel;
-                break;
-            }
+            nb[q * k + j] = static_cast<int32_t>(rel);
+            if (r < 0 && rel < lim) r = rel;
         }
-        if (r >= 0) up[q] = r + L.srs[i];
+        if (r >= 0) up[q] = r;
         else fallback[atomicAdd(n_fallback, 1u)] = static_cast<uint32_t>(q);
     }
 }
 
-// one wave per listed query: (distance bits, index) minimum over its prefix
+// one workgroup per listed query: (distance bits, index) minimum over the
+// prefix, 4 independent loads in flight per thread
 __global__ void __launch_bounds__(256) up_fallback_kernel(const float* __restrict__ cat, UpLevels L,
                                                           const uint32_t* __restrict__ fallback,
                                                           const uint32_t* __restrict__ n_fallback,
                                                           int64_t* __restrict__ up) {
-    const int lane = threadIdx.x & 63;
-    const int64_t waves = static_cast<int64_t>(gridDim.x) * (blockDim.x >> 6);
+    __shared__ uint64_t red[4];
     const int64_t cnt = *n_fallback;
-    for (int64_t w = blockIdx.x * static_cast<int64_t>(blockDim.x >> 6) + (threadIdx.x >> 6); w < cnt; w += waves) {
+    for (int64_t w = blockIdx.x; w < cnt; w += gridDim.x) {
         const int64_t q = fallback[w];
         const int i = up_level(q, L);
         const float qx = cat[3 * q], qy = cat[3 * q + 1], qz = cat[3 * q + 2];
+        const float* base = cat + 3 * L.rs[i];
+        const int64_t m = L.nxt[i];
         uint64_t best = ~0ull;
-        for (int64_t r = lane; r < L.nxt[i]; r += 64) {
-            const int64_t p = L.rs[i] + r;
-            const float d = dist_l2(cat[3 * p], cat[3 * p + 1], cat[3 * p + 2], qx, qy, qz);
-            const uint64_t key = (static_cast<uint64_t>(__float_as_uint(d)) << 32) | static_cast<uint32_t>(r);
-            best = key < best ? key : best;
+        constexpr int U = 4;
+        for (int64_t r0 = threadIdx.x; r0 < m; r0 += U * 256) {
+            float px[U], py[U], pz[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = r0 + u * 256;
+                const bool ok = r < m;
+                px[u] = ok ? base[3 * r] : 0.f;
+                py[u] = ok ? base[3 * r + 1] : 0.f;
+                pz[u] = ok ? base[3 * r + 2] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = r0 + u * 256;
+                if (r < m) {
+                    const float d = dist_l2(px[u], py[u], pz[u], qx, qy, qz);
+                    const uint64_t key = (static_cast<uint64_t>(__float_as_uint(d)) << 32) | static_cast<uint32_t>(r);
+                    best = key < best ? key : best;
+                }
+            }
         }
         for (int o = 32; o >= 1; o >>= 1) {
             const uint64_t other = __shfl_xor(best, o, 64);
             best = other < best ? other : best;
         }
-        if (lane == 0 && best != ~0ull) up[q] = static_cast<int64_t>(static_cast<uint32_t>(best)) + L.srs[i];
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int j = 1; j < 4; ++j) best = red[j] < best ? red[j] : best;
+            if (best != ~0ull) up[q] = static_cast<int64_t>(static_cast<uint32_t>(best));
+        }
+        __syncthreads();
+    }
+}
+
+// dst[i] = src[perm(i)], perm a keyed bijection of [0, n): a 4-round Feistel
+// network on the smallest even bit width covering n, cycle-walked into range
+// (the patch shuffle of semseg_spatially_regular.py:100 — any uniformly
+// random order serves; one launch instead of a sort of random keys)
+__device__ __forceinline__ uint32_t feistel_mix(uint32_t x, uint32_t key) {
+    x ^= key;
+    x *= 0x9E3779B1u;
+    x ^= x >> 15;
+    x *= 0x85EBCA77u;
+    x ^= x >> 13;
+    return x;
+}
+
+__global__ void random_permute_kernel(const int64_t* __restrict__ src, int64_t n, int half, uint64_t seed,
+                                      int64_t* __restrict__ dst) {
+    const uint32_t mask = (1u << half) - 1u;
+    const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+    const uint32_t keys[4] = {k0, k1, k0 ^ 0xA5A5A5A5u, k1 ^ 0x3C3C3C3Cu};
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        uint32_t v = static_cast<uint32_t>(i);
+        do {
+            uint32_t l = v >> half, r = v & mask;
+#pragma unroll
+            for (int rd = 0; rd < 4; ++rd) {
+                const uint32_t t = l ^ (feistel_mix(r, keys[rd]) & mask);
+                l = r;
+                r = t;
+            }
+            v = (l << half) | r;
+        } while (v >= static_cast<uint64_t>(n));
+        dst[i] = src[v];
+    }
+}
+
+// test_probs[idxs[i]] = smooth * test_probs[idxs[i]] + (1 - smooth) * probs[i]
+// (randlanet.py:441-465) with the reference's dtypes: a float16 store
+// multiplies in float16 (f16(f16(smooth) * p16), exact product rounded once),
+// adds the float32 new term in float32 and rounds to the store; keep masks
+// duplicate indices to their last occurrence (numpy semantics)
+template <bool HALF>
+__global__ void update_probs_kernel(const float* __restrict__ probs, const int64_t* __restrict__ idxs,
+                                    const uint8_t* __restrict__ keep, int64_t n, int c, float smooth_store,
+                                    float new_w, void* __restrict__ store) {
+    const int64_t total = n * c;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t i = e / c;
+        if (keep && !keep[i]) continue;
+        const int64_t o = idxs[i] * c + (e - i * c);
+        const float b = probs[e] * new_w;
+        if constexpr (HALF) {
+            __half* t = static_cast<__half*>(store);
+            const float a = __half2float(__float2half_rn(__half2float(t[o]) * smooth_store));
+            t[o] = __float2half_rn(a + b);
+        } else {
+            float* t = static_cast<float*>(store);
+            t[o] = t[o] * smooth_store + b;
+        }
     }
 }
 
@@ -202,9 +300,52 @@ __global__ void __launch_bounds__(256) up_fallback_kernel(const float* __restric
 using namespace o3dml;
 
 O3DML_API int o3dml_randla_possibility_min(const double* possibility, int64_t n, const float* sub, int64_t* argmin,
-                                           float* center, double* host_min, void* stream) {
+                                           float* center, double* host_min, void* workspace, size_t workspace_bytes,
+                                           void* stream) {
     O3DML_GUARD_BEGIN
-    possibility_min_kernel<<<1, 1024, 0, as_stream(stream)>>>(possibility, n, sub, argmin, center, host_min);
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    double* pv = ws.take<double>(kMinBlocks);
+    int64_t* pi = ws.take<int64_t>(kMinBlocks);
+    possibility_min_partial_kernel<<<kMinBlocks, 256, 0, st>>>(possibility, n, pv, pi);
+    O3DML_LAUNCH_CHECK();
+    possibility_min_final_kernel<<<1, 64, 0, st>>>(pv, pi, n, sub, argmin, center, host_min);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+O3DML_API size_t o3dml_randla_possibility_min_workspace_size() {
+    return ws_bytes<double>(kMinBlocks) + ws_bytes<int64_t>(kMinBlocks);
+}
+
+O3DML_API int o3dml_random_permute(const int64_t* src, int64_t n, uint64_t seed, int64_t* dst, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "random_permute: n out of range");
+    if (n == 0) return 0;
+    int bits = 1;
+    while ((int64_t(1) << bits) < n) ++bits;
+    const int half = (bits + 1) / 2;
+    random_permute_kernel<<<stream_grid(n, 256), 256, 0, as_stream(stream)>>>(src, n, half, seed, dst);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_randla_update_probs(const float* probs, const int64_t* idxs, const uint8_t* keep, int64_t n,
+                                        int c, double smooth, int store_half, void* test_probs, void* stream) {
+    O3DML_GUARD_BEGIN
+    if (n == 0) return 0;
+    hipStream_t st = as_stream(stream);
+    const unsigned g = stream_grid(n * c, 256);
+    // (1 - smooth) in double, then float32: the reference's Python scalar
+    // times a float32 array (0.050000000000000044 -> 0.05f)
+    const float new_w = static_cast<float>(1.0 - smooth);
+    if (store_half) {  // the Python scalar becomes the store's dtype (numpy), the new term stays f32
+        const float s16 = __half2float(__float2half_rn(static_cast<float>(smooth)));
+        update_probs_kernel<true><<<g, 256, 0, st>>>(probs, idxs, keep, n, c, s16, new_w, test_probs);
+    } else {
+        update_probs_kernel<false><<<g, 256, 0, st>>>(probs, idxs, keep, n, c, static_cast<float>(smooth), new_w,
+                                                      test_probs);
+    }
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }
@@ -230,7 +371,7 @@ O3DML_API int o3dml_randla_patch_update(const float* sub, const int64_t* idxs, i
 }
 
 // levels: nlev (<= 4) entries each of rs (nlev + 1), nxt, srs (host arrays)
-O3DML_API int o3dml_randla_up_from_knn(const int32_t* nb, int k, const float* cat, int nlev, const int64_t* rs,
+O3DML_API int o3dml_randla_up_from_knn(int32_t* nb, int k, const float* cat, int nlev, const int64_t* rs,
                                        const int64_t* nxt, const int64_t* srs, int64_t* up, void* workspace,
                                        size_t workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
@@ -252,7 +393,7 @@ O3DML_API int o3dml_randla_up_from_knn(const int32_t* nb, int k, const float* ca
     O3DML_CHECK_HIP(hipMemsetAsync(cntr, 0, sizeof(uint32_t), st));
     up_from_knn_kernel<<<stream_grid(total, 256), 256, 0, st>>>(nb, k, total, L, up, list, cntr);
     O3DML_LAUNCH_CHECK();
-    up_fallback_kernel<<<256, 256, 0, st>>>(cat, L, list, cntr, up);
+    up_fallback_kernel<<<512, 256, 0, st>>>(cat, L, list, cntr, up);
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }

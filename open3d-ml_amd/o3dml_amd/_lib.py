@@ -85,13 +85,18 @@ SIGNATURES = {
     "o3dml_randla_att_pool": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "o3dml_randla_gather_max": (c_i32, [c_p, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
     # randla_sampler.hip
-    "o3dml_randla_possibility_min": (c_i32, [c_p, c_i64, c_p, c_p, c_p, c_p, c_p]),
+    "o3dml_randla_possibility_min": (c_i32, [c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "o3dml_randla_possibility_min_workspace_size": (c_sz, []),
+    "o3dml_random_permute": (c_i32, [c_p, c_i64, c_u64, c_p, c_p]),
+    "o3dml_randla_update_probs": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_f64, c_i32, c_p, c_p]),
     "o3dml_randla_patch_workspace_size": (c_sz, [c_i64]),
     "o3dml_randla_patch_update": (c_i32, [c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "o3dml_randla_up_from_knn": (c_i32, [c_p, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "o3dml_randla_up_workspace_size": (c_sz, [c_i64]),
     # dense.hip
-    "o3dml_dense_act": (c_i32, [c_p, c_i32, c_p, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_i32, c_f32, c_p, c_p]),
+    "o3dml_dense_act_workspace_size": (c_sz, [c_i64, c_i32, c_i32]),
+    "o3dml_dense_act": (c_i32, [c_p, c_i32, c_p, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_i32, c_f32, c_p, c_p, c_sz,
+                                c_p]),
     "o3dml_calculate_grid_workspace_size": (c_sz, [c_i64]),
     "o3dml_calculate_grid_count": (c_i32, [c_p, c_i64, c_p, c_p, c_sz, c_p]),
     "o3dml_calculate_grid_fill": (c_i32, [c_i64, c_p, c_p, c_sz, c_p]),

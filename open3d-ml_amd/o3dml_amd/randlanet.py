@@ -81,9 +81,11 @@ def dense_act(a1, w, b, slope=None, a2=None, a2_index=None):
     k2 = 0 if a2 is None else a2.shape[1]
     m = w.shape[0]
     out = torch.empty((n, m), dtype=torch.float32, device=a1.device)
+    nbytes = _lib.load().o3dml_dense_act_workspace_size(n, k1 + k2, m)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=a1.device) if nbytes else None
     _lib.call("o3dml_dense_act", ptr(a1.contiguous()), k1, ptr(None if a2 is None else a2.contiguous()), k2,
-              ptr(a2_index), ptr(w), ptr(b), n, m, int(slope is not None), float(slope or 0.0), ptr(out),
-              stream_handle(a1.device))
+              ptr(a2_index), ptr(w), ptr(b), n, m, int(slope is not None), float(slope or 0.0), ptr(out), ptr(ws),
+              0 if ws is None else ws.numel(), stream_handle(a1.device))
     return out
 
 
@@ -402,9 +404,11 @@ class RandLANet(nn.Module):
 def up_from_knn(nb_all, cat, rs, nxt, srs, scratch=None):
     """Up-sampling indices of the RandLA levels from the batched k-lists
     (csrc/randla_sampler.hip): for every point of the concatenated levels
-    (level i = cat[rs[i]:rs[i+1]]), the index in the concatenated levels 1..L
-    (srs[i] + position) of its nearest point among the first nxt[i] points of
-    its level — knn_search(level i+1, level i, 1) without a second search."""
+    (level i = cat[rs[i]:rs[i+1]]), the position within level i+1 of its
+    nearest point among the first nxt[i] points of its level —
+    knn_search(level i+1, level i, 1) - srs[i] without a second search.
+    nb_all (int32, indices into the concatenation) is rewritten IN PLACE to
+    indices relative to each row's own level."""
     total = int(rs[-1])
     up = torch.empty(total, dtype=torch.int64, device=cat.device)
     nbytes = _lib.load().o3dml_randla_up_workspace_size(total)
@@ -454,6 +458,7 @@ class SemSegInference:
         self.probs_dtype = probs_dtype
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
+        self.rng = np.random.default_rng(seed)  # patch-shuffle keys (host side: no device round trip)
         self.stats = {}
 
     def preprocess(self, points):
@@ -472,15 +477,18 @@ class SemSegInference:
         n_pts = cfg["num_points"]
         dev = self.device
         if idxs is not None:
-            idxs = idxs.to(dev).long()
-        elif sub.shape[0] < n_pts:
-            extra = torch.randint(0, sub.shape[0], (n_pts - sub.shape[0],), generator=self.gen, device=dev)
-            idxs = torch.cat([torch.arange(sub.shape[0], device=dev), extra])
-            idxs = idxs[torch.randperm(idxs.shape[0], generator=self.gen, device=dev)]
+            idxs = idxs.to(dev).long().contiguous()
         else:
-            idxs = ops.knn_search(sub, center.view(1, 3), n_pts).neighbors_index.long()
-            idxs = idxs[torch.randperm(idxs.shape[0], generator=self.gen, device=dev)]
-        idxs = idxs.contiguous()
+            if sub.shape[0] < n_pts:
+                extra = torch.randint(0, sub.shape[0], (n_pts - sub.shape[0],), generator=self.gen, device=dev)
+                crop = torch.cat([torch.arange(sub.shape[0], device=dev), extra])
+            else:
+                crop = ops.knn_search(sub, center.view(1, 3), n_pts, index_dtype=torch.int64).neighbors_index
+            # the shuffle (random.shuffle, semseg_spatially_regular.py:100): a
+            # keyed random bijection, one launch (o3dml_random_permute)
+            idxs = torch.empty_like(crop)
+            _lib.call("o3dml_random_permute", ptr(crop), crop.shape[0], int(self.rng.integers(0, 2**63)),
+                      ptr(idxs), stream_handle(dev))
         # duplicates (a cloud smaller than a patch): the last one's value, as
         # numpy's possibilities[idxs] += delta
         keep = _last_occurrence(idxs, sub.shape[0]).to(torch.uint8) if sub.shape[0] < idxs.shape[0] else None
@@ -520,24 +528,24 @@ class SemSegInference:
         multiplies in float16 (numpy casts the Python scalar to the array's
         dtype), the new term is float32, the sum float32 rounded to the store;
         duplicate indices keep the last one (numpy semantics)."""
+        keep = None
         if test_probs.shape[0] < idxs.shape[0]:  # a patch larger than the cloud repeats points
-            keep = _last_occurrence(idxs, test_probs.shape[0])
-            idxs, probs = idxs[keep], probs[keep]
-        old = test_probs[idxs]
-        a = old * torch.tensor(self.test_smooth, dtype=test_probs.dtype, device=old.device)
-        b = probs.float() * torch.tensor(1 - self.test_smooth, dtype=torch.float32, device=old.device)
-        test_probs[idxs] = (a.float() + b).to(test_probs.dtype)
+            keep = _last_occurrence(idxs, test_probs.shape[0]).to(torch.uint8)
+        _lib.call("o3dml_randla_update_probs", ptr(probs.float().contiguous()), ptr(idxs), ptr(keep), idxs.shape[0],
+                  test_probs.shape[1], float(self.test_smooth), int(test_probs.dtype == torch.float16),
+                  ptr(test_probs), stream_handle(test_probs.device))
 
     def _levels(self, pc, nb_all, up_all, plan):
-        """Per-layer (coords, nbrs, subs, ups) views of the batched kNN results."""
+        """Per-layer (coords, nbrs, subs, ups) views of the batched kNN results
+        (already level-relative: up_from_knn); no kernels."""
         sizes, rs, srs = plan
         coords, nbrs, subs, ups = [], [], [], []
         for i in range(self.model.cfg["num_layers"]):
-            nb = (nb_all[rs[i]:rs[i + 1]] - int(rs[i])).contiguous()
-            coords.append(pc[:sizes[i]].contiguous())
+            nb = nb_all[rs[i]:rs[i + 1]]
+            coords.append(pc[:sizes[i]])
             nbrs.append(nb)
-            subs.append(nb[:sizes[i + 1]].contiguous())
-            ups.append(up_all[rs[i]:rs[i + 1]] - int(srs[i]))
+            subs.append(nb[:sizes[i + 1]])
+            ups.append(up_all[rs[i]:rs[i + 1]])
         return coords, nbrs, subs, ups
 
     def _patch_probs(self, pc, nb_all, up_all, plan):
@@ -587,13 +595,14 @@ class SemSegInference:
         arg = torch.empty(1, dtype=torch.int64, device=self.device)
         center = torch.empty(3, dtype=torch.float32, device=self.device)
         host_min = torch.empty(1, dtype=torch.float64, pin_memory=True)
+        mws = self._ws("min", _lib.load().o3dml_randla_possibility_min_workspace_size())
         st = stream_handle(self.device)
         ready = torch.cuda.Event()
         while True:
             # min + first argmin of the possibilities, the centre point; the
             # minimum straight into pinned memory: the one host read per patch
             _lib.call("o3dml_randla_possibility_min", ptr(possibility), n_sub, ptr(sub), ptr(arg), ptr(center),
-                      host_min.data_ptr(), st)
+                      host_min.data_ptr(), ptr(mws), mws.numel(), st)
             ready.record(torch.cuda.current_stream(self.device))
             ready.synchronize()
             if float(host_min[0]) > 0.5:

@@ -36,9 +36,8 @@ def _build_map(nidx, kidx, nimp, rs, n_in, K, normalize, out_importance, want_in
               mws.numel(), st)
     if status[0] & 2:
         raise RuntimeError("sparse_conv: neighbors_kernel_index out of range for the filter")
-    if status[0] & 1:
-        raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index "
-                           "(non-lattice neighbourhood); not representable by the dense kernel map")
+    if status[0] & 1:  # handled by _conv_layers
+        raise _DuplicateKernelIndex()
     if tile_order:
         _lib.call("o3dml_sparse_conv_tile_order", ptr(mws), mws.numel(), n_out, n_in, K, int(bool(want_inv)), st)
     return mws, n_out
@@ -122,6 +121,59 @@ def conv_grads(filters, inp_features, grad_out, neighbors_index, neighbors_kerne
     return _backward(W, x, mws, ss, meta, grad_out.to(dev), need_w, need_x)
 
 
+class _DuplicateKernelIndex(Exception):
+    """Two neighbours of one output share a kernel index (see _conv_layers)."""
+
+
+def _conv_layers(f, x, b, nidx, kidx, nimp, rs, sscale, normalize, oimp, K):
+    """Open3D sums EVERY (neighbour, kernel index) pair of an output; the dense
+    kernel map holds one input per (output, kernel index).  Pairs that share
+    (output, kernel index) — layers.SparseConv on positions off one voxel
+    lattice — are split into layers by their rank within that (output, k)
+    group, in CSR order: layer l holds the l-th pair of every group, so each
+    layer is a valid dense map.  out = sum of the layers' HIP GEMMs (each with
+    its own autograd node), then the per-output normalisation / importance
+    over ALL the output's pairs.  Index bookkeeping only in torch."""
+    dev = x.device
+    n_out = rs.shape[0] - 1
+    P = nidx.shape[0]
+    counts = rs[1:] - rs[:-1]
+    o = torch.repeat_interleave(torch.arange(n_out, device=dev), counts)
+    key = o * K + kidx.long()
+    order = torch.sort(key, stable=True).indices
+    sk = key[order]
+    pos = torch.arange(P, device=dev)
+    start = torch.ones(P, dtype=torch.bool, device=dev)
+    start[1:] = sk[1:] != sk[:-1]
+    first = torch.cummax(torch.where(start, pos, torch.zeros_like(pos)), 0).values
+    rank = torch.empty(P, dtype=torch.int64, device=dev)
+    rank[order] = pos - first
+    n_layers = int(rank.max().item()) + 1
+    want_grad = torch.is_grad_enabled() and (f.requires_grad or x.requires_grad or (b is not None and b.requires_grad))
+    out = None
+    for layer in range(n_layers):
+        sel = torch.nonzero(rank == layer).squeeze(1)  # CSR order kept: rows stay grouped by output
+        c = torch.bincount(o[sel], minlength=n_out)
+        lrs = torch.zeros(n_out + 1, dtype=torch.int64, device=dev)
+        lrs[1:] = torch.cumsum(c, 0)
+        part = _ConvFn.apply(f, x, b if layer == 0 else None, nidx[sel].contiguous(), kidx[sel].contiguous(),
+                             None if nimp is None else nimp[sel].contiguous(), lrs, sscale, False, None, want_grad)
+        out = part if out is None else out + part
+    scale = None
+    if normalize:
+        w = nimp if nimp is not None else torch.ones(P, dtype=torch.float32, device=dev)
+        den = torch.zeros(n_out, dtype=torch.float32, device=dev).index_add_(0, o, w)
+        scale = torch.where(den != 0, 1.0 / den, torch.ones_like(den))  # as Open3D: no division by 0
+    if oimp is not None:
+        scale = oimp if scale is None else scale * oimp
+    if scale is not None:
+        if b is not None:  # Open3D scales the convolution, then adds the bias
+            out = (out - b) * scale[:, None] + b
+        else:
+            out = out * scale[:, None]
+    return out
+
+
 def _conv(filters, inp_features, bias, neighbors_index, neighbors_kernel_index, neighbors_importance,
           neighbors_row_splits, sscale, normalize, out_importance):
     dev = gpu_device(inp_features, filters)
@@ -138,7 +190,11 @@ def _conv(filters, inp_features, bias, neighbors_index, neighbors_kernel_index, 
     b = None if bias is None else (bias.to(dev) if not bias.is_cuda else bias)
     want_grad = torch.is_grad_enabled() and (f.requires_grad or x.requires_grad or
                                              (b is not None and b.requires_grad))
-    out = _ConvFn.apply(f, x, b, nidx, kidx, nimp, rs, sscale, bool(normalize), oimp, want_grad)
+    try:
+        out = _ConvFn.apply(f, x, b, nidx, kidx, nimp, rs, sscale, bool(normalize), oimp, want_grad)
+    except _DuplicateKernelIndex:
+        out = _conv_layers(f, x, b, nidx, kidx, nimp, rs, sscale, bool(normalize), oimp,
+                           int(np.prod(f.shape[:-2])))
     return out.cpu() if back_cpu else out
 
 

@@ -131,13 +131,15 @@ def test_up_from_knn_equals_second_search(cuda):
     rs = np.concatenate([[0], np.cumsum(sizes[:4])]).astype(np.int64)
     srs = np.concatenate([[0], np.cumsum(sizes[1:])]).astype(np.int64)
     nb = ops.knn_search(cat, cat, 16, rs, rs).neighbors_index.view(-1, 16)
+    nb0 = nb.clone()
     got = up_from_knn(nb, cat, rs, np.asarray(sizes[1:], np.int64), srs)
     sup = torch.cat([pc[:s] for s in sizes[1:]]).contiguous()
     ref = ops.knn_search(sup, cat, 1, srs, rs).neighbors_index.long()
-    assert torch.equal(got, ref)
+    lvl = torch.repeat_interleave(torch.arange(4, device=cuda), torch.tensor(sizes[:4], device=cuda))
+    assert torch.equal(got, ref - torch.from_numpy(srs[:4]).to(cuda)[lvl])  # relative to level i+1
+    assert torch.equal(nb.long(), nb0.long() - torch.from_numpy(rs[:4]).to(cuda)[lvl][:, None])  # rebased
     # the fallback path really ran: points whose 16 lie outside the prefix
-    rel = nb[:45056].long()
-    assert ((rel >= 11264).all(1)).sum() > 0
+    assert ((nb[:45056] >= 11264).all(1)).sum() > 0
 
 
 def test_patch_update_matches_reference_arithmetic(cuda):
@@ -155,8 +157,9 @@ def test_patch_update_matches_reference_arithmetic(cuda):
     arg = torch.empty(1, dtype=torch.int64, device=cuda)
     center = torch.empty(3, device=cuda)
     host_min = torch.empty(1, dtype=torch.float64, pin_memory=True)
+    mws = torch.empty(lib.o3dml_randla_possibility_min_workspace_size(), dtype=torch.uint8, device=cuda)
     _lib.call("o3dml_randla_possibility_min", ptr(poss_t), 20000, ptr(sub_t), ptr(arg), ptr(center),
-              host_min.data_ptr(), stream_handle(cuda))
+              host_min.data_ptr(), ptr(mws), mws.numel(), stream_handle(cuda))
     torch.cuda.synchronize()
     assert int(arg) == int(np.argmin(poss)) == 17 and float(host_min[0]) == poss.min()
     assert np.array_equal(center.cpu().numpy(), sub[17])
@@ -175,3 +178,36 @@ def test_patch_update_matches_reference_arithmetic(cuda):
     rc = ref_pc.copy()
     rc[:, [0, 1]] = rc[:, [0, 1]] - rc.mean(0)[[0, 1]]
     np.testing.assert_allclose(pc.cpu().numpy(), rc, rtol=0, atol=1e-5)
+
+
+def test_random_permute_is_a_permutation(cuda):
+    from o3dml_amd import _lib
+    from o3dml_amd._util import ptr, stream_handle
+    for n in (1, 2, 45056, 65537):
+        src = torch.arange(n, device=cuda) * 3
+        dst = torch.empty_like(src)
+        _lib.call("o3dml_random_permute", ptr(src), n, 12345, ptr(dst), stream_handle(cuda))
+        assert torch.equal(torch.sort(dst).values, src)
+        if n > 1000:
+            assert (dst != src).float().mean() > 0.99  # actually shuffled
+            d2 = torch.empty_like(src)
+            _lib.call("o3dml_random_permute", ptr(src), n, 12345, ptr(d2), stream_handle(cuda))
+            assert torch.equal(dst, d2)  # keyed: deterministic
+
+
+def test_update_probs_matches_reference_float16(cuda):
+    """o3dml_randla_update_probs == the reference's numpy float16 EMA
+    (randlanet.py:462: f16 store, Python scalars) bit for bit."""
+    from o3dml_amd import _lib
+    from o3dml_amd._util import ptr, stream_handle
+    rng = np.random.default_rng(9)
+    tp = rng.random((3000, 19)).astype(np.float16)
+    probs = rng.random((1000, 19)).astype(np.float32)
+    idxs = rng.permutation(3000)[:1000]
+    ref = tp.copy()
+    ref[idxs] = 0.95 * ref[idxs] + (1 - 0.95) * probs
+    t = torch.from_numpy(tp).to(cuda)
+    _lib.call("o3dml_randla_update_probs", ptr(torch.from_numpy(probs).to(cuda)),
+              ptr(torch.from_numpy(idxs.astype(np.int64)).to(cuda)), None, 1000, 19, 0.95, 1, ptr(t),
+              stream_handle(cuda))
+    assert np.array_equal(t.cpu().numpy(), ref)

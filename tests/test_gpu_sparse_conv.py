@@ -228,3 +228,50 @@ def test_bf16_split_products_match_exact_f32(cuda, cin, cout):
         lib.o3dml_sparse_conv_set_exact(prev)
     for e6, e1 in zip(errs[0], errs[1]):
         assert e6 <= 3 * e1 + 1e-7, (errs[0], errs[1])
+
+
+@pytest.mark.parametrize("normalize,importance", [(False, False), (True, False), (True, True)])
+def test_duplicate_kernel_indices(cuda, normalize, importance):
+    """Off-lattice positions: several neighbours of one output share a kernel
+    index (Open3D sums every pair).  The pairs are split into dense-map layers
+    (sparse_conv._conv_layers); forward vs the oracle (which sums the CSR pairs
+    directly), filter and feature gradients vs float64 autograd of the CSR
+    convolution, through layers.SparseConv's search rulebook."""
+    from o3dml_amd import layers, ops
+    rng = np.random.default_rng(31)
+    pos = (rng.random((1500, 3)) * 12).astype(np.float32)  # continuous positions: ~1.7 points per voxel
+    inp = torch.from_numpy(pos).to(cuda)
+    conv = layers.SparseConv(8, 16, [3, 3, 3], use_bias=True, normalize=normalize).to(cuda)
+    torch.nn.init.normal_(conv.bias)
+    conv.lattice_rulebook = False
+    nb, kidx = conv._rulebook(inp, inp, 1.0, None, False, 1.0)
+    idx, rs, kid = (nb.neighbors_index.cpu().numpy(), nb.neighbors_row_splits.cpu().numpy(), kidx.cpu().numpy())
+    o = np.repeat(np.arange(len(rs) - 1), np.diff(rs))
+    assert len(np.unique(o * 27 + kid)) < len(kid)  # duplicates present
+    x = torch.randn((1500, 8), device=cuda, requires_grad=True)
+    nimp = torch.rand(len(idx), device=cuda) if importance else None
+    W = conv.kernel
+    out = ops.sparse_conv(W, x, None, nb.neighbors_index, kidx, nimp, nb.neighbors_row_splits,
+                          normalize=normalize) + conv.bias
+    ref = O.sparse_conv(W.detach().cpu().numpy(), x.detach().cpu().numpy(), idx, kid, rs,
+                        neighbors_importance=None if nimp is None else nimp.cpu().numpy(),
+                        normalize=normalize) + conv.bias.detach().cpu().numpy()
+    _close(out.detach().cpu().numpy(), ref)
+    # the layer path (bias in the epilogue, normalisation after the layer sum)
+    _close(conv(x, inp, inp, 1.0).detach().cpu().numpy(), ref)
+    go = torch.randn_like(out)
+    gW, gx = torch.autograd.grad(out, (W, x), go)
+    W64 = W.detach().cpu().double().requires_grad_(True)
+    x64 = x.detach().cpu().double().requires_grad_(True)
+    Wf = W64.reshape(27, 8, 16)
+    contrib = torch.einsum("pc,pcd->pd", x64[torch.from_numpy(idx).long()], Wf[torch.from_numpy(kid).long()])
+    if importance:
+        contrib = contrib * nimp.cpu().double()[:, None]
+    r64 = torch.zeros((len(rs) - 1, 16), dtype=torch.float64).index_add_(0, torch.from_numpy(o), contrib)
+    if normalize:
+        w = nimp.cpu().double() if importance else torch.ones(len(idx), dtype=torch.float64)
+        den = torch.zeros(len(rs) - 1, dtype=torch.float64).index_add_(0, torch.from_numpy(o), w)
+        r64 = r64 / torch.where(den != 0, den, torch.ones_like(den))[:, None]
+    gW64, gx64 = torch.autograd.grad(r64, (W64, x64), go.cpu().double())
+    _close(gW.cpu().numpy(), gW64.numpy())
+    _close(gx.cpu().numpy(), gx64.numpy())
