@@ -392,6 +392,21 @@ int o3dml_kpconv_weighted_features_backward(const float* q_pts, int64_t n, const
                                             int cin, const float* kernel_points, int K, int kp_per_query,
                                             float extent, int influence, int closest, float* grad_features,
                                             void* stream);
+/* Deformable training (kp_per_query): per-query neighbours with no kernel
+ * point within extent are dropped in forward and backward, as the
+ * reference's in_range filter (kpconv.py:1076-1103).  _kernel_point_grad:
+ * grad_kp f32 [n,K,3] and grad_mod f32 [n,K] (nullable) from grad WF
+ * (before the modulation) for per-query kernel points [n,K,3].
+ * _min_d2_columns: per (query, kernel point) the neighbour column nearest
+ * to it (shadow at 1e6 included; min_d2 of kpconv.py:1071). */
+int o3dml_kpconv_kernel_point_grad(const float* q_pts, int64_t n, const float* s_pts, int64_t n_support,
+                                   const void* neighbors, int index_bits, int nb, const float* features, int cin,
+                                   const float* grad_wf, const float* kernel_points, int K, float extent,
+                                   int influence, int closest, const float* modulations, float* grad_kp,
+                                   float* grad_mod, void* stream);
+int o3dml_kpconv_min_d2_columns(const float* q_pts, int64_t n, const float* s_pts, int64_t n_support,
+                                const void* neighbors, int index_bits, int nb, const float* kernel_points, int K,
+                                int32_t* columns, void* stream);
 
 /* ---- KPFCNN pooling (kpconv.py:821-858 max_pool /
  * closest_pool).  x f32 [n_support, c]; inds [n, ld] int32/int64 (index

@@ -23,20 +23,35 @@ namespace o3dml {
 
 constexpr int kKpMaxK = 32;    // kernel points
 
+// gaussian sigma^2 term of the reference's radius_gaussian (kpconv.py:808-818,
+// eps 1e-9 in the denominator)
+__device__ __forceinline__ float kp_gauss_den(float extent) {
+    const float sig = 0.3f * extent;
+    return 2.f * (sig * sig) + 1e-9f;
+}
+
+// Influences of one neighbour (offset d = p - q) on the K kernel points into
+// wrow.  Returns false when DEFORM and no kernel point is within extent: the
+// deformable reference drops such neighbours before the influences
+// (kpconv.py:1076-1103, the in_range / topk filter), which matters for the
+// constant and gaussian influences.
 template <int INFL, bool CLOSEST>
-__device__ __forceinline__ void kp_influences(float dx, float dy, float dz, const float* __restrict__ kq, int K,
-                                              float extent, float* __restrict__ wrow) {
+__device__ __forceinline__ bool kp_influences(float dx, float dy, float dz, const float* __restrict__ kq, int K,
+                                              float extent, bool deform, float* __restrict__ wrow) {
     float best = INFINITY;
     int bk = 0;
+    bool in_range = false;
+    const float e2 = extent * extent;
 #pragma unroll
     for (int k = 0; k < kKpMaxK; ++k) {  // compile-time indices: wrow may live in registers
         if (k >= K) continue;
         const float ex = dx - kq[3 * k], ey = dy - kq[3 * k + 1], ez = dz - kq[3 * k + 2];
         const float d2 = ex * ex + ey * ey + ez * ez;
+        in_range = in_range || d2 < e2;
         float v;
         if constexpr (INFL == 0) v = 1.f;
         else if constexpr (INFL == 1) v = fmaxf(1.f - sqrtf(d2) / extent, 0.f);
-        else v = __expf(-d2 / (2.f * (0.3f * extent) * (0.3f * extent)));
+        else v = __expf(-d2 / kp_gauss_den(extent));
         if (CLOSEST && d2 < best) {
             best = d2;
             bk = k;
@@ -48,6 +63,7 @@ __device__ __forceinline__ void kp_influences(float dx, float dy, float dz, cons
         for (int k = 0; k < kKpMaxK; ++k)
             if (k < K && k != bk) wrow[k] = 0.f;
     }
+    return in_range || !deform;
 }
 
 template <int INFL, bool CLOSEST, class TI>
@@ -79,10 +95,11 @@ __global__ void __launch_bounds__(256) kpconv_wf_kernel(const float* __restrict_
                     const int64_t v = static_cast<int64_t>(nbr[q * nb + j]);
                     if (v >= 0 && v < n_support) idx = v;  // shadow neighbours contribute zero
                 }
+                if (idx >= 0 && !kp_influences<INFL, CLOSEST>(s_pts[3 * idx] - qx, s_pts[3 * idx + 1] - qy,
+                                                              s_pts[3 * idx + 2] - qz, kq, K, extent, kp_per_query,
+                                                              w[lane]))
+                    idx = -1;  // deformable: out of every kernel point's range
                 ids[lane] = static_cast<int32_t>(idx);
-                if (idx >= 0)
-                    kp_influences<INFL, CLOSEST>(s_pts[3 * idx] - qx, s_pts[3 * idx + 1] - qy, s_pts[3 * idx + 2] - qz,
-                                                 kq, K, extent, w[lane]);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -148,10 +165,11 @@ __global__ void __launch_bounds__(256) kpconv_wf_backward_kernel(const float* __
                     const int64_t v = static_cast<int64_t>(nbr[q * nb + j]);
                     if (v >= 0 && v < n_support) idx = v;
                 }
+                if (idx >= 0 && !kp_influences<INFL, CLOSEST>(s_pts[3 * idx] - qx, s_pts[3 * idx + 1] - qy,
+                                                              s_pts[3 * idx + 2] - qz, kq, K, extent, kp_per_query,
+                                                              w[lane]))
+                    idx = -1;
                 ids[lane] = static_cast<int32_t>(idx);
-                if (idx >= 0)
-                    kp_influences<INFL, CLOSEST>(s_pts[3 * idx] - qx, s_pts[3 * idx + 1] - qy, s_pts[3 * idx + 2] - qz,
-                                                 kq, K, extent, w[lane]);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -172,6 +190,152 @@ __global__ void __launch_bounds__(256) kpconv_wf_backward_kernel(const float* __
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
         }
+    }
+}
+
+// Gradient w.r.t. per-query (deformed) kernel points and modulations
+// (deformable KPConv training, kpconv.py:1005-1159): with A[j][k] =
+// dWF[q][k][:] . x[j][:] (dWF before the modulation),
+//   dkp[q][k] = m[q][k] * sum_j A[j][k] * dw(j,k)/dkp,
+//   dm[q][k]  = sum_j A[j][k] * w(j,k),
+// dw/dkp = diff / (extent * |diff|) (linear, inside the support),
+// w * diff / sigma'^2 (gaussian, sigma'^2 = den / 2), 0 (constant), diff =
+// (p_j - q) - kp_k; closest mode: only each neighbour's nearest kernel point.
+// One wave per query: lanes = neighbours (64 at a time); the query's dWF rows
+// staged per 64-channel block in LDS and read as broadcasts, each lane
+// streaming its neighbour's feature row; sums over neighbours by DPP.
+template <int INFL, bool CLOSEST, class TI>
+__global__ void __launch_bounds__(256) kpconv_kp_grad_kernel(const float* __restrict__ q_pts,
+                                                             const float* __restrict__ s_pts, int64_t n_support,
+                                                             const TI* __restrict__ nbr, int64_t n, int nb,
+                                                             const float* __restrict__ x, int cin,
+                                                             const float* __restrict__ dwf,
+                                                             const float* __restrict__ kp, int K, float extent,
+                                                             const float* __restrict__ modulations,
+                                                             float* __restrict__ dkp, float* __restrict__ dmod) {
+    __shared__ float g_all[4][kKpMaxK][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float(*G)[64] = g_all[wv];
+    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+    for (int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + wv; q < n; q += nwaves) {
+        const float qx = q_pts[3 * q], qy = q_pts[3 * q + 1], qz = q_pts[3 * q + 2];
+        const float* kq = kp + q * K * 3;
+        float gk[kKpMaxK][3], gm[kKpMaxK];
+#pragma unroll
+        for (int k = 0; k < kKpMaxK; ++k) gk[k][0] = gk[k][1] = gk[k][2] = gm[k] = 0.f;
+        for (int j0 = 0; j0 < nb; j0 += 64) {
+            const int j = j0 + lane;
+            int64_t idx = -1;
+            if (j < nb) {
+                const int64_t v = static_cast<int64_t>(nbr[q * nb + j]);
+                if (v >= 0 && v < n_support) idx = v;
+            }
+            float px = 0.f, py = 0.f, pz = 0.f, w[kKpMaxK];
+            if (idx >= 0) {
+                px = s_pts[3 * idx] - qx;
+                py = s_pts[3 * idx + 1] - qy;
+                pz = s_pts[3 * idx + 2] - qz;
+                if (!kp_influences<INFL, CLOSEST>(px, py, pz, kq, K, extent, true, w)) idx = -1;
+            }
+            // A[j][k] = dWF[q][k][:] . x[j][:]
+            float a[kKpMaxK];
+#pragma unroll
+            for (int k = 0; k < kKpMaxK; ++k) a[k] = 0.f;
+            for (int c0 = 0; c0 < cin; c0 += 64) {
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int k = 0; k < kKpMaxK; ++k)
+                    if (k < K) G[k][lane] = c0 + lane < cin ? dwf[(q * K + k) * cin + c0 + lane] : 0.f;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (idx >= 0) {
+                    const float* xr = x + idx * cin;
+                    const int cn = min(64, cin - c0);
+                    for (int cc = 0; cc < cn; ++cc) {
+                        const float xv = xr[c0 + cc];
+#pragma unroll
+                        for (int k = 0; k < kKpMaxK; ++k)
+                            if (k < K) a[k] = __builtin_fmaf(G[k][cc], xv, a[k]);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (idx >= 0) {
+#pragma unroll
+                for (int k = 0; k < kKpMaxK; ++k) {
+                    if (k >= K) continue;
+                    gm[k] = __builtin_fmaf(a[k], w[k], gm[k]);
+                    if constexpr (INFL == 0) continue;
+                    if (CLOSEST && w[k] == 0.f) continue;  // not this neighbour's closest kernel point
+                    const float ex = px - kq[3 * k], ey = py - kq[3 * k + 1], ez = pz - kq[3 * k + 2];
+                    float f;
+                    if constexpr (INFL == 1) {
+                        const float d = sqrtf(ex * ex + ey * ey + ez * ez);
+                        f = (d > 0.f && d < extent) ? a[k] / (extent * d) : 0.f;
+                    } else {
+                        f = a[k] * w[k] * 2.f / kp_gauss_den(extent);
+                    }
+                    gk[k][0] = __builtin_fmaf(f, ex, gk[k][0]);
+                    gk[k][1] = __builtin_fmaf(f, ey, gk[k][1]);
+                    gk[k][2] = __builtin_fmaf(f, ez, gk[k][2]);
+                }
+            }
+        }
+        // sums over the 64 lanes (neighbours)
+#pragma unroll
+        for (int k = 0; k < kKpMaxK; ++k) {
+            if (k >= K) continue;
+            float v0 = gk[k][0], v1 = gk[k][1], v2 = gk[k][2], v3 = gm[k];
+            for (int o = 32; o >= 1; o >>= 1) {
+                v0 += __shfl_xor(v0, o, 64);
+                v1 += __shfl_xor(v1, o, 64);
+                v2 += __shfl_xor(v2, o, 64);
+                v3 += __shfl_xor(v3, o, 64);
+            }
+            if (lane == 0) {
+                const float m = modulations ? modulations[q * K + k] : 1.f;
+                dkp[(q * K + k) * 3] = m * v0;
+                dkp[(q * K + k) * 3 + 1] = m * v1;
+                dkp[(q * K + k) * 3 + 2] = m * v2;
+                if (dmod) dmod[q * K + k] = v3;
+            }
+        }
+    }
+}
+
+// min_d2 of the deformable reference (kpconv.py:1071): for every (query,
+// kernel point) the neighbour column with the smallest squared distance to
+// the kernel point, shadow neighbours at (1e6, 1e6, 1e6) included; the first
+// minimum wins.  The caller recomputes the distance from that column with
+// torch ops, so the fitting loss differentiates into the kernel points.
+template <class TI>
+__global__ void kpconv_min_d2_kernel(const float* __restrict__ q_pts, const float* __restrict__ s_pts,
+                                     int64_t n_support, const TI* __restrict__ nbr, int64_t n, int nb,
+                                     const float* __restrict__ kp, int K, int32_t* __restrict__ col) {
+    const int64_t total = n * K;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t q = e / K;
+        const float kx = kp[3 * e], ky = kp[3 * e + 1], kz = kp[3 * e + 2];
+        const float qx = q_pts[3 * q], qy = q_pts[3 * q + 1], qz = q_pts[3 * q + 2];
+        float best = INFINITY;
+        int bj = 0;
+        for (int j = 0; j < nb; ++j) {
+            const int64_t v = static_cast<int64_t>(nbr[q * nb + j]);
+            const bool real = v >= 0 && v < n_support;
+            const float px = (real ? s_pts[3 * v] : 1e6f) - qx, py = (real ? s_pts[3 * v + 1] : 1e6f) - qy,
+                        pz = (real ? s_pts[3 * v + 2] : 1e6f) - qz;
+            const float ex = px - kx, ey = py - ky, ez = pz - kz;
+            const float d2 = ex * ex + ey * ey + ez * ez;
+            if (d2 < best) {
+                best = d2;
+                bj = j;
+            }
+        }
+        col[e] = bj;
     }
 }
 
@@ -284,6 +448,57 @@ O3DML_API int o3dml_kpconv_weighted_features_backward(const float* q_pts, int64_
     else
         launch_kp<true, int64_t>(influence, closest, g, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
                                  grad_wf, cin, kernel_points, K, kp_per_query, extent, nullptr, grad_features);
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_kpconv_kernel_point_grad(const float* q_pts, int64_t n, const float* s_pts, int64_t n_support,
+                                             const void* neighbors, int index_bits, int nb, const float* features,
+                                             int cin, const float* grad_wf, const float* kernel_points, int K,
+                                             float extent, int influence, int closest, const float* modulations,
+                                             float* grad_kp, float* grad_mod, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(K >= 1 && K <= kKpMaxK, "KPConv: kernel points must be in [1, %d]", kKpMaxK);
+    O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
+    O3DML_REQUIRE(influence >= 0 && influence <= 2, "KPConv: influence must be constant, linear or gaussian");
+    if (n == 0) return 0;
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n, 4), 1 << 20));
+    hipStream_t st = as_stream(stream);
+#define O3DML_KPG(I, C, T)                                                                                       \
+    kpconv_kp_grad_kernel<I, C, T><<<g, 256, 0, st>>>(q_pts, s_pts, n_support, static_cast<const T*>(neighbors), \
+                                                      n, nb, features, cin, grad_wf, kernel_points, K, extent,   \
+                                                      modulations, grad_kp, grad_mod)
+#define O3DML_KPG_T(I, C)                                        \
+    do {                                                         \
+        if (index_bits == 32) O3DML_KPG(I, C, int32_t);          \
+        else O3DML_KPG(I, C, int64_t);                           \
+    } while (0)
+    if (influence == 0) {
+        if (closest) O3DML_KPG_T(0, true); else O3DML_KPG_T(0, false);
+    } else if (influence == 1) {
+        if (closest) O3DML_KPG_T(1, true); else O3DML_KPG_T(1, false);
+    } else {
+        if (closest) O3DML_KPG_T(2, true); else O3DML_KPG_T(2, false);
+    }
+#undef O3DML_KPG_T
+#undef O3DML_KPG
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_kpconv_min_d2_columns(const float* q_pts, int64_t n, const float* s_pts, int64_t n_support,
+                                          const void* neighbors, int index_bits, int nb, const float* kernel_points,
+                                          int K, int32_t* columns, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
+    if (n == 0) return 0;
+    const unsigned g = stream_grid(n * K, 256);
+    if (index_bits == 32)
+        kpconv_min_d2_kernel<int32_t><<<g, 256, 0, as_stream(stream)>>>(
+                q_pts, s_pts, n_support, static_cast<const int32_t*>(neighbors), n, nb, kernel_points, K, columns);
+    else
+        kpconv_min_d2_kernel<int64_t><<<g, 256, 0, as_stream(stream)>>>(
+                q_pts, s_pts, n_support, static_cast<const int64_t*>(neighbors), n, nb, kernel_points, K, columns);
+    O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }
 

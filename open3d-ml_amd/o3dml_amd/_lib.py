@@ -73,6 +73,9 @@ SIGNATURES = {
                                                c_i32, c_f32, c_i32, c_i32, c_p, c_p, c_p]),
     "o3dml_kpconv_weighted_features_backward": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p,
                                                         c_i32, c_i32, c_f32, c_i32, c_i32, c_p, c_p]),
+    "o3dml_kpconv_kernel_point_grad": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p,
+                                               c_i32, c_f32, c_i32, c_i32, c_p, c_p, c_p, c_p]),
+    "o3dml_kpconv_min_d2_columns": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p]),
     "o3dml_kpconv_pool_max": (c_i32, [c_p, c_i64, c_i32, c_p, c_i32, c_i64, c_i64, c_i32, c_p, c_p, c_p]),
     "o3dml_kpconv_pool_max_backward": (c_i32, [c_p, c_p, c_i64, c_i32, c_i64, c_p, c_p]),
     "o3dml_pillar_features": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32,

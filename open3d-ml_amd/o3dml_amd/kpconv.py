@@ -9,8 +9,10 @@ influences of every (neighbour, kernel point) + weighted feature sums, with
 shadow neighbours skipped) followed by one dense GEMM
 [n, K*Cin] @ [K*Cin, Cout].  Gradients flow to the features and the weights
 (feature gradient by the fused backward kernel with fp32 atomics); the
-kernel-point positions are constants, as in the reference (requires_grad
-False); deformable offsets are inference-only here.
+shared kernel-point positions are constants, as in the reference
+(requires_grad False); deformable convolutions train end to end: the HIP
+kernel-point / modulation gradient (o3dml_kpconv_kernel_point_grad) flows
+into the offset convolution, and min_d2 feeds p2p_fitting_regularizer.
 """
 import math
 
@@ -31,44 +33,82 @@ class _WeightedFeatures(torch.autograd.Function):
         K = kp.shape[-2]
         cin = x.shape[1]
         out = torch.empty((n, K, cin), dtype=torch.float32, device=x.device)
+        kpd = kp.detach().contiguous()
+        mod = None if modulations is None else modulations.detach().contiguous()
         _lib.call("o3dml_kpconv_weighted_features", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr),
-                  index_bits(nbr.dtype), nb, ptr(x), cin, ptr(kp), K, int(kp_per_query), float(extent), influence,
-                  int(closest), ptr(modulations), ptr(out), stream_handle(x.device))
-        ctx.save_for_backward(q_pts, s_pts, nbr, kp)
-        ctx.meta = (kp_per_query, extent, influence, closest, x.shape[0], cin)
+                  index_bits(nbr.dtype), nb, ptr(x), cin, ptr(kpd), K, int(kp_per_query), float(extent), influence,
+                  int(closest), ptr(mod), ptr(out), stream_handle(x.device))
+        ctx.save_for_backward(x, q_pts, s_pts, nbr, kpd, mod if mod is not None else torch.empty(0, device=x.device))
+        ctx.meta = (kp_per_query, extent, influence, closest, x.shape[0], cin, mod is not None)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        q_pts, s_pts, nbr, kp = ctx.saved_tensors
-        kp_per_query, extent, influence, closest, n_s, cin = ctx.meta
+        x, q_pts, s_pts, nbr, kp, mod = ctx.saved_tensors
+        kp_per_query, extent, influence, closest, n_s, cin, has_mod = ctx.meta
         n, nb = nbr.shape
-        dx = torch.zeros((n_s, cin), dtype=torch.float32, device=g.device)
-        _lib.call("o3dml_kpconv_weighted_features_backward", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr),
-                  index_bits(nbr.dtype), nb, ptr(g.contiguous()), cin, ptr(kp), kp.shape[-2], int(kp_per_query),
-                  float(extent), influence, int(closest), ptr(dx), stream_handle(g.device))
-        return dx, None, None, None, None, None, None, None, None, None
+        K = kp.shape[-2]
+        g = g.contiguous()
+        dx = dkp = dmod = None
+        if ctx.needs_input_grad[0]:
+            gm = g * mod[:, :, None] if has_mod else g  # the modulation scales dWF (kpconv.py:1149-1150)
+            dx = torch.zeros((n_s, cin), dtype=torch.float32, device=g.device)
+            _lib.call("o3dml_kpconv_weighted_features_backward", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr),
+                      index_bits(nbr.dtype), nb, ptr(gm.contiguous()), cin, ptr(kp), K, int(kp_per_query),
+                      float(extent), influence, int(closest), ptr(dx), stream_handle(g.device))
+        if ctx.needs_input_grad[4] or (has_mod and ctx.needs_input_grad[9]):
+            if not kp_per_query:
+                raise NotImplementedError("KPConv: gradients w.r.t. shared (non-deformed) kernel points")
+            dkp = torch.empty((n, K, 3), dtype=torch.float32, device=g.device)
+            dm = torch.empty((n, K), dtype=torch.float32, device=g.device) if has_mod else None
+            _lib.call("o3dml_kpconv_kernel_point_grad", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr),
+                      index_bits(nbr.dtype), nb, ptr(x), cin, ptr(g), ptr(kp), K, float(extent), influence,
+                      int(closest), ptr(mod) if has_mod else None, ptr(dkp), ptr(dm), stream_handle(g.device))
+            dmod = dm
+        return dx, None, None, None, dkp, None, None, None, None, dmod
+
+
+def min_d2(q_pts, s_pts, neighb_inds, kernel_points):
+    """The deformable reference's min_d2 [n, K] (kpconv.py:1071): squared
+    distance from each (deformed) kernel point to its nearest neighbour, the
+    shadow neighbour at 1e6 included.  The nearest column comes from the HIP
+    kernel; the distance is recomputed with torch ops so p2p_fitting_regularizer
+    differentiates into the kernel points (kpconv.py:2167-2209)."""
+    dev = kernel_points.device
+    nbr = neighb_inds if neighb_inds.dtype in (torch.int32, torch.int64) else neighb_inds.long()
+    n, nb = nbr.shape
+    K = kernel_points.shape[-2]
+    col = torch.empty((n, K), dtype=torch.int32, device=dev)
+    _lib.call("o3dml_kpconv_min_d2_columns", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr.contiguous()),
+              index_bits(nbr.dtype), nb, ptr(kernel_points.detach().contiguous()), K, ptr(col),
+              stream_handle(dev))
+    s_ext = torch.cat((s_pts, torch.zeros_like(s_pts[:1, :]) + 1e6), 0)
+    ids = torch.gather(nbr.long(), 1, col.long()).clamp_(0, s_pts.shape[0])
+    nbp = s_ext[ids] - q_pts.unsqueeze(1)  # [n, K, 3]
+    return torch.sum((nbp - kernel_points) ** 2, dim=2)
 
 
 def weighted_features(q_pts, s_pts, neighb_inds, x, kernel_points, extent, influence="linear",
                       aggregation_mode="sum", modulations=None):
     """WF[n, k, :] = sum_j influence(|s_j - q_n - kp_k|) * x[j] over the neighbours
     of q_n (shadow index = len(s_pts) contributes zero): kpconv.py:1046-1145.
-    kernel_points [K, 3] or per-query [n, K, 3]; modulations [n, K] or None."""
+    kernel_points [K, 3] or per-query [n, K, 3] (deformable: differentiable,
+    out-of-range neighbours dropped as the reference's filter does);
+    modulations [n, K] or None (differentiable)."""
     dev = gpu_device(x)
     if influence not in _INFLUENCE:
         raise ValueError("Unknown influence function type (config.KP_influence)")
     if aggregation_mode not in ("sum", "closest"):
         raise ValueError("Unknown convolution mode. Should be 'closest' or 'sum'")
-    if kernel_points.requires_grad or (modulations is not None and modulations.requires_grad):
-        raise NotImplementedError("KPConv: gradients w.r.t. kernel points / modulations are not supported")
+    if kernel_points.requires_grad and kernel_points.dim() != 3:
+        raise NotImplementedError("KPConv: gradients w.r.t. shared (non-deformed) kernel points are not supported")
     qp = to_dev(q_pts, dev, torch.float32)
     sp = to_dev(s_pts, dev, torch.float32)
     nbr = to_dev(neighb_inds, dev)
     if nbr.dtype not in (torch.int32, torch.int64):
         nbr = nbr.long()
-    kp = to_dev(kernel_points.detach(), dev, torch.float32)
-    mod = None if modulations is None else to_dev(modulations.detach(), dev, torch.float32)
+    kp = kernel_points.to(dev).float()
+    mod = None if modulations is None else modulations.to(dev).float()
     xx = x if x.is_cuda else x.to(dev)
     return _WeightedFeatures.apply(xx.float().contiguous(), qp, sp, nbr.contiguous(), kp, kp.dim() == 3,
                                    float(extent), _INFLUENCE[influence], aggregation_mode == "closest", mod)
@@ -141,7 +181,9 @@ class KPConv(nn.Module):
             else:
                 unscaled = self.offset_features.view(-1, self.K, self.p_dim)
             self.deformed_KP = unscaled * self.KP_extent + self.kernel_points
-            kp = self.deformed_KP.contiguous()
+            kp = self.deformed_KP
+            # distances kept for p2p_fitting_regularizer (kpconv.py:1071)
+            self.min_d2 = min_d2(q_pts, s_pts, neighb_inds, kp)
         wf = weighted_features(q_pts, s_pts, neighb_inds, x, kp, self.KP_extent, self.KP_influence,
                                self.aggregation_mode, modulations)
         n = wf.shape[0]

@@ -348,10 +348,16 @@ class KPFCNN(nn.Module):
         return self.head_softmax(x, batch)
 
     def get_loss(self, logits, labels, class_weights=None):
-        """Cross entropy over the valid labels (kpconv.py:315-351; deformable
-        regularisation is zero for the rigid architectures)."""
-        if any(isinstance(m, KPConv) and m.deformable for m in self.modules()):
-            raise NotImplementedError("KPFCNN.get_loss: deformable fitting regularisation is not supported")
+        """Cross entropy over the valid labels + the point-to-point fitting
+        regulariser of the deformable KPConvs (kpconv.py:315-351; zero for the
+        rigid architectures).  The parts are kept as output_loss / reg_loss."""
+        self.output_loss = self._ce(logits, labels, class_weights)
+        if self.deform_fitting_mode != "point2point":
+            raise ValueError("Unknown fitting mode: " + str(self.deform_fitting_mode))
+        self.reg_loss = p2p_fitting_regularizer(self)
+        return self.output_loss + self.reg_loss
+
+    def _ce(self, logits, labels, class_weights=None):
         labels = labels.to(logits.device).long()
         valid = torch.ones_like(labels, dtype=torch.bool)
         for ign in self.cfg.ignored_label_inds:
@@ -362,6 +368,29 @@ class KPFCNN(nn.Module):
         w = None if class_weights is None else torch.as_tensor(class_weights, dtype=torch.float32,
                                                                device=logits.device)
         return F.cross_entropy(logits[valid], lut[labels[valid]], weight=w)
+
+
+def p2p_fitting_regularizer(net):
+    """kpconv.py:2167-2209: for every deformable KPConv, the L1 mean of the
+    normalised squared distance from each deformed kernel point to its nearest
+    input point (fitting) and a repulsion between the normalised kernel points
+    of one query (other points detached); deform_fitting_power * (2 * fitting
+    + repulsive).  min_d2 / deformed_KP come from the last forward
+    (kpconv.min_d2: the distances differentiate into the kernel points)."""
+    fitting = 0
+    repulsive = 0
+    l1 = torch.nn.functional.l1_loss
+    for m in net.modules():
+        if isinstance(m, KPConv) and m.deformable:
+            kp_min_d2 = m.min_d2 / (m.KP_extent ** 2)
+            fitting = fitting + l1(kp_min_d2, torch.zeros_like(kp_min_d2))
+            locs = m.deformed_KP / m.KP_extent
+            for i in range(net.K):
+                other = torch.cat([locs[:, :i, :], locs[:, i + 1:, :]], dim=1).detach()
+                dist = torch.sqrt(torch.sum((other - locs[:, i:i + 1, :]) ** 2, dim=2))
+                rep = torch.sum(torch.clamp_max(dist - net.repulse_extent, max=0.0) ** 2, dim=1)
+                repulsive = repulsive + l1(rep, torch.zeros_like(rep)) / net.K
+    return net.deform_fitting_power * (2 * fitting + repulsive)
 
 
 # ---------------------------------------------------------------------------

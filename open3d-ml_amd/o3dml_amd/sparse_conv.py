@@ -127,32 +127,38 @@ class _DuplicateKernelIndex(Exception):
 
 def _conv_layers(f, x, b, nidx, kidx, nimp, rs, sscale, normalize, oimp, K):
     """Open3D sums EVERY (neighbour, kernel index) pair of an output; the dense
-    kernel map holds one input per (output, kernel index).  Pairs that share
-    (output, kernel index) — layers.SparseConv on positions off one voxel
-    lattice — are split into layers by their rank within that (output, k)
-    group, in CSR order: layer l holds the l-th pair of every group, so each
-    layer is a valid dense map.  out = sum of the layers' HIP GEMMs (each with
-    its own autograd node), then the per-output normalisation / importance
-    over ALL the output's pairs.  Index bookkeeping only in torch."""
+    kernel map holds one input per (output, kernel index) and its inverse (the
+    input gradient) one output per (input, kernel index).  Off one voxel
+    lattice (layers.SparseConv on arbitrary positions) pairs share those, so
+    the pairs are split into layers, each a valid pair of maps: every round
+    takes each remaining pair that comes first (in CSR order) among the
+    remaining pairs of its (output, k) AND of its (input, k) — a matching,
+    never empty (the first remaining pair qualifies).  out = sum of the
+    layers' HIP GEMMs (each its own autograd node), then the per-output
+    normalisation / importance over ALL the output's pairs.  Index
+    bookkeeping only in torch."""
     dev = x.device
     n_out = rs.shape[0] - 1
+    n_in = x.shape[0]
     P = nidx.shape[0]
     counts = rs[1:] - rs[:-1]
     o = torch.repeat_interleave(torch.arange(n_out, device=dev), counts)
-    key = o * K + kidx.long()
-    order = torch.sort(key, stable=True).indices
-    sk = key[order]
+    ko = o * K + kidx.long()
+    ki = nidx.long() * K + kidx.long()
     pos = torch.arange(P, device=dev)
-    start = torch.ones(P, dtype=torch.bool, device=dev)
-    start[1:] = sk[1:] != sk[:-1]
-    first = torch.cummax(torch.where(start, pos, torch.zeros_like(pos)), 0).values
-    rank = torch.empty(P, dtype=torch.int64, device=dev)
-    rank[order] = pos - first
-    n_layers = int(rank.max().item()) + 1
+    left = torch.ones(P, dtype=torch.bool, device=dev)
+    big = torch.iinfo(torch.int64).max
+    layers = []
+    while bool(left.any()):
+        p_left = torch.where(left, pos, torch.full_like(pos, big))
+        m_o = torch.full((n_out * K,), big, dtype=torch.int64, device=dev).scatter_reduce_(0, ko, p_left, "amin")
+        m_i = torch.full((n_in * K,), big, dtype=torch.int64, device=dev).scatter_reduce_(0, ki, p_left, "amin")
+        take = left & (m_o[ko] == pos) & (m_i[ki] == pos)
+        layers.append(torch.nonzero(take).squeeze(1))  # CSR order kept: rows stay grouped by output
+        left &= ~take
     want_grad = torch.is_grad_enabled() and (f.requires_grad or x.requires_grad or (b is not None and b.requires_grad))
     out = None
-    for layer in range(n_layers):
-        sel = torch.nonzero(rank == layer).squeeze(1)  # CSR order kept: rows stay grouped by output
+    for layer, sel in enumerate(layers):
         c = torch.bincount(o[sel], minlength=n_out)
         lrs = torch.zeros(n_out + 1, dtype=torch.int64, device=dev)
         lrs[1:] = torch.cumsum(c, 0)

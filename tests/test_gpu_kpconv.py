@@ -106,3 +106,83 @@ def test_kpconv_deformable_modulated_forward(cuda):
     ref_off = _ref(q, s, nbr, x, kp, 0.06, conv.offset_conv.weights.detach().double().cpu()) + \
         conv.offset_bias.detach().double().cpu()
     _close(off, ref_off)
+
+
+def _ref_deformable(q, s, nbr, x, conv, extent, influence, mode, modulated):
+    """The deformable reference forward (kpconv.py:1005-1159) in float64: the
+    rigid offset KPConv, offsets * extent + kernel points, the in-range filter
+    (a neighbour with no deformed kernel point within extent is dropped),
+    modulations 2 sigmoid(.), and min_d2 (shadow point at 1e6 included)."""
+    K = conv.K
+    kp = conv.kernel_points.detach().double().cpu()
+    Wo = conv.offset_conv.weights.detach().double().cpu().requires_grad_(True)
+    bo = conv.offset_bias.detach().double().cpu().requires_grad_(True)
+    W = conv.weights.detach().double().cpu().requires_grad_(True)
+    off = _ref(q, s, nbr, x, kp, extent, Wo, influence, mode) + bo
+    if modulated:
+        unscaled = off[:, :3 * K].view(-1, K, 3)
+        mod = 2 * torch.sigmoid(off[:, 3 * K:])
+    else:
+        unscaled, mod = off.view(-1, K, 3), None
+    dkp = unscaled * extent + kp
+    s1 = torch.cat([s, torch.zeros_like(s[:1]) + 1e6], 0)
+    nb = s1[nbr] - q[:, None, :]
+    d2 = ((nb[:, :, None, :] - dkp[:, None, :, :]) ** 2).sum(3)
+    min_d2 = d2.min(1).values
+    in_range = (d2 < extent ** 2).any(2)
+    if influence == "constant":
+        w = torch.ones_like(d2)
+    elif influence == "linear":
+        w = torch.clamp(1 - torch.sqrt(d2) / extent, min=0.0)
+    else:
+        w = torch.exp(-d2 / (2 * (0.3 * extent) ** 2 + 1e-9))
+    w = w * in_range[:, :, None]
+    if mode == "closest":
+        w = w * torch.nn.functional.one_hot(torch.argmin(d2, 2), K)
+    xx = torch.cat([x, torch.zeros_like(x[:1])], 0)
+    wf = torch.matmul(w.transpose(1, 2), xx[nbr])
+    if mod is not None:
+        wf = wf * mod[:, :, None]
+    out = torch.matmul(wf.permute(1, 0, 2), W).sum(0)
+    return out, min_d2, dkp, (W, Wo, bo)
+
+
+@pytest.mark.parametrize("influence,mode,modulated", [("linear", "sum", False), ("linear", "sum", True),
+                                                      ("gaussian", "sum", False), ("linear", "closest", False)])
+def test_deformable_kpconv_training(cuda, influence, mode, modulated):
+    """Deformable KPConv trains end to end: gradients of
+    sum(out * g) + the p2p fitting regulariser w.r.t. the weights, the offset
+    KPConv's weights and the offset bias against the float64 restatement of
+    the reference; min_d2 and the deformed kernel points as well."""
+    from o3dml_amd import kpfcnn
+    from o3dml_amd.kpconv import KPConv
+    q, s, nbr, x = _data(n=500, ns=800, nb=40, cin=16, seed=7)
+    torch.manual_seed(1)
+    conv = KPConv(15, 3, 16, 24, KP_extent=0.06, radius=0.1, KP_influence=influence, aggregation_mode=mode,
+                  deformable=True, modulated=modulated).to(cuda)
+    with torch.no_grad():  # offsets of a useful size (the reference initialises the offset weights to 0)
+        conv.offset_conv.weights.normal_(0, 0.05)
+        conv.offset_bias.normal_(0, 0.1)
+    out = conv(q.float().to(cuda), s.float().to(cuda), nbr.to(cuda), x.float().to(cuda))
+    ref, ref_min_d2, ref_dkp, (W, Wo, bo) = _ref_deformable(q, s, nbr, x, conv, 0.06, influence, mode, modulated)
+    _close(out, ref)
+    _close(conv.deformed_KP, ref_dkp)
+    _close(conv.min_d2, ref_min_d2)
+    g = torch.randn(out.shape, generator=torch.Generator().manual_seed(2), dtype=torch.float64)
+    net = type("Net", (), {})()
+    net.modules = lambda: [conv]
+    net.K, net.repulse_extent, net.deform_fitting_power = 15, 1.2, 1.0
+    loss = (out * g.float().to(cuda)).sum() + kpfcnn.p2p_fitting_regularizer(net)
+    loss.backward()
+    # the same regulariser on the float64 reference
+    reg = 2 * torch.nn.functional.l1_loss(ref_min_d2 / 0.06 ** 2, torch.zeros_like(ref_min_d2))
+    locs = ref_dkp / 0.06
+    for i in range(15):
+        other = torch.cat([locs[:, :i, :], locs[:, i + 1:, :]], dim=1).detach()
+        dist = torch.sqrt(torch.sum((other - locs[:, i:i + 1, :]) ** 2, dim=2))
+        rep = torch.sum(torch.clamp_max(dist - 1.2, max=0.0) ** 2, dim=1)
+        reg = reg + torch.nn.functional.l1_loss(rep, torch.zeros_like(rep)) / 15
+    ((ref * g).sum() + reg).backward()
+    _close(conv.weights.grad, W.grad)
+    _close(conv.offset_conv.weights.grad, Wo.grad, rtol=1e-3)
+    _close(conv.offset_bias.grad, bo.grad, rtol=1e-3)
