@@ -14,7 +14,9 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+# O3DML_ORACLE_LIB selects another build of the same source (the sanitizer
+# build `make -C oracle asan`, tests/test_sanitizers.py)
+_LIB_PATH = os.environ.get("O3DML_ORACLE_LIB", os.path.join(_HERE, "_build", "liboracle.so"))
 _lib = None
 
 METRICS = {"L1": 0, "L2": 1, "Linf": 2}

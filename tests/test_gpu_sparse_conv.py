@@ -249,7 +249,9 @@ def test_duplicate_kernel_indices(cuda, normalize, importance):
     o = np.repeat(np.arange(len(rs) - 1), np.diff(rs))
     assert len(np.unique(o * 27 + kid)) < len(kid)  # duplicates present
     x = torch.randn((1500, 8), device=cuda, requires_grad=True)
-    nimp = torch.rand(len(idx), device=cuda) if importance else None
+    # per-input-point importance, gathered per pair (the layer's inp_importance)
+    pimp = torch.rand(1500, device=cuda) if importance else None
+    nimp = pimp[nb.neighbors_index.long()] if importance else None
     W = conv.kernel
     out = ops.sparse_conv(W, x, None, nb.neighbors_index, kidx, nimp, nb.neighbors_row_splits,
                           normalize=normalize) + conv.bias
@@ -258,7 +260,10 @@ def test_duplicate_kernel_indices(cuda, normalize, importance):
                         normalize=normalize) + conv.bias.detach().cpu().numpy()
     _close(out.detach().cpu().numpy(), ref)
     # the layer path (bias in the epilogue, normalisation after the layer sum)
-    _close(conv(x, inp, inp, 1.0).detach().cpu().numpy(), ref)
+    ref_l = ref if not importance else O.sparse_conv(
+        W.detach().cpu().numpy(), x.detach().cpu().numpy(), idx, kid, rs, inp_importance=pimp.cpu().numpy(),
+        normalize=normalize) + conv.bias.detach().cpu().numpy()
+    _close(conv(x, inp, inp, 1.0, inp_importance=pimp).detach().cpu().numpy(), ref_l)
     go = torch.randn_like(out)
     gW, gx = torch.autograd.grad(out, (W, x), go)
     W64 = W.detach().cpu().double().requires_grad_(True)
