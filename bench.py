@@ -203,7 +203,7 @@ def make_scan(seed):
     return pts, rng.integers(0, 20, pts.shape[0]).astype(np.int32)
 
 
-def randla_frames(dev, frames):
+def randla_frames(dev, frames, cpu=False):
     """RandLA-Net GPU inference (SemSegInference, randlanet_semantickitti.yml:
     45,056-pt patches, k=16, 4 layers, grid 0.06, random-init weights) on C2
     scans: one frame = the full possibility loop until every sub-point > 0.5."""
@@ -221,10 +221,78 @@ def randla_frames(dev, frames):
         patches += inf.stats["patches"]
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t
-    return {"frames_per_s": round(frames / dt, 3), "ms_per_frame": round(dt / frames * 1e3, 2),
-            "patches_per_frame": round(patches / frames, 2), "frames": frames,
-            "config": "C2: 120,000-pt synthetic 64-beam scan, RandLANet semantickitti cfg, fp32, random init",
-            "cpu_reference_s_per_frame_8cores_survey": 10.6}
+    out = {"frames_per_s": round(frames / dt, 3), "ms_per_frame": round(dt / frames * 1e3, 2),
+           "patches_per_frame": round(patches / frames, 2), "frames": frames,
+           "config": "C2: 120,000-pt synthetic 64-beam scan, RandLANet semantickitti cfg, fp32, random init",
+           "cpu_reference_s_per_frame_8cores_survey": 10.6}
+    if cpu:
+        out["cpu_baseline"] = randla_cpu_baseline(model, make_scan(0)[0], patches / frames)
+        out["cpu_baseline"]["gpu_speedup"] = round(out["cpu_baseline"]["value"] / (dt / frames), 1)
+    return out
+
+
+def randla_cpu_baseline(model, scan, patches_per_frame, max_patches=3, budget_s=20.0):
+    """Measured CPU leg of C2 on this host (the reference's
+    run_inference on CPU: semseg_spatially_regular.py:79-109, randlanet.py:
+    115-239, 441-465): the same RandLANet weights through the model's torch
+    path on torch.get_num_threads() cores, grid subsampling by the C oracle
+    (OpenMP), every kNN by scipy's cKDTree (workers=-1; the reference uses
+    sklearn's KDTree for the crop / projection and nanoflann for the k = 16
+    lists).  Sample: the frame set-up (subsample + 1-NN projection) plus up to
+    3 whole patches (crop, shuffle, possibility update, 4-level kNN, forward,
+    softmax, float16 EMA); s/frame = set-up + patches_per_frame (measured on
+    the GPU run of the same config) x mean patch time."""
+    import oracle as O
+    from scipy.spatial import cKDTree
+    from o3dml_amd.randlanet import RandLANet
+    cpu_model = RandLANet(num_points=45056, num_classes=19)
+    cpu_model.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    cpu_model.eval()
+    for prm in cpu_model.parameters():
+        prm.requires_grad_(False)
+    cfg = cpu_model.cfg
+    n_pts, k, L = cfg["num_points"], cfg["num_neighbors"], cfg["num_layers"]
+    t0 = time.perf_counter()
+    sub = O.subsample(scan, sampleDl=cfg["grid_size"])
+    tree = cKDTree(sub)
+    tree.query(scan, k=1, workers=-1)  # projection of the raw points
+    t_setup = time.perf_counter() - t0
+    rng = np.random.default_rng(0)
+    poss = rng.random(len(sub)) * 1e-3
+    probs16 = np.zeros((len(sub), cfg["num_classes"]), np.float16)
+    times = []
+    while len(times) < max_patches and (not times or sum(times) < budget_s):
+        t = time.perf_counter()
+        cid = int(np.argmin(poss))
+        center = sub[cid]
+        idx = tree.query(center[None], k=min(n_pts, len(sub)), workers=-1)[1][0]
+        rng.shuffle(idx)
+        pc = sub[idx].astype(np.float32)
+        d = np.sum(np.square(pc - center), 1)
+        poss[idx] += np.square(1 - d / np.max(d))
+        pc[:, :2] -= center[:2]
+        coords, nbrs, subs, ups = [], [], [], []
+        cur = pc
+        for i in range(L):
+            nb = cKDTree(cur).query(cur, k=k, workers=-1)[1]
+            nxt = cur[: cur.shape[0] // cfg["sub_sampling_ratio"][i]]
+            coords.append(torch.from_numpy(cur)[None])
+            nbrs.append(torch.from_numpy(nb)[None])
+            subs.append(torch.from_numpy(nb[: nxt.shape[0]])[None])
+            ups.append(torch.from_numpy(cKDTree(nxt).query(cur, k=1, workers=-1)[1].reshape(-1, 1))[None])
+            cur = nxt
+        inputs = {"features": torch.from_numpy(pc)[None], "coords": coords + [torch.from_numpy(cur)[None]],
+                  "neighbor_indices": nbrs, "sub_idx": subs, "interp_idx": ups}
+        with torch.enable_grad():  # the torch (non-fused) path; no parameter requires grad
+            logits = cpu_model(inputs)[0]
+        p = torch.softmax(logits, -1).numpy()
+        probs16[idx] = probs16[idx] * np.float16(0.95) + np.float32(0.05) * p
+        times.append(time.perf_counter() - t)
+    t_patch = float(np.mean(times))
+    return {"value": round(t_setup + patches_per_frame * t_patch, 3), "unit": "s/frame",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"frame set-up + {len(times)} patches of 45,056 pts ({t_patch:.2f} s each, set-up "
+                      f"{t_setup:.2f} s) x {patches_per_frame:.2f} patches/frame"}
 
 
 def make_c3(seed=0, n=20000):
@@ -641,7 +709,7 @@ def run(args):
         if world == 1 and args.kpconv_steps > 0:
             out["kpconv"] = kpconv_bench(dev, args.kpconv_steps)
         if world == 1 and args.randla_frames > 0:
-            out["randlanet"] = randla_frames(dev, args.randla_frames)
+            out["randlanet"] = randla_frames(dev, args.randla_frames, cpu=not args.no_cpu_baseline)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -279,6 +279,12 @@ int o3dml_three_interpolate(const float* features, const int32_t* idx, const flo
                             int64_t m, int64_t n, float* out, void* stream);
 int o3dml_three_interpolate_grad(const float* grad_out, const int32_t* idx, const float* weight, int64_t B, int64_t C,
                                  int64_t n, int64_t m, float* grad_features, void* stream);
+/* deterministic three_interpolate_grad: fixed summation order (pairs grouped
+ * by source point with a stable radix sort); grad_features fully written */
+size_t o3dml_three_interpolate_grad_workspace_size(int64_t B, int64_t n, int64_t m);
+int o3dml_three_interpolate_grad_det(const float* grad_out, const int32_t* idx, const float* weight, int64_t B,
+                                     int64_t C, int64_t n, int64_t m, float* grad_features, void* workspace,
+                                     size_t workspace_bytes, void* stream);
 
 /* ---- rotated BEV NMS: replaces open3d.ml.torch.ops.nms
  * (ml3d/torch/utils/objdet_helper.py:27, called by multiclass_nms :346 from
@@ -310,7 +316,7 @@ int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const int32_t* n
                                 int* status_host, void* workspace, size_t workspace_bytes, void* stream);
 /* split-K partial sums for the forward GEMM (deep levels with few output
  * rows split the offset x Cin reduction across waves; 0 when unsplit) */
-size_t o3dml_sparse_conv_forward_workspace_size(int64_t n_out, int K, int cin, int cout);
+size_t o3dml_sparse_conv_forward_workspace_size(int64_t n_out, int64_t n_in, int K, int cin, int cout);
 int o3dml_sparse_conv_forward(const float* filters, int K, int cin, int cout, const float* inp_features, int64_t n_in,
                               const float* inp_importance, int has_neighbors_importance, int use_out_scale,
                               const float* bias, int64_t n_out, float* out_features, void* map_workspace,
@@ -342,6 +348,13 @@ int o3dml_sparse_conv_backward(const float* filters, int K, int cin, int cout, c
  * Env O3DML_SPARSE_CONV_EXACT sets the initial mode.  Returns the previous
  * mode (-1 for a mode > 2, nothing changed); exact < 0 only queries. */
 int o3dml_sparse_conv_set_exact(int exact);
+/* Operand presplit for the bf16x6 / bf16x3 products (default OFF, measured
+ * slower on MI355X; see sparse_conv.hip): the hi /
+ * mid / lo bf16 planes of the source rows and filters are made once per GEMM
+ * (workspace from the *_workspace_size functions) and the GEMM kernel only
+ * loads them; the sums are bit-identical to the in-kernel split.  on = 0 / 1
+ * sets, < 0 queries; returns the previous setting. */
+int o3dml_sparse_conv_set_presplit(int on);
 int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* query_positions,
                                    const int32_t* neighbors_index, const int64_t* neighbors_row_splits,
                                    int64_t n_query, const int32_t* ksize_host, float voxel_size, int mirror,
@@ -392,6 +405,17 @@ int o3dml_kpconv_weighted_features_backward(const float* q_pts, int64_t n, const
                                             int cin, const float* kernel_points, int K, int kp_per_query,
                                             float extent, int influence, int closest, float* grad_features,
                                             void* stream);
+/* Deterministic variant (selected under torch.use_deterministic_algorithms):
+ * grad_features fully written (no zeroing needed), each support summing its
+ * (query, column) pairs in ascending order after a stable radix sort of the
+ * neighbour matrix by support index; workspace from
+ * o3dml_kpconv_inverse_workspace_size(n, nb, n_support). */
+size_t o3dml_kpconv_inverse_workspace_size(int64_t n, int nb, int64_t n_support);
+int o3dml_kpconv_weighted_features_backward_det(const float* q_pts, int64_t n, const float* s_pts, int64_t n_support,
+                                                const void* neighbors, int index_bits, int nb, const float* grad_wf,
+                                                int cin, const float* kernel_points, int K, int kp_per_query,
+                                                float extent, int influence, int closest, float* grad_features,
+                                                void* workspace, size_t workspace_bytes, void* stream);
 /* Deformable training (kp_per_query): per-query neighbours with no kernel
  * point within extent are dropped in forward and backward, as the
  * reference's in_range filter (kpconv.py:1076-1103).  _kernel_point_grad:
@@ -418,6 +442,11 @@ int o3dml_kpconv_pool_max(const float* x, int64_t n_support, int c, const void* 
                           int64_t n, int nb, float* out, int32_t* argmax, void* stream);
 int o3dml_kpconv_pool_max_backward(const float* grad_out, const int32_t* argmax, int64_t n, int c, int64_t n_support,
                                    float* grad_x, void* stream);
+/* deterministic: gathers over the inverse of inds (workspace
+ * o3dml_kpconv_inverse_workspace_size(n, nb, n_support)); grad_x fully written */
+int o3dml_kpconv_pool_max_backward_det(const float* grad_out, const int32_t* argmax, const void* inds, int index_bits,
+                                       int64_t ld, int64_t n, int nb, int c, int64_t n_support, float* grad_x,
+                                       void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- PointPillars pillars (point_pillars.py:352-380,
  * 509-552, 567-601).

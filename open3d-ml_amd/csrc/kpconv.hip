@@ -18,6 +18,7 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "primitives.hpp"
 
 namespace o3dml {
 
@@ -383,6 +384,112 @@ __global__ void __launch_bounds__(256) pool_max_backward_kernel(const float* __r
     }
 }
 
+// ---- deterministic backward (torch.use_deterministic_algorithms(True)) ----
+// The two scatter-adds above (fp32 atomics, summation order = scheduling
+// order) become fixed-order gathers: the pairs p = q * nb + j of the
+// neighbour matrix are radix-sorted (stably) by support index
+// (prim::build_inverse), and one wave per support sums its pairs in
+// ascending p.  Bitwise identical run to run; extra cost: the sort and, in
+// the feature gradient, re-reading dWF[q] per pair (only the kernel points
+// with non-zero influence).
+template <class TI>
+__global__ void kp_pair_keys_kernel(const TI* __restrict__ nbr, int64_t ld, int64_t n, int nb, int64_t n_support,
+                                    uint32_t* __restrict__ keys) {
+    const int64_t total = n * nb;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t q = e / nb;
+        const int64_t v = static_cast<int64_t>(nbr[q * ld + (e - q * nb)]);
+        keys[e] = static_cast<uint32_t>(v >= 0 && v < n_support ? v : n_support);
+    }
+}
+
+template <class TI>
+static prim::Inverse kp_inverse(const void* nbr, int64_t ld, int64_t n, int nb, int64_t n_support, Workspace& ws,
+                                hipStream_t st) {
+    uint32_t* keys = ws.take<uint32_t>(n * nb);
+    kp_pair_keys_kernel<TI><<<stream_grid(n * nb, 256), 256, 0, st>>>(static_cast<const TI*>(nbr), ld, n, nb,
+                                                                      n_support, keys);
+    O3DML_LAUNCH_CHECK();
+    return prim::build_inverse(keys, n * nb, n_support, ws, st);
+}
+
+template <int INFL, bool CLOSEST>
+__global__ void __launch_bounds__(256) kpconv_wf_backward_det_kernel(
+        const float* __restrict__ q_pts, const float* __restrict__ s_pts, int64_t n_support,
+        const uint32_t* __restrict__ pairs, const int64_t* __restrict__ off, int nb, const float* __restrict__ dwf,
+        int cin, const float* __restrict__ kp, int K, int kp_per_query, float extent, float* __restrict__ dx) {
+    __shared__ float w_all[4][64][kKpMaxK + 1];
+    __shared__ int32_t q_all[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float(*w)[kKpMaxK + 1] = w_all[wv];
+    int32_t* qs = q_all[wv];
+    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+    for (int64_t s = static_cast<int64_t>(blockIdx.x) * 4 + wv; s < n_support; s += nwaves) {
+        const float sx = s_pts[3 * s], sy = s_pts[3 * s + 1], sz = s_pts[3 * s + 2];
+        const int64_t beg = off[s], end = off[s + 1];
+        for (int c0 = 0; c0 < cin; c0 += 64) {
+            const int c = c0 + lane;
+            float acc = 0.f;
+            for (int64_t p0 = beg; p0 < end; p0 += 64) {
+                const int64_t p = p0 + lane;
+                int32_t q = -1;
+                if (p < end) {
+                    q = static_cast<int32_t>(pairs[p] / static_cast<uint32_t>(nb));
+                    const float* kq = kp + (kp_per_query ? static_cast<int64_t>(q) * K * 3 : 0);
+                    if (!kp_influences<INFL, CLOSEST>(sx - q_pts[3 * q], sy - q_pts[3 * q + 1], sz - q_pts[3 * q + 2],
+                                                      kq, K, extent, kp_per_query, w[lane]))
+                        q = -1;
+                }
+                qs[lane] = q;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int jn = end - p0 < 64 ? static_cast<int>(end - p0) : 64;
+                if (c < cin) {
+                    for (int jj = 0; jj < jn; ++jj) {
+                        const int32_t qq = qs[jj];
+                        if (qq < 0) continue;
+                        const float* g = dwf + static_cast<int64_t>(qq) * K * cin + c;
+                        for (int k = 0; k < K; ++k) {
+                            const float wk = w[jj][k];
+                            if (wk != 0.f) acc = __builtin_fmaf(wk, g[static_cast<int64_t>(k) * cin], acc);
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (c < cin) dx[s * cin + c] = acc;
+        }
+    }
+}
+
+// dx[s, ch] = sum over the queries q whose pooled row holds s (each q once,
+// ascending) with argmax[q, ch] == s of g[q, ch]
+__global__ void __launch_bounds__(256) pool_max_backward_det_kernel(const float* __restrict__ g,
+                                                                    const int32_t* __restrict__ argmax,
+                                                                    const uint32_t* __restrict__ pairs,
+                                                                    const int64_t* __restrict__ off, int nb, int c,
+                                                                    int64_t n_support, float* __restrict__ dx) {
+    const int64_t total = n_support * c;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t s = e / c;
+        const int ch = static_cast<int>(e - s * c);
+        float acc = 0.f;
+        int64_t prev = -1;
+        for (int64_t p = off[s]; p < off[s + 1]; ++p) {
+            const int64_t q = pairs[p] / static_cast<uint32_t>(nb);
+            if (q == prev) continue;  // s repeated in row q: one argmax entry
+            prev = q;
+            if (argmax[q * c + ch] == s) acc += g[q * c + ch];
+        }
+        dx[e] = acc;
+    }
+}
+
 template <bool BWD, class TI>
 static void launch_kp(int influence, int closest, unsigned g, hipStream_t st, const float* qp, const float* sp,
                       int64_t ns, const void* nbr, int64_t n, int nb, const float* in, int cin, const float* kp, int K,
@@ -448,6 +555,43 @@ O3DML_API int o3dml_kpconv_weighted_features_backward(const float* q_pts, int64_
     else
         launch_kp<true, int64_t>(influence, closest, g, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
                                  grad_wf, cin, kernel_points, K, kp_per_query, extent, nullptr, grad_features);
+    O3DML_GUARD_END
+}
+
+O3DML_API size_t o3dml_kpconv_inverse_workspace_size(int64_t n, int nb, int64_t n_support) {
+    return prim::inverse_workspace_bytes(n * (nb > 0 ? nb : 0), n_support);
+}
+
+O3DML_API int o3dml_kpconv_weighted_features_backward_det(const float* q_pts, int64_t n, const float* s_pts,
+                                                          int64_t n_support, const void* neighbors, int index_bits,
+                                                          int nb, const float* grad_wf, int cin,
+                                                          const float* kernel_points, int K, int kp_per_query,
+                                                          float extent, int influence, int closest,
+                                                          float* grad_features, void* workspace,
+                                                          size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(K >= 1 && K <= kKpMaxK, "KPConv: kernel points must be in [1, %d]", kKpMaxK);
+    O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
+    O3DML_REQUIRE(nb >= 0, "KPConv: negative neighbour count");
+    if (n_support == 0) return 0;
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    const prim::Inverse inv = index_bits == 32 ? kp_inverse<int32_t>(neighbors, nb, n, nb, n_support, ws, st)
+                                               : kp_inverse<int64_t>(neighbors, nb, n, nb, n_support, ws, st);
+    const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n_support, 4), 1 << 20));
+#define O3DML_KPD(I, C)                                                                                         \
+    kpconv_wf_backward_det_kernel<I, C><<<g, 256, 0, st>>>(q_pts, s_pts, n_support, inv.pairs, inv.off, nb,     \
+                                                           grad_wf, cin, kernel_points, K, kp_per_query, extent, \
+                                                           grad_features)
+    if (influence == 0) {
+        if (closest) O3DML_KPD(0, true); else O3DML_KPD(0, false);
+    } else if (influence == 1) {
+        if (closest) O3DML_KPD(1, true); else O3DML_KPD(1, false);
+    } else {
+        if (closest) O3DML_KPD(2, true); else O3DML_KPD(2, false);
+    }
+#undef O3DML_KPD
+    O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }
 
@@ -527,6 +671,25 @@ O3DML_API int o3dml_kpconv_pool_max_backward(const float* grad_out, const int32_
     if (n == 0) return 0;
     pool_max_backward_kernel<<<stream_grid(n * c, 256, 256 * 16), 256, 0, as_stream(stream)>>>(grad_out, argmax, n, c,
                                                                                             n_support, grad_x);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_kpconv_pool_max_backward_det(const float* grad_out, const int32_t* argmax, const void* inds,
+                                                 int index_bits, int64_t ld, int64_t n, int nb, int c,
+                                                 int64_t n_support, float* grad_x, void* workspace,
+                                                 size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(c > 0, "pool: channels must be > 0");
+    O3DML_REQUIRE(nb >= 0 && nb <= ld, "pool: columns (%d) must be in [0, row stride %lld]", nb, (long long)ld);
+    O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
+    if (n_support == 0) return 0;
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    const prim::Inverse inv = index_bits == 32 ? kp_inverse<int32_t>(inds, ld, n, nb, n_support, ws, st)
+                                               : kp_inverse<int64_t>(inds, ld, n, nb, n_support, ws, st);
+    pool_max_backward_det_kernel<<<stream_grid(n_support * c, 256, 256 * 16), 256, 0, st>>>(
+            grad_out, argmax, inv.pairs, inv.off, nb > 0 ? nb : 1, c, n_support, grad_x);
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }

@@ -12,6 +12,7 @@
 // ball_query / three_nn stream the support cloud through LDS tiles shared by
 // the 256 queries of a workgroup.
 #include "common.hpp"
+#include "primitives.hpp"
 
 namespace o3dml {
 
@@ -280,6 +281,42 @@ __global__ void three_interpolate_grad_kernel(const float* __restrict__ grad, co
     }
 }
 
+// deterministic gradient (torch.use_deterministic_algorithms(True)): the
+// 3 n pairs of each batch are grouped by source point (prim::build_inverse,
+// key b * m + idx) and each grad_features element sums its pairs in
+// ascending (i, j) order instead of 3 fp32 atomics per pair.
+__global__ void three_interp_keys_kernel(const int32_t* __restrict__ idx, int64_t B, int64_t n, int64_t m,
+                                         uint32_t* __restrict__ keys) {
+    const int64_t total = B * n * 3;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t b = e / (3 * n);
+        const int64_t v = idx[e];
+        keys[e] = static_cast<uint32_t>(v >= 0 && v < m ? b * m + v : B * m);
+    }
+}
+
+__global__ void three_interpolate_grad_det_kernel(const float* __restrict__ grad, const float* __restrict__ w,
+                                                  const uint32_t* __restrict__ pairs, const int64_t* __restrict__ off,
+                                                  int64_t B, int64_t C, int64_t n, int64_t m,
+                                                  float* __restrict__ out) {
+    const int64_t total = B * C * m;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t t = e % m;
+        const int64_t bc = e / m;
+        const int64_t b = bc / C;
+        const int64_t key = b * m + t;
+        const float* g = grad + bc * n - b * n;  // g[b * n + i] = grad[b, c, i]
+        float acc = 0.f;
+        for (int64_t p = off[key]; p < off[key + 1]; ++p) {
+            const uint32_t pr = pairs[p];
+            acc += g[pr / 3] * w[pr];
+        }
+        out[e] = acc;
+    }
+}
+
 }  // namespace o3dml
 
 using namespace o3dml;
@@ -361,6 +398,32 @@ O3DML_API int o3dml_three_interpolate_grad(const float* grad_out, const int32_t*
     if (total == 0) return 0;
     three_interpolate_grad_kernel<<<stream_grid(total, 256), 256, 0, st>>>(grad_out, idx, weight, (int)B, (int)C,
                                                                           (int)n, (int)m, grad_features);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+O3DML_API size_t o3dml_three_interpolate_grad_workspace_size(int64_t B, int64_t n, int64_t m) {
+    return prim::inverse_workspace_bytes(B * n * 3, B * m);
+}
+
+// deterministic three_interpolate_grad (fixed summation order; no memset needed)
+O3DML_API int o3dml_three_interpolate_grad_det(const float* grad_out, const int32_t* idx, const float* weight,
+                                               int64_t B, int64_t C, int64_t n, int64_t m, float* grad_features,
+                                               void* workspace, size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    const int64_t total = B * C * m;
+    if (total == 0) return 0;
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    uint32_t* keys = ws.take<uint32_t>(B * n * 3);
+    if (n > 0) {
+        three_interp_keys_kernel<<<stream_grid(B * n * 3, 256), 256, 0, st>>>(idx, B, n, m, keys);
+        O3DML_LAUNCH_CHECK();
+    }
+    const prim::Inverse inv = prim::build_inverse(keys, B * n * 3, B * m, ws, st);
+    three_interpolate_grad_det_kernel<<<stream_grid(total, 256, 256 * 16), 256, 0, st>>>(grad_out, weight, inv.pairs,
+                                                                                       inv.off, B, C, n, m,
+                                                                                       grad_features);
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }

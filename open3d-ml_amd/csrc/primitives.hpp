@@ -407,5 +407,48 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
     }
 }
 
+// Segment starts of a sorted key array: off[s] = first position whose key is
+// >= s (lower bound), for s in [0, nseg]; keys >= nseg sort after every
+// segment.  One thread per segment boundary (binary search).
+template <class K>
+__global__ void segment_offsets_kernel(const K* __restrict__ skeys, int64_t total, int64_t nseg,
+                                       int64_t* __restrict__ off) {
+    for (int64_t s = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; s <= nseg;
+         s += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        int64_t lo = 0, hi = total;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (static_cast<int64_t>(skeys[mid]) < s) lo = mid + 1;
+            else hi = mid;
+        }
+        off[s] = lo;
+    }
+}
+
+// Inverse of a scatter: pairs whose destination is keys[p] (keys >= nseg are
+// dropped) grouped by destination in ascending p (the sort is stable).  Lets a
+// scatter-add become a fixed-order gather (run-to-run bitwise identical).
+struct Inverse {
+    const uint32_t* pairs;  // pair ids, grouped by destination
+    const int64_t* off;     // [nseg + 1] group starts
+};
+
+inline size_t inverse_workspace_bytes(int64_t total, int64_t nseg) {
+    return 3 * ws_bytes<uint32_t>(total) + ws_bytes<int64_t>(nseg + 1) + radix_sort_workspace_bytes<uint32_t>(total);
+}
+
+// keys: [total] destination per pair, in workspace-owned or caller memory
+inline Inverse build_inverse(const uint32_t* keys, int64_t total, int64_t nseg, Workspace& ws, hipStream_t st) {
+    O3DML_REQUIRE(total < (int64_t(1) << 32) && nseg < (int64_t(1) << 32) - 1,
+                  "inverse: %lld pairs / %lld groups exceed 32-bit ids", (long long)total, (long long)nseg);
+    uint32_t* skeys = ws.take<uint32_t>(total);
+    uint32_t* pairs = ws.take<uint32_t>(total);
+    int64_t* off = ws.take<int64_t>(nseg + 1);
+    radix_sort_pairs<uint32_t>(keys, nullptr, skeys, pairs, total, bits_needed(static_cast<uint64_t>(nseg)), ws, st);
+    segment_offsets_kernel<uint32_t><<<stream_grid(nseg + 1, 256), 256, 0, st>>>(skeys, total, nseg, off);
+    O3DML_LAUNCH_CHECK();
+    return Inverse{pairs, off};
+}
+
 }  // namespace prim
 }  // namespace o3dml

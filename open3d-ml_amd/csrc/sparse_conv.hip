@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <array>
 #include <vector>
 
 #include "primitives.hpp"
@@ -888,6 +889,219 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
 }
 
 // --------------------------------------------------------------------------
+// implicit GEMM on presplit operands (bf16x6 / bf16x3, the default product
+// precision): the hi / mid / lo split of every operand element is done ONCE
+// per call by presplit_kernel — per input row (with the eval prologue and the
+// row importance folded in, as gemm_finish applies them) and per filter
+// element — instead of once per (row, column block, stage) inside the GEMM:
+// the split kernels above spend ~11 VALU instructions per MFMA on it (VALU-
+// bound: 21.8 VALU per MFMA measured with addressing), here the stage loop is
+// DMA + ds_read + MFMA only.  The planes hold exactly the values
+// split_bf16x8 produces in the other kernels and the MFMAs run in the same
+// order, so the sums are bit-identical to implicit_gemm_lds/shared_kernel.
+// Needs cin % 8 == 0 (16-B pieces of 8 bf16) and no per-pair scale (pscale:
+// neighbour importance, which cannot be folded per row).
+//
+// Tile: 32 output rows x NW column blocks (wave w: block w).  A per plane:
+// LDS image [32 rows][4 pieces of 16 B], piece p of row r in slot
+// p ^ ((r >> 2) & 3) (lane (i, h) reads pieces 2h, 2h + 1 of row i: 16
+// consecutive lanes hit 16 distinct 4-bank groups), filled with
+// global_load_lds_dwordx4 (16 rows per instruction, the NP planes x 2 halves
+// dealt over the NW waves); double-buffered when NW > 1 (a barrier per stage
+// publishes it), single-buffered for one wave.  B fragments come straight
+// from the filter planes into registers (L2-resident).
+// --------------------------------------------------------------------------
+template <int NT>
+__global__ void __launch_bounds__(256) presplit_kernel(const float* __restrict__ x, int64_t n, int cin,
+                                                       const float* __restrict__ ps, const float* __restrict__ pb,
+                                                       const float* __restrict__ rscale, bf16x8* __restrict__ hi,
+                                                       bf16x8* __restrict__ mid, bf16x8* __restrict__ lo) {
+    const int g8 = cin >> 3;
+    const int64_t total = n * g8;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t r = e / g8;
+        const int c = static_cast<int>(e - r * g8) * 8;
+        const float4 v0 = *reinterpret_cast<const float4*>(x + r * cin + c);
+        const float4 v1 = *reinterpret_cast<const float4*>(x + r * cin + c + 4);
+        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        const float sc = rscale ? rscale[r] : 1.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (ps ? pre_act(v[j], ps[c + j], pb[c + j]) : v[j]) * sc;
+        bf16x8 h, m, l;
+        split_bf16x8<NT>(v, h, m, l);
+        hi[e] = h;
+        mid[e] = m;
+        if constexpr (NT == 6) lo[e] = l;
+    }
+}
+
+template <int NT, int NW, int RB>
+__global__ void __launch_bounds__(NW * 64)
+implicit_gemm_split_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, const int* order_flag,
+                           int K, int64_t n_out, const __bf16* __restrict__ ap, int64_t plane_a,
+                           const __bf16* __restrict__ bp /*[plane][K][cout][cin]*/, int64_t plane_b, int cin,
+                           int cout, const float* __restrict__ oscale, const float* __restrict__ bias,
+                           float* __restrict__ out, int nsplit, float* __restrict__ part,
+                           const float* __restrict__ residual) {
+    constexpr int NP = NT == 6 ? 3 : 2;  // planes: hi, mid (, lo)
+    constexpr int NB = NW == 1 ? 1 : 2;  // A image buffers
+    constexpr int R = 32 * RB;           // output rows per tile
+    constexpr int NI = 2 * NP * RB;      // DMA instructions per stage (16 rows of one plane each)
+    __shared__ __attribute__((aligned(16))) __bf16 abuf[NB][RB][NP][32 * 32];
+    __shared__ int32_t mtile[R * 32];
+    __shared__ int32_t orow[R];
+    const int64_t o0 = static_cast<int64_t>(blockIdx.x) * R;
+    if (o0 >= n_out) return;  // whole workgroup, before any barrier
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int i = lane & 31, h = lane >> 5;
+    const int col = (blockIdx.y * NW + w) * 32 + i;
+    if (order && *order_flag == 0) order = nullptr;
+    for (int t = threadIdx.x; t < R; t += NW * 64) {
+        const int64_t oo = o0 + t;
+        orow[t] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < R * K; e += NW * 64) {
+        const int rr = e / K;
+        const int32_t orr = orow[rr];
+        mtile[e] = orr >= 0 ? map[static_cast<int64_t>(orr) * K + (e - rr * K)] : -1;
+    }
+    __syncthreads();
+    unsigned used = 0u;  // identical in every wave (same rows)
+    for (int k = h; k < K; k += 2) {
+        bool any = false;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) any |= mtile[(32 * rb + i) * K + k] >= 0;
+        const uint64_t b = __ballot(any);
+        used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
+    }
+    used = __builtin_amdgcn_readlane(used, 32) | __builtin_amdgcn_readlane(used, 0);
+    f32x16 acc[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[rb][r] = 0.f;
+    const int nch = (cin + 31) >> 5;
+    const int s = blockIdx.z;
+    const int j0 = split_stage(used, nch, K, s, nsplit);
+    const int j1 = split_stage(used, nch, K, s + 1, nsplit);
+    const __bf16* zp = reinterpret_cast<const __bf16*>(g_zero_page);
+    // this wave's DMA share of one stage: instructions q = w, w + NW, ... of
+    // the NI (row block, plane, 16-row half) triples; map reads first, then the DMAs
+    auto issue = [&](int buf, int k, int c0, bool live) {
+        constexpr int NQ = (NI + NW - 1) / NW;
+        int32_t mq[NQ];
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) {
+            const int q = w + NW * t;
+            const int r = 32 * (q / (2 * NP)) + 16 * (q & 1) + (lane >> 2);
+            mq[t] = (q < NI && live) ? mtile[r * K + k] : -1;
+        }
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) {
+            const int q = w + NW * t;
+            if (q >= NI) continue;  // wave-uniform
+            const int rb = q / (2 * NP), pl = (q % (2 * NP)) >> 1;
+            const int r = 16 * (q & 1) + (lane >> 2);  // row within the block
+            const int c = c0 + 8 * ((lane & 3) ^ ((r >> 2) & 3));
+            const __bf16* ga = (mq[t] >= 0 && c < cin) ? ap + pl * plane_a + static_cast<int64_t>(mq[t]) * cin + c : zp;
+            glds16(reinterpret_cast<const float*>(ga),
+                   reinterpret_cast<float*>(&abuf[buf][rb][pl][16 * 32 * (q & 1)]));
+        }
+    };
+    auto bload = [&](bf16x8 (&nb)[NP][2], int k, int c0, bool live) {
+        const bool colv = live && col < cout;
+        const int64_t wo = (static_cast<int64_t>(k) * cout + (colv ? col : 0)) * cin;
+#pragma unroll
+        for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int c = c0 + 16 * h + 8 * t;
+                nb[pl][t] = *reinterpret_cast<const bf16x8*>((colv && c < cin) ? bp + pl * plane_b + wo + c : zp);
+            }
+    };
+    if (j0 < j1) {  // uniform over the workgroup
+        unsigned u = used;
+        for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
+        int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
+        bf16x8 nb[NP][2];
+        issue(0, k, c0, true);
+        bload(nb, k, c0, true);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int j = j0; j < j1; ++j) {
+            const int buf = NB == 1 ? 0 : ((j - j0) & 1);
+            bf16x8 fa[RB][NP][2], fb[NP][2];
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int slot = (2 * h + t) ^ ((i >> 2) & 3);
+                        fa[rb][pl][t] = *reinterpret_cast<const bf16x8*>(&abuf[buf][rb][pl][32 * i + 8 * slot]);
+                    }
+#pragma unroll
+            for (int pl = 0; pl < NP; ++pl)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) fb[pl][t] = nb[pl][t];
+            c0 += 32;
+            if (c0 >= cin) {
+                c0 = 0;
+                u &= u - 1u;
+                k = u ? __builtin_ctz(u) : 0;
+            }
+            const bool live = j + 1 < j1;
+            // one buffer: this stage's fragments are out of LDS before the next DMA
+            if constexpr (NB == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            issue(NB == 1 ? 0 : buf ^ 1, k, c0, live);
+            bload(nb, k, c0, live);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)  // per accumulator: the order of mfma_stage_split
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) {
+                    if constexpr (NT == 6) {
+                        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[rb][1][t], fb[1][t], acc[rb], 0, 0, 0);
+                        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[rb][2][t], fb[0][t], acc[rb], 0, 0, 0);
+                        acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[rb][0][t], fb[2][t], acc[rb], 0, 0, 0);
+                    }
+                    acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[rb][1][t], fb[0][t], acc[rb], 0, 0, 0);
+                    acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[rb][0][t], fb[1][t], acc[rb], 0, 0, 0);
+                    acc[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[rb][0][t], fb[0][t], acc[rb], 0, 0, 0);
+                }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own share of stage j+1 landed
+            __syncthreads();  // every share landed; stage j's buffer free
+        }
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+        if (nsplit > 1) {
+            float* P = part + static_cast<int64_t>(s) * n_out * cout;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t orr = orow[32 * rb + (r & 3) + 8 * (r >> 2) + 4 * h];
+                if (orr >= 0 && col < cout) P[orr * cout + col] = acc[rb][r];
+            }
+            continue;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t orr = orow[32 * rb + (r & 3) + 8 * (r >> 2) + 4 * h];
+            if (orr >= 0 && col < cout) {
+                float v = acc[rb][r];
+                if (oscale) v *= oscale[orr];
+                if (bias) v += bias[col];
+                if (residual) v += residual[orr * cout + col];
+                out[orr * cout + col] = v;
+            }
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
 // dW: per offset pair lists, split-K slabs
 // --------------------------------------------------------------------------
 // k-major flags: flag[k*n_out + o] = map[o*K+k] >= 0
@@ -1257,19 +1471,113 @@ static size_t gemm_split_bytes(int64_t n_out, int K, int cin, int cout) {
     return ns > 1 ? ws_bytes<float>(ns * n_out * cout) : 0;
 }
 
-static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, const int* order_flag, int K, int64_t n_out, const float* src,
-                     const float* sscale,
-                     const float* pscale, const float* Wt, int cin, int cout, const float* oscale, const float* bias,
-                     float* out, float* part, size_t part_bytes, GemmPrologue pre = {nullptr, nullptr},
-                     const float* residual = nullptr) {
+// Presplit operands (implicit_gemm_split_kernel) — OFF by default: measured
+// on the C4 3^3 map (tools/gemm_probe.py, profiles/r03/sparse_conv_presplit_ab.txt)
+// it is slower than the in-kernel split at every width and row blocking
+// (32->32: 78 vs 69.5 us, 128->128: 382 vs 367 us at its best RB = 2).  The
+// in-kernel split's VALU work hides under the MFMA / L2 latency; what bounds
+// these kernels is the L2 -> LDS / register traffic of the gathered rows and
+// the per-stage filter fragments, which the 6-B bf16 planes raise by 1.5x.
+// O3DML_GEMM_PRESPLIT=1 or o3dml_sparse_conv_set_presplit(1) turns it on.
+static bool g_presplit = [] {
+    const char* e = std::getenv("O3DML_GEMM_PRESPLIT");
+    return e ? std::atoi(e) != 0 : false;
+}();
+
+// presplit operand planes: 3 bf16 planes of the n_src x cin source rows and of
+// the K x cout x cin filters (0 while presplit is off)
+static size_t presplit_bytes(int64_t n_src, int K, int cin, int cout) {
+    if (!g_presplit) return 0;
+    return 3 * ws_bytes<uint16_t>(n_src * cin) + 3 * ws_bytes<uint16_t>(static_cast<int64_t>(K) * cout * cin);
+}
+
+// everything run_gemm may take from its workspace
+static size_t gemm_ws_bytes(int64_t n_out, int64_t n_src, int K, int cin, int cout) {
+    return gemm_split_bytes(n_out, K, cin, cout) + presplit_bytes(n_src, K, cin, cout);
+}
+
+static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, const int* order_flag, int K,
+                     int64_t n_out, const float* src, int64_t n_src, const float* sscale, const float* pscale,
+                     const float* Wt, int cin, int cout, const float* oscale, const float* bias, float* out,
+                     Workspace ws, GemmPrologue pre = {nullptr, nullptr}, const float* residual = nullptr) {
     if (n_out == 0 || cout == 0) return;
     const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0 &&
                       (reinterpret_cast<uintptr_t>(Wt) % 16) == 0;
     int ns = gemm_splits(n_out, K, cin, cout);
-    if (!part || part_bytes < sizeof(float) * static_cast<size_t>(ns) * n_out * cout) ns = 1;
+    float* part = nullptr;
+    if (ns > 1) {
+        const size_t pb = ws_bytes<float>(static_cast<int64_t>(ns) * n_out * cout);
+        if (ws.base && ws.used + pb <= ws.size) part = ws.take<float>(static_cast<int64_t>(ns) * n_out * cout);
+        else ns = 1;
+    }
     const dim3 g(static_cast<unsigned>(ceil_div(n_out, 32 * (kGemmThreads / 64))),
                  static_cast<unsigned>(ceil_div(cout, 32)), static_cast<unsigned>(ns));
     O3DML_REQUIRE(pre.scale == nullptr || cin <= kPreMax, "sparse_conv: prologue needs cin <= %d", kPreMax);
+    const int nt_mode = gemm_nt();
+    if (g_presplit && nt_mode != 0 && vec4 && cin % 8 == 0 && pscale == nullptr && ws.base &&
+        ws.used + presplit_bytes(n_src, K, cin, cout) <= ws.size) {
+        // operands split once (implicit_gemm_split_kernel); the split passes
+        // belong to the GEMM's time
+        TimedRegion tr("sparse_conv_gemm", st);
+        const int64_t pa = n_src * cin, pbn = static_cast<int64_t>(K) * cout * cin;
+        __bf16* ap = reinterpret_cast<__bf16*>(ws.take<uint16_t>(3 * pa));
+        __bf16* bpl = reinterpret_cast<__bf16*>(ws.take<uint16_t>(3 * pbn));
+        auto planes = [](__bf16* b, int64_t n) {
+            return std::array<bf16x8*, 3>{reinterpret_cast<bf16x8*>(b), reinterpret_cast<bf16x8*>(b + n),
+                                          reinterpret_cast<bf16x8*>(b + 2 * n)};
+        };
+        const auto A = planes(ap, pa), B = planes(bpl, pbn);
+        if (n_src > 0) {
+            if (nt_mode == 6)
+                presplit_kernel<6><<<stream_grid(pa / 8, 256), 256, 0, st>>>(src, n_src, cin, pre.scale, pre.shift,
+                                                                             sscale, A[0], A[1], A[2]);
+            else
+                presplit_kernel<3><<<stream_grid(pa / 8, 256), 256, 0, st>>>(src, n_src, cin, pre.scale, pre.shift,
+                                                                             sscale, A[0], A[1], A[2]);
+            O3DML_LAUNCH_CHECK();
+        }
+        if (nt_mode == 6)
+            presplit_kernel<6><<<stream_grid(pbn / 8, 256), 256, 0, st>>>(Wt, static_cast<int64_t>(K) * cout, cin,
+                                                                          nullptr, nullptr, nullptr, B[0], B[1], B[2]);
+        else
+            presplit_kernel<3><<<stream_grid(pbn / 8, 256), 256, 0, st>>>(Wt, static_cast<int64_t>(K) * cout, cin,
+                                                                          nullptr, nullptr, nullptr, B[0], B[1], B[2]);
+        O3DML_LAUNCH_CHECK();
+        const int nw = cout >= 128 && cout % 128 == 0 ? 4 : (cout >= 64 ? 2 : 1);
+        static const int env_rb = [] {
+            const char* e = std::getenv("O3DML_GEMM_SPLIT_RB");
+            return e ? std::atoi(e) : 0;
+        }();
+        // row blocks per tile: each B fragment (the filters, streamed from L2
+        // per stage) feeds RB accumulators
+        const int rb = env_rb == 1 || env_rb == 2 || env_rb == 4 ? env_rb : 2;
+        const dim3 gs(static_cast<unsigned>(ceil_div(n_out, 32 * rb)), static_cast<unsigned>(ceil_div(cout, 32 * nw)),
+                      static_cast<unsigned>(ns));
+#define O3DML_GEMM_SP(NT, W, B)                                                                                   \
+    implicit_gemm_split_kernel<NT, W, B><<<gs, W * 64, 0, st>>>(map, order, order_flag, K, n_out, ap, pa, bpl,    \
+                                                                 pbn, cin, cout, oscale, bias, out, ns, part,      \
+                                                                 residual)
+#define O3DML_GEMM_SP_W(NT, B)                                                                     \
+    do {                                                                                           \
+        if (nw == 4) O3DML_GEMM_SP(NT, 4, B); else if (nw == 2) O3DML_GEMM_SP(NT, 2, B); else O3DML_GEMM_SP(NT, 1, B); \
+    } while (0)
+#define O3DML_GEMM_SP_RB(NT)                                                                  \
+    do {                                                                                      \
+        if (rb == 4) O3DML_GEMM_SP_W(NT, 4); else if (rb == 2) O3DML_GEMM_SP_W(NT, 2); else O3DML_GEMM_SP_W(NT, 1); \
+    } while (0)
+        if (nt_mode == 6) O3DML_GEMM_SP_RB(6); else O3DML_GEMM_SP_RB(3);
+#undef O3DML_GEMM_SP_RB
+#undef O3DML_GEMM_SP_W
+#undef O3DML_GEMM_SP
+        O3DML_LAUNCH_CHECK();
+        tr.end();
+        if (ns > 1) {
+            split_reduce_kernel<<<stream_grid(n_out * cout, 256), 256, 0, st>>>(part, ns, n_out, cout, oscale, bias,
+                                                                               residual, out);
+            O3DML_LAUNCH_CHECK();
+        }
+        return;
+    }
 #define O3DML_GEMM_LAUNCH(V, P)                                                                                    \
     implicit_gemm_kernel<V, P><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, \
                                                            bias, out, ns, part, pre, residual)
@@ -1801,16 +2109,15 @@ O3DML_API int o3dml_sparse_conv_forward_fused(const float* filters_t, int K, int
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
     ws.take<float>(static_cast<int64_t>(K) * cin * cout);  // (unused Wt slot: filters_t comes transposed)
-    run_gemm(st, map, order, oflag, K, n_out, inp_features, nullptr, nullptr, filters_t, cin, cout, nullptr, bias,
-             out_features,
-             reinterpret_cast<float*>(ws.base + ws.used), ws.size - ws.used, GemmPrologue{pre_scale, pre_shift},
-             residual);
+    run_gemm(st, map, order, oflag, K, n_out, inp_features, n_in, nullptr, nullptr, filters_t, cin, cout, nullptr,
+             bias, out_features, ws, GemmPrologue{pre_scale, pre_shift}, residual);
     O3DML_GUARD_END
 }
 
-// split-K partial sums of o3dml_sparse_conv_forward (0 when no split is used)
-O3DML_API size_t o3dml_sparse_conv_forward_workspace_size(int64_t n_out, int K, int cin, int cout) {
-    return ws_bytes<float>(static_cast<int64_t>(K) * cin * cout) + gemm_split_bytes(n_out, K, cin, cout);
+// transposed filters, split-K partial sums and the presplit operand planes of
+// o3dml_sparse_conv_forward(_fused)
+O3DML_API size_t o3dml_sparse_conv_forward_workspace_size(int64_t n_out, int64_t n_in, int K, int cin, int cout) {
+    return ws_bytes<float>(static_cast<int64_t>(K) * cin * cout) + gemm_ws_bytes(n_out, n_in, K, cin, cout);
 }
 
 // out [n_out, cout] = oscale * sum_k gather(inp) @ W[k] (+ bias).  filters:
@@ -1831,9 +2138,9 @@ O3DML_API int o3dml_sparse_conv_forward(const float* filters, int K, int cin, in
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
     const float* wt = forward_filters(filters, K, cin, cout, ws, st);
-    run_gemm(st, map, order, oflag, K, n_out, inp_features, inp_importance, has_neighbors_importance ? pscale : nullptr, wt,
-             cin, cout, use_out_scale ? oscale : nullptr, bias, out_features,
-             reinterpret_cast<float*>(ws.base + ws.used), ws.size - ws.used);
+    run_gemm(st, map, order, oflag, K, n_out, inp_features, n_in, inp_importance,
+             has_neighbors_importance ? pscale : nullptr, wt, cin, cout, use_out_scale ? oscale : nullptr, bias,
+             out_features, ws);
     O3DML_GUARD_END
 }
 
@@ -1849,7 +2156,7 @@ static int dw_chunks(int64_t n_out, int K, int cin, int cout) {
 O3DML_API size_t o3dml_sparse_conv_backward_workspace_size(int64_t n_out, int64_t n_in, int K, int cin, int cout) {
     const int nchunk = dw_chunks(n_out, K, cin, cout);
     return ws_bytes<float>(static_cast<int64_t>(K) * cin * cout) + ws_bytes<float>(n_out * cout) +
-           gemm_split_bytes(n_in, K, cout, cin) + ws_bytes<int64_t>(n_out * K) * 2 + ws_bytes<int32_t>(n_out * K) +
+           gemm_ws_bytes(n_in, n_out, K, cout, cin) + ws_bytes<int64_t>(n_out * K) * 2 + ws_bytes<int32_t>(n_out * K) +
            ws_bytes<int64_t>(K + 1) + ws_bytes<int64_t>(K + 2) +
            (nchunk > 1 ? ws_bytes<float>(static_cast<int64_t>(K) * (nchunk + 1) * cin * cout) : 0) +
            prim::scan_workspace_bytes(n_out * K);
@@ -1875,8 +2182,10 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
     float* wt = ws.take<float>(static_cast<int64_t>(K) * cin * cout);
     float* g = ws.take<float>(n_out * cout);  // unused slot kept for layout stability
     (void)g;
-    const size_t split_bytes = gemm_split_bytes(n_in, K, cout, cin);
-    float* split = split_bytes ? ws.take<float>(static_cast<int64_t>(split_bytes / sizeof(float))) : nullptr;
+    // the dIn GEMM's scratch (split-K partials, presplit planes)
+    const size_t gemm_bytes = gemm_ws_bytes(n_in, n_out, K, cout, cin);
+    Workspace gws(ws.base + ws.used, std::min(gemm_bytes, ws.size - ws.used));
+    if (gemm_bytes) ws.take<uint8_t>(static_cast<int64_t>(gemm_bytes));
     const float* os = use_out_scale ? oscale : nullptr;
     if (grad_inp && n_in > 0) {
         // dIn[i] = sscale[i] * sum_k (g[inv[i,k]] * oscale[o] * pscale) @ W[k]^T: a
@@ -1885,8 +2194,8 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
         // The per-row out-scale belongs to the gathered rows (source = grad_out):
         // fold it in as sscale; pair importance via the inverse pscale.
         (void)wt;
-        run_gemm(st, inv, iorder, ioflag, K, n_in, grad_out, os, has_neighbors_importance ? ipscale : nullptr, filters, cout, cin,
-                 inp_importance, nullptr, grad_inp, split, split_bytes);
+        run_gemm(st, inv, iorder, ioflag, K, n_in, grad_out, n_out, os, has_neighbors_importance ? ipscale : nullptr,
+                 filters, cout, cin, inp_importance, nullptr, grad_inp, gws);
     }
     if (grad_filters) {
         const int64_t KC = static_cast<int64_t>(K) * cin * cout;
@@ -1952,6 +2261,13 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
 }
 
 // ksize_host[3] = filter dims (k0,k1,k2) = (z,y,x) extents.
+// presplit operands on (1, default) / off (0); < 0 queries.  Returns the previous setting.
+O3DML_API int o3dml_sparse_conv_set_presplit(int on) {
+    const int prev = g_presplit ? 1 : 0;
+    if (on >= 0) g_presplit = on != 0;
+    return prev;
+}
+
 O3DML_API int o3dml_sparse_conv_set_exact(int exact) {
     const int prev = gemm_mode();
     if (exact >= 0) {

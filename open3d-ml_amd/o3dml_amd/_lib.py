@@ -73,11 +73,17 @@ SIGNATURES = {
                                                c_i32, c_f32, c_i32, c_i32, c_p, c_p, c_p]),
     "o3dml_kpconv_weighted_features_backward": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p,
                                                         c_i32, c_i32, c_f32, c_i32, c_i32, c_p, c_p]),
+    "o3dml_kpconv_inverse_workspace_size": (c_sz, [c_i64, c_i32, c_i64]),
+    "o3dml_kpconv_weighted_features_backward_det": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32,
+                                                            c_p, c_i32, c_i32, c_f32, c_i32, c_i32, c_p, c_p, c_sz,
+                                                            c_p]),
     "o3dml_kpconv_kernel_point_grad": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p,
                                                c_i32, c_f32, c_i32, c_i32, c_p, c_p, c_p, c_p]),
     "o3dml_kpconv_min_d2_columns": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p]),
     "o3dml_kpconv_pool_max": (c_i32, [c_p, c_i64, c_i32, c_p, c_i32, c_i64, c_i64, c_i32, c_p, c_p, c_p]),
     "o3dml_kpconv_pool_max_backward": (c_i32, [c_p, c_p, c_i64, c_i32, c_i64, c_p, c_p]),
+    "o3dml_kpconv_pool_max_backward_det": (c_i32, [c_p, c_p, c_p, c_i32, c_i64, c_i64, c_i32, c_i32, c_i64, c_p, c_p,
+                                                   c_sz, c_p]),
     "o3dml_pillar_features": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_f32, c_f32, c_f32, c_f32,
                                       c_p, c_p]),
     "o3dml_pillar_scatter": (c_i32, [c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p]),
@@ -114,13 +120,16 @@ SIGNATURES = {
     "o3dml_three_nn": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p]),
     "o3dml_three_interpolate": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
     "o3dml_three_interpolate_grad": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p]),
+    "o3dml_three_interpolate_grad_workspace_size": (c_sz, [c_i64, c_i64, c_i64]),
+    "o3dml_three_interpolate_grad_det": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_sz, c_p]),
     "o3dml_nms_workspace_size": (c_sz, [c_i64]),
     "o3dml_nms": (c_i32, [c_p, c_p, c_i64, c_f32, c_p, c_p, c_p, c_sz, c_p]),
     # sparse_conv.hip
     "o3dml_sparse_conv_map_workspace_size": (c_sz, [c_i64, c_i64, c_i32]),
     "o3dml_sparse_conv_build_map": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_i32, c_p, c_p,
                                             c_sz, c_p]),
-    "o3dml_sparse_conv_forward_workspace_size": (c_sz, [c_i64, c_i32, c_i32, c_i32]),
+    "o3dml_sparse_conv_forward_workspace_size": (c_sz, [c_i64, c_i64, c_i32, c_i32, c_i32]),
+    "o3dml_sparse_conv_set_presplit": (c_i32, [c_i32]),
     "o3dml_sparse_conv_forward_fused": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64,
                                                 c_p, c_p, c_sz, c_p, c_sz, c_p]),
     "o3dml_sparse_conv_forward": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i64, c_p,

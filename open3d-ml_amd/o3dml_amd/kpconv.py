@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from ._util import gpu_device, index_bits, ptr, stream_handle, to_dev
+from ._util import gpu_device, index_bits, ptr, stream_handle, to_dev, workspace
 
 _INFLUENCE = {"constant": 0, "linear": 1, "gaussian": 2}
 
@@ -52,10 +52,19 @@ class _WeightedFeatures(torch.autograd.Function):
         dx = dkp = dmod = None
         if ctx.needs_input_grad[0]:
             gm = g * mod[:, :, None] if has_mod else g  # the modulation scales dWF (kpconv.py:1149-1150)
-            dx = torch.zeros((n_s, cin), dtype=torch.float32, device=g.device)
-            _lib.call("o3dml_kpconv_weighted_features_backward", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr),
-                      index_bits(nbr.dtype), nb, ptr(gm.contiguous()), cin, ptr(kp), K, int(kp_per_query),
-                      float(extent), influence, int(closest), ptr(dx), stream_handle(g.device))
+            gm = gm.contiguous()
+            if torch.are_deterministic_algorithms_enabled():
+                # fixed-order gather over the inverse neighbour lists (no fp32 atomics)
+                dx = torch.empty((n_s, cin), dtype=torch.float32, device=g.device)
+                ws = workspace(_lib.load().o3dml_kpconv_inverse_workspace_size(n, nb, n_s), g.device)
+                _lib.call("o3dml_kpconv_weighted_features_backward_det", ptr(q_pts), n, ptr(s_pts), n_s, ptr(nbr),
+                          index_bits(nbr.dtype), nb, ptr(gm), cin, ptr(kp), K, int(kp_per_query), float(extent),
+                          influence, int(closest), ptr(dx), ptr(ws), ws.numel(), stream_handle(g.device))
+            else:
+                dx = torch.zeros((n_s, cin), dtype=torch.float32, device=g.device)
+                _lib.call("o3dml_kpconv_weighted_features_backward", ptr(q_pts), n, ptr(s_pts), n_s, ptr(nbr),
+                          index_bits(nbr.dtype), nb, ptr(gm), cin, ptr(kp), K, int(kp_per_query), float(extent),
+                          influence, int(closest), ptr(dx), stream_handle(g.device))
         if ctx.needs_input_grad[4] or (has_mod and ctx.needs_input_grad[9]):
             if not kp_per_query:
                 raise NotImplementedError("KPConv: gradients w.r.t. shared (non-deformed) kernel points")

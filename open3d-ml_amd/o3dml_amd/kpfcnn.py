@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib, ops
-from ._util import index_bits, ptr, stream_handle, to_dev
+from ._util import index_bits, ptr, stream_handle, to_dev, workspace
 from .kpconv import KPConv
 
 
@@ -43,16 +43,23 @@ class _PoolMax(torch.autograd.Function):
         if n and c:
             _lib.call("o3dml_kpconv_pool_max", ptr(x), ns, c, ptr(inds), index_bits(inds.dtype), ld, n, nb, ptr(out),
                       ptr(arg), stream_handle(x.device))
-        ctx.save_for_backward(arg)
-        ctx.shape = (ns, c)
+        ctx.save_for_backward(arg, inds)
+        ctx.shape = (ns, c, nb)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        (arg,) = ctx.saved_tensors
-        ns, c = ctx.shape
+        arg, inds = ctx.saved_tensors
+        ns, c, nb = ctx.shape
+        n, ld = inds.shape
+        if c and ns and torch.are_deterministic_algorithms_enabled():
+            # fixed-order gather over the inverse of inds (no fp32 atomics)
+            dx = torch.empty((ns, c), dtype=torch.float32, device=g.device)
+            ws = workspace(_lib.load().o3dml_kpconv_inverse_workspace_size(n, nb, ns), g.device)
+            _lib.call("o3dml_kpconv_pool_max_backward_det", ptr(g.contiguous()), ptr(arg), ptr(inds),
+                      index_bits(inds.dtype), ld, n, nb, c, ns, ptr(dx), ptr(ws), ws.numel(), stream_handle(g.device))
+            return dx, None, None
         dx = torch.zeros((ns, c), dtype=torch.float32, device=g.device)
-        n = g.shape[0]
         if n and c:
             _lib.call("o3dml_kpconv_pool_max_backward", ptr(g.contiguous()), ptr(arg), n, c, ns, ptr(dx),
                       stream_handle(g.device))

@@ -549,13 +549,20 @@ def three_interpolate(feats, idx, weights):
 
 def three_interpolate_grad(grad_out, idx, weights, M):
     """Open3D ``ops.three_interpolate_grad`` (pointnet2_utils.py:184):
-    grad_out [B,C,n] -> [B,C,M] (fp32 atomic accumulation)."""
+    grad_out [B,C,n] -> [B,C,M].  fp32 atomic accumulation, as the reference;
+    under ``torch.use_deterministic_algorithms(True)`` a fixed-order gather
+    (pairs grouped by source point with a stable radix sort) instead."""
     dev = gpu_device(grad_out, idx, weights)
     B, C, n = grad_out.shape
     g = to_dev(grad_out, dev, torch.float32)
     i = to_dev(idx, dev, torch.int32)
     w = to_dev(weights, dev, torch.float32)
     out = torch.empty((B, C, int(M)), dtype=torch.float32, device=dev)
+    if torch.are_deterministic_algorithms_enabled():
+        ws = workspace(_lib.load().o3dml_three_interpolate_grad_workspace_size(B, n, int(M)), dev)
+        _lib.call("o3dml_three_interpolate_grad_det", ptr(g), ptr(i), ptr(w), B, C, n, int(M), ptr(out), ptr(ws),
+                  ws.numel(), stream_handle(dev))
+        return back_to(out, grad_out)
     _lib.call("o3dml_three_interpolate_grad", ptr(g), ptr(i), ptr(w), B, C, n, int(M), ptr(out), stream_handle(dev))
     return back_to(out, grad_out)
 

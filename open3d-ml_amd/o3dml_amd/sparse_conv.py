@@ -82,7 +82,7 @@ class _ConvFn(torch.autograd.Function):
         x = inp_features.detach().contiguous()
         out = torch.empty((n_out, cout), dtype=torch.float32, device=dev)
         use_os = int(bool(normalize) or out_importance is not None)
-        fws = workspace(lib.o3dml_sparse_conv_forward_workspace_size(n_out, K, cin, cout), dev)
+        fws = workspace(lib.o3dml_sparse_conv_forward_workspace_size(n_out, n_in, K, cin, cout), dev)
         _lib.call("o3dml_sparse_conv_forward", ptr(W), K, cin, cout, ptr(x), n_in, ptr(sscale), int(nimp is not None),
                   use_os, ptr(bias.detach().contiguous() if bias is not None else None), n_out, ptr(out), ptr(mws),
                   mws.numel(), ptr(fws), fws.numel(), st)
@@ -371,7 +371,7 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
         res = None if residual is None else residual.contiguous()
         if res is not None and tuple(res.shape) != (n_out, cout):
             raise ValueError("sparse_conv: residual must be [n_out, cout]")
-        fws = workspace(lib.o3dml_sparse_conv_forward_workspace_size(n_out, K, cin, cout), dev)
+        fws = workspace(lib.o3dml_sparse_conv_forward_workspace_size(n_out, n_in, K, cin, cout), dev)
         _lib.call("o3dml_sparse_conv_forward_fused", ptr(_transposed_filters(f)), K, cin, cout,
                   ptr(x.detach().contiguous()), n_in, ptr(ps), ptr(pb), ptr(res),
                   ptr(None if b is None else b.detach().contiguous()), n_out, ptr(out), ptr(mws), mws.numel(),
