@@ -230,7 +230,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                  float* __restrict__ tdist, uint32_t* __restrict__ over, int64_t* __restrict__ n_over,
                  const int64_t* __restrict__ rs, TIdx* __restrict__ out_idx, float* __restrict__ out_dist,
                  const int64_t* __restrict__ total, int64_t cap, const uint32_t* __restrict__ dir,
-                 int64_t dir_cap) {
+                 int64_t dir_cap, int qlog) {
     __shared__ float4 cand[kCandCap];
     __shared__ float4 qsh[64];
     __shared__ int64_t qrow[MODE == 0 ? 1 : 64];  // MODE 0: the row is the query id (qsh .w)
@@ -240,7 +240,9 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
     // MODE 1 of a bounded fill whose rows do not fit the caller's capacity:
     // nothing is written (the caller re-runs the fill with exact buffers)
     const int64_t m = MODE == 1 && cap >= 0 && *total > cap ? 0 : (m_dev ? *m_dev : m_host);
-    const int64_t nchunks = MODE == 0 ? (m + 63) >> 6 : m;  // MODE 1: one query per wave
+    // MODE 0: 2^qlog queries per wave (64; 32 or 16 when there are too few
+    // queries to give every SIMD a few waves); MODE 1: one query per wave
+    const int64_t nchunks = MODE == 0 ? (m + (1 << qlog) - 1) >> qlog : m;
     // buffer resource over pts[0 .. 2 n_pts + 1] (bucket order, the far
     // sentinel, the class sub-lists p2) when its byte size fits the 32-bit range
     const bool pts_rsrc_ok = n_pts < 0x07FFFFFEu;
@@ -260,8 +262,8 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
     const bool xcd_map = static_cast<int64_t>(gridDim.x) == 8 * per;
     int64_t chunk = xcd_map ? static_cast<int64_t>(blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
     for (; chunk < nchunks; chunk = xcd_map ? nchunks : chunk + gridDim.x) {
-        const int64_t t = MODE == 0 ? (chunk << 6) + lane : chunk;
-        const bool valid = t < m && (MODE == 0 || lane == 0);
+        const int64_t t = MODE == 0 ? (chunk << qlog) + lane : chunk;
+        const bool valid = t < m && (MODE == 0 ? lane < (1 << qlog) : lane == 0);
         float4 q4 = far;
         QueryBins qb;
 #pragma unroll
@@ -707,7 +709,6 @@ __global__ void __launch_bounds__(256) bucket_classes_kernel(const float* __rest
     const int64_t nbins = H[nb];
     const bool with_dir = dir != nullptr && nbins <= dir_cap;  // else the search streams whole buckets
     float4* p2 = pts + n_pts + 1;
-    const float inf = __builtin_huge_valf();
     const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
     const uint64_t lt = lanemask_lt();
     // XCD-contiguous (xcd_block): each XCD orders the buckets whose points its
@@ -929,6 +930,21 @@ static bool frs_self_order(int64_t n_batch, const int64_t* prs_host, int64_t n_p
     return mx < O3DML_FRS_SELF_ORDER_MAX;
 }
 
+// log2 of the queries per wave of the MODE 0 search: 64 while that still
+// gives >= 4096 waves (4 per SIMD), else 32 / 16 — a small call (one C1 scene,
+// 65,536 queries: 1,024 waves of 64) is latency-bound on one wave per SIMD.
+// More waves of fewer queries split a few groups that 64-query waves keep
+// whole (more bucket streaming), which only pays while the chip is short of waves.
+static int frs_qlog(int64_t m) {
+    static const int env = [] {
+        const char* e = std::getenv("O3DML_FRS_QLOG");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (env >= 4 && env <= 6) return env;
+    if (m >= 4096 * 64) return 6;
+    return m >= 4096 * 32 ? 5 : 4;
+}
+
 static unsigned group_grid(int64_t m, int queries_per_wave = 64) {
     const int64_t per = ((m + queries_per_wave - 1) / queries_per_wave + 7) / 8;
     return static_cast<unsigned>(std::max<int64_t>(8, std::min<int64_t>(8 * per, 1 << 20)));
@@ -942,11 +958,11 @@ static void launch_group(int metric, bool ignore, bool with_dist, bool rel16, hi
                          float thr, int nb, const int64_t* qrs, const uint32_t* hts, const int64_t* prs,
                          uint32_t* counts, uint32_t* tidx, float* tdist, uint32_t* over, int64_t* n_over,
                          const int64_t* rs, TIdx* idx, float* dist, const uint32_t* dir, int64_t dir_cap,
-                         const int64_t* total = nullptr, int64_t cap = -1) {
+                         const int64_t* total = nullptr, int64_t cap = -1, int qlog = 6) {
 #define O3DML_GRP(M, I, D, R)                                                                                   \
     frs_group_kernel<M, I, D, MODE, TIdx, R><<<grid, 64, 0, st>>>(pts, n_pts, cs, qpts, qsel, qkeys, bshift, m, m_dev, \
                                                                    r, inv, thr, nb, qrs, hts, prs, counts, tidx,  \
-                                                                   tdist, over, n_over, rs, idx, dist, total, cap, dir, dir_cap)
+                                                                   tdist, over, n_over, rs, idx, dist, total, cap, dir, dir_cap, qlog)
 #define O3DML_GRP_R(M, I, D)                                  \
     do {                                                      \
         if (MODE == 0 && rel16)                               \
@@ -1163,13 +1179,15 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
     }
     {
         TimedRegion tr("frs_group_search", st);
+        const int qlog = frs_qlog(n_queries);
         launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0,
-                                 rel16_rows(n_batch, points_row_splits_host, n_queries), st, group_grid(n_queries), pl.pts,
+                                 rel16_rows(n_batch, points_row_splits_host, n_queries), st,
+                                 group_grid(n_queries, 1 << qlog), pl.pts,
                                  static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts,
                                  self_order ? pl.qorder : nullptr, qkeys, bshift,
                                  n_queries, nullptr, radius, inv, thr, (int)n_batch, queries_row_splits,
                                  hash_table_splits, points_row_splits, pl.counts, pl.tidx, pl.tdist, pl.over,
-                                 pl.scalars, nullptr, nullptr, nullptr, pl.dir, pl.dir_cap);
+                                 pl.scalars, nullptr, nullptr, nullptr, pl.dir, pl.dir_cap, nullptr, -1, qlog);
     }
     Workspace sws = ws;
     prim::scan<uint32_t, int64_t>(pl.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
