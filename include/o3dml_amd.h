@@ -256,6 +256,12 @@ int o3dml_calculate_grid_fill(int64_t n_points, float* out_positions, void* work
  * item, first max_p cells kept (max_p <= 0: all). _count writes the number of
  * output points to *n_out_host. -------------------------------------------- */
 size_t o3dml_grid_subsample_workspace_size(int64_t n_points, int64_t n_batch);
+/* count without a host synchronisation (KPFCNN collate: several counts read
+ * back in one transfer): out device int64 [2 + n_batch] = output points,
+ * grid-too-large flag (must be 0), output points per batch item. */
+int o3dml_grid_subsample_count_async(const float* points, int64_t n_points, int64_t n_batch,
+                                     const int64_t* row_splits, float dl, int64_t max_p, int64_t* out,
+                                     void* workspace, size_t workspace_bytes, void* stream);
 int o3dml_grid_subsample_count(const float* points, int64_t n_points, int64_t n_batch, const int64_t* row_splits,
                                const int64_t* row_splits_host, float dl, int64_t max_p, int64_t* n_out_host,
                                void* workspace, size_t workspace_bytes, void* stream);

@@ -13,8 +13,10 @@
 //
 // Shapes: K <= 768, M <= 512, N = 176 .. 45,056 rows.  The deep levels have
 // few rows (704 x 768 -> 512), so the K loop is split over blocks until the
-// grid holds ~4 blocks per CU (deterministic two-pass reduction: per-split
-// f32 partial slabs, then a fixed-order sum + bias + activation); the K loop
+// grid holds ~4 blocks per CU (deterministic reduction: per-split f32 partial
+// slabs summed in split order by dense_split_reduce_kernel, which adds the
+// bias and applies the activation; optionally the last block of each tile
+// does it instead, see fused_reduce); the K loop
 // itself keeps the next 32-wide chunk in registers while the current one is
 // consumed from LDS, so one barrier pair per chunk and the global loads are in
 // flight during the FMAs.  f32 FMA accumulation in K order within a split.
@@ -22,8 +24,10 @@
 // ty + 16 i, columns tx + 16 j); A chunk [32][16 TR + 1], W chunk [32][16 TC + 1]
 // (k-major, conflict-free stores: the +1 row pitch rotates the banks).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
+#include "counters.hpp"
 
 namespace o3dml {
 
@@ -35,7 +39,8 @@ __global__ void __launch_bounds__(256) dense_act_kernel(const float* __restrict_
                                                         const int64_t* __restrict__ a2_index,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         int64_t n, int m, int k_per_split, float slope, int act,
-                                                        float* __restrict__ out) {
+                                                        float* __restrict__ out, float* __restrict__ part,
+                                                        uint32_t* __restrict__ counters) {
     constexpr int RB = 16 * TR, CB = 16 * TC;
     constexpr int LA = TR * kDenseKC / 16, LW = TC * kDenseKC / 16;  // loads per thread per chunk
     __shared__ float As[kDenseKC][RB + 1];
@@ -95,7 +100,7 @@ __global__ void __launch_bounds__(256) dense_act_kernel(const float* __restrict_
         }
         __syncthreads();
     }
-    float* dst = SPLIT ? out + static_cast<int64_t>(blockIdx.z) * n * m : out;
+    float* dst = SPLIT ? part + static_cast<int64_t>(blockIdx.z) * n * m : out;
 #pragma unroll
     for (int i = 0; i < TR; ++i) {
         const int64_t r = r0 + ty + 16 * i;
@@ -108,9 +113,47 @@ __global__ void __launch_bounds__(256) dense_act_kernel(const float* __restrict_
             if (!SPLIT) {
                 v += bias ? bias[c] : 0.f;
                 if (act) v = v >= 0.f ? v : v * slope;
+                dst[r * m + c] = v;
+            } else if (counters) {
+                // slab entries as agent-scope stores: written through to the
+                // device-coherent level, no L2 write-back fence needed
+                __hip_atomic_store(dst + r * m + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                dst[r * m + c] = v;
             }
-            dst[r * m + c] = v;
         }
+    }
+    if constexpr (SPLIT) {
+        if (!counters) return;  // dense_split_reduce_kernel finishes
+        // arrival once this block's slab stores are complete; the last of the
+        // tile's gridDim.z blocks sums the slabs in split order, reading them
+        // with agent-scope loads (past the non-coherent caches).  A device-
+        // scope fence here would write back the whole L2 per block (8 XCDs:
+        // measured 2x slower RandLA frames).
+        __shared__ uint32_t s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t tile = blockIdx.y * gridDim.x + blockIdx.x;
+        if (threadIdx.x == 0) s_last = atomicAdd(counters + tile, 1u) == gridDim.z - 1;
+        __syncthreads();
+        if (!s_last) return;
+#pragma unroll
+        for (int i = 0; i < TR; ++i) {
+            const int64_t r = r0 + ty + 16 * i;
+            if (r >= n) continue;
+#pragma unroll
+            for (int j = 0; j < TC; ++j) {
+                const int c = c0 + tx + 16 * j;
+                if (c >= m) continue;
+                float v = 0.f;
+                for (unsigned sp = 0; sp < gridDim.z; ++sp)
+                    v += __hip_atomic_load(part + sp * n * m + r * m + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v += bias ? bias[c] : 0.f;
+                if (act) v = v >= 0.f ? v : v * slope;
+                out[r * m + c] = v;
+            }
+        }
+        if (threadIdx.x == 0) atomicExch(counters + tile, 0u);  // ready for the next launch
     }
 }
 
@@ -173,10 +216,20 @@ O3DML_API int o3dml_dense_act(const float* a1, int k1, const float* a2, int k2, 
         part = ws.take<float>(static_cast<int64_t>(p.splits) * n * m);
     }
     const dim3 grid(p.gx, p.gy, static_cast<unsigned>(p.splits));
-    float* dst = p.splits > 1 ? part : out;
+    // Split-K finished by each tile's last block (O3DML_DENSE_FUSED_REDUCE=1):
+    // bit-identical, but OFF by default — measured on RandLA (same-session
+    // A/B, graph-replayed patches) 15.8-16.0 vs 14.6-14.9 ms/frame: the
+    // agent-scope (write-through) slab traffic costs more than the reduce
+    // launch it saves, and a device-scope fence instead is 2x slower still.
+    static const bool fused_reduce = [] {
+        const char* e = std::getenv("O3DML_DENSE_FUSED_REDUCE");
+        return e ? std::atoi(e) != 0 : false;
+    }();
+    uint32_t* counters =
+            p.splits > 1 && fused_reduce ? tile_counters(st, static_cast<int64_t>(p.gx) * p.gy) : nullptr;
 #define O3DML_DENSE(TR, TC, S)                                                                                   \
     dense_act_kernel<TR, TC, S><<<grid, 256, 0, st>>>(a1, k1, a2, k2, a2_index, weight, bias, n, m,             \
-                                                      p.k_per_split, slope, act, dst)
+                                                      p.k_per_split, slope, act, out, part, counters)
 #define O3DML_DENSE_S(TR, TC)                          \
     do {                                               \
         if (p.splits > 1) O3DML_DENSE(TR, TC, true);   \
@@ -190,7 +243,7 @@ O3DML_API int o3dml_dense_act(const float* a1, int k1, const float* a2, int k2, 
 #undef O3DML_DENSE_S
 #undef O3DML_DENSE
     O3DML_LAUNCH_CHECK();
-    if (p.splits > 1) {
+    if (p.splits > 1 && !counters) {
         dense_split_reduce_kernel<<<stream_grid(n * m, 256), 256, 0, st>>>(part, p.splits, n, m, bias, slope, act,
                                                                           out);
         O3DML_LAUNCH_CHECK();

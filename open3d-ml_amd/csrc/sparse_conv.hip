@@ -29,6 +29,7 @@
 #include <array>
 #include <vector>
 
+#include "counters.hpp"
 #include "primitives.hpp"
 
 namespace o3dml {
@@ -252,6 +253,55 @@ __device__ __forceinline__ void gemm_finish(GemmStage& st, int c0, int h, const 
     for (int s = 0; s < 16; ++s) st.a[s] = (PRE ? pre_act(st.a[s], lps[cb + s], lpb[cb + s]) : st.a[s]) * sc;
 }
 
+// Split-K store: the wave writes its raw 32 x 32 partial tile into slab s;
+// with tile counters (counters.hpp) the LAST of the nsplit waves owning the
+// tile then sums the slabs in split order and applies split_reduce_kernel's
+// epilogue (same arithmetic, same bits) — no reduce launch.  orow32: the 32
+// output rows of the tile (-1 = none).
+__device__ __forceinline__ void split_store_finish(const f32x16& acc, const int32_t* orow32, int h, int col,
+                                                   int lane, int s, int nsplit, int64_t n_out, int cout,
+                                                   float* __restrict__ part, uint32_t* __restrict__ counters,
+                                                   int64_t tile, const float* __restrict__ oscale,
+                                                   const float* __restrict__ bias,
+                                                   const float* __restrict__ residual, float* __restrict__ out) {
+    const int64_t total = n_out * cout;
+    float* P = part + static_cast<int64_t>(s) * total;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t orr = orow32[(r & 3) + 8 * (r >> 2) + 4 * h];
+        if (orr >= 0 && col < cout) {
+            if (counters)  // agent-scope store: written through to the device-coherent level
+                __hip_atomic_store(P + orr * cout + col, acc[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                P[orr * cout + col] = acc[r];
+        }
+    }
+    if (!counters) return;  // split_reduce_kernel finishes
+    // arrival once the slab stores are complete (no device-scope fence: on the
+    // 8-XCD part it writes back the whole L2 per wave); the last wave reads
+    // the slabs with agent-scope loads
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t prev = 0;
+    if (lane == 0) prev = atomicAdd(counters + tile, 1u);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev != static_cast<uint32_t>(nsplit - 1)) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t orr = orow32[(r & 3) + 8 * (r >> 2) + 4 * h];
+        if (orr >= 0 && col < cout) {
+            const int64_t e = orr * cout + col;
+            float v = 0.f;
+            for (int sp = 0; sp < nsplit; ++sp)
+                v += __hip_atomic_load(part + sp * total + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (oscale) v *= oscale[orr];
+            if (bias) v += bias[col];
+            if (residual) v += residual[e];
+            out[e] = v;
+        }
+    }
+    if (lane == 0) atomicExch(counters + tile, 0u);  // ready for the next launch
+}
+
 template <bool VEC4, bool PRE>
 __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, const int* order_flag,
@@ -260,7 +310,8 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict_
                      const float* __restrict__ sscale, const float* __restrict__ pscale,
                      const float* __restrict__ Wt /*[K][cout][cin]*/, int cin, int cout,
                      const float* __restrict__ oscale, const float* __restrict__ bias, float* __restrict__ out,
-                     int nsplit, float* __restrict__ part, GemmPrologue pre, const float* __restrict__ residual) {
+                     int nsplit, float* __restrict__ part, GemmPrologue pre, const float* __restrict__ residual,
+                     uint32_t* __restrict__ counters) {
     __shared__ float lpre[PRE ? 2 * (kPreMax + 32) : 1];
     float* lps = lpre;
     float* lpb = lpre + (PRE ? kPreMax + 32 : 0);
@@ -365,13 +416,11 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict_
             if (j + 2 >= j1) break;
         }
     }
-    if (nsplit > 1) {  // raw partial sums; split_reduce_kernel applies oscale / bias / residual
-        float* P = part + static_cast<int64_t>(s) * n_out * cout;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int64_t orr = orow[(r & 3) + 8 * (r >> 2) + 4 * h];
-            if (orr >= 0 && col < cout) P[orr * cout + col] = acc[r];
-        }
+    if (nsplit > 1) {  // raw partial sums; the tile's last wave (or split_reduce_kernel) finishes
+        split_store_finish(acc, orow, h, col, lane, s, nsplit, n_out, cout, part, counters,
+                           (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * (kGemmThreads / 64) +
+                                   (threadIdx.x >> 6),
+                           oscale, bias, residual, out);
         return;
     }
     // epilogue: C/D map row = (r&3) + 8*(r>>2) + 4*(lane>>5), col = lane&31
@@ -545,7 +594,7 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
                          const float* __restrict__ pscale, const float* __restrict__ Wt /*[K][cout][cin]*/, int cin,
                          int cout, const float* __restrict__ oscale, const float* __restrict__ bias,
                          float* __restrict__ out, int nsplit, float* __restrict__ part, GemmPrologue pre,
-                         const float* __restrict__ residual) {
+                         const float* __restrict__ residual, uint32_t* __restrict__ counters) {
     __shared__ float lpre[PRE ? 2 * (kPreMax + 32) : 1];
     __shared__ __attribute__((aligned(16))) float stage_all[kGemmThreads / 64][BREG ? 1 : 2][32 * 32];
     __shared__ int32_t mtile_all[kGemmThreads / 64][32 * 32];
@@ -634,12 +683,9 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead DMA has landed before the wave exits
     }
     if (nsplit > 1) {
-        float* P = part + static_cast<int64_t>(s) * n_out * cout;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int64_t orr = orow[(r & 3) + 8 * (r >> 2) + 4 * h];
-            if (orr >= 0 && col < cout) P[orr * cout + col] = acc[r];
-        }
+        split_store_finish(acc, orow, h, col, lane, s, nsplit, n_out, cout, part, counters,
+                           (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * (kGemmThreads / 64) + w,
+                           oscale, bias, residual, out);
         return;
     }
 #pragma unroll
@@ -764,7 +810,7 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
                             const float* __restrict__ pscale, const float* __restrict__ Wt /*[K][cout][cin]*/,
                             int cin, int cout, const float* __restrict__ oscale, const float* __restrict__ bias,
                             float* __restrict__ out, int nsplit, float* __restrict__ part, GemmPrologue pre,
-                            const float* __restrict__ residual) {
+                            const float* __restrict__ residual, uint32_t* __restrict__ counters) {
     constexpr int R = 32 * RB;
     __shared__ float lpre[PRE ? 2 * (kPreMax + 32) : 1];
     __shared__ __attribute__((aligned(16))) float abuf[2][R * 32];
@@ -866,12 +912,9 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
         if (nsplit > 1) {
-            float* P = part + static_cast<int64_t>(s) * n_out * cout;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t orr = orow[32 * rb + (r & 3) + 8 * (r >> 2) + 4 * h];
-                if (orr >= 0 && col < cout) P[orr * cout + col] = acc[rb][r];
-            }
+            split_store_finish(acc[rb], orow + 32 * rb, h, col, lane, s, nsplit, n_out, cout, part, counters,
+                               ((static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * NW + w) * RB + rb,
+                               oscale, bias, residual, out);
             continue;
         }
 #pragma unroll
@@ -943,7 +986,7 @@ implicit_gemm_split_kernel(const int32_t* __restrict__ map, const int32_t* __res
                            const __bf16* __restrict__ bp /*[plane][K][cout][cin]*/, int64_t plane_b, int cin,
                            int cout, const float* __restrict__ oscale, const float* __restrict__ bias,
                            float* __restrict__ out, int nsplit, float* __restrict__ part,
-                           const float* __restrict__ residual) {
+                           const float* __restrict__ residual, uint32_t* __restrict__ counters) {
     constexpr int NP = NT == 6 ? 3 : 2;  // planes: hi, mid (, lo)
     constexpr int NB = NW == 1 ? 1 : 2;  // A image buffers
     constexpr int R = 32 * RB;           // output rows per tile
@@ -1079,12 +1122,9 @@ implicit_gemm_split_kernel(const int32_t* __restrict__ map, const int32_t* __res
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
         if (nsplit > 1) {
-            float* P = part + static_cast<int64_t>(s) * n_out * cout;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t orr = orow[32 * rb + (r & 3) + 8 * (r >> 2) + 4 * h];
-                if (orr >= 0 && col < cout) P[orr * cout + col] = acc[rb][r];
-            }
+            split_store_finish(acc[rb], orow + 32 * rb, h, col, lane, s, nsplit, n_out, cout, part, counters,
+                               ((static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * NW + w) * RB + rb,
+                               oscale, bias, residual, out);
             continue;
         }
 #pragma unroll
@@ -1513,6 +1553,18 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
     const dim3 g(static_cast<unsigned>(ceil_div(n_out, 32 * (kGemmThreads / 64))),
                  static_cast<unsigned>(ceil_div(cout, 32)), static_cast<unsigned>(ns));
     O3DML_REQUIRE(pre.scale == nullptr || cin <= kPreMax, "sparse_conv: prologue needs cin <= %d", kPreMax);
+    // split-K finished by each tile's last wave (split_store_finish); the wave
+    // tiles of every kernel variant number ceil(n_out / 32) x ceil(cout / 32)
+    // rounded up to whole workgroups
+    // OFF by default: neutral on the C4 layer (0.172-0.177 ms either way, same
+    // session) — kept selectable (O3DML_GEMM_FUSED_REDUCE=1), bit-identical
+    static const bool fused_reduce = [] {
+        const char* e = std::getenv("O3DML_GEMM_FUSED_REDUCE");
+        return e ? std::atoi(e) != 0 : false;
+    }();
+    uint32_t* counters = nullptr;
+    if (ns > 1 && fused_reduce)
+        counters = tile_counters(st, (ceil_div(n_out, 128) + 1) * 4 * (ceil_div(cout, 32) + 4));
     const int nt_mode = gemm_nt();
     if (g_presplit && nt_mode != 0 && vec4 && cin % 8 == 0 && pscale == nullptr && ws.base &&
         ws.used + presplit_bytes(n_src, K, cin, cout) <= ws.size) {
@@ -1556,7 +1608,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #define O3DML_GEMM_SP(NT, W, B)                                                                                   \
     implicit_gemm_split_kernel<NT, W, B><<<gs, W * 64, 0, st>>>(map, order, order_flag, K, n_out, ap, pa, bpl,    \
                                                                  pbn, cin, cout, oscale, bias, out, ns, part,      \
-                                                                 residual)
+                                                                 residual, counters)
 #define O3DML_GEMM_SP_W(NT, B)                                                                     \
     do {                                                                                           \
         if (nw == 4) O3DML_GEMM_SP(NT, 4, B); else if (nw == 2) O3DML_GEMM_SP(NT, 2, B); else O3DML_GEMM_SP(NT, 1, B); \
@@ -1571,7 +1623,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #undef O3DML_GEMM_SP
         O3DML_LAUNCH_CHECK();
         tr.end();
-        if (ns > 1) {
+        if (ns > 1 && !counters) {
             split_reduce_kernel<<<stream_grid(n_out * cout, 256), 256, 0, st>>>(part, ns, n_out, cout, oscale, bias,
                                                                                residual, out);
             O3DML_LAUNCH_CHECK();
@@ -1580,7 +1632,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
     }
 #define O3DML_GEMM_LAUNCH(V, P)                                                                                    \
     implicit_gemm_kernel<V, P><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, \
-                                                           bias, out, ns, part, pre, residual)
+                                                           bias, out, ns, part, pre, residual, counters)
     static const bool lds_path = [] {
         const char* e = std::getenv("O3DML_GEMM_LDS");
         return e ? std::atoi(e) != 0 : true;
@@ -1606,7 +1658,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #define O3DML_GEMM_SH(P, X, W, B)                                                                               \
     implicit_gemm_shared_kernel<P, X, W, B><<<gs, W * 64, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
                                                                    pscale, Wt, cin, cout, oscale, bias, out, ns,  \
-                                                                   part, pre, residual)
+                                                                   part, pre, residual, counters)
 #define O3DML_GEMM_SH_RB(P, X, W) \
     if (rb == 2) O3DML_GEMM_SH(P, X, W, 2); else O3DML_GEMM_SH(P, X, W, 1);
 #define O3DML_GEMM_SH_NT(P, W)                          \
@@ -1627,7 +1679,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #define O3DML_GEMM_LDS(P, BR, X)                                                                                  \
     implicit_gemm_lds_kernel<P, BR, X><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
                                                                    pscale, Wt, cin, cout, oscale, bias, out, ns,  \
-                                                                   part, pre, residual)
+                                                                   part, pre, residual, counters)
         const int nt = gemm_nt();
         if (nt == 6) {
             if (pre.scale) O3DML_GEMM_LDS(true, true, 6); else O3DML_GEMM_LDS(false, true, 6);
@@ -1647,7 +1699,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #undef O3DML_GEMM_LAUNCH
     O3DML_LAUNCH_CHECK();
     tr.end();
-    if (ns > 1) {
+    if (ns > 1 && !counters) {
         split_reduce_kernel<<<stream_grid(n_out * cout, 256), 256, 0, st>>>(part, ns, n_out, cout, oscale, bias,
                                                                            residual, out);
         O3DML_LAUNCH_CHECK();

@@ -242,6 +242,59 @@ __global__ void sub_lengths_kernel(const int64_t* __restrict__ bfirst, const int
     }
 }
 
+// Grid of each batch item on the device, in the host's float arithmetic
+// (origin = floor(min / dl) * dl, cells = floor((max - origin) / dl) + 1; the
+// library builds with -ffp-contract=off and IEEE division, so the same
+// roundings): no bbox read-back.  out[1] = 1 if a grid exceeds the 64-bit key
+// range (checked by the host with the totals).
+__global__ void sub_grid_kernel(const float* __restrict__ bbox, const int64_t* __restrict__ rs, int nb, float dl,
+                                SubBatch* __restrict__ sb, int64_t* __restrict__ out) {
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    const float inv = 1.0f / dl;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        SubBatch x;
+        x.dl = dl;
+        if (rs[b + 1] == rs[b]) {
+            x.ox = x.oy = x.oz = 0.f;
+            x.nx = x.ny = 1;
+        } else {
+            const float* bb = bbox + 6 * b;
+            x.ox = floorf(bb[0] * inv) * dl;
+            x.oy = floorf(bb[1] * inv) * dl;
+            x.oz = floorf(bb[2] * inv) * dl;
+            const float ex = floorf((bb[3] - x.ox) / dl), ey = floorf((bb[4] - x.oy) / dl),
+                        ez = floorf((bb[5] - x.oz) / dl);
+            if (!(ex < 1e15f && ey < 1e15f && ez < 1e15f)) {
+                bad = 1;
+                x.nx = x.ny = 1;
+            } else {
+                x.nx = static_cast<uint64_t>(ex) + 1;
+                x.ny = static_cast<uint64_t>(ey) + 1;
+                const uint64_t nz = static_cast<uint64_t>(ez) + 1;
+                if (static_cast<double>(x.nx) * x.ny * nz >= 2.8e14) bad = 1;
+            }
+        }
+        sb[b] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) out[1] = bad;
+}
+
+// out[0] = output points, out[2 + b] = output points of batch item b
+__global__ void sub_totals_kernel(const int64_t* __restrict__ incl, int64_t n, const int64_t* __restrict__ keep_incl,
+                                  const int64_t* __restrict__ bfirst, int nb, int64_t* __restrict__ out) {
+    const int64_t nseg = n > 0 ? incl[n - 1] : 0;
+    if (threadIdx.x == 0) out[0] = nseg > 0 ? keep_incl[nseg - 1] : 0;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        const int64_t f0 = bfirst[b], f1 = bfirst[b + 1];
+        const int64_t k0 = f0 == 0 ? 0 : keep_incl[f0 - 1];
+        const int64_t k1 = f1 == 0 ? 0 : keep_incl[f1 - 1];
+        out[2 + b] = k1 - k0;
+    }
+}
+
 // Shared "sorted segments" state in the workspace front (same layout for the
 // count and fill phases).
 struct SegState {
@@ -400,72 +453,67 @@ O3DML_API int o3dml_voxelize_fill(int64_t n_points, int ndim, int64_t n_batch, c
 O3DML_API size_t o3dml_grid_subsample_workspace_size(int64_t n_points, int64_t n_batch) {
     return seg_state_bytes(n_points, static_cast<int>(n_batch)) + ws_bytes<uint64_t>(n_points) +
            ws_bytes<SubBatch>(n_batch) + ws_bytes<float>(6 * n_batch) + sort_segments_ws_bytes(n_points) +
-           prim::scan_workspace_bytes(n_points);
+           prim::scan_workspace_bytes(n_points) + ws_bytes<int64_t>(2 + n_batch);
 }
 
-// Phase 1: grid per batch item (KPConv float arithmetic, on the host for the
-// origin), sort, caps.  Writes the number of output points to *n_out_host.
-O3DML_API int o3dml_grid_subsample_count(const float* points, int64_t n_points, int64_t n_batch,
-                                         const int64_t* row_splits, const int64_t* row_splits_host, float dl,
-                                         int64_t max_p, int64_t* n_out_host, void* workspace, size_t workspace_bytes,
-                                         void* stream) {
+// Phase 1 without a host synchronisation: grid per batch item (on the device,
+// sub_grid_kernel), sort, caps; out (device int64 [2 + n_batch]) receives the
+// number of output points, a grid-too-large flag and the output points per
+// batch item — the caller reads them (with other values) in one transfer.
+O3DML_API int o3dml_grid_subsample_count_async(const float* points, int64_t n_points, int64_t n_batch,
+                                               const int64_t* row_splits, float dl, int64_t max_p, int64_t* out,
+                                               void* workspace, size_t workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
     O3DML_REQUIRE(dl > 0.f, "sampleDl must be > 0");
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
     const int nb = static_cast<int>(n_batch);
+    if (n_points == 0) {
+        O3DML_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(int64_t) * (2 + nb), st));
+        return 0;
+    }
     SegState s = take_seg_state(ws, n_points, nb);
     uint64_t* keys = ws.take<uint64_t>(n_points);
     SubBatch* sb_d = ws.take<SubBatch>(nb);
     float* bbox_d = ws.take<float>(6 * nb);
-    std::vector<SubBatch> sb(nb);
-    if (n_points > 0) {
-        launch_bbox(points, row_splits, nb, bbox_d, st);
-        O3DML_LAUNCH_CHECK();
-        std::vector<float> bb(6 * nb);
-        O3DML_CHECK_HIP(hipMemcpyAsync(bb.data(), bbox_d, sizeof(float) * 6 * nb, hipMemcpyDeviceToHost, st));
-        O3DML_CHECK_HIP(hipStreamSynchronize(st));
-        const float inv = 1.0f / dl;
-        for (int b = 0; b < nb; ++b) {
-            SubBatch& x = sb[b];
-            x.dl = dl;
-            if (row_splits_host[b + 1] == row_splits_host[b]) {
-                x.ox = x.oy = x.oz = 0.f;
-                x.nx = x.ny = 1;
-                continue;
-            }
-            volatile float t0 = bb[6 * b] * inv, t1 = bb[6 * b + 1] * inv, t2 = bb[6 * b + 2] * inv;
-            x.ox = std::floor(static_cast<float>(t0)) * dl;
-            x.oy = std::floor(static_cast<float>(t1)) * dl;
-            x.oz = std::floor(static_cast<float>(t2)) * dl;
-            volatile float ex = (bb[6 * b + 3] - x.ox) / dl, ey = (bb[6 * b + 4] - x.oy) / dl,
-                           ez = (bb[6 * b + 5] - x.oz) / dl;
-            x.nx = static_cast<uint64_t>(std::floor(static_cast<float>(ex))) + 1;
-            x.ny = static_cast<uint64_t>(std::floor(static_cast<float>(ey))) + 1;
-            const uint64_t nz = static_cast<uint64_t>(std::floor(static_cast<float>(ez))) + 1;
-            O3DML_REQUIRE(static_cast<double>(x.nx) * x.ny * nz < 2.8e14, "grid_subsample: grid too large");
-        }
-        O3DML_CHECK_HIP(hipMemcpyAsync(sb_d, sb.data(), sizeof(SubBatch) * nb, hipMemcpyHostToDevice, st));
-        O3DML_CHECK_HIP(hipStreamSynchronize(st));
-        sub_keys_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(points, n_points, row_splits, nb, sb_d, keys);
-        O3DML_LAUNCH_CHECK();
-    }
+    launch_bbox(points, row_splits, nb, bbox_d, st);
+    O3DML_LAUNCH_CHECK();
+    sub_grid_kernel<<<1, 256, 0, st>>>(bbox_d, row_splits, nb, dl, sb_d, out);
+    O3DML_LAUNCH_CHECK();
+    sub_keys_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(points, n_points, row_splits, nb, sb_d, keys);
+    O3DML_LAUNCH_CHECK();
     const uint64_t invalid = ~uint64_t(0);
     sort_segments(keys, n_points, 48 + prim::bits_needed(static_cast<uint64_t>(nb > 1 ? nb - 1 : 0)), invalid, nb,
                   true, 48, s, ws, st);
-    if (n_points > 0) {
-        sub_caps_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(s.start, s.incl, n_points, s.sk, s.bfirst, max_p,
-                                                                   s.keep);
-        O3DML_LAUNCH_CHECK();
-        Workspace sws = ws;
-        prim::scan<int64_t, int64_t>(s.keep, s.keep_incl, n_points, true, sws, st);
-    }
-    vox_totals_kernel<<<1, 64, 0, st>>>(s.incl, n_points, s.keep_incl, s.keep_incl, s.scalars + 1);
+    sub_caps_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(s.start, s.incl, n_points, s.sk, s.bfirst, max_p,
+                                                               s.keep);
     O3DML_LAUNCH_CHECK();
-    int64_t tot[3];
-    O3DML_CHECK_HIP(hipMemcpyAsync(tot, s.scalars + 1, sizeof(tot), hipMemcpyDeviceToHost, st));
+    Workspace sws = ws;
+    prim::scan<int64_t, int64_t>(s.keep, s.keep_incl, n_points, true, sws, st);
+    sub_totals_kernel<<<1, 256, 0, st>>>(s.incl, n_points, s.keep_incl, s.bfirst, nb, out);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+// Phase 1 with the read-back: writes the number of output points to *n_out_host.
+O3DML_API int o3dml_grid_subsample_count(const float* points, int64_t n_points, int64_t n_batch,
+                                         const int64_t* row_splits, const int64_t* row_splits_host, float dl,
+                                         int64_t max_p, int64_t* n_out_host, void* workspace, size_t workspace_bytes,
+                                         void* stream) {
+    O3DML_GUARD_BEGIN
+    (void)row_splits_host;
+    hipStream_t st = as_stream(stream);
+    const size_t front = o3dml_grid_subsample_workspace_size(n_points, n_batch) - ws_bytes<int64_t>(2 + n_batch);
+    O3DML_REQUIRE(workspace_bytes >= front + ws_bytes<int64_t>(2), "grid_subsample: workspace too small");
+    int64_t* out = reinterpret_cast<int64_t*>(static_cast<char*>(workspace) + front);
+    const int rc = o3dml_grid_subsample_count_async(points, n_points, n_batch, row_splits, dl, max_p, out, workspace,
+                                                    front, stream);
+    if (rc != 0) return rc;
+    int64_t tot[2];
+    O3DML_CHECK_HIP(hipMemcpyAsync(tot, out, sizeof(tot), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
-    *n_out_host = tot[1];
+    O3DML_REQUIRE(tot[1] == 0, "grid_subsample: grid too large");
+    *n_out_host = tot[0];
     O3DML_GUARD_END
 }
 

@@ -88,8 +88,11 @@ def min_d2(q_pts, s_pts, neighb_inds, kernel_points):
     n, nb = nbr.shape
     K = kernel_points.shape[-2]
     col = torch.empty((n, K), dtype=torch.int32, device=dev)
-    _lib.call("o3dml_kpconv_min_d2_columns", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr.contiguous()),
-              index_bits(nbr.dtype), nb, ptr(kernel_points.detach().contiguous()), K, ptr(col),
+    # operands bound to names: a temporary freed inside the argument list could
+    # be handed to the next temporary by the caching allocator before the launch
+    nbr_c, kp_c = nbr.contiguous(), kernel_points.detach().contiguous()
+    _lib.call("o3dml_kpconv_min_d2_columns", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr_c),
+              index_bits(nbr.dtype), nb, ptr(kp_c), K, ptr(col),
               stream_handle(dev))
     s_ext = torch.cat((s_pts, torch.zeros_like(s_pts[:1, :]) + 1e6), 0)
     ids = torch.gather(nbr.long(), 1, col.long()).clamp_(0, s_pts.shape[0])

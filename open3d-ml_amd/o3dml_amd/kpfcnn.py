@@ -436,8 +436,11 @@ def _rotate(points, splits, R, transpose=False):
     """p' = p @ R[b] per batch element in fp32 with the reference's rounding
     ((p0 R0j + p1 R1j) + p2 R2j, each product rounded; kpconv.py:2087-2090)."""
     Rt = to_dev(np.ascontiguousarray(R.transpose(0, 2, 1) if transpose else R), points.device)
+    # the repeats through the non-blocking upload and output_size given: no
+    # host synchronisation (a pageable copy / a size read would stall the stream)
     b = torch.repeat_interleave(torch.arange(len(splits) - 1, device=points.device),
-                                torch.as_tensor(np.diff(splits), device=points.device))
+                                to_dev(np.diff(splits).astype(np.int64), points.device),
+                                output_size=int(splits[-1]))
     Rb = Rt[b]  # [N, 3, 3]
     return (points[:, 0:1] * Rb[:, 0] + points[:, 1:2] * Rb[:, 1]) + points[:, 2:3] * Rb[:, 2]
 
@@ -478,6 +481,80 @@ def batch_neighbors(queries, supports, q_lengths, s_lengths, radius, hash_table=
                                          hash_table=hash_table)
 
 
+# ---------------------------------------------------------------------------
+# collate in two host reads per layer: every search count / subsampling count
+# of a stage is queued, then their sizes come back in ONE pinned transfer
+# (the reference reads each size separately: ~9 host round trips per layer)
+# ---------------------------------------------------------------------------
+def _read_host(dev, vals):
+    """Device int64 values (scalars or 1-D) -> Python ints, one transfer + one wait."""
+    flat = torch.cat([v.reshape(-1).to(torch.int64) for v in vals])
+    host = ops._pinned_slot(dev, flat.numel())
+    host.copy_(flat, non_blocking=True)
+    ready = torch.cuda.Event()
+    ready.record(torch.cuda.current_stream(dev))
+    ready.synchronize()
+    return host.tolist()
+
+
+def _dense_begin(queries, supports, q_lengths, s_lengths, radius, table=None):
+    """batch_neighbors, count phase: (rs, state, device [total, long rows, width])."""
+    rs, state = ops._frs_count(supports, queries, radius, _splits(s_lengths), _splits(q_lengths),
+                               None if table is None else table.hash_table_splits,
+                               None if table is None else table.hash_table_index,
+                               None if table is None else table.hash_table_cell_splits, "L2", False, False)
+    m = queries.shape[0]
+    vals = (torch.stack([rs[-1], state[1][:8].view(torch.int64)[0], (rs[1:] - rs[:-1]).max()]) if m
+            else torch.zeros(3, dtype=torch.int64, device=rs.device))
+    return rs, state, vals, supports.shape[0], m
+
+
+def _dense_end(b, host):
+    """batch_neighbors, fill phase from the host values [total, long rows, width]."""
+    rs, state, _, n_sup, m = b
+    if m == 0:
+        return torch.zeros((0, 0), dtype=torch.int32, device=rs.device)
+    total, n_over, width = host
+    idx, dist = ops._frs_alloc(state, total, torch.int32)
+    ops._frs_launch_fill(rs, state, idx, dist, -1, 1 | (2 if n_over else 0))
+    return ops.ragged_to_dense(idx.reshape(-1, 1), rs, width,
+                               torch.tensor([n_sup], dtype=torch.int32)).squeeze(2)
+
+
+def _subsample_begin(points, lengths, sampleDl, rotations=None):
+    """batch_grid_subsampling, count phase (rotation drawn here, as the reference)."""
+    lengths = np.asarray(lengths, np.int64)
+    splits = np.zeros(len(lengths) + 1, np.int64)
+    splits[1:] = np.cumsum(lengths)
+    R = random_rotations(len(lengths)) if rotations is None else np.asarray(rotations, np.float32)
+    pts = _rotate(points, splits, R).contiguous()
+    dev = pts.device
+    lib = _lib.load()
+    n, B = pts.shape[0], len(lengths)
+    ws = workspace(lib.o3dml_grid_subsample_workspace_size(n, B), dev)
+    out = torch.empty(2 + B, dtype=torch.int64, device=dev)
+    _lib.call("o3dml_grid_subsample_count_async", ptr(pts), n, B, ptr(to_dev(splits, dev)), float(sampleDl), 0,
+              ptr(out), ptr(ws), ws.numel(), stream_handle(dev))
+    return pts, n, B, ws, out, R
+
+
+def _subsample_end(b, host):
+    """batch_grid_subsampling, fill phase from host [points, flag, lengths...]."""
+    pts, n, B, ws, _, R = b
+    if host[1]:
+        raise RuntimeError("grid_subsample: grid too large")
+    S = int(host[0])
+    s_len = np.asarray(host[2:2 + B], np.int64)
+    dev = pts.device
+    out_p = torch.empty((S, 3), dtype=torch.float32, device=dev)
+    out_l = torch.empty(B, dtype=torch.int64, device=dev)
+    _lib.call("o3dml_grid_subsample_fill", ptr(pts), n, B, None, 0, None, 0, ptr(out_p), None, None, ptr(out_l),
+              ptr(ws), ws.numel(), stream_handle(dev))
+    s_splits = np.zeros(B + 1, np.int64)
+    s_splits[1:] = np.cumsum(s_len)
+    return _rotate(out_p, s_splits, R, transpose=True), s_len
+
+
 def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_lengths, neighborhood_limits=(),
                         rotations=None):
     """concat_batcher.py:186-283 on the GPU.  ``rotations`` optionally fixes
@@ -502,22 +579,30 @@ def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_len
             continue
         deform = any("deformable" in b for b in layer_blocks)
         table = None  # hash table of this layer's points at r_normal: shared by the conv and pool searches
+        # stage 1: the conv search count and the subsampling count, one read
+        conv_b = sub_b = None
         if layer_blocks:
             r = r_normal * cfg.deform_radius / cfg.conv_radius if deform else r_normal
             if r == r_normal:
                 table = ops.build_spatial_hash_table(stacked_points, r, _splits(stack_lengths))
-            conv_i = batch_neighbors(stacked_points, stacked_points, stack_lengths, stack_lengths, r, table)
-        else:
-            conv_i = empty
-        if "pool" in block or "strided" in block:
+            conv_b = _dense_begin(stacked_points, stacked_points, stack_lengths, stack_lengths, r, table)
+        pooling = "pool" in block or "strided" in block
+        if pooling:
             dl = 2 * r_normal / cfg.conv_radius
             rot = None if rotations is None else rotations[sub_i]
             sub_i += 1
-            pool_p, pool_b = batch_grid_subsampling(stacked_points, stack_lengths, dl, rotations=rot)
+            sub_b = _subsample_begin(stacked_points, stack_lengths, dl, rotations=rot)
+        host = _read_host(dev, ([conv_b[2]] if conv_b else []) + ([sub_b[4]] if sub_b else []))
+        conv_i = _dense_end(conv_b, host[:3]) if conv_b else empty
+        if pooling:
+            pool_p, pool_b = _subsample_end(sub_b, host[3:] if conv_b else host)
             r = r_normal * cfg.deform_radius / cfg.conv_radius if "deformable" in block else r_normal
-            pool_i = batch_neighbors(pool_p, stacked_points, pool_b, stack_lengths, r,
-                                     table if r == r_normal else None)
-            up_i = batch_neighbors(stacked_points, pool_p, stack_lengths, pool_b, 2 * r)
+            # stage 2: the pool and up-sampling search counts, one read
+            pb = _dense_begin(pool_p, stacked_points, pool_b, stack_lengths, r, table if r == r_normal else None)
+            ub = _dense_begin(stacked_points, pool_p, stack_lengths, pool_b, 2 * r)
+            host = _read_host(dev, [pb[2], ub[2]])
+            pool_i = _dense_end(pb, host[:3])
+            up_i = _dense_end(ub, host[3:])
         else:
             pool_i = empty
             pool_p = torch.zeros((0, 3), dtype=torch.float32, device=dev)

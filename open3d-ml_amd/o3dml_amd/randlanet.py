@@ -83,7 +83,11 @@ def dense_act(a1, w, b, slope=None, a2=None, a2_index=None):
     out = torch.empty((n, m), dtype=torch.float32, device=a1.device)
     nbytes = _lib.load().o3dml_dense_act_workspace_size(n, k1 + k2, m)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=a1.device) if nbytes else None
-    _lib.call("o3dml_dense_act", ptr(a1.contiguous()), k1, ptr(None if a2 is None else a2.contiguous()), k2,
+    # operands bound to names: a temporary freed inside the argument list could
+    # be handed to the next temporary by the caching allocator before the launch
+    a1 = a1.contiguous()
+    a2 = None if a2 is None else a2.contiguous()
+    _lib.call("o3dml_dense_act", ptr(a1), k1, ptr(a2), k2,
               ptr(a2_index), ptr(w), ptr(b), n, m, int(slope is not None), float(slope or 0.0), ptr(out), ptr(ws),
               0 if ws is None else ws.numel(), stream_handle(a1.device))
     return out

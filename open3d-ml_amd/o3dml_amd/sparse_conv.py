@@ -372,9 +372,10 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
         if res is not None and tuple(res.shape) != (n_out, cout):
             raise ValueError("sparse_conv: residual must be [n_out, cout]")
         fws = workspace(lib.o3dml_sparse_conv_forward_workspace_size(n_out, n_in, K, cin, cout), dev)
+        x_c, b_c = x.detach().contiguous(), None if b is None else b.detach().contiguous()
         _lib.call("o3dml_sparse_conv_forward_fused", ptr(_transposed_filters(f)), K, cin, cout,
-                  ptr(x.detach().contiguous()), n_in, ptr(ps), ptr(pb), ptr(res),
-                  ptr(None if b is None else b.detach().contiguous()), n_out, ptr(out), ptr(mws), mws.numel(),
+                  ptr(x_c), n_in, ptr(ps), ptr(pb), ptr(res),
+                  ptr(b_c), n_out, ptr(out), ptr(mws), mws.numel(),
                   ptr(fws), fws.numel(), stream_handle(dev))
         return out if _late_ok(late) else None
     empty = torch.empty(0, dtype=torch.int64, device=dev)

@@ -207,7 +207,33 @@ def test_update_probs_matches_reference_float16(cuda):
     ref = tp.copy()
     ref[idxs] = 0.95 * ref[idxs] + (1 - 0.95) * probs
     t = torch.from_numpy(tp).to(cuda)
-    _lib.call("o3dml_randla_update_probs", ptr(torch.from_numpy(probs).to(cuda)),
-              ptr(torch.from_numpy(idxs.astype(np.int64)).to(cuda)), None, 1000, 19, 0.95, 1, ptr(t),
-              stream_handle(cuda))
+    p_d = torch.from_numpy(probs).to(cuda)  # named: a temporary could be recycled before the launch
+    i_d = torch.from_numpy(idxs.astype(np.int64)).to(cuda)
+    _lib.call("o3dml_randla_update_probs", ptr(p_d), ptr(i_d), None, 1000, 19, 0.95, 1, ptr(t), stream_handle(cuda))
     assert np.array_equal(t.cpu().numpy(), ref)
+
+
+def test_dense_fused_split_reduce_bitwise(cuda):
+    """The optional split-K finish in the last-arriving block of each tile
+    (O3DML_DENSE_FUSED_REDUCE=1, per-tile counters) against the default
+    two-launch form: same split order, so bit-identical (child processes:
+    the switch is read once)."""
+    import os
+    import subprocess
+    import sys
+    code = ("import torch,sys; sys.path.insert(0,'open3d-ml_amd'); from o3dml_amd.randlanet import dense_act;"
+            "torch.manual_seed(0); r=[]\n"
+            "for n,k,m in ((704,768,512),(2816,256,128),(176,512,512),(45056,8,16)):\n"
+            "  a=torch.randn((n,k),device='cuda'); w=torch.randn((m,k),device='cuda')/k**0.5; b=torch.randn(m,device='cuda')\n"
+            "  r.append(dense_act(a,w,b,0.2).cpu())\n"
+            "torch.save(r, sys.argv[1])")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for flag in ("1", "0"):
+        path = os.path.join(root, "gpurun_out", f"dense_reduce_{flag}.pt")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        env = dict(os.environ, O3DML_DENSE_FUSED_REDUCE=flag)
+        subprocess.run([sys.executable, "-c", code, path], check=True, env=env, cwd=root, timeout=120)
+        outs.append(torch.load(path, weights_only=True))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

@@ -339,3 +339,41 @@ def test_presplit_fused_eval_bitwise_equal(cuda):
         assert torch.equal(outs[0], outs[1])
     finally:
         lib.o3dml_sparse_conv_set_presplit(prev)
+
+
+def test_split_k_last_wave_finish_bitwise(cuda):
+    """Split-K GEMMs (deep SparseConvUnet levels) optionally finish in the
+    last-arriving wave of each tile (O3DML_GEMM_FUSED_REDUCE=1) instead of a
+    split_reduce_kernel launch: same slab order and epilogue, so
+    bit-identical (child processes: the switch is read once).  Eval (BN/ReLU prologue +
+    residual epilogue) and a training forward + backward (dIn split too)."""
+    import os
+    import subprocess
+    import sys
+    code = ("import sys, types, torch; sys.path.insert(0, 'open3d-ml_amd')\n"
+            "from o3dml_amd.sparseconvnet import SparseConvUnet\n"
+            "torch.manual_seed(0)\n"
+            "m = SparseConvUnet(multiplier=16, residual_blocks=True, conv_block_reps=1, num_classes=5).cuda()\n"
+            "g = torch.Generator().manual_seed(1)\n"
+            "pos = (torch.rand((30000, 3), generator=g) * torch.tensor([200., 200., 30.])).cuda()\n"
+            "inp = types.SimpleNamespace(point=[pos], feat=[torch.rand((30000, 3), generator=g).cuda()],"
+            " batch_lengths=[30000])\n"
+            "m.eval()\n"
+            "with torch.no_grad():\n"
+            "    a = m(inp)\n"
+            "m.train()\n"
+            "out = m(inp)\n"
+            "out.square().sum().backward()\n"
+            "torch.save([a.cpu(), out.detach().cpu()] + [p.grad.cpu() for p in m.parameters() if p.grad is not None],"
+            " sys.argv[1])\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for flag in ("1", "0"):
+        path = os.path.join(root, "gpurun_out", f"sc_reduce_{flag}.pt")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        env = dict(os.environ, O3DML_GEMM_FUSED_REDUCE=flag)
+        subprocess.run([sys.executable, "-c", code, path], check=True, env=env, cwd=root, timeout=180)
+        outs.append(torch.load(path, weights_only=True))
+    assert len(outs[0]) == len(outs[1]) > 2
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

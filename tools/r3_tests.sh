@@ -5,7 +5,7 @@ cd ${GRAFT_REPO_ROOT:-/root/repo}
 D=gpurun_out/${TAG:-r3}
 mkdir -p $D
 timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -v --maxfail=10 --timeout 120 --timeout-method thread \
-    ${PYTEST_ARGS:-} > $D/pytest.log 2>&1; rc=$?
+    ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > $D/pytest.log 2>&1; rc=$?
 tail -15 $D/pytest.log
 [ $rc -le 1 ] || exit $rc
 if [ -n "${BENCH:-}" ]; then
