@@ -189,6 +189,9 @@ int o3dml_randla_possibility_min(const double* possibility, int64_t n, const flo
 /* dst[i] = src[perm(i)], perm a keyed (seed) bijection of [0, n) (Feistel
  * network + cycle walking): the patch shuffle. */
 int o3dml_random_permute(const int64_t* src, int64_t n, uint64_t seed, int64_t* dst, void* stream);
+/* keyed from device state: seed_state u64 [2] (base, counter), key =
+ * splitmix64(base + counter), then counter += 1 (capturable patch step) */
+int o3dml_random_permute_dev(const int64_t* src, int64_t n, uint64_t* seed_state, int64_t* dst, void* stream);
 /* test_probs[idxs[i]] = smooth * test_probs[idxs[i]] + (1 - smooth) * probs[i]
  * (randlanet.py:441-465), probs f32 [n, c]; store f16 (store_half: the
  * reference's float16 test_probs arithmetic) or f32; keep masks duplicates. */

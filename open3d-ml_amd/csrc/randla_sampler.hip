@@ -246,8 +246,19 @@ __device__ __forceinline__ uint32_t feistel_mix(uint32_t x, uint32_t key) {
     return x;
 }
 
+// seed_state (device u64 [2]: base, patch counter): the patch's key is
+// splitmix64(base + counter), so a captured patch step draws a new
+// permutation per replay (seed_advance_kernel bumps the counter after it)
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
 __global__ void random_permute_kernel(const int64_t* __restrict__ src, int64_t n, int half, uint64_t seed,
-                                      int64_t* __restrict__ dst) {
+                                      const uint64_t* __restrict__ seed_state, int64_t* __restrict__ dst) {
+    if (seed_state) seed = splitmix64(seed_state[0] + seed_state[1]);
     const uint32_t mask = (1u << half) - 1u;
     const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
     const uint32_t keys[4] = {k0, k1, k0 ^ 0xA5A5A5A5u, k1 ^ 0x3C3C3C3Cu};
@@ -325,7 +336,30 @@ O3DML_API int o3dml_random_permute(const int64_t* src, int64_t n, uint64_t seed,
     int bits = 1;
     while ((int64_t(1) << bits) < n) ++bits;
     const int half = (bits + 1) / 2;
-    random_permute_kernel<<<stream_grid(n, 256), 256, 0, as_stream(stream)>>>(src, n, half, seed, dst);
+    random_permute_kernel<<<stream_grid(n, 256), 256, 0, as_stream(stream)>>>(src, n, half, seed, nullptr, dst);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+__global__ void seed_advance_kernel(uint64_t* seed_state) {
+    if (threadIdx.x == 0) seed_state[1] += 1;
+}
+
+// The same permutation keyed from device state (seed_state u64 [2]: base,
+// counter; key = splitmix64(base + counter)), then counter += 1 — no host
+// argument changes between patches, so the patch step can be a replayed graph.
+O3DML_API int o3dml_random_permute_dev(const int64_t* src, int64_t n, uint64_t* seed_state, int64_t* dst,
+                                       void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "random_permute: n out of range");
+    hipStream_t st = as_stream(stream);
+    if (n > 0) {
+        int bits = 1;
+        while ((int64_t(1) << bits) < n) ++bits;
+        random_permute_kernel<<<stream_grid(n, 256), 256, 0, st>>>(src, n, (bits + 1) / 2, 0, seed_state, dst);
+        O3DML_LAUNCH_CHECK();
+    }
+    seed_advance_kernel<<<1, 64, 0, st>>>(seed_state);
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }

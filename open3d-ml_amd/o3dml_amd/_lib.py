@@ -97,6 +97,7 @@ SIGNATURES = {
     "o3dml_randla_possibility_min": (c_i32, [c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "o3dml_randla_possibility_min_workspace_size": (c_sz, []),
     "o3dml_random_permute": (c_i32, [c_p, c_i64, c_u64, c_p, c_p]),
+    "o3dml_random_permute_dev": (c_i32, [c_p, c_i64, c_p, c_p, c_p]),
     "o3dml_randla_update_probs": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_f64, c_i32, c_p, c_p]),
     "o3dml_randla_patch_workspace_size": (c_sz, [c_i64]),
     "o3dml_randla_patch_update": (c_i32, [c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),

@@ -435,6 +435,143 @@ def _last_occurrence(idxs, n):
     return last[idxs] == pos
 
 
+_CAP_STEP = 16384  # cloud capacity granularity of a patch-step state (and graph)
+_FAR = 1.0e9       # padding points: never within a patch of a real point
+
+
+class _PatchStep:
+    """One whole patch of the spatially-regular sampler as a fixed sequence of
+    launches over preallocated buffers — crop kNN (k = num_points), keyed
+    shuffle (device seed state), possibility update + recentring, the
+    per-level k-lists (one batched search), up-sampling ids, the network,
+    the test_probs EMA and the next centre (min possibility into pinned
+    memory) — with no host synchronisation and no host value that changes
+    between patches, so it is captured once as a HIP graph and replayed per
+    patch (SemSegInference.run).  The cloud lives in a buffer of ``cap``
+    points (sub-sampled cloud + far padding with possibility +inf: never a
+    centre, never in a crop), so clouds of similar size reuse the graph."""
+
+    def __init__(self, inf, cap):
+        model, dev = inf.model, inf.device
+        cfg = model.cfg
+        lib = _lib.load()
+        self.inf, self.cap, self.dev = inf, cap, dev
+        k, n_pts = cfg["num_neighbors"], cfg["num_points"]
+        self.n_pts = n_pts
+        self.sub = torch.empty((cap, 3), dtype=torch.float32, device=dev)
+        self.poss = torch.empty(cap, dtype=torch.float64, device=dev)
+        self.probs = torch.zeros((cap, cfg["num_classes"]), dtype=inf.probs_dtype, device=dev)
+        self.seeds = torch.zeros(2, dtype=torch.int64, device=dev)  # u64 base, counter
+        self.arg = torch.empty(1, dtype=torch.int64, device=dev)
+        self.center = torch.empty(3, dtype=torch.float32, device=dev)
+        self.host_min = torch.empty(1, dtype=torch.float64, pin_memory=True)
+        self.min_ws = torch.empty(max(lib.o3dml_randla_possibility_min_workspace_size(), 1), dtype=torch.uint8,
+                                  device=dev)
+        # crop: one query (the centre) against the padded cloud
+        self.crop_prs = np.array([0, cap], np.int64)
+        self.crop_qrs = np.array([0, 1], np.int64)
+        self.crop_prs_d = torch.from_numpy(self.crop_prs).to(dev)
+        self.crop_qrs_d = torch.from_numpy(self.crop_qrs).to(dev)
+        self.crop_rs = torch.empty(2, dtype=torch.int64, device=dev)
+        self.crop_ws = torch.empty(max(lib.o3dml_knn_search_workspace_size(cap, 1, n_pts, 1), 1),
+                                   dtype=torch.uint8, device=dev)
+        self.crop = torch.empty(n_pts, dtype=torch.int64, device=dev)
+        self.idxs = torch.empty(n_pts, dtype=torch.int64, device=dev)
+        self.pc = torch.empty((n_pts, 3), dtype=torch.float32, device=dev)
+        self.patch_ws = torch.empty(max(lib.o3dml_randla_patch_workspace_size(n_pts), 1), dtype=torch.uint8,
+                                    device=dev)
+        # levels: prefixes of the shuffled patch, one batched self-kNN
+        L = cfg["num_layers"]
+        sizes = [n_pts]
+        for i in range(L):
+            sizes.append(sizes[-1] // cfg["sub_sampling_ratio"][i])
+        self.sizes = sizes
+        self.rs = np.concatenate([[0], np.cumsum(sizes[:L])]).astype(np.int64)
+        self.srs = np.concatenate([[0], np.cumsum(sizes[1:])]).astype(np.int64)
+        self.nxt = np.asarray(sizes[1:], np.int64)
+        total = int(self.rs[-1])
+        self.rs_d = torch.from_numpy(self.rs).to(dev)
+        self.cat = torch.empty((total, 3), dtype=torch.float32, device=dev)
+        self.k = k
+        self.knn_rs = torch.empty(total + 1, dtype=torch.int64, device=dev)
+        self.knn_ws = torch.empty(max(lib.o3dml_knn_search_workspace_size(total, total, k, L), 1),
+                                  dtype=torch.uint8, device=dev)
+        self.nb = torch.empty((total, k), dtype=torch.int32, device=dev)
+        self.up = torch.empty(total, dtype=torch.int64, device=dev)
+        self.up_ws = torch.empty(max(lib.o3dml_randla_up_workspace_size(total), 1), dtype=torch.uint8, device=dev)
+        self.plan = (sizes, self.rs, self.srs)
+        self.graph = None
+
+    def begin(self, sub, poss0, base_seed):
+        """Load a frame: the sub-sampled cloud, its initial possibilities, a
+        fresh shuffle key; the first centre."""
+        n = sub.shape[0]
+        self.sub[:n].copy_(sub)
+        self.sub[n:].fill_(_FAR)
+        self.poss[:n].copy_(poss0)
+        self.poss[n:].fill_(float("inf"))
+        self.probs.zero_()
+        self.seeds.copy_(torch.tensor([base_seed, 0], dtype=torch.int64))
+        self._next_centre(stream_handle(self.dev))
+
+    def _next_centre(self, st):
+        _lib.call("o3dml_randla_possibility_min", ptr(self.poss), self.cap, ptr(self.sub), ptr(self.arg),
+                  ptr(self.center), self.host_min.data_ptr(), ptr(self.min_ws), self.min_ws.numel(), st)
+
+    def step(self):
+        """The launches of one patch (graph-capturable)."""
+        inf, st, n_pts = self.inf, stream_handle(self.dev), self.n_pts
+        k, L = self.k, len(self.nxt)
+        # crop: the num_points nearest sub-points of the centre, (distance, index) order
+        _lib.call("o3dml_knn_search_count", ptr(self.sub), self.cap, ptr(self.center), 1, n_pts, 1,
+                  ptr(self.crop_prs_d), ptr(self.crop_qrs_d), self.crop_prs.ctypes.data, self.crop_qrs.ctypes.data,
+                  0, 0, 0, ptr(self.crop_rs), ptr(self.crop_ws), self.crop_ws.numel(), st)
+        _lib.call("o3dml_knn_search_fill", ptr(self.sub), self.cap, ptr(self.center), 1, n_pts, 1,
+                  ptr(self.crop_qrs_d), self.crop_prs.ctypes.data, self.crop_qrs.ctypes.data, 0, 0,
+                  ptr(self.crop_rs), 64, ptr(self.crop), None, ptr(self.crop_ws), self.crop_ws.numel(), st)
+        # the shuffle (random.shuffle, semseg_spatially_regular.py:100): keyed bijection
+        _lib.call("o3dml_random_permute_dev", ptr(self.crop), n_pts, ptr(self.seeds), ptr(self.idxs), st)
+        # pc = sub[idxs], possibilities += delta, x / y recentred
+        _lib.call("o3dml_randla_patch_update", ptr(self.sub), ptr(self.idxs), n_pts, ptr(self.center), None,
+                  ptr(self.poss), ptr(self.pc), ptr(self.patch_ws), self.patch_ws.numel(), st)
+        torch.cat([self.pc[:self.sizes[i]] for i in range(L)], out=self.cat)
+        total = self.cat.shape[0]
+        _lib.call("o3dml_knn_search_count", ptr(self.cat), total, ptr(self.cat), total, k, L, ptr(self.rs_d),
+                  ptr(self.rs_d), self.rs.ctypes.data, self.rs.ctypes.data, 0, 0, 1, ptr(self.knn_rs),
+                  ptr(self.knn_ws), self.knn_ws.numel(), st)
+        _lib.call("o3dml_knn_search_fill", ptr(self.cat), total, ptr(self.cat), total, k, L, ptr(self.rs_d),
+                  self.rs.ctypes.data, self.rs.ctypes.data, 0, 0, ptr(self.knn_rs), 32, ptr(self.nb), None,
+                  ptr(self.knn_ws), self.knn_ws.numel(), st)
+        _lib.call("o3dml_randla_up_from_knn", ptr(self.nb), k, ptr(self.cat), L, self.rs.ctypes.data,
+                  self.nxt.ctypes.data, self.srs.ctypes.data, ptr(self.up), ptr(self.up_ws), self.up_ws.numel(), st)
+        probs = inf._patch_probs(self.pc, self.nb, self.up, self.plan)
+        inf.update_probs(self.probs, self.idxs, probs)
+        self._next_centre(st)
+
+    def run_step(self, use_graph):
+        if not use_graph:
+            self.step()
+            return
+        if self.graph is None:
+            # warm-up outside the capture (allocator, lazy library state), on
+            # a state copy: the warm-up must not move this frame's state
+            saved = (self.poss.clone(), self.probs.clone(), self.seeds.clone(), self.center.clone(),
+                     self.arg.clone())
+            side = torch.cuda.Stream(self.dev)
+            side.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    self.step()
+            torch.cuda.current_stream(self.dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.step()
+            for t, v in zip((self.poss, self.probs, self.seeds, self.center, self.arg), saved):
+                t.copy_(v)
+            self.graph = g
+        self.graph.replay()
+
+
 class SemSegInference:
     """GPU ``run_inference`` for RandLA-Net with the spatially-regular patch
     sampler.  ``run(points)`` -> (predicted labels [N] int64, probabilities
@@ -583,6 +720,19 @@ class SemSegInference:
         graph.replay()
         return out
 
+    def _patch_step(self, n_sub):
+        """The patch-step state (and its graph) for a cloud of n_sub points,
+        kept on the model per (device, capacity, dtype, smooth)."""
+        cap = -(-n_sub // _CAP_STEP) * _CAP_STEP
+        key = (str(self.device), cap, self.probs_dtype, self.test_smooth)
+        cur = self.model.__dict__.get("_o3dml_patch_step")
+        if cur is None or cur[0] != key:
+            cur = (key, _PatchStep(self, cap))
+            self.model.__dict__["_o3dml_patch_step"] = cur
+        step = cur[1]
+        step.inf = self
+        return step
+
     @torch.no_grad()
     def run(self, points, patch_hook=None, init_possibility=None):
         self.model.eval()
@@ -594,6 +744,22 @@ class SemSegInference:
             possibility = torch.as_tensor(init_possibility, dtype=torch.float64).to(self.device).clone()
         else:
             possibility = torch.rand(n_sub, generator=self.gen, device=self.device, dtype=torch.float64) * 1e-3
+        if patch_hook is None and n_sub >= self.model.cfg["num_points"]:
+            # the whole patch as one replayed graph (or the same launches eagerly)
+            step = self._patch_step(n_sub)
+            step.begin(sub, possibility, int(self.rng.integers(0, 2**63)))
+            patches = 0
+            ready = torch.cuda.Event()
+            while True:
+                ready.record(torch.cuda.current_stream(self.device))
+                ready.synchronize()
+                if float(step.host_min[0]) > 0.5:
+                    break
+                step.run_step(self.use_graph)
+                patches += 1
+            self.stats = {"patches": patches, "sub_points": n_sub, "centers": []}
+            probs = step.probs[:n_sub][proj]
+            return probs.argmax(1), probs
         test_probs = torch.zeros((n_sub, C), dtype=self.probs_dtype, device=self.device)
         patches, centers = 0, []
         arg = torch.empty(1, dtype=torch.int64, device=self.device)
