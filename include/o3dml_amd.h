@@ -82,6 +82,10 @@ int o3dml_fixed_radius_search_count(const float* points, int64_t n_points, const
  * event without a separate device-to-host copy. */
 int o3dml_fixed_radius_search_totals(const int64_t* neighbors_row_splits, int64_t n_queries, void* workspace,
                                      int64_t* totals, void* stream);
+/* device int64 [3] = total, number of rows longer than 64, widest row (no
+ * host transfer: the caller batches several sizes into one read) */
+int o3dml_fixed_radius_search_sizes(const int64_t* neighbors_row_splits, int64_t n_queries, const void* workspace,
+                                    int64_t* sizes, void* stream);
 /* index_bits 32 or 64 (index_dtype); neighbors_distance nullable (squared for L2). */
 int o3dml_fixed_radius_search_fill(const float* points, int64_t n_points, const float* queries,
                                    int64_t n_queries, float radius, int64_t n_batch,

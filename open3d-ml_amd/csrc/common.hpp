@@ -148,6 +148,16 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+template <class T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const T o = __shfl_xor(v, d, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
 // Squared L2 distance with the contraction pattern shared with the oracle:
 // fma(dz,dz, fma(dy,dy, dx*dx)), dx = p - q.
 __device__ __forceinline__ float dist_l2(float px, float py, float pz, float qx, float qy, float qz) {

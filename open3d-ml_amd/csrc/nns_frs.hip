@@ -1095,6 +1095,26 @@ __global__ void frs_totals_kernel(const int64_t* __restrict__ rs, int64_t m, con
     }
 }
 
+// out = [total, overflow count, widest row] (the dense neighbour matrix of
+// KPConv's batch_neighbors needs the width): one workgroup
+__global__ void __launch_bounds__(1024) frs_sizes_kernel(const int64_t* __restrict__ rs, int64_t m,
+                                                         const int64_t* __restrict__ scalars,
+                                                         int64_t* __restrict__ out) {
+    int64_t w = 0;
+    for (int64_t q = threadIdx.x; q < m; q += blockDim.x) w = max(w, rs[q + 1] - rs[q]);
+    w = wave_max(w);
+    __shared__ int64_t part[16];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t r = 0;
+        for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) r = max(r, part[i]);
+        out[0] = rs[m];
+        out[1] = scalars[0];
+        out[2] = r;
+    }
+}
+
 static bool rel16_rows(int64_t n_batch, const int64_t* prs_host, int64_t n_queries) {
     if (!prs_host || !O3DML_FRS_REL16) return false;
     if (n_queries > 0x7FFFFFFF / (2 * kRowCap)) return false;  // the rows' buffer resource covers < 2^31 B
@@ -1200,6 +1220,17 @@ O3DML_API int o3dml_fixed_radius_search_totals(const int64_t* neighbors_row_spli
     hipStream_t st = as_stream(stream);
     frs_totals_kernel<<<1, 64, 0, st>>>(neighbors_row_splits, n_queries, static_cast<const int64_t*>(workspace),
                                         totals);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+// device int64 [3] = total, rows longer than 64, widest row — for callers
+// that read several sizes back in one transfer (KPFCNN collate)
+O3DML_API int o3dml_fixed_radius_search_sizes(const int64_t* neighbors_row_splits, int64_t n_queries,
+                                              const void* workspace, int64_t* sizes, void* stream) {
+    O3DML_GUARD_BEGIN
+    frs_sizes_kernel<<<1, 1024, 0, as_stream(stream)>>>(neighbors_row_splits, n_queries,
+                                                        static_cast<const int64_t*>(workspace), sizes);
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
 }

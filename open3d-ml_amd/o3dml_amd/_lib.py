@@ -42,6 +42,7 @@ SIGNATURES = {
                                                c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_p,
                                                c_p, c_sz, c_p]),
     "o3dml_fixed_radius_search_totals": (c_i32, [c_p, c_i64, c_p, c_p, c_p]),
+    "o3dml_fixed_radius_search_sizes": (c_i32, [c_p, c_i64, c_p, c_p, c_p]),
     "o3dml_fixed_radius_search_fill_bounded": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p, c_p,
                                                        c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_p,
                                                        c_i64, c_i32, c_p, c_sz, c_p]),

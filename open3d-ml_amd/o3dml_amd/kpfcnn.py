@@ -486,27 +486,45 @@ def batch_neighbors(queries, supports, q_lengths, s_lengths, radius, hash_table=
 # of a stage is queued, then their sizes come back in ONE pinned transfer
 # (the reference reads each size separately: ~9 host round trips per layer)
 # ---------------------------------------------------------------------------
-def _read_host(dev, vals):
-    """Device int64 values (scalars or 1-D) -> Python ints, one transfer + one wait."""
-    flat = torch.cat([v.reshape(-1).to(torch.int64) for v in vals])
-    host = ops._pinned_slot(dev, flat.numel())
-    host.copy_(flat, non_blocking=True)
-    ready = torch.cuda.Event()
-    ready.record(torch.cuda.current_stream(dev))
-    ready.synchronize()
-    return host.tolist()
+class _Reads:
+    """Device int64 slots that several collate steps fill with their sizes,
+    read back in ONE pinned transfer (one buffer per device, reused: every
+    read waits for its transfer before the slots are handed out again)."""
+    _bufs = {}
+
+    def __init__(self, dev):
+        self.dev = dev
+        buf = _Reads._bufs.get(dev)
+        if buf is None:
+            buf = _Reads._bufs[dev] = torch.empty(256, dtype=torch.int64, device=dev)
+        self.buf, self.used = buf, 0
+
+    def take(self, k):
+        if self.used + k > self.buf.numel():
+            raise RuntimeError("collate: too many batch items for the size slots")
+        off = self.used
+        self.used += k
+        return self.buf[off:off + k]
+
+    def read(self):
+        host = ops._pinned_slot(self.dev, self.used)
+        host.copy_(self.buf[:self.used], non_blocking=True)
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.dev))
+        ready.synchronize()
+        return host.tolist()
 
 
-def _dense_begin(queries, supports, q_lengths, s_lengths, radius, table=None):
-    """batch_neighbors, count phase: (rs, state, device [total, long rows, width])."""
+def _dense_begin(reads, queries, supports, q_lengths, s_lengths, radius, table=None):
+    """batch_neighbors, count phase; [total, long rows, width] into 3 slots."""
     rs, state = ops._frs_count(supports, queries, radius, _splits(s_lengths), _splits(q_lengths),
                                None if table is None else table.hash_table_splits,
                                None if table is None else table.hash_table_index,
                                None if table is None else table.hash_table_cell_splits, "L2", False, False)
     m = queries.shape[0]
-    vals = (torch.stack([rs[-1], state[1][:8].view(torch.int64)[0], (rs[1:] - rs[:-1]).max()]) if m
-            else torch.zeros(3, dtype=torch.int64, device=rs.device))
-    return rs, state, vals, supports.shape[0], m
+    slot = reads.take(3)
+    _lib.call("o3dml_fixed_radius_search_sizes", ptr(rs), m, ptr(state[1]), ptr(slot), stream_handle(rs.device))
+    return rs, state, slot, supports.shape[0], m
 
 
 def _dense_end(b, host):
@@ -521,7 +539,7 @@ def _dense_end(b, host):
                                torch.tensor([n_sup], dtype=torch.int32)).squeeze(2)
 
 
-def _subsample_begin(points, lengths, sampleDl, rotations=None):
+def _subsample_begin(reads, points, lengths, sampleDl, rotations=None):
     """batch_grid_subsampling, count phase (rotation drawn here, as the reference)."""
     lengths = np.asarray(lengths, np.int64)
     splits = np.zeros(len(lengths) + 1, np.int64)
@@ -532,7 +550,7 @@ def _subsample_begin(points, lengths, sampleDl, rotations=None):
     lib = _lib.load()
     n, B = pts.shape[0], len(lengths)
     ws = workspace(lib.o3dml_grid_subsample_workspace_size(n, B), dev)
-    out = torch.empty(2 + B, dtype=torch.int64, device=dev)
+    out = reads.take(2 + B)
     _lib.call("o3dml_grid_subsample_count_async", ptr(pts), n, B, ptr(to_dev(splits, dev)), float(sampleDl), 0,
               ptr(out), ptr(ws), ws.numel(), stream_handle(dev))
     return pts, n, B, ws, out, R
@@ -581,26 +599,29 @@ def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_len
         table = None  # hash table of this layer's points at r_normal: shared by the conv and pool searches
         # stage 1: the conv search count and the subsampling count, one read
         conv_b = sub_b = None
+        reads = _Reads(dev)
         if layer_blocks:
             r = r_normal * cfg.deform_radius / cfg.conv_radius if deform else r_normal
             if r == r_normal:
                 table = ops.build_spatial_hash_table(stacked_points, r, _splits(stack_lengths))
-            conv_b = _dense_begin(stacked_points, stacked_points, stack_lengths, stack_lengths, r, table)
+            conv_b = _dense_begin(reads, stacked_points, stacked_points, stack_lengths, stack_lengths, r, table)
         pooling = "pool" in block or "strided" in block
         if pooling:
             dl = 2 * r_normal / cfg.conv_radius
             rot = None if rotations is None else rotations[sub_i]
             sub_i += 1
-            sub_b = _subsample_begin(stacked_points, stack_lengths, dl, rotations=rot)
-        host = _read_host(dev, ([conv_b[2]] if conv_b else []) + ([sub_b[4]] if sub_b else []))
+            sub_b = _subsample_begin(reads, stacked_points, stack_lengths, dl, rotations=rot)
+        host = reads.read()
         conv_i = _dense_end(conv_b, host[:3]) if conv_b else empty
         if pooling:
             pool_p, pool_b = _subsample_end(sub_b, host[3:] if conv_b else host)
             r = r_normal * cfg.deform_radius / cfg.conv_radius if "deformable" in block else r_normal
             # stage 2: the pool and up-sampling search counts, one read
-            pb = _dense_begin(pool_p, stacked_points, pool_b, stack_lengths, r, table if r == r_normal else None)
-            ub = _dense_begin(stacked_points, pool_p, stack_lengths, pool_b, 2 * r)
-            host = _read_host(dev, [pb[2], ub[2]])
+            reads = _Reads(dev)
+            pb = _dense_begin(reads, pool_p, stacked_points, pool_b, stack_lengths, r,
+                              table if r == r_normal else None)
+            ub = _dense_begin(reads, stacked_points, pool_p, stack_lengths, pool_b, 2 * r)
+            host = reads.read()
             pool_i = _dense_end(pb, host[:3])
             up_i = _dense_end(ub, host[3:])
         else:
