@@ -350,73 +350,6 @@ __global__ void __launch_bounds__(kBsThreads) block_sort_pairs(const K* __restri
     }
 }
 
-// Faster small sort when the masked key and the input position pack into 64
-// bits (key bits + 13 <= 64): elements are the unique u64 (key << 13 | pos),
-// each thread sorts 8 in registers, then 10 rounds of merge-path merges
-// through two 64 KiB LDS buffers (one barrier per round instead of the
-// bitonic network's 91).  Unique elements, so any correct sort is the stable
-// (key, position) order.
-__device__ __forceinline__ void cas_u64(uint64_t& a, uint64_t& b) {
-    const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
-    a = lo;
-    b = hi;
-}
-
-template <class K>
-__global__ void __launch_bounds__(kBsThreads) block_merge_sort_pairs(const K* __restrict__ kin,
-                                                                     const uint32_t* __restrict__ vin,
-                                                                     K* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                                     int n, K mask) {
-    __shared__ uint64_t buf[2][kBsMax];
-    const int t = threadIdx.x;
-    uint64_t v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int i = 8 * t + j;
-        v[j] = i < n ? (static_cast<uint64_t>(kin[i] & mask) << 13) | static_cast<uint64_t>(i) : ~0ull;
-    }
-    // Batcher odd-even merge sort of 8 (19 compare-exchanges)
-    cas_u64(v[0], v[1]); cas_u64(v[2], v[3]); cas_u64(v[4], v[5]); cas_u64(v[6], v[7]);
-    cas_u64(v[0], v[2]); cas_u64(v[1], v[3]); cas_u64(v[4], v[6]); cas_u64(v[5], v[7]);
-    cas_u64(v[1], v[2]); cas_u64(v[5], v[6]);
-    cas_u64(v[0], v[4]); cas_u64(v[1], v[5]); cas_u64(v[2], v[6]); cas_u64(v[3], v[7]);
-    cas_u64(v[2], v[4]); cas_u64(v[3], v[5]);
-    cas_u64(v[1], v[2]); cas_u64(v[3], v[4]); cas_u64(v[5], v[6]);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) buf[0][8 * t + j] = v[j];
-    __syncthreads();
-    int src = 0;
-    for (int L = 8; L < kBsMax; L <<= 1) {
-        const uint64_t* S = buf[src];
-        uint64_t* D = buf[src ^ 1];
-        const int d = (8 * t) & (2 * L - 1);  // this thread's output diagonal within its pair of runs
-        const int base = 8 * t - d;
-        const uint64_t* A = S + base;
-        const uint64_t* B = A + L;
-        int lo = d > L ? d - L : 0, hi = d < L ? d : L;
-        while (lo < hi) {  // how many of the first d outputs come from A
-            const int mid = (lo + hi) >> 1;
-            if (A[mid] < B[d - 1 - mid]) lo = mid + 1;
-            else hi = mid;
-        }
-        int ia = lo, ib = d - lo;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const bool take_a = ib >= L || (ia < L && A[ia] < B[ib]);
-            D[base + d + j] = take_a ? A[ia] : B[ib];
-            ia += take_a;
-            ib += !take_a;
-        }
-        __syncthreads();
-        src ^= 1;
-    }
-    for (int i = t; i < n; i += kBsThreads) {
-        const uint32_t p = static_cast<uint32_t>(buf[src][i] & 0x1fffu);
-        kout[i] = kin[p];
-        vout[i] = vin ? vin[p] : p;
-    }
-}
-
 inline int bits_needed(uint64_t max_key) {
     int b = 0;
     while (b < 64 && (max_key >> b) != 0) ++b;
@@ -444,12 +377,11 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
     }
     if (n <= kBsMax) {
         const K mask = end_bit >= static_cast<int>(8 * sizeof(K)) ? ~K(0) : ((K(1) << end_bit) - 1);
-        if (end_bit + 13 <= 64)
-            block_merge_sort_pairs<K><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out,
-                                                                static_cast<int>(n), mask);
-        else
-            block_sort_pairs<K><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, static_cast<int>(n),
-                                                          mask);
+        // (a merge-path merge sort of packed (key, position) words measured
+        // slower here: 46 vs 37 us at ~4k keys — dependent LDS latency of the
+        // per-round binary searches)
+        block_sort_pairs<K><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, static_cast<int>(n),
+                                                      mask);
         O3DML_LAUNCH_CHECK();
         return;
     }
