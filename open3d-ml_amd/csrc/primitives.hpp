@@ -7,6 +7,8 @@
 // Header-only templates, instantiated per translation unit (no -fgpu-rdc).
 #pragma once
 
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace o3dml {
@@ -309,44 +311,95 @@ __global__ void copy_pairs(const K* __restrict__ kin, const uint32_t* __restrict
 constexpr int kBsMax = 8192;
 constexpr int kBsThreads = 1024;
 
-template <class K>
+// Element i lives in thread i % 1024, register slot i / 1024, so a
+// compare-exchange partner i ^ j is the same thread's other slot for
+// j >= 1024 (register swap), another lane of the same wave for j < 64
+// (__shfl_xor), and only for 64 <= j < 1024 another wave (through LDS, two
+// barriers): 22 of the 91 stages of an 8192-element network touch LDS.
+template <class K, int S>
 __global__ void __launch_bounds__(kBsThreads) block_sort_pairs(const K* __restrict__ kin,
                                                                const uint32_t* __restrict__ vin,
                                                                K* __restrict__ kout, uint32_t* __restrict__ vout,
                                                                int n, K mask) {
-    __shared__ K sk[kBsMax];
-    __shared__ uint32_t sp[kBsMax];
+    constexpr int N = S * kBsThreads;
+    __shared__ K sk[N];
+    __shared__ uint32_t sp[N];
     const int t = threadIdx.x;
-    int N = 1;
-    while (N < n) N <<= 1;
-    for (int i = t; i < N; i += kBsThreads) {
-        sk[i] = i < n ? (kin[i] & mask) : ~K(0);
-        sp[i] = i < n ? static_cast<uint32_t>(i) : 0xffffffffu;
+    K key[S];
+    uint32_t pos[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int i = s * kBsThreads + t;
+        key[s] = i < n ? (kin[i] & mask) : ~K(0);
+        pos[s] = i < n ? static_cast<uint32_t>(i) : 0xffffffffu;
     }
-    __syncthreads();
+    // the element of slot s takes its partner's (ok, op) or keeps its own
+    auto settle = [&](int s, int i, int j, int k, K ok, uint32_t op) {
+        const bool mine_gt = key[s] > ok || (key[s] == ok && pos[s] > op);
+        const bool lower = (i & j) == 0, asc = (i & k) == 0;
+        const bool keep = (lower == asc) ? !mine_gt : mine_gt;
+        if (!keep) {
+            key[s] = ok;
+            pos[s] = op;
+        }
+    };
     for (int k = 2; k <= N; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = t; i < N; i += kBsThreads) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const K a = sk[i], b = sk[ixj];
-                    const uint32_t pa = sp[i], pb = sp[ixj];
-                    const bool gt = a > b || (a == b && pa > pb);
-                    if (gt == ((i & k) == 0)) {
-                        sk[i] = b;
-                        sk[ixj] = a;
-                        sp[i] = pb;
-                        sp[ixj] = pa;
+            if (j >= kBsThreads) {  // same thread, slots s and s ^ (j / 1024)
+                // slot distance as a compile-time constant: the register
+                // arrays are never indexed dynamically (that would spill them)
+                auto slots = [&](auto js_c) {
+                    constexpr int js = decltype(js_c)::value;
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        if ((s & js) || (s | js) >= S) continue;
+                        const int s2 = s | js;
+                        const int i = s * kBsThreads + t;
+                        const bool gt = key[s] > key[s2] || (key[s] == key[s2] && pos[s] > pos[s2]);
+                        if (gt == ((i & k) == 0)) {
+                            const K tk = key[s];
+                            key[s] = key[s2];
+                            key[s2] = tk;
+                            const uint32_t tp = pos[s];
+                            pos[s] = pos[s2];
+                            pos[s2] = tp;
+                        }
                     }
+                };
+                const int js = j / kBsThreads;
+                if (js == 1) slots(std::integral_constant<int, 1>{});
+                else if (js == 2) slots(std::integral_constant<int, 2>{});
+                else slots(std::integral_constant<int, 4>{});
+            } else if (j < 64) {  // same wave
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const K ok = __shfl_xor(key[s], j, 64);
+                    const uint32_t op = __shfl_xor(pos[s], j, 64);
+                    settle(s, s * kBsThreads + t, j, k, ok, op);
                 }
+            } else {  // another wave of the workgroup
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    sk[s * kBsThreads + t] = key[s];
+                    sp[s * kBsThreads + t] = pos[s];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const int i = s * kBsThreads + t;
+                    settle(s, i, j, k, sk[i ^ j], sp[i ^ j]);
+                }
+                __syncthreads();
             }
-            __syncthreads();
         }
     }
-    for (int i = t; i < n; i += kBsThreads) {
-        const uint32_t p = sp[i];
-        kout[i] = kin[p];
-        vout[i] = vin ? vin[p] : p;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int i = s * kBsThreads + t;
+        if (i < n) {
+            kout[i] = kin[pos[s]];
+            vout[i] = vin ? vin[pos[s]] : pos[s];
+        }
     }
 }
 
@@ -378,10 +431,17 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
     if (n <= kBsMax) {
         const K mask = end_bit >= static_cast<int>(8 * sizeof(K)) ? ~K(0) : ((K(1) << end_bit) - 1);
         // (a merge-path merge sort of packed (key, position) words measured
-        // slower here: 46 vs 37 us at ~4k keys — dependent LDS latency of the
+        // slower: 46 vs 37 us at ~4k keys — dependent LDS latency of the
         // per-round binary searches)
-        block_sort_pairs<K><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, static_cast<int>(n),
-                                                      mask);
+        const int ni = static_cast<int>(n);
+        if (n <= kBsThreads)
+            block_sort_pairs<K, 1><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);
+        else if (n <= 2 * kBsThreads)
+            block_sort_pairs<K, 2><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);
+        else if (n <= 4 * kBsThreads)
+            block_sort_pairs<K, 4><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);
+        else
+            block_sort_pairs<K, 8><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);
         O3DML_LAUNCH_CHECK();
         return;
     }
