@@ -27,7 +27,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib, ops
-from ._util import ptr, stream_handle
+from ._util import metric_code, ptr, stream_handle
 
 _BN_EPS = 1e-6
 
@@ -523,11 +523,12 @@ class _PatchStep:
         inf, st, n_pts = self.inf, stream_handle(self.dev), self.n_pts
         k, L = self.k, len(self.nxt)
         # crop: the num_points nearest sub-points of the centre, (distance, index) order
+        l2 = metric_code("L2")
         _lib.call("o3dml_knn_search_count", ptr(self.sub), self.cap, ptr(self.center), 1, n_pts, 1,
                   ptr(self.crop_prs_d), ptr(self.crop_qrs_d), self.crop_prs.ctypes.data, self.crop_qrs.ctypes.data,
-                  0, 0, 0, ptr(self.crop_rs), ptr(self.crop_ws), self.crop_ws.numel(), st)
+                  l2, 0, 0, ptr(self.crop_rs), ptr(self.crop_ws), self.crop_ws.numel(), st)
         _lib.call("o3dml_knn_search_fill", ptr(self.sub), self.cap, ptr(self.center), 1, n_pts, 1,
-                  ptr(self.crop_qrs_d), self.crop_prs.ctypes.data, self.crop_qrs.ctypes.data, 0, 0,
+                  ptr(self.crop_qrs_d), self.crop_prs.ctypes.data, self.crop_qrs.ctypes.data, l2, 0,
                   ptr(self.crop_rs), 64, ptr(self.crop), None, ptr(self.crop_ws), self.crop_ws.numel(), st)
         # the shuffle (random.shuffle, semseg_spatially_regular.py:100): keyed bijection
         _lib.call("o3dml_random_permute_dev", ptr(self.crop), n_pts, ptr(self.seeds), ptr(self.idxs), st)
@@ -537,10 +538,10 @@ class _PatchStep:
         torch.cat([self.pc[:self.sizes[i]] for i in range(L)], out=self.cat)
         total = self.cat.shape[0]
         _lib.call("o3dml_knn_search_count", ptr(self.cat), total, ptr(self.cat), total, k, L, ptr(self.rs_d),
-                  ptr(self.rs_d), self.rs.ctypes.data, self.rs.ctypes.data, 0, 0, 1, ptr(self.knn_rs),
+                  ptr(self.rs_d), self.rs.ctypes.data, self.rs.ctypes.data, l2, 0, 1, ptr(self.knn_rs),
                   ptr(self.knn_ws), self.knn_ws.numel(), st)
         _lib.call("o3dml_knn_search_fill", ptr(self.cat), total, ptr(self.cat), total, k, L, ptr(self.rs_d),
-                  self.rs.ctypes.data, self.rs.ctypes.data, 0, 0, ptr(self.knn_rs), 32, ptr(self.nb), None,
+                  self.rs.ctypes.data, self.rs.ctypes.data, l2, 0, ptr(self.knn_rs), 32, ptr(self.nb), None,
                   ptr(self.knn_ws), self.knn_ws.numel(), st)
         _lib.call("o3dml_randla_up_from_knn", ptr(self.nb), k, ptr(self.cat), L, self.rs.ctypes.data,
                   self.nxt.ctypes.data, self.srs.ctypes.data, ptr(self.up), ptr(self.up_ws), self.up_ws.numel(), st)

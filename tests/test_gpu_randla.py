@@ -237,3 +237,46 @@ def test_dense_fused_split_reduce_bitwise(cuda):
         outs.append(torch.load(path, weights_only=True))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_patch_step_equals_ops(cuda):
+    """The capturable patch step (SemSegInference._patch_step, direct ABI
+    calls over padded static buffers) produces exactly what the op-level
+    pipeline would: the crop = ops.knn_search(sub, centre, num_points) (L2,
+    (distance, index) order), the shuffled indices a permutation of it, the
+    per-level k-lists = ops.knn_search on the levels, the up-sampling ids =
+    a second 1-NN search, and the possibility update of the crop."""
+    from o3dml_amd import ops
+    from o3dml_amd.randlanet import RandLANet, SemSegInference
+    torch.manual_seed(0)
+    m = RandLANet(num_points=4096).to(cuda)
+    rng = np.random.default_rng(3)
+    pts = np.stack([rng.uniform(-20, 20, 30000), rng.uniform(-20, 20, 30000), rng.uniform(-2, 2, 30000)], 1)
+    pts = torch.from_numpy(pts.astype(np.float32)).to(cuda)
+    inf = SemSegInference(m, seed=0, use_graph=False)
+    sub, _ = inf.preprocess(pts)
+    n = sub.shape[0]
+    step = inf._patch_step(n)
+    p0 = torch.rand(n, generator=torch.Generator(device=cuda).manual_seed(5), device=cuda, dtype=torch.float64)
+    step.begin(sub, p0, 123)
+    center = step.center.clone()
+    assert int(step.arg) == int(torch.argmin(p0))
+    with torch.no_grad():
+        step.step()
+    crop = ops.knn_search(sub, center.view(1, 3), 4096, index_dtype=torch.int64).neighbors_index
+    assert torch.equal(step.crop, crop)
+    assert torch.equal(torch.sort(step.idxs).values, torch.sort(crop).values)
+    sizes, rs, _ = step.plan
+    cat = step.cat
+    ref = ops.knn_search(cat, cat, 16, rs, rs).neighbors_index.view(-1, 16).long()
+    base = torch.repeat_interleave(torch.from_numpy(rs[:-1]).to(cuda), torch.from_numpy(np.diff(rs)).to(cuda))
+    assert torch.equal(step.nb.long(), ref - base[:, None])  # rewritten level-relative by up_from_knn
+    for i in range(len(sizes) - 1):
+        lvl, nxt = cat[rs[i]:rs[i + 1]], cat[rs[i]:rs[i] + sizes[i + 1]]
+        up = ops.knn_search(nxt, lvl, 1, index_dtype=torch.int64).neighbors_index
+        assert torch.equal(step.up[rs[i]:rs[i + 1]], up)
+    grew = step.poss[:n][crop] > p0[crop]  # delta = (1 - d / d_max)^2: 0 only at the farthest point
+    assert torch.all(step.poss[:n][crop] >= p0[crop]) and int(grew.sum()) >= crop.numel() - 1
+    untouched = torch.ones(n, dtype=torch.bool, device=cuda)
+    untouched[crop] = False
+    assert torch.equal(step.poss[:n][untouched], p0[untouched])
