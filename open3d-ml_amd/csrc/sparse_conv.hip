@@ -245,8 +245,11 @@ __device__ __forceinline__ int split_stage(unsigned used, int nch, int K, int s,
     return __builtin_popcount(below) * nch + (own ? cc : 0);
 }
 
-template <bool PRE>
+template <bool PRE, bool SC = true>
 __device__ __forceinline__ void gemm_finish(GemmStage& st, int c0, int h, const float* lps, const float* lpb) {
+    // no prologue and no scales: the factor is 1, and a missing row was
+    // gathered from the zero page already — nothing to do (same bits)
+    if constexpr (!PRE && !SC) return;
     const int cb = c0 + 16 * h;
     const float sc = st.v != 0.f ? st.s1 * st.s2 : 0.f;
 #pragma unroll
@@ -465,7 +468,9 @@ __device__ __forceinline__ void glds16(const float* g, float* lds_wave_base) {
 // row factors of lane (i, h)'s row i into st.
 // BREG: B (the filters, L2-resident) as fragment-shaped 16-B loads straight
 // into st.b instead of through LDS — half the LDS per wave, so more waves.
-template <bool BREG>
+// SC: row / pair scales present (importance, normalisation); without them the
+// factors are 1 and no per-stage scale loads are issued
+template <bool BREG, bool SC = true>
 __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_t* mtile, int K, int k, int c0,
                                           int lane, int64_t o, int i, int col0, const float* __restrict__ src,
                                           const float* __restrict__ sscale, const float* __restrict__ pscale,
@@ -506,8 +511,12 @@ __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_
         }
     }
     const bool valid = mi >= 0;
-    st.s1 = *(sscale ? sscale + (valid ? mi : 0) : g_one_page);
-    st.s2 = *(pscale ? pscale + (valid ? o : 0) * K + k : g_one_page);
+    if constexpr (SC) {
+        st.s1 = *(sscale ? sscale + (valid ? mi : 0) : g_one_page);
+        st.s2 = *(pscale ? pscale + (valid ? o : 0) * K + k : g_one_page);
+    } else {
+        st.s1 = st.s2 = 1.f;
+    }
     st.v = valid ? 1.f : 0.f;
 }
 
@@ -586,7 +595,7 @@ __device__ __forceinline__ void mfma_stage(const Stage& cu, f32x16& acc) {
     }
 }
 
-template <bool PRE, bool BREG, int NT = 0>
+template <bool PRE, bool BREG, int NT = 0, bool SC = true>
 __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order,
                          const int* order_flag, int K, int64_t n_out,
@@ -654,7 +663,8 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
         int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
         GemmStage nx, cu;
-        lds_issue<BREG>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout, true, nx);
+        lds_issue<BREG, SC>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout, true,
+                            nx);
         for (int j = j0; j < j1; ++j) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage j in LDS, its row factors in nx
             lds_read<BREG>(abuf, bbuf, i, h, cu);
@@ -673,11 +683,11 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
                 k = u ? __builtin_ctz(u) : 0;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffer read out before the next DMA
-            lds_issue<BREG>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout,
+            lds_issue<BREG, SC>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout,
                             j + 1 < j1, nx);
             __builtin_amdgcn_sched_barrier(0);
             (void)kj;
-            gemm_finish<PRE>(cu, cj, h, lps, lpb);
+            gemm_finish<PRE, SC>(cu, cj, h, lps, lpb);
             mfma_stage<NT>(cu, acc);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead DMA has landed before the wave exits
@@ -1676,10 +1686,16 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #undef O3DML_GEMM_SH_NT
 #undef O3DML_GEMM_SH
     } else if (vec4 && lds_path) {
-#define O3DML_GEMM_LDS(P, BR, X)                                                                                  \
-    implicit_gemm_lds_kernel<P, BR, X><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
-                                                                   pscale, Wt, cin, cout, oscale, bias, out, ns,  \
-                                                                   part, pre, residual, counters)
+#define O3DML_GEMM_LDS_SC(P, BR, X, SCL)                                                                          \
+    implicit_gemm_lds_kernel<P, BR, X, SCL><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src,    \
+                                                                        sscale, pscale, Wt, cin, cout, oscale,    \
+                                                                        bias, out, ns, part, pre, residual,       \
+                                                                        counters)
+#define O3DML_GEMM_LDS(P, BR, X)                                      \
+    do {                                                              \
+        if (sscale || pscale) O3DML_GEMM_LDS_SC(P, BR, X, true);      \
+        else O3DML_GEMM_LDS_SC(P, BR, X, false);                      \
+    } while (0)
         const int nt = gemm_nt();
         if (nt == 6) {
             if (pre.scale) O3DML_GEMM_LDS(true, true, 6); else O3DML_GEMM_LDS(false, true, 6);
@@ -1691,6 +1707,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
             if (breg) O3DML_GEMM_LDS(false, true, 0); else O3DML_GEMM_LDS(false, false, 0);
         }
 #undef O3DML_GEMM_LDS
+#undef O3DML_GEMM_LDS_SC
     } else if (pre.scale) {
         if (vec4) O3DML_GEMM_LAUNCH(true, true); else O3DML_GEMM_LAUNCH(false, true);
     } else {
