@@ -749,7 +749,7 @@ struct SharedStage {
     float sc[RB];  // row factor (importance x pair scale, 0 for a missing row)
 };
 
-template <int RB>
+template <int RB, bool SC = true>
 __device__ __forceinline__ void shared_regs(const int32_t* mtile, int K, int k, int c0, int lane, const int64_t* o,
                                             int i, int col, const float* __restrict__ sscale,
                                             const float* __restrict__ pscale, const float* __restrict__ Wt, int cin,
@@ -771,8 +771,12 @@ __device__ __forceinline__ void shared_regs(const int32_t* mtile, int K, int k, 
     for (int rb = 0; rb < RB; ++rb) {
         const int32_t mi = live ? mtile[(32 * rb + i) * K + k] : -1;
         v[rb] = mi >= 0;
-        s1[rb] = *(sscale ? sscale + (v[rb] ? mi : 0) : g_one_page);
-        s2[rb] = *(pscale ? pscale + (v[rb] ? o[rb] : 0) * K + k : g_one_page);
+        if constexpr (SC) {
+            s1[rb] = *(sscale ? sscale + (v[rb] ? mi : 0) : g_one_page);
+            s2[rb] = *(pscale ? pscale + (v[rb] ? o[rb] : 0) * K + k : g_one_page);
+        } else {
+            s1[rb] = s2[rb] = 1.f;
+        }
     }
 }
 
@@ -812,7 +816,7 @@ __device__ __forceinline__ void mfma_stage_rb(const SharedStage<RB>& cu, f32x16 
 // The tile: 32*RB output rows (RB row blocks) x NW column blocks; wave w owns
 // column block w for all RB row blocks, so each stage's B fragment (the
 // filters, read by every wave of every tile) feeds RB accumulators.
-template <bool PRE, int NT, int NW, int RB>
+template <bool PRE, int NT, int NW, int RB, bool SC = true>
 __global__ void __launch_bounds__(NW * 64)
 implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order,
                             const int* order_flag, int K, int64_t n_out,
@@ -881,7 +885,7 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
         float s1[RB], s2[RB];
         bool vv[RB];
         shared_issue<NW, RB>(abuf[0], mtile, K, k, c0, lane, w, src, cin, true);
-        shared_regs<RB>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, true, nx, s1, s2, vv);
+        shared_regs<RB, SC>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, true, nx, s1, s2, vv);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         for (int j = j0; j < j1; ++j) {
@@ -906,14 +910,18 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
             const bool live = j + 1 < j1;
             // the other buffer was last read in stage j-1, before that stage's barrier
             shared_issue<NW, RB>(abuf[b ^ 1], mtile, K, k, c0, lane, w, src, cin, live);
-            shared_regs<RB>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, live, nx, s1, s2, vv);
+            shared_regs<RB, SC>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, live, nx, s1, s2,
+                                vv);
             __builtin_amdgcn_sched_barrier(0);
             const int cbb = cj + 16 * h;
+            if constexpr (PRE || SC) {  // without both the factor is 1 and missing rows are zero already
 #pragma unroll
-            for (int rb = 0; rb < RB; ++rb)
+                for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    cu.a[rb][r] = (PRE ? pre_act(cu.a[rb][r], lps[cbb + r], lpb[cbb + r]) : cu.a[rb][r]) * cu.sc[rb];
+                    for (int r = 0; r < 16; ++r)
+                        cu.a[rb][r] =
+                                (PRE ? pre_act(cu.a[rb][r], lps[cbb + r], lpb[cbb + r]) : cu.a[rb][r]) * cu.sc[rb];
+            }
             mfma_stage_rb<NT, RB>(cu, acc);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own share of stage j+1 landed
             __syncthreads();  // every share landed; stage j's buffer free
@@ -1665,10 +1673,16 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
         }();
         const dim3 gs(static_cast<unsigned>(ceil_div(n_out, 32 * rb)), static_cast<unsigned>(ceil_div(cout, 32 * nw)),
                       static_cast<unsigned>(ns));
-#define O3DML_GEMM_SH(P, X, W, B)                                                                               \
-    implicit_gemm_shared_kernel<P, X, W, B><<<gs, W * 64, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, \
-                                                                   pscale, Wt, cin, cout, oscale, bias, out, ns,  \
-                                                                   part, pre, residual, counters)
+#define O3DML_GEMM_SH_SC(P, X, W, B, SCL)                                                                      \
+    implicit_gemm_shared_kernel<P, X, W, B, SCL><<<gs, W * 64, 0, st>>>(map, order, order_flag, K, n_out, src,   \
+                                                                        sscale, pscale, Wt, cin, cout, oscale,   \
+                                                                        bias, out, ns, part, pre, residual,      \
+                                                                        counters)
+#define O3DML_GEMM_SH(P, X, W, B)                                     \
+    do {                                                              \
+        if (sscale || pscale) O3DML_GEMM_SH_SC(P, X, W, B, true);     \
+        else O3DML_GEMM_SH_SC(P, X, W, B, false);                     \
+    } while (0)
 #define O3DML_GEMM_SH_RB(P, X, W) \
     if (rb == 2) O3DML_GEMM_SH(P, X, W, 2); else O3DML_GEMM_SH(P, X, W, 1);
 #define O3DML_GEMM_SH_NT(P, W)                          \
@@ -1685,6 +1699,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #undef O3DML_GEMM_SH_RB
 #undef O3DML_GEMM_SH_NT
 #undef O3DML_GEMM_SH
+#undef O3DML_GEMM_SH_SC
     } else if (vec4 && lds_path) {
 #define O3DML_GEMM_LDS_SC(P, BR, X, SCL)                                                                          \
     implicit_gemm_lds_kernel<P, BR, X, SCL><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src,    \

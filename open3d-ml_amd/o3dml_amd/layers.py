@@ -203,7 +203,20 @@ class SparseConvTranspose(SparseConv):
     def forward(self, inp_features, inp_positions, out_positions, voxel_size, out_importance=None,
                 fixed_radius_search_hash_table=None):
         if self.normalize:
-            raise NotImplementedError("SparseConvTranspose(normalize=True) is not supported")
+            # each input's contribution divided by its number of output
+            # neighbours (the inp_neighbors_* relation of ops.sparse_conv_transpose:
+            # the same pairs grouped by input)
+            nb, kidx = self._rulebook(inp_positions, out_positions, voxel_size, fixed_radius_search_hash_table,
+                                      True, -1.0)
+            n_in = inp_features.shape[0]
+            cnt = torch.bincount(nb.neighbors_index.long(), minlength=n_in)
+            irs = torch.zeros(n_in + 1, dtype=torch.int64, device=cnt.device)
+            torch.cumsum(cnt, 0, out=irs[1:])
+            out = sc.sparse_conv_transpose(self.kernel, out_importance, inp_features, None, None, irs,
+                                           nb.neighbors_index, kidx, None, nb.neighbors_row_splits, normalize=True)
+            if self.bias is not None:
+                out = out + self.bias
+            return self.activation(out) if self.activation else out
         out = self._lattice(inp_features, inp_positions, out_positions, voxel_size, fixed_radius_search_hash_table,
                             True, -1.0, bias=None, out_importance=out_importance)
         if out is not None:

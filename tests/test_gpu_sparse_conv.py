@@ -377,3 +377,35 @@ def test_split_k_last_wave_finish_bitwise(cuda):
     assert len(outs[0]) == len(outs[1]) > 2
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_transposed_conv_normalize(cuda):
+    """layers.SparseConvTranspose(normalize=True): every input's contribution
+    divided by its number of output neighbours (ops.sparse_conv_transpose's
+    inp_neighbors_* relation), against a float64 restatement over the same
+    rulebook; the gradients through the registered backward."""
+    from o3dml_amd import layers
+    vox = torch.from_numpy(_voxels(4000, 24, 8)).to(cuda)
+    coarse = torch.unique(torch.floor(vox / 2), dim=0) * 2 + 1.0  # stride-2 lattice
+    torch.manual_seed(0)
+    conv = layers.SparseConvTranspose(16, 24, [3, 3, 3], use_bias=True, normalize=True).to(cuda)
+    torch.nn.init.normal_(conv.bias)
+    x = torch.randn((coarse.shape[0], 16), device=cuda, requires_grad=True)
+    out = conv(x, coarse, vox, 2.0)
+    nb, kidx = conv._rulebook(coarse, vox, 2.0, None, True, -1.0)
+    idx = nb.neighbors_index.long().cpu()
+    rs = nb.neighbors_row_splits.cpu()
+    o = torch.repeat_interleave(torch.arange(vox.shape[0]), rs[1:] - rs[:-1])
+    cnt = torch.bincount(idx, minlength=coarse.shape[0]).double()
+    W = conv.kernel.detach().double().cpu().reshape(27, 16, 24)
+    x64 = x.detach().double().cpu()
+    contrib = torch.einsum("pc,pcd->pd", x64[idx] / cnt[idx][:, None], W[kidx.long().cpu()])
+    ref = torch.zeros((vox.shape[0], 24), dtype=torch.float64).index_add_(0, o, contrib) + conv.bias.detach().double().cpu()
+    _close(out.detach().cpu().numpy(), ref.numpy())
+    go = torch.randn_like(out)
+    gx, = torch.autograd.grad(out, x, go)
+    x64r = x64.clone().requires_grad_(True)
+    contrib = torch.einsum("pc,pcd->pd", x64r[idx] / cnt[idx][:, None], W[kidx.long().cpu()])
+    r = torch.zeros((vox.shape[0], 24), dtype=torch.float64).index_add_(0, o, contrib)
+    gx64, = torch.autograd.grad(r, x64r, go.double().cpu())
+    _close(gx.cpu().numpy(), gx64.numpy())
