@@ -115,6 +115,42 @@ int o3dml_fixed_radius_search_fill_bounded(const float* points, int64_t n_points
                                            void* neighbors_index, float* neighbors_distance, int64_t capacity,
                                            int parts, void* workspace, size_t workspace_bytes, void* stream);
 
+/* layers.FixedRadiusSearch forward in one call (kpconv.py:2021-2023 builds the
+ * table, then searches; Open3D's layer does the same in two ops).  workspace
+ * >= _layer_workspace_size (the search plan + scratch for the table build).
+ * stage 0: the table build into hash_table_index / hash_table_cell_splits
+ * when build_table (else they hold a table of these points at this radius),
+ * the count, totals[0..1] = (total, rows longer than 64) written by the
+ * scan's last tile (nullable; may be pinned host memory), sizes[0..2] = (total,
+ * rows longer than 64, widest row) on the device (nullable), count_done
+ * (nullable hipEvent_t) recorded, and — when capacity >= 0 — the row copy into
+ * buffers of `capacity` entries (as _fill_bounded parts 1; nothing written
+ * when the total exceeds it).  stage 1..3: _fill_bounded with parts = stage
+ * (the re-run of long rows; exact buffers after a short capacity). */
+size_t o3dml_fixed_radius_search_layer_workspace_size(int64_t n_points, int64_t n_queries, int64_t n_batch,
+                                                      int64_t total_bins);
+int o3dml_fixed_radius_search_layer(const float* points, int64_t n_points, const float* queries,
+                                    int64_t n_queries, float radius, int64_t n_batch,
+                                    const int64_t* points_row_splits, const int64_t* queries_row_splits,
+                                    const int64_t* points_row_splits_host, const uint32_t* hash_table_splits,
+                                    const uint32_t* hash_table_splits_host, int64_t total_bins,
+                                    uint32_t* hash_table_index, uint32_t* hash_table_cell_splits, int build_table,
+                                    int metric, int ignore_query_point, int self_search, int with_distances,
+                                    int64_t* neighbors_row_splits, int64_t* totals, int64_t* sizes, int index_bits,
+                                    void* neighbors_index, float* neighbors_distance, int64_t capacity, int stage,
+                                    void* count_done, void* workspace, size_t workspace_bytes, void* stream);
+/* The fill of a counted search (_layer or _count workspace) as KPConv's dense
+ * neighbour matrix (kpconv.py:2002-2034 batch_neighbors = fixed_radius_search
+ * + ragged_to_dense): int32 [M, width] (width >= the widest row), row q = its
+ * neighbours in the canonical order then pad_value.  parts as _fill_bounded. */
+int o3dml_fixed_radius_search_fill_dense(const float* queries, int64_t n_points, int64_t n_queries, float radius,
+                                         int64_t n_batch, const int64_t* points_row_splits,
+                                         const int64_t* queries_row_splits, const int64_t* points_row_splits_host,
+                                         const uint32_t* hash_table_splits, const uint32_t* hash_table_cell_splits,
+                                         int metric, int ignore_query_point, const int64_t* neighbors_row_splits,
+                                         int64_t width, int32_t pad_value, int32_t* neighbors_dense, int parts,
+                                         void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- kNN: replaces open3d.ml.torch.ops.knn_search / layers.KNNSearch
  * (ml3d/torch/models/point_transformer.py:724-729) and
  * open3d.core.nns.NearestNeighborSearch.knn_search
@@ -272,6 +308,12 @@ int o3dml_grid_subsample_count_async(const float* points, int64_t n_points, int6
 int o3dml_grid_subsample_count(const float* points, int64_t n_points, int64_t n_batch, const int64_t* row_splits,
                                const int64_t* row_splits_host, float dl, int64_t max_p, int64_t* n_out_host,
                                void* workspace, size_t workspace_bytes, void* stream);
+/* The random grid orientation of KPConv's batch_grid_subsampling
+ * (kpconv.py:2063-2090): out = p @ R_b (transpose: p @ R_b^T) for the points
+ * of batch item b, rotations f32 [B,3,3] on the device, the reference's fp32
+ * rounding ((p0 R0j + p1 R1j) + p2 R2j); out may alias points. */
+int o3dml_rotate_batched(const float* points, int64_t n_points, int64_t n_batch, const int64_t* row_splits,
+                         const float* rotations, int transpose, float* out, void* stream);
 int o3dml_grid_subsample_fill(const float* points, int64_t n_points, int64_t n_batch, const float* features, int fdim,
                               const int32_t* classes, int ldim, float* out_points, float* out_features,
                               int32_t* out_classes, int64_t* out_lengths, void* workspace, size_t workspace_bytes,

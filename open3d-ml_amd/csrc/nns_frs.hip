@@ -230,7 +230,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                  float* __restrict__ tdist, uint32_t* __restrict__ over, int64_t* __restrict__ n_over,
                  const int64_t* __restrict__ rs, TIdx* __restrict__ out_idx, float* __restrict__ out_dist,
                  const int64_t* __restrict__ total, int64_t cap, const uint32_t* __restrict__ dir,
-                 int64_t dir_cap, int qlog) {
+                 int64_t dir_cap, int qlog, int64_t dense_w) {
     __shared__ float4 cand[kCandCap];
     __shared__ float4 qsh[64];
     __shared__ int64_t qrow[MODE == 0 ? 1 : 64];  // MODE 0: the row is the query id (qsh .w)
@@ -283,7 +283,8 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
             if constexpr (REL16) pbase = static_cast<uint32_t>(prs[b]);
             const uint32_t first = hts[b], tsize = hts[b + 1] - first;
             qb = query_bins(q4.x, q4.y, q4.z, r, inv, first, tsize);
-            if constexpr (MODE == 1) row = rs[qid];
+            // MODE 1 into a dense [M, dense_w] matrix: row qid starts at qid * dense_w
+            if constexpr (MODE == 1) row = dense_w > 0 ? static_cast<int64_t>(qid) * dense_w : rs[qid];
         }
         uint64_t todo = __builtin_amdgcn_ballot_w64(valid);
         while (todo) {
@@ -609,6 +610,34 @@ __global__ void __launch_bounds__(256) group_rows_copy_kernel(int64_t m, const u
                     if constexpr (DIST) dist[ou + lane] = dv[u];
                 }
             }
+        }
+    }
+}
+
+// Final rows into a dense int32 [M, width] matrix padded with `pad` (KPConv's
+// batch_neighbors, kpconv.py:2002-2034: fixed_radius_search + ragged_to_dense
+// in one pass).  One wave per row; rows longer than kRowCap get only their
+// padding here (the MODE 1 re-run writes their entries at row * width).
+template <bool REL16>
+__global__ void __launch_bounds__(256) group_rows_dense_kernel(int64_t m, const uint32_t* __restrict__ counts,
+                                                               const int64_t* __restrict__ qrs,
+                                                               const int64_t* __restrict__ prs, int nb,
+                                                               const uint32_t* __restrict__ tidx, int64_t width,
+                                                               int32_t pad, int32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (static_cast<int64_t>(gridDim.x) * blockDim.x) >> 6;
+    const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tidx);
+    for (int64_t t = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6; t < m; t += nwaves) {
+        const uint32_t c = counts[t];
+        const int64_t n = c <= static_cast<uint32_t>(kRowCap) ? static_cast<int64_t>(c) : 0;  // entries copied here
+        const int64_t n_all = static_cast<int64_t>(c);
+        const uint32_t pb = REL16 ? static_cast<uint32_t>(prs[batch_of(t, qrs, nb)]) : 0u;
+        int32_t* row = out + t * width;
+        for (int64_t j = lane; j < width; j += 64) {
+            if (j < n)
+                row[j] = static_cast<int32_t>(REL16 ? t16[t * kRowCap + j] + pb : tidx[t * kRowCap + j]);
+            else if (j >= n_all)
+                row[j] = pad;
         }
     }
 }
@@ -958,11 +987,12 @@ static void launch_group(int metric, bool ignore, bool with_dist, bool rel16, hi
                          float thr, int nb, const int64_t* qrs, const uint32_t* hts, const int64_t* prs,
                          uint32_t* counts, uint32_t* tidx, float* tdist, uint32_t* over, int64_t* n_over,
                          const int64_t* rs, TIdx* idx, float* dist, const uint32_t* dir, int64_t dir_cap,
-                         const int64_t* total = nullptr, int64_t cap = -1, int qlog = 6) {
+                         const int64_t* total = nullptr, int64_t cap = -1, int qlog = 6, int64_t dense_w = 0) {
 #define O3DML_GRP(M, I, D, R)                                                                                   \
     frs_group_kernel<M, I, D, MODE, TIdx, R><<<grid, 64, 0, st>>>(pts, n_pts, cs, qpts, qsel, qkeys, bshift, m, m_dev, \
                                                                    r, inv, thr, nb, qrs, hts, prs, counts, tidx,  \
-                                                                   tdist, over, n_over, rs, idx, dist, total, cap, dir, dir_cap, qlog)
+                                                                   tdist, over, n_over, rs, idx, dist, total, cap, dir, dir_cap, qlog, \
+                                                                   dense_w)
 #define O3DML_GRP_R(M, I, D)                                  \
     do {                                                      \
         if (MODE == 0 && rel16)                               \
@@ -1138,27 +1168,27 @@ O3DML_API size_t o3dml_fixed_radius_search_workspace_size(int64_t n_points, int6
            std::max(prim::scan_workspace_bytes(n_queries), prim::radix_sort_workspace_bytes<uint32_t>(n_queries));
 }
 
-O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_points, const float* queries,
-                                              int64_t n_queries, float radius, int64_t n_batch,
-                                              const int64_t* points_row_splits, const int64_t* queries_row_splits,
-                                              const int64_t* points_row_splits_host,
-                                              const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
-                                              const uint32_t* hash_table_cell_splits, int metric,
-                                              int ignore_query_point, int self_search, int with_distances,
-                                              int64_t* neighbors_row_splits, void* workspace,
-                                              size_t workspace_bytes, void* stream) {
-    O3DML_GUARD_BEGIN
+namespace o3dml {
+// The count phase; totals (nullable, e.g. pinned host memory): [total, rows
+// longer than kRowCap] written by the scan's last tile.
+static void frs_count_impl(const float* points, int64_t n_points, const float* queries, int64_t n_queries,
+                           float radius, int64_t n_batch, const int64_t* points_row_splits,
+                           const int64_t* queries_row_splits, const int64_t* points_row_splits_host,
+                           const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
+                           const uint32_t* hash_table_cell_splits, int metric, int ignore_query_point,
+                           int self_search, int with_distances, int64_t* neighbors_row_splits, void* workspace,
+                           size_t workspace_bytes, hipStream_t st, int64_t* totals) {
     O3DML_REQUIRE(metric >= 0 && metric <= 2, "metric must be L1(0), L2(1) or Linf(2)");
     O3DML_REQUIRE(radius > 0.f, "radius must be > 0");
     O3DML_REQUIRE(n_queries < (int64_t(1) << 31) && n_points < (int64_t(1) << 31), "too many points");
     O3DML_REQUIRE(n_batch >= 1, "need at least one batch item");
-    hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
     FrsPlan pl = take_plan(ws, n_points, n_queries, n_batch, with_distances != 0);
     if (n_queries == 0 || n_points == 0) {
         O3DML_CHECK_HIP(hipMemsetAsync(pl.scalars, 0, sizeof(int64_t) * 4, st));
         O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t) * (n_queries + 1), st));
-        return 0;
+        if (totals) frs_totals_kernel<<<1, 64, 0, st>>>(neighbors_row_splits, n_queries, pl.scalars, totals);
+        return;
     }
     const float thr = metric == kL2 ? radius * radius : radius;
     const float inv = 1.0f / (2.0f * radius);
@@ -1210,7 +1240,25 @@ O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_poi
                                  pl.scalars, nullptr, nullptr, nullptr, pl.dir, pl.dir_cap, nullptr, -1, qlog);
     }
     Workspace sws = ws;
-    prim::scan<uint32_t, int64_t>(pl.counts, neighbors_row_splits + 1, n_queries, true, sws, st);
+    prim::scan<uint32_t, int64_t>(pl.counts, neighbors_row_splits + 1, n_queries, true, sws, st, totals,
+                                  pl.scalars);
+}
+}  // namespace o3dml
+
+O3DML_API int o3dml_fixed_radius_search_count(const float* points, int64_t n_points, const float* queries,
+                                              int64_t n_queries, float radius, int64_t n_batch,
+                                              const int64_t* points_row_splits, const int64_t* queries_row_splits,
+                                              const int64_t* points_row_splits_host,
+                                              const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
+                                              const uint32_t* hash_table_cell_splits, int metric,
+                                              int ignore_query_point, int self_search, int with_distances,
+                                              int64_t* neighbors_row_splits, void* workspace,
+                                              size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    frs_count_impl(points, n_points, queries, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
+                   points_row_splits_host, hash_table_splits, hash_table_index, hash_table_cell_splits, metric,
+                   ignore_query_point, self_search, with_distances, neighbors_row_splits, workspace,
+                   workspace_bytes, as_stream(stream), nullptr);
     O3DML_GUARD_END
 }
 
@@ -1252,27 +1300,27 @@ O3DML_API int o3dml_fixed_radius_search_fill(const float* points, int64_t n_poin
             neighbors_distance, -1, 3, workspace, workspace_bytes, stream);
 }
 
-O3DML_API int o3dml_fixed_radius_search_fill_bounded(
-        const float* points, int64_t n_points, const float* queries, int64_t n_queries, float radius,
-        int64_t n_batch, const int64_t* points_row_splits, const int64_t* queries_row_splits,
-        const int64_t* points_row_splits_host, const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
-        const uint32_t* hash_table_cell_splits, int metric, int ignore_query_point, int self_search,
-        int with_distances, const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
-        float* neighbors_distance, int64_t capacity, int parts, void* workspace, size_t workspace_bytes,
-        void* stream) {
-    O3DML_GUARD_BEGIN
-    (void)points;
-    (void)hash_table_index;
-    (void)self_search;
+namespace o3dml {
+// The fill phase: CSR rows (dense_w = 0) or a dense int32 [M, dense_w] matrix
+// padded with `pad` (neighbors_row_splits then only bounds nothing: capacity -1).
+static void frs_fill_impl(const float* queries, int64_t n_points, int64_t n_queries, float radius, int64_t n_batch,
+                          const int64_t* points_row_splits, const int64_t* queries_row_splits,
+                          const int64_t* points_row_splits_host, const uint32_t* hash_table_splits,
+                          const uint32_t* hash_table_cell_splits, int metric, int ignore_query_point,
+                          int with_distances, const int64_t* neighbors_row_splits, int index_bits,
+                          void* neighbors_index, float* neighbors_distance, int64_t capacity, int parts,
+                          int64_t dense_w, int32_t pad, void* workspace, size_t workspace_bytes, hipStream_t st) {
     O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
     O3DML_REQUIRE(!with_distances || neighbors_distance, "with_distances needs a distance buffer");
-    if (n_queries == 0 || n_points == 0) return 0;
-    hipStream_t st = as_stream(stream);
+    O3DML_REQUIRE(dense_w == 0 || (index_bits == 32 && !with_distances && capacity < 0),
+                  "dense rows are int32 without distances");
+    if (n_queries == 0 || n_points == 0) return;
     Workspace ws(workspace, workspace_bytes);
     FrsPlan pl = take_plan(ws, n_points, n_queries, n_batch, with_distances != 0);  // built by _count (same workspace)
     const float thr = metric == kL2 ? radius * radius : radius;
     const float inv = 1.0f / (2.0f * radius);
     int64_t* rs = const_cast<int64_t*>(neighbors_row_splits);
+    const bool rel16 = rel16_rows(n_batch, points_row_splits_host, n_queries);
     float* dist = with_distances ? neighbors_distance : nullptr;
     const int dev = stream_device(st);
     DeviceScope dscope(dev);
@@ -1283,10 +1331,20 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
         side_lock = std::unique_lock<std::mutex>(side->mu);
         O3DML_CHECK_HIP(hipEventRecord(side->fork, st));
     }
-    if (parts & 1) {
+    if ((parts & 1) && dense_w > 0) {
+        const unsigned gd = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_queries, 4), 1 << 16)));
+        if (rel16)
+            group_rows_dense_kernel<true><<<gd, 256, 0, st>>>(n_queries, pl.counts, queries_row_splits,
+                                                              points_row_splits, (int)n_batch, pl.tidx, dense_w, pad,
+                                                              static_cast<int32_t*>(neighbors_index));
+        else
+            group_rows_dense_kernel<false><<<gd, 256, 0, st>>>(n_queries, pl.counts, queries_row_splits,
+                                                               points_row_splits, (int)n_batch, pl.tidx, dense_w, pad,
+                                                               static_cast<int32_t*>(neighbors_index));
+        O3DML_LAUNCH_CHECK();
+    } else if (parts & 1) {
         TimedRegion tr("frs_group_rows", st);
         const unsigned gc = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_queries, 256), 1 << 16)));
-        const bool rel16 = rel16_rows(n_batch, points_row_splits_host, n_queries);
 #define O3DML_GCOPY3(D, R, T)                                                                                   \
     group_rows_copy_kernel<D, R, T><<<gc, 256, 0, st>>>(n_queries, pl.counts, rs, queries_row_splits,          \
                                                         points_row_splits, (int)n_batch, pl.tidx, pl.tdist,    \
@@ -1307,7 +1365,7 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
     // rows longer than kRowCap: re-run those queries straight into the final
     // rows; the overflow count stays on the device (no host round trip), so a
     // fixed grid strides over however many there are (usually none)
-    if (!(parts & 2)) return 0;  // the caller read a zero overflow count
+    if (!(parts & 2)) return;  // the caller read a zero overflow count
     O3DML_CHECK_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
     const hipStream_t st_main = st;
     st = side->s;
@@ -1319,8 +1377,8 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
                                  0,
                                  pl.scalars, radius, inv, thr, (int)n_batch, queries_row_splits, hash_table_splits,
                                  points_row_splits, nullptr, nullptr, nullptr, pl.over, nullptr, rs,
-                                 static_cast<int32_t*>(neighbors_index), dist, pl.dir, pl.dir_cap, rs + n_queries,
-                                 capacity);
+                                 static_cast<int32_t*>(neighbors_index), dist, pl.dir, pl.dir_cap,
+                                 dense_w > 0 ? nullptr : rs + n_queries, capacity, 6, dense_w);
     else
         launch_group<1, int64_t>(metric, ignore_query_point != 0, dist != nullptr, false, st, go, pl.pts,
                                  static_cast<uint32_t>(n_points), hash_table_cell_splits, qraw, nullptr, nullptr, 32,
@@ -1331,5 +1389,105 @@ O3DML_API int o3dml_fixed_radius_search_fill_bounded(
                                  capacity);
     O3DML_CHECK_HIP(hipEventRecord(side->join, st));
     O3DML_CHECK_HIP(hipStreamWaitEvent(st_main, side->join, 0));
+}
+}  // namespace o3dml
+
+O3DML_API int o3dml_fixed_radius_search_fill_bounded(
+        const float* points, int64_t n_points, const float* queries, int64_t n_queries, float radius,
+        int64_t n_batch, const int64_t* points_row_splits, const int64_t* queries_row_splits,
+        const int64_t* points_row_splits_host, const uint32_t* hash_table_splits, const uint32_t* hash_table_index,
+        const uint32_t* hash_table_cell_splits, int metric, int ignore_query_point, int self_search,
+        int with_distances, const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
+        float* neighbors_distance, int64_t capacity, int parts, void* workspace, size_t workspace_bytes,
+        void* stream) {
+    O3DML_GUARD_BEGIN
+    (void)points;
+    (void)hash_table_index;
+    (void)self_search;
+    frs_fill_impl(queries, n_points, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
+                  points_row_splits_host, hash_table_splits, hash_table_cell_splits, metric, ignore_query_point,
+                  with_distances, neighbors_row_splits, index_bits, neighbors_index, neighbors_distance, capacity,
+                  parts, 0, 0, workspace, workspace_bytes, as_stream(stream));
+    O3DML_GUARD_END
+}
+
+O3DML_API int o3dml_fixed_radius_search_fill_dense(
+        const float* queries, int64_t n_points, int64_t n_queries, float radius, int64_t n_batch,
+        const int64_t* points_row_splits, const int64_t* queries_row_splits, const int64_t* points_row_splits_host,
+        const uint32_t* hash_table_splits, const uint32_t* hash_table_cell_splits, int metric,
+        int ignore_query_point, const int64_t* neighbors_row_splits, int64_t width, int32_t pad_value,
+        int32_t* neighbors_dense, int parts, void* workspace, size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(width >= 1, "dense width must be >= 1 (the widest row)");
+    frs_fill_impl(queries, n_points, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
+                  points_row_splits_host, hash_table_splits, hash_table_cell_splits, metric, ignore_query_point, 0,
+                  neighbors_row_splits, 32, neighbors_dense, nullptr, -1, parts, width, pad_value, workspace,
+                  workspace_bytes, as_stream(stream));
+    O3DML_GUARD_END
+}
+
+// ---------------------------------------------------------------------------
+// layers.FixedRadiusSearch in one call (the host cost of a small search is
+// several Python-side launches otherwise): optional table build into the
+// caller's table buffers, count, totals to pinned memory and/or sizes to the
+// device, the count-done event, the speculative row copy.
+// ---------------------------------------------------------------------------
+namespace o3dml {
+static size_t layer_search_bytes(int64_t n, int64_t m, int64_t nb, int64_t total_bins) {
+    const size_t scratch = std::max(std::max(prim::scan_workspace_bytes(m), prim::radix_sort_workspace_bytes<uint32_t>(m)),
+                                    o3dml_build_spatial_hash_table_workspace_size(n, total_bins));
+    return plan_bytes(n, m, nb) + scratch;
+}
+}  // namespace o3dml
+
+O3DML_API size_t o3dml_fixed_radius_search_layer_workspace_size(int64_t n_points, int64_t n_queries,
+                                                                int64_t n_batch, int64_t total_bins) {
+    return layer_search_bytes(n_points, n_queries, n_batch, total_bins);
+}
+
+O3DML_API int o3dml_fixed_radius_search_layer(
+        const float* points, int64_t n_points, const float* queries, int64_t n_queries, float radius,
+        int64_t n_batch, const int64_t* points_row_splits, const int64_t* queries_row_splits,
+        const int64_t* points_row_splits_host, const uint32_t* hash_table_splits,
+        const uint32_t* hash_table_splits_host, int64_t total_bins, uint32_t* hash_table_index,
+        uint32_t* hash_table_cell_splits, int build_table, int metric, int ignore_query_point, int self_search,
+        int with_distances, int64_t* neighbors_row_splits, int64_t* totals, int64_t* sizes, int index_bits,
+        void* neighbors_index, float* neighbors_distance, int64_t capacity, int stage, void* count_done,
+        void* workspace, size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(stage >= 0 && stage <= 3, "stage must be 0 (build + count [+ copy]) or fill parts 1..3");
+    const size_t need = layer_search_bytes(n_points, n_queries, n_batch, total_bins);
+    O3DML_REQUIRE(workspace_bytes >= need, "layer workspace too small");
+    hipStream_t st = as_stream(stream);
+    if (stage > 0) {
+        frs_fill_impl(queries, n_points, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
+                      points_row_splits_host, hash_table_splits, hash_table_cell_splits, metric, ignore_query_point,
+                      with_distances, neighbors_row_splits, index_bits, neighbors_index, neighbors_distance,
+                      capacity, stage, 0, 0, workspace, need, st);
+        return 0;
+    }
+    if (build_table) {  // the table's scratch is the search plan's scratch tail (free until the count)
+        const size_t plan = plan_bytes(n_points, n_queries, n_batch);
+        const int rc = o3dml_build_spatial_hash_table(points, n_points, radius, n_batch, points_row_splits,
+                                                      hash_table_splits, hash_table_splits_host, total_bins,
+                                                      hash_table_index, hash_table_cell_splits,
+                                                      static_cast<char*>(workspace) + plan, need - plan, stream);
+        if (rc) return rc;
+    }
+    frs_count_impl(points, n_points, queries, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
+                   points_row_splits_host, hash_table_splits, hash_table_index, hash_table_cell_splits, metric,
+                   ignore_query_point, self_search, with_distances, neighbors_row_splits, workspace, need, st, totals);
+    if (sizes) {  // [total, rows longer than 64, widest row] on the device
+        frs_sizes_kernel<<<1, 1024, 0, st>>>(neighbors_row_splits, n_queries, static_cast<const int64_t*>(workspace),
+                                             sizes);
+        O3DML_LAUNCH_CHECK();
+    }
+    // the host waits for the totals only, not for the row copy queued next
+    if (count_done) O3DML_CHECK_HIP(hipEventRecord(static_cast<hipEvent_t>(count_done), st));
+    if (capacity >= 0)
+        frs_fill_impl(queries, n_points, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
+                      points_row_splits_host, hash_table_splits, hash_table_cell_splits, metric, ignore_query_point,
+                      with_distances, neighbors_row_splits, index_bits, neighbors_index, neighbors_distance,
+                      capacity, 1, 0, 0, workspace, need, st);
     O3DML_GUARD_END
 }

@@ -83,13 +83,17 @@ __global__ void bin_boundaries_kernel(const uint32_t* __restrict__ skeys, int64_
 //            peers, per-wave counts in LDS), ids written to their slots.
 // ---------------------------------------------------------------------------
 constexpr int kSmallTable = 4096;
-constexpr int kHashChunk = 4096;  // points per chunk = 4 waves x 16 rows of 64
+// points per chunk = 4 waves x 16 rows of 64; calls with few points take
+// chunks of 1024 (4 rows per wave) so more workgroups share the work (one
+// 65,536-point scene: 16 -> 64 workgroups)
+constexpr int kHashChunk = 4096;
+constexpr int kHashChunkSmall = 1024;
 constexpr int kHashWaves = 4;
 
 __global__ void __launch_bounds__(256) hash_plan_kernel(const int64_t* __restrict__ prs, int nb,
                                                         const uint32_t* __restrict__ hts,
                                                         int64_t* __restrict__ chunk_start,
-                                                        int64_t* __restrict__ hist_off) {
+                                                        int64_t* __restrict__ hist_off, int chunk) {
     __shared__ int64_t wsum[2][4];
     int64_t carry_c = 0, carry_h = 0;
     for (int b0 = 0; b0 < nb; b0 += 256) {
@@ -97,7 +101,7 @@ __global__ void __launch_bounds__(256) hash_plan_kernel(const int64_t* __restric
         int64_t c = 0, h = 0;
         if (b < nb) {
             const int64_t n = prs[b + 1] - prs[b];
-            c = n > kHashChunk ? ceil_div(n, kHashChunk) : 1;
+            c = n > chunk ? ceil_div(n, chunk) : 1;
             h = c * static_cast<int64_t>(hts[b + 1] - hts[b]);
         }
         const int64_t ic = wave_inclusive_scan(c), ih = wave_inclusive_scan(h);
@@ -148,7 +152,8 @@ __global__ void __launch_bounds__(256) hash_chunk_hist_kernel(const float* __res
                                                               const uint32_t* __restrict__ hts,
                                                               const int64_t* __restrict__ chunk_start,
                                                               const int64_t* __restrict__ hist_off,
-                                                              uint32_t* __restrict__ bins, uint32_t* __restrict__ hist) {
+                                                              uint32_t* __restrict__ bins, uint32_t* __restrict__ hist,
+                                                              int chunk) {
     extern __shared__ uint32_t h[];  // [max bins per item]
     int b;
     int64_t c;
@@ -157,7 +162,7 @@ __global__ void __launch_bounds__(256) hash_chunk_hist_kernel(const float* __res
     const uint32_t k64 = pow64_mod(tsize);
     for (uint32_t i = threadIdx.x; i < tsize; i += 256) h[i] = 0;
     __syncthreads();
-    const int64_t p0 = prs[b] + c * kHashChunk, p1 = min(prs[b + 1], p0 + kHashChunk);
+    const int64_t p0 = prs[b] + c * chunk, p1 = min(prs[b + 1], p0 + chunk);
     for (int64_t i = p0 + threadIdx.x; i < p1; i += 256) {
         const uint32_t bin = point_bin_k(points[3 * i], points[3 * i + 1], points[3 * i + 2], inv, tsize, k64);
         bins[i] = bin;
@@ -168,86 +173,124 @@ __global__ void __launch_bounds__(256) hash_chunk_hist_kernel(const float* __res
     for (uint32_t i = threadIdx.x; i < tsize; i += 256) out[i] = h[i];
 }
 
-// Per batch item (one workgroup): every bin's column of chunk counts becomes
-// the chunk's first slot of that bin (exclusive scan over the chunks plus the
-// bin's start inside the item, a scan over the bins); cell_splits too.
-__global__ void __launch_bounds__(1024) hash_hist_scan_kernel(int nb, const int64_t* __restrict__ prs,
-                                                              const uint32_t* __restrict__ hts,
-                                                              const int64_t* __restrict__ chunk_start,
-                                                              const int64_t* __restrict__ hist_off,
-                                                              uint32_t* __restrict__ hist,
-                                                              uint32_t* __restrict__ cell_splits) {
-    __shared__ uint32_t wsum[16];
-    const int b = blockIdx.x;
-    const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+// Per (batch item, slice of 64 bins), 4 waves: every bin's column of chunk
+// counts becomes each chunk's first slot of that bin relative to the bin's
+// start inside the item (exclusive scan over the chunks: wave q scans a
+// quarter of the chunks, the quarters' sums meet in LDS), and the bin's total
+// goes to bin_tot — the scan over the bins is done by the scatter kernel.
+// (One workgroup per item scanned the columns before: a single 65,536-point
+// item of 64 chunks took 11 us in one workgroup.)
+constexpr int kColBins = 64;
+__global__ void __launch_bounds__(256) hash_hist_colscan_kernel(int nslices, const uint32_t* __restrict__ hts,
+                                                                const int64_t* __restrict__ chunk_start,
+                                                                const int64_t* __restrict__ hist_off,
+                                                                uint32_t* __restrict__ hist,
+                                                                uint32_t* __restrict__ bin_tot) {
+    __shared__ uint32_t qsum[4][kColBins];
+    const int b = blockIdx.x / nslices, s = blockIdx.x % nslices;
+    const int q = wave_id(), lane = lane_id();
     const uint32_t first = hts[b], tsize = hts[b + 1] - first;
-    const int64_t item0 = prs[b];
+    const uint32_t bin = static_cast<uint32_t>(s * kColBins + lane);
+    if (static_cast<uint32_t>(s * kColBins) >= tsize) return;  // whole workgroup
+    const bool valid = bin < tsize;
     const int64_t nchunks = chunk_start[b + 1] - chunk_start[b];
-    uint32_t* H = hist + hist_off[b];
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < tsize; b0 += 1024) {  // bins b0 + t
-        const uint32_t bin = b0 + t;
-        uint32_t tot = 0;
-        if (bin < tsize) {
-            int64_t cc = 0;
-            for (; cc + 4 <= nchunks; cc += 4) {  // independent loads in flight
-                const uint32_t v0 = H[cc * tsize + bin], v1 = H[(cc + 1) * tsize + bin],
-                               v2 = H[(cc + 2) * tsize + bin], v3 = H[(cc + 3) * tsize + bin];
-                tot += (v0 + v1) + (v2 + v3);
-            }
-            for (; cc < nchunks; ++cc) tot += H[cc * tsize + bin];
+    const int64_t c0 = nchunks * q / 4, c1 = nchunks * (q + 1) / 4;
+    uint32_t* H = hist + hist_off[b] + bin;
+    uint32_t sum = 0;
+    if (valid) {
+        int64_t cc = c0;
+        for (; cc + 8 <= c1; cc += 8) {  // independent loads in flight
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = H[(cc + u) * tsize];
+            sum += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
         }
-        const uint32_t inc = wave_inclusive_scan(tot);
-        if (lane == 63) wsum[w] = inc;
-        __syncthreads();
-        uint32_t start = carry + inc - tot, all = 0;
-        for (int ww = 0; ww < 16; ++ww) {
-            start += ww < w ? wsum[ww] : 0u;
-            all += wsum[ww];
-        }
-        if (bin < tsize) {
-            cell_splits[first + bin] = static_cast<uint32_t>(item0 + start);
-            uint32_t run = start;
-            for (int64_t cc = 0; cc < nchunks; ++cc) {
-                const uint32_t v = H[cc * tsize + bin];
-                H[cc * tsize + bin] = run;
-                run += v;
-            }
-        }
-        carry += all;
-        __syncthreads();
+        for (; cc < c1; ++cc) sum += H[cc * tsize];
     }
-    if (b == nb - 1 && t == 0) cell_splits[first + tsize] = static_cast<uint32_t>(prs[nb]);
+    qsum[q][lane] = sum;
+    __syncthreads();
+    uint32_t run = 0;
+    for (int k = 0; k < q; ++k) run += qsum[k][lane];
+    if (valid) {
+        if (q == 3) bin_tot[first + bin] = run + sum;
+        int64_t cc = c0;
+        for (; cc + 8 <= c1; cc += 8) {  // 8 loads in flight, then the 8 bases
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = H[(cc + u) * tsize];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                H[(cc + u) * tsize] = run;
+                run += v[u];
+            }
+        }
+        for (; cc < c1; ++cc) {
+            const uint32_t v = H[cc * tsize];
+            H[cc * tsize] = run;
+            run += v;
+        }
+    }
 }
 
 // Per chunk: ranks the chunk's points stably and writes their ids; the chunk's
-// first slot per bin comes from hash_hist_scan_kernel.
+// first slot per bin = the bin's start inside the item (exclusive scan of the
+// item's bin totals, done here in LDS; chunk 0 also writes the item's
+// cell_splits) + the chunk's offset from hash_hist_colscan_kernel.
+template <int CHUNK>
 __global__ void __launch_bounds__(256) hash_chunk_scatter_kernel(int nb, const int64_t* __restrict__ prs,
                                                                  const uint32_t* __restrict__ hts,
                                                                  const int64_t* __restrict__ chunk_start,
                                                                  const int64_t* __restrict__ hist_off,
                                                                  const uint32_t* __restrict__ bins,
                                                                  const uint32_t* __restrict__ hist,
+                                                                 const uint32_t* __restrict__ bin_tot,
+                                                                 uint32_t* __restrict__ cell_splits,
                                                                  uint32_t* __restrict__ hti, int max_bins) {
-    constexpr int kRows = kHashChunk / 64 / kHashWaves;  // rows of 64 per wave
-    extern __shared__ uint32_t wc_all[];                // [kHashWaves][max_bins]: counts, then bases
+    constexpr int kRows = CHUNK / 64 / kHashWaves;  // rows of 64 per wave
+    // [kHashWaves][max_bins]: counts, then bases; then [max_bins] bin starts
+    extern __shared__ uint32_t wc_all[];
+    __shared__ uint32_t wsum[kHashWaves];
     int b;
     int64_t c;
     if (!hash_chunk_of(chunk_start, nb, b, c)) return;
     const int t = threadIdx.x, w = wave_id(), lane = lane_id();
-    const uint32_t tsize = hts[b + 1] - hts[b];
+    const uint32_t first = hts[b], tsize = hts[b + 1] - first;
     const int64_t item0 = prs[b], item_end = prs[b + 1];
     const uint32_t* base = hist + hist_off[b] + c * tsize;
     uint32_t* wc = wc_all + w * max_bins;
+    uint32_t* bstart = wc_all + kHashWaves * max_bins;
     for (uint32_t i = t; i < tsize; i += 256)
 #pragma unroll
         for (int ww = 0; ww < kHashWaves; ++ww) wc_all[ww * max_bins + i] = 0;
-    __syncthreads();
+    {  // bin starts: exclusive scan of the item's bin totals, 256-bin rounds
+        uint32_t carry = 0;
+        for (uint32_t b0 = 0; b0 < tsize; b0 += 256) {
+            const uint32_t i = b0 + t;
+            const uint32_t v = i < tsize ? bin_tot[first + i] : 0u;
+            const uint32_t inc = wave_inclusive_scan(v);
+            if (lane == 63) wsum[w] = inc;
+            __syncthreads();
+            uint32_t st = carry + inc - v, all = 0;
+#pragma unroll
+            for (int ww = 0; ww < kHashWaves; ++ww) {
+                st += ww < w ? wsum[ww] : 0u;
+                all += wsum[ww];
+            }
+            if (i < tsize) {
+                bstart[i] = st;
+                if (c == 0) cell_splits[first + i] = static_cast<uint32_t>(item0 + st);
+            }
+            carry += all;
+            __syncthreads();
+        }
+        if (c == 0 && b == nb - 1 && t == 0) cell_splits[first + tsize] = static_cast<uint32_t>(prs[nb]);
+    }
+    __syncthreads();  // the zeroed counts (tsize >= 1: the loop above has barriers too)
     // each wave ranks its contiguous rows in order (peers = same bin, found
     // with one ballot per bin bit), running per-bin counts in LDS — LDS
     // operations of one wave execute in order, no barrier between rows
-    const int64_t p0 = item0 + c * kHashChunk;
-    const int64_t pend = min(item_end, p0 + kHashChunk);
+    const int64_t p0 = item0 + c * CHUNK;
+    const int64_t pend = min(item_end, p0 + CHUNK);
     const int nbits = tsize > 1 ? 32 - __builtin_clz(tsize - 1) : 0;
     const uint64_t lt = lanemask_lt();
     uint32_t dig[kRows], loff[kRows];
@@ -271,7 +314,7 @@ __global__ void __launch_bounds__(256) hash_chunk_scatter_kernel(int nb, const i
     __syncthreads();
     // per-wave bases: chunk base + counts of the earlier waves (stable)
     for (uint32_t i = t; i < tsize; i += 256) {
-        uint32_t a = base[i];
+        uint32_t a = bstart[i] + base[i];
 #pragma unroll
         for (int ww = 0; ww < kHashWaves; ++ww) {
             const uint32_t cw = wc_all[ww * max_bins + i];
@@ -312,9 +355,11 @@ O3DML_API size_t o3dml_build_spatial_hash_table_workspace_size(int64_t n_points,
     // <= kSmallTable bins: sum_b chunks_b T_b <= sum_b (N_b / chunk + 1) T_b)
     // and the plan — the larger of the two
     const size_t radix = ws_bytes<uint32_t>(n_points) * 2 + prim::radix_sort_workspace_bytes<uint32_t>(n_points);
+    // chunks of 1024 (small calls): sum_b (N_b / 1024 + 1) T_b <= 4 N + T
     const int64_t nb_ub = total_bins;  // every batch item has >= 1 bin
-    const size_t small = ws_bytes<uint32_t>(n_points) + ws_bytes<uint32_t>(n_points + total_bins) +
-                         2 * ws_bytes<int64_t>(nb_ub + 1);
+    const int64_t hist_ub = (ceil_div(n_points, kHashChunk) < 512 ? 4 * n_points : n_points) + total_bins;
+    const size_t small = ws_bytes<uint32_t>(n_points) + ws_bytes<uint32_t>(hist_ub) +
+                         ws_bytes<uint32_t>(total_bins) + 2 * ws_bytes<int64_t>(nb_ub + 1);
     return std::max(radix, small);
 }
 
@@ -340,23 +385,33 @@ O3DML_API int o3dml_build_spatial_hash_table(const float* points, int64_t n_poin
     }
     if (small) {
         uint32_t* bins = ws.take<uint32_t>(n_points);
-        uint32_t* hist = ws.take<uint32_t>(n_points + total_bins);
+        // small calls (fewer than 512 chunks of 4096) take chunks of 1024
+        const int chunk = ceil_div(n_points, kHashChunk) < 512 ? kHashChunkSmall : kHashChunk;
+        uint32_t* hist = ws.take<uint32_t>((chunk == kHashChunkSmall ? 4 * n_points : n_points) + total_bins);
+        uint32_t* bin_tot = ws.take<uint32_t>(total_bins);
         int64_t* chunk_start = ws.take<int64_t>(n_batch + 1);
         int64_t* hist_off = ws.take<int64_t>(n_batch + 1);
         hash_plan_kernel<<<1, 256, 0, st>>>(points_row_splits, (int)n_batch, hash_table_splits, chunk_start,
-                                            hist_off);
+                                            hist_off, chunk);
         O3DML_LAUNCH_CHECK();
-        const unsigned grid = static_cast<unsigned>(ceil_div(n_points, kHashChunk) + n_batch);  // >= chunk count
+        const unsigned grid = static_cast<unsigned>(ceil_div(n_points, chunk) + n_batch);  // >= chunk count
         hash_chunk_hist_kernel<<<grid, 256, sizeof(uint32_t) * max_bins, st>>>(
-                points, inv, (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist);
+                points, inv, (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist,
+                chunk);
         O3DML_LAUNCH_CHECK();
-        hash_hist_scan_kernel<<<static_cast<unsigned>(n_batch), 1024, 0, st>>>(
-                (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, hist,
-                hash_table_cell_splits);
+        const int nslices = static_cast<int>(ceil_div(max_bins, kColBins));
+        hash_hist_colscan_kernel<<<static_cast<unsigned>(n_batch * nslices), 256, 0, st>>>(
+                nslices, hash_table_splits, chunk_start, hist_off, hist, bin_tot);
         O3DML_LAUNCH_CHECK();
-        hash_chunk_scatter_kernel<<<grid, 256, sizeof(uint32_t) * kHashWaves * max_bins, st>>>(
-                (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist,
-                hash_table_index, static_cast<int>(max_bins));
+        const size_t lds = sizeof(uint32_t) * (kHashWaves + 1) * max_bins;
+        if (chunk == kHashChunkSmall)
+            hash_chunk_scatter_kernel<kHashChunkSmall><<<grid, 256, lds, st>>>(
+                    (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist, bin_tot,
+                    hash_table_cell_splits, hash_table_index, static_cast<int>(max_bins));
+        else
+            hash_chunk_scatter_kernel<kHashChunk><<<grid, 256, lds, st>>>(
+                    (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist, bin_tot,
+                    hash_table_cell_splits, hash_table_index, static_cast<int>(max_bins));
         O3DML_LAUNCH_CHECK();
         return 0;
     }

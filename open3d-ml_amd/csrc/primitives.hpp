@@ -42,15 +42,29 @@ __global__ void __launch_bounds__(kScanBlock) scan_tile_sums(const TIn* __restri
 
 // Scan one tile (striped coalesced load -> LDS -> blocked per-thread scan).
 // offsets (nullable): exclusive carry-in per tile.
+// raw_sums (nullable): the tiles' plain sums — the tile adds up its
+// predecessors itself (no separate scan of the sums: one launch fewer).
+// tail (nullable, e.g. pinned host memory): the last tile writes the total
+// to tail[0] and, with tail_src, tail_src[0] to tail[1].
 template <class TIn, class TOut>
 __global__ void __launch_bounds__(kScanBlock) scan_tile_apply(const TIn* in, TOut* out, int64_t n,
                                                               const int64_t* __restrict__ offsets,
-                                                              int inclusive) {
+                                                              int inclusive,
+                                                              const int64_t* __restrict__ raw_sums = nullptr,
+                                                              int64_t* tail = nullptr,
+                                                              const int64_t* tail_src = nullptr) {
     // +1 pad per 8 elements keeps the blocked LDS reads off one bank
     __shared__ int64_t tile[kScanTile + kScanTile / 8];
     __shared__ int64_t wsum[kScanBlock / 64];
+    __shared__ int64_t carry_in[kScanBlock / 64];
     const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
     const int t = threadIdx.x;
+    if (raw_sums) {  // (uniform branch) carry = sum of the earlier tiles' sums
+        int64_t c = 0;
+        for (int64_t j = t; j < static_cast<int64_t>(blockIdx.x); j += kScanBlock) c += raw_sums[j];
+        c = wave_sum(c);
+        if (lane_id() == 0) carry_in[wave_id()] = c;
+    }
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) {
         const int e = k * kScanBlock + t;
@@ -70,6 +84,8 @@ __global__ void __launch_bounds__(kScanBlock) scan_tile_apply(const TIn* in, TOu
     if (lane_id() == 63) wsum[wave_id()] = incl;
     __syncthreads();
     int64_t run = incl - acc + (offsets ? offsets[blockIdx.x] : 0);
+    if (raw_sums)
+        for (int w = 0; w < kScanBlock / 64; ++w) run += carry_in[w];
     for (int w = 0; w < wave_id(); ++w) run += wsum[w];
 #pragma unroll
     for (int j = 0; j < kScanItems; ++j) {
@@ -77,6 +93,10 @@ __global__ void __launch_bounds__(kScanBlock) scan_tile_apply(const TIn* in, TOu
         const int64_t x = v[j];
         tile[e + (e >> 3)] = inclusive ? run + x : run;
         run += x;
+    }
+    if (tail && blockIdx.x == gridDim.x - 1 && t == kScanBlock - 1) {  // run = the inclusive total
+        tail[0] = run;
+        if (tail_src) tail[1] = tail_src[0];
     }
     __syncthreads();
 #pragma unroll
@@ -97,23 +117,38 @@ inline size_t scan_workspace_bytes(int64_t n) {
     return b;
 }
 
+// Tiles up to which every tile sums its predecessors' sums itself (two
+// launches: sums, apply); more tiles scan the sums recursively (three+).
+constexpr int64_t kScanDirectTiles = 1024;
+
 // out[i] = sum_{j<=i} in[j] (inclusive) or sum_{j<i} in[j] (exclusive).
-// in == out is allowed.
+// in == out is allowed.  tail (nullable): total -> tail[0] (and tail_src[0]
+// -> tail[1]) written by the last tile, e.g. into pinned host memory.
 template <class TIn, class TOut>
-void scan(const TIn* in, TOut* out, int64_t n, bool inclusive, Workspace& ws, hipStream_t st) {
+void scan(const TIn* in, TOut* out, int64_t n, bool inclusive, Workspace& ws, hipStream_t st,
+          int64_t* tail = nullptr, const int64_t* tail_src = nullptr) {
     if (n <= 0) return;
     const int64_t tiles = ceil_div(n, kScanTile);
     if (tiles == 1) {
-        scan_tile_apply<TIn, TOut><<<1, kScanBlock, 0, st>>>(in, out, n, nullptr, inclusive);
+        scan_tile_apply<TIn, TOut><<<1, kScanBlock, 0, st>>>(in, out, n, nullptr, inclusive, nullptr, tail,
+                                                             tail_src);
         O3DML_LAUNCH_CHECK();
         return;
     }
     int64_t* sums = ws.take<int64_t>(tiles);
     scan_tile_sums<TIn><<<static_cast<unsigned>(tiles), kScanBlock, 0, st>>>(in, n, sums);
     O3DML_LAUNCH_CHECK();
+    if (tiles <= kScanDirectTiles) {
+        scan_tile_apply<TIn, TOut><<<static_cast<unsigned>(tiles), kScanBlock, 0, st>>>(in, out, n, nullptr,
+                                                                                       inclusive, sums, tail,
+                                                                                       tail_src);
+        O3DML_LAUNCH_CHECK();
+        return;
+    }
     scan<int64_t, int64_t>(sums, sums, tiles, false, ws, st);
     scan_tile_apply<TIn, TOut><<<static_cast<unsigned>(tiles), kScanBlock, 0, st>>>(in, out, n, sums,
-                                                                                   inclusive);
+                                                                                   inclusive, nullptr, tail,
+                                                                                   tail_src);
     O3DML_LAUNCH_CHECK();
 }
 

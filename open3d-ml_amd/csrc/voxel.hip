@@ -450,6 +450,46 @@ O3DML_API int o3dml_voxelize_fill(int64_t n_points, int ndim, int64_t n_batch, c
 }
 
 // ---------------------------------------------------------------------------
+namespace o3dml {
+// p' = p R_b (transpose: p R_b^T) for the points of batch item b, in fp32 with
+// the reference's rounding: (p0 R0j + p1 R1j) + p2 R2j, every product rounded
+// (no contraction; kpconv.py:2087-2090 batch_grid_subsampling's rotations)
+__global__ void __launch_bounds__(256) rotate_batched_kernel(const float* __restrict__ pts, int64_t n, int nb,
+                                                             const int64_t* __restrict__ rs,
+                                                             const float* __restrict__ R, int transpose,
+                                                             float* __restrict__ out) {
+    __shared__ int64_t s_rs[kLdsSplits];
+    const int64_t* rsp = stage_splits(s_rs, rs, nb);
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const float* r = R + 9 * batch_of(i, rsp, nb);
+        const float p0 = pts[3 * i], p1 = pts[3 * i + 1], p2 = pts[3 * i + 2];
+        float o[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float r0 = transpose ? r[3 * j] : r[j], r1 = transpose ? r[3 * j + 1] : r[3 + j],
+                        r2 = transpose ? r[3 * j + 2] : r[6 + j];
+            o[j] = (p0 * r0 + p1 * r1) + p2 * r2;
+        }
+        out[3 * i] = o[0];
+        out[3 * i + 1] = o[1];
+        out[3 * i + 2] = o[2];
+    }
+}
+}  // namespace o3dml
+
+O3DML_API int o3dml_rotate_batched(const float* points, int64_t n_points, int64_t n_batch,
+                                   const int64_t* row_splits, const float* rotations, int transpose, float* out,
+                                   void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(n_batch >= 1, "need at least one batch item");
+    if (n_points == 0) return 0;
+    rotate_batched_kernel<<<stream_grid(n_points, 256), 256, 0, as_stream(stream)>>>(
+            points, n_points, (int)n_batch, row_splits, rotations, transpose, out);
+    O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
 O3DML_API size_t o3dml_grid_subsample_workspace_size(int64_t n_points, int64_t n_batch) {
     return seg_state_bytes(n_points, static_cast<int>(n_batch)) + ws_bytes<uint64_t>(n_points) +
            ws_bytes<SubBatch>(n_batch) + ws_bytes<float>(6 * n_batch) + sort_segments_ws_bytes(n_points) +

@@ -46,6 +46,12 @@ SIGNATURES = {
     "o3dml_fixed_radius_search_fill_bounded": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p, c_p,
                                                        c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_p, c_i32, c_p, c_p,
                                                        c_i64, c_i32, c_p, c_sz, c_p]),
+    "o3dml_fixed_radius_search_layer_workspace_size": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
+    "o3dml_fixed_radius_search_layer": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i64, c_p, c_p, c_p, c_p, c_p,
+                                                c_i64, c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_i32, c_p, c_p, c_p,
+                                                c_i32, c_p, c_p, c_i64, c_i32, c_p, c_p, c_sz, c_p]),
+    "o3dml_fixed_radius_search_fill_dense": (c_i32, [c_p, c_i64, c_i64, c_f32, c_i64, c_p, c_p, c_p, c_p, c_p,
+                                                     c_i32, c_i32, c_p, c_i64, c_i32, c_p, c_i32, c_p, c_sz, c_p]),
     # nns_knn.hip
     "o3dml_knn_search_workspace_size": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
     "o3dml_knn_search_count": (c_i32, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i32, c_i32,
@@ -114,6 +120,7 @@ SIGNATURES = {
     "o3dml_grid_subsample_workspace_size": (c_sz, [c_i64, c_i64]),
     "o3dml_grid_subsample_count": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_f32, c_i64, c_p, c_p, c_sz, c_p]),
     "o3dml_grid_subsample_count_async": (c_i32, [c_p, c_i64, c_i64, c_p, c_f32, c_i64, c_p, c_p, c_sz, c_p]),
+    "o3dml_rotate_batched": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_i32, c_p, c_p]),
     "o3dml_grid_subsample_fill": (c_i32, [c_p, c_i64, c_i64, c_p, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_sz,
                                           c_p]),
     # pointnet2.hip

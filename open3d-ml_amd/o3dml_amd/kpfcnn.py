@@ -434,15 +434,17 @@ def random_rotations(B, rng=np.random):
 
 def _rotate(points, splits, R, transpose=False):
     """p' = p @ R[b] per batch element in fp32 with the reference's rounding
-    ((p0 R0j + p1 R1j) + p2 R2j, each product rounded; kpconv.py:2087-2090)."""
-    Rt = to_dev(np.ascontiguousarray(R.transpose(0, 2, 1) if transpose else R), points.device)
-    # the repeats through the non-blocking upload and output_size given: no
-    # host synchronisation (a pageable copy / a size read would stall the stream)
-    b = torch.repeat_interleave(torch.arange(len(splits) - 1, device=points.device),
-                                to_dev(np.diff(splits).astype(np.int64), points.device),
-                                output_size=int(splits[-1]))
-    Rb = Rt[b]  # [N, 3, 3]
-    return (points[:, 0:1] * Rb[:, 0] + points[:, 1:2] * Rb[:, 1]) + points[:, 2:3] * Rb[:, 2]
+    ((p0 R0j + p1 R1j) + p2 R2j, each product rounded; kpconv.py:2087-2090):
+    one HIP launch (o3dml_rotate_batched), the rotations through a pinned
+    non-blocking upload."""
+    dev = points.device
+    pts = points.contiguous()
+    out = torch.empty_like(pts)
+    B = len(splits) - 1
+    _lib.call("o3dml_rotate_batched", ptr(pts), pts.shape[0], B, ptr(to_dev(np.asarray(splits, np.int64), dev)),
+              ptr(to_dev(np.ascontiguousarray(R, np.float32), dev)), int(bool(transpose)), ptr(out),
+              stream_handle(dev))
+    return out
 
 
 def batch_grid_subsampling(points, lengths, sampleDl, rotations=None, random_grid_orient=True):
@@ -516,27 +518,22 @@ class _Reads:
 
 
 def _dense_begin(reads, queries, supports, q_lengths, s_lengths, radius, table=None):
-    """batch_neighbors, count phase; [total, long rows, width] into 3 slots."""
-    rs, state = ops._frs_count(supports, queries, radius, _splits(s_lengths), _splits(q_lengths),
-                               None if table is None else table.hash_table_splits,
-                               None if table is None else table.hash_table_index,
-                               None if table is None else table.hash_table_cell_splits, "L2", False, False)
-    m = queries.shape[0]
-    slot = reads.take(3)
-    _lib.call("o3dml_fixed_radius_search_sizes", ptr(rs), m, ptr(state[1]), ptr(slot), stream_handle(rs.device))
-    return rs, state, slot, supports.shape[0], m
+    """batch_neighbors, count phase (one library call: the supports' hash
+    table — built here unless ``table``, an earlier search over the same
+    supports at this radius, holds it — the count, [total, long rows, width]
+    into 3 device slots)."""
+    return ops._layer_count(supports, queries, radius, _splits(s_lengths), _splits(q_lengths), table=table,
+                            sizes=reads.take(3))
 
 
-def _dense_end(b, host):
-    """batch_neighbors, fill phase from the host values [total, long rows, width]."""
-    rs, state, _, n_sup, m = b
-    if m == 0:
-        return torch.zeros((0, 0), dtype=torch.int32, device=rs.device)
-    total, n_over, width = host
-    idx, dist = ops._frs_alloc(state, total, torch.int32)
-    ops._frs_launch_fill(rs, state, idx, dist, -1, 1 | (2 if n_over else 0))
-    return ops.ragged_to_dense(idx.reshape(-1, 1), rs, width,
-                               torch.tensor([n_sup], dtype=torch.int32)).squeeze(2)
+def _dense_end(x, host):
+    """batch_neighbors, fill phase from the host values [total, long rows,
+    width]: the rows written straight into the dense matrix padded with the
+    shadow index (no CSR, no ragged_to_dense pass)."""
+    _total, n_over, width = host
+    if x.m == 0 or width == 0:
+        return torch.full((x.m, width), x.n, dtype=torch.int32, device=x.dev)
+    return ops._layer_fill_dense(x, int(width), x.n, 1 | (2 if n_over else 0))
 
 
 def _subsample_begin(reads, points, lengths, sampleDl, rotations=None):
@@ -596,15 +593,15 @@ def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_len
             layer_blocks.append(block)
             continue
         deform = any("deformable" in b for b in layer_blocks)
-        table = None  # hash table of this layer's points at r_normal: shared by the conv and pool searches
-        # stage 1: the conv search count and the subsampling count, one read
+        # stage 1: the conv search count and the subsampling count, one read;
+        # the conv search's hash table (this layer's points at its radius) is
+        # shared with the pool search when the radii agree
         conv_b = sub_b = None
+        r_conv = None
         reads = _Reads(dev)
         if layer_blocks:
-            r = r_normal * cfg.deform_radius / cfg.conv_radius if deform else r_normal
-            if r == r_normal:
-                table = ops.build_spatial_hash_table(stacked_points, r, _splits(stack_lengths))
-            conv_b = _dense_begin(reads, stacked_points, stacked_points, stack_lengths, stack_lengths, r, table)
+            r_conv = r_normal * cfg.deform_radius / cfg.conv_radius if deform else r_normal
+            conv_b = _dense_begin(reads, stacked_points, stacked_points, stack_lengths, stack_lengths, r_conv)
         pooling = "pool" in block or "strided" in block
         if pooling:
             dl = 2 * r_normal / cfg.conv_radius
@@ -619,7 +616,7 @@ def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_len
             # stage 2: the pool and up-sampling search counts, one read
             reads = _Reads(dev)
             pb = _dense_begin(reads, pool_p, stacked_points, pool_b, stack_lengths, r,
-                              table if r == r_normal else None)
+                              conv_b if r == r_conv else None)
             ub = _dense_begin(reads, stacked_points, pool_p, stack_lengths, pool_b, 2 * r)
             host = reads.read()
             pool_i = _dense_end(pb, host[:3])

@@ -24,12 +24,12 @@ class FixedRadiusSearch(torch.nn.Module):
             points_row_splits = torch.LongTensor([0, points.shape[0]])
         if queries_row_splits is None:
             queries_row_splits = torch.LongTensor([0, queries.shape[0]])
-        if hash_table is None:
-            table = ops.build_spatial_hash_table(points, radius, points_row_splits,
-                                                 hash_table_size_factor,
-                                                 max_hash_table_size=self.max_hash_table_size)
-        else:
-            table = hash_table
+        if hash_table is None:  # table build + search in one library call
+            return ops._fixed_radius_search_layer(points, queries, radius, points_row_splits, queries_row_splits,
+                                                  hash_table_size_factor, self.max_hash_table_size,
+                                                  self.index_dtype, self.metric, self.ignore_query_point,
+                                                  self.return_distances)
+        table = hash_table
         return ops.fixed_radius_search(points, queries, radius, points_row_splits, queries_row_splits,
                                        hash_table_splits=table.hash_table_splits,
                                        hash_table_index=table.hash_table_index,

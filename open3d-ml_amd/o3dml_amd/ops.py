@@ -7,7 +7,7 @@ reference calls some ops from DataLoader workers on CPU tensors); they are then
 staged to the GPU and the results returned on the CPU.  There is no CPU
 compute path.
 """
-from collections import namedtuple
+from collections import OrderedDict, namedtuple
 
 import numpy as np
 import torch
@@ -238,6 +238,164 @@ def fixed_radius_search_dense(points, queries, radius, points_row_splits, querie
     width = int(width)
     return ragged_to_dense(idx.reshape(-1, 1), rs, width,
                            torch.tensor([points.shape[0]], dtype=torch.int32)).squeeze(2)
+
+
+# layers.FixedRadiusSearch without a given table: the table build, the count,
+# the totals and the speculative row copy in ONE library call
+# (o3dml_fixed_radius_search_layer), the batch layout (row splits, table
+# splits, their device copies, the workspace size) cached per layout — a
+# small search costs one ctypes call and three allocations on the host.
+_LAYER_PLANS = OrderedDict()
+_LAYER_EVENTS = {}
+
+
+def _splits_key(rs, n):
+    if rs is None:
+        return None, np.array([0, n], np.int64)
+    if isinstance(rs, torch.Tensor) and rs.device.type == "cpu" and rs.dtype == torch.int64 and rs.dim() == 1:
+        a = rs.numpy()
+        return a.tobytes(), a
+    a = row_splits_host(rs, n)
+    return a.tobytes(), a
+
+
+def _layer_plan(dev, n, m, points_row_splits, queries_row_splits, factor, max_table):
+    pkey, prs = _splits_key(points_row_splits, n)
+    qkey, qrs = (pkey, prs) if queries_row_splits is points_row_splits else _splits_key(queries_row_splits, m)
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, n, m, pkey, qkey, float(factor), int(max_table))
+    plan = _LAYER_PLANS.get(key)
+    if plan is not None:
+        _LAYER_PLANS.move_to_end(key)
+        return plan
+    # copies: the arrays may be views of the caller's tensors
+    prs = row_splits_host(prs, n).copy()
+    qrs = row_splits_host(qrs, m).copy()
+    if len(prs) != len(qrs):
+        raise RuntimeError("points_row_splits and queries_row_splits must have the same length")
+    lib = _lib.load()
+    B = len(prs) - 1
+    splits = np.zeros(B + 1, np.uint32)
+    T = lib.o3dml_hash_table_splits(B, prs.ctypes.data, float(factor), int(max_table), splits.ctypes.data)
+    same_splits = np.array_equal(prs, qrs)
+    prs_d = torch.from_numpy(prs).to(dev)
+    qrs_d = prs_d if same_splits else torch.from_numpy(qrs).to(dev)
+    hts_d = torch.from_numpy(splits.view(np.int32)).to(dev)
+    plan = (prs, qrs, splits, T, prs_d, qrs_d, hts_d, same_splits,
+            lib.o3dml_fixed_radius_search_layer_workspace_size(n, m, B, T))
+    _LAYER_PLANS[key] = plan
+    if len(_LAYER_PLANS) > 32:
+        _LAYER_PLANS.popitem(last=False)
+    return plan
+
+
+class _LayerSearch:
+    """A counted search of the one-call path: the arguments every later call
+    repeats, the workspace, row splits and the hash table it was given or
+    built (int32 [N + T + 1]: index, then cell splits)."""
+    __slots__ = ("head", "tail", "ws", "ws_bytes", "rs", "tab", "keep", "n", "m", "dev", "st")
+
+
+def _layer_count(points, queries, radius, points_row_splits, queries_row_splits, hash_table_size_factor=1 / 64,
+                 max_hash_table_size=33554432, metric="L2", ignore_query_point=False, return_distances=False,
+                 table=None, totals=None, sizes=None, count_done=None, index_bits_=32, idx=None, dist=None,
+                 capacity=-1):
+    """Stage 0 of o3dml_fixed_radius_search_layer: the table build (or
+    ``table``, a previous _LayerSearch over the same points at this radius),
+    the count, totals (pinned) and/or sizes (device) and, with capacity >= 0,
+    the speculative row copy.  Returns the _LayerSearch for the fills."""
+    dev = gpu_device(points, queries)
+    check_points("points", points)
+    check_points("queries", queries)
+    mcode = metric_code(metric)
+    r = scalar(radius)
+    if not r > 0:
+        raise RuntimeError("radius must be > 0")
+    n, m = points.shape[0], queries.shape[0]
+    prs, _qrs, splits, T, prs_d, qrs_d, hts_d, same_splits, ws_bytes = _layer_plan(
+        dev, n, m, points_row_splits, queries_row_splits, hash_table_size_factor, max_hash_table_size)
+    pts = to_dev(points, dev)
+    same = same_splits and points.data_ptr() == queries.data_ptr() and n == m
+    qry = pts if same else to_dev(queries, dev)
+    st = stream_handle(dev)
+    x = _LayerSearch()
+    x.ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    x.ws_bytes = ws_bytes
+    x.rs = torch.empty(m + 1, dtype=torch.int64, device=dev)
+    build = table is None
+    x.tab = torch.empty(n + T + 1, dtype=torch.int32, device=dev) if build else table.tab
+    x.head = (ptr(pts), n, ptr(qry), m, r, len(prs) - 1, ptr(prs_d), ptr(qrs_d), prs.ctypes.data, ptr(hts_d),
+              splits.ctypes.data, T, ptr(x.tab), ptr(x.tab) + 4 * n)
+    x.tail = (mcode, int(bool(ignore_query_point)), int(same), int(bool(return_distances)), ptr(x.rs))
+    x.keep = (pts, qry, prs, prs_d, qrs_d, hts_d, splits)
+    x.n, x.m, x.dev, x.st = n, m, dev, st
+    _lib.call("o3dml_fixed_radius_search_layer", *x.head, int(build), *x.tail, None if totals is None else
+              totals.data_ptr(), None if sizes is None else ptr(sizes), index_bits_, ptr(idx), ptr(dist), capacity,
+              0, count_done, ptr(x.ws), ws_bytes, st)
+    return x
+
+
+def _layer_fill(x, idx, dist, capacity, parts, index_bits_=32):
+    """Stage 1..3 (parts) of a counted _LayerSearch into CSR buffers."""
+    _lib.call("o3dml_fixed_radius_search_layer", *x.head, 0, *x.tail, None, None, index_bits_, ptr(idx), ptr(dist),
+              capacity, parts, None, ptr(x.ws), x.ws_bytes, x.st)
+
+
+def _layer_fill_dense(x, width, pad, parts):
+    """The counted search as KPConv's dense neighbour matrix int32 [M, width]
+    padded with `pad` (o3dml_fixed_radius_search_fill_dense)."""
+    out = torch.empty((x.m, width), dtype=torch.int32, device=x.dev)
+    h = x.head
+    if x.m:
+        _lib.call("o3dml_fixed_radius_search_fill_dense", h[2], h[1], h[3], h[4], h[5], h[6], h[7], h[8], h[9],
+                  h[13], x.tail[0], x.tail[1], x.tail[4], width, pad, ptr(out), parts, ptr(x.ws), x.ws_bytes, x.st)
+    return out
+
+
+def _fixed_radius_search_layer(points, queries, radius, points_row_splits, queries_row_splits,
+                               hash_table_size_factor, max_hash_table_size, index_dtype, metric,
+                               ignore_query_point, return_distances):
+    """layers.FixedRadiusSearch forward (table built here): the same result as
+    build_spatial_hash_table + fixed_radius_search."""
+    dev = gpu_device(points, queries)
+    bits = index_bits(index_dtype)
+    r = scalar(radius)
+    m = queries.shape[0]
+    key = (r, metric_code(metric), points.shape[0], m)
+    guess = _FRS_DENSITY.get(key)
+    elem = (4 if bits == 32 else 8) + (4 if return_distances else 0)
+    cap = -1 if guess is None else int(m * guess * 1.0625) + 1024
+    if cap * elem > _FRS_GUESS_MAX_BYTES:
+        cap = -1
+    itype = torch.int32 if bits == 32 else torch.int64
+    idx = torch.empty(max(cap, 0), dtype=itype, device=dev)
+    dist = torch.empty(max(cap, 0) if return_distances else 0, dtype=torch.float32, device=dev)
+    host = _pinned_slot(dev, 2)
+    ev = _LAYER_EVENTS.get(dev)
+    if ev is None:  # recorded by the library after the count, before the row copy
+        ev = _LAYER_EVENTS[dev] = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))  # creates the HIP event on this device
+    x = _layer_count(points, queries, r, points_row_splits, queries_row_splits, hash_table_size_factor,
+                     max_hash_table_size, metric, ignore_query_point, return_distances, totals=host,
+                     count_done=ev.cuda_event, index_bits_=bits, idx=idx,
+                     dist=dist if return_distances else None, capacity=cap)
+    ev.synchronize()
+    total, n_over = host.tolist()
+    if cap < 0 or total > cap:  # no guess, or it was short: exact buffers, both parts
+        idx = torch.empty(total, dtype=itype, device=dev)
+        dist = torch.empty(total if return_distances else 0, dtype=torch.float32, device=dev)
+        _layer_fill(x, idx, dist if return_distances else None, -1, 1 | (2 if n_over else 0), bits)
+    else:
+        if n_over:
+            _layer_fill(x, idx, dist if return_distances else None, cap, 2, bits)
+        compact = cap > _FRS_SLACK * total + 1024
+        idx = idx[:total].clone() if compact else idx[:total]
+        if return_distances:
+            dist = dist[:total].clone() if compact else dist[:total]
+    if m > 0:
+        _FRS_DENSITY[key] = total / m
+        if len(_FRS_DENSITY) > 64:
+            _FRS_DENSITY.pop(next(iter(_FRS_DENSITY)))
+    return FixedRadiusSearchResult(back_to(idx, points), back_to(x.rs, points), back_to(dist, points))
 
 
 # ---------------------------------------------------------------------------

@@ -269,12 +269,14 @@ def test_frs_query_order(cuda, mode, monkeypatch):
     assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
 
 
-@pytest.mark.parametrize("n,rs_mid", [(300000, None), (90000, [5, 5, 40000])])
+@pytest.mark.parametrize("n,rs_mid", [(300000, None), (90000, [5, 5, 40000]),
+                                      (2200000, [5, 5] + [65536 * k for k in range(1, 33)])])
 def test_hash_table_paths(cuda, n, rs_mid):
     """Both hash-table builders against the oracle: tables of > 4,096 bins in a
     batch item take the radix-sort path (300,000 points -> 4,687 bins), smaller
-    ones the chunked counting sort (several 4,096-point chunks per item, empty
-    and one-point items), each bit-exact; the FRS on top stays exact."""
+    ones the chunked counting sort — chunks of 1,024 points below 2^21 points
+    per call (several chunks per item, empty and one-point items), of 4,096
+    above (C1-shaped items) — each bit-exact; the FRS on top stays exact."""
     from o3dml_amd import ops
     pts = _cloud(n, 21)
     rs = np.array([0] + (rs_mid or []) + [n], np.int64)
@@ -284,8 +286,75 @@ def test_hash_table_paths(cuda, n, rs_mid):
     assert np.array_equal(ht.hash_table_splits.numpy().astype(np.uint32), osp)
     assert np.array_equal(ht.hash_table_cell_splits.cpu().numpy().astype(np.uint32), oc)
     assert np.array_equal(ht.hash_table_index.cpu().numpy().astype(np.uint32), oi)
+    if n > 1000000:
+        return  # the oracle search would take minutes
     res = ops.fixed_radius_search(t, t, 0.02, torch.from_numpy(rs), torch.from_numpy(rs), ht.hash_table_splits,
                                   ht.hash_table_index, ht.hash_table_cell_splits)
     ri, rr, _ = O.fixed_radius_search(pts, pts, 0.02, rs, rs, hash_table=(oi, oc, osp))
     assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), rr)
     assert np.array_equal(res.neighbors_index.cpu().numpy(), ri)
+
+
+@pytest.mark.parametrize("guess", [None, 0.0, 1e3])
+@pytest.mark.parametrize("dist,dt", [(False, torch.int32), (True, torch.int64)])
+def test_frs_layer_one_call(cuda, guess, dist, dt):
+    """layers.FixedRadiusSearch without a given table runs the table build,
+    count, totals and speculative row copy as one library call
+    (o3dml_fixed_radius_search_layer): no capacity guess, a guess far too small
+    (exact re-run) and far too large (sliced rows), with rows longer than 64
+    (the overflow re-run), an empty item, different queries and a repeated
+    layout (cached plan) — every result equals the oracle's."""
+    from o3dml_amd import layers, ops
+    pts = _cloud(20000, 61)
+    pts[:300] = (0.5 + _cloud(300, 62) * 0.01).astype(np.float32)
+    qry = _cloud(7000, 63)
+    rs = np.array([0, 12000, 12000, 20000], np.int64)
+    qs = np.array([0, 3000, 3000, 7000], np.int64)
+    r = 0.05
+    t, tq = torch.from_numpy(pts).to(cuda), torch.from_numpy(qry).to(cuda)
+    nns = layers.FixedRadiusSearch(return_distances=dist, index_dtype=dt)
+    idt = np.int64 if dt == torch.int64 else np.int32
+    for a, b, ars, brs in ((t, t, rs, rs), (t, tq, rs, qs), (t, t, rs, rs)):
+        key = (float(r), 1, a.shape[0], b.shape[0])
+        ops._FRS_DENSITY.pop(key, None)
+        if guess is not None:
+            ops._FRS_DENSITY[key] = guess
+        res = nns(a, b, r, torch.from_numpy(ars), torch.from_numpy(brs))
+        oi, ors, od = O.fixed_radius_search(a.cpu().numpy(), b.cpu().numpy(), r, ars, brs, return_distances=dist,
+                                            index_dtype=idt)
+        assert res.neighbors_index.dtype == dt and res.neighbors_index.numel() == len(oi)
+        assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+        assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+        if dist:
+            assert np.array_equal(res.neighbors_distance.cpu().numpy(), od)
+
+
+def test_frs_dense_one_call(cuda):
+    """KPConv's batch_neighbors through the one-call path: the dense matrix
+    written straight from the temp rows (rows longer than 64 by the re-run at
+    row * width), a table shared with a second search over the same supports,
+    and an empty query set — equal to the oracle rows padded with the shadow
+    index."""
+    from o3dml_amd import kpfcnn
+    pts = _cloud(9000, 71)
+    pts[:200] = (0.3 + _cloud(200, 72) * 0.01).astype(np.float32)  # rows > 64
+    qry = _cloud(3000, 73)
+    sl, ql = [5000, 4000], [1000, 2000]
+    t, tq = torch.from_numpy(pts).to(cuda), torch.from_numpy(qry).to(cuda)
+    rs = np.array([0, 5000, 9000], np.int64)
+    qs = np.array([0, 1000, 3000], np.int64)
+    reads = kpfcnn._Reads(cuda)
+    a = kpfcnn._dense_begin(reads, t, t, sl, sl, 0.05)
+    b = kpfcnn._dense_begin(reads, tq, t, ql, sl, 0.05, a)
+    e = kpfcnn._dense_begin(reads, tq[:0], t, [0, 0], sl, 0.05, a)
+    host = reads.read()
+    for x, h, q, qrs in ((a, host[0:3], pts, rs), (b, host[3:6], qry, qs)):
+        d = kpfcnn._dense_end(x, h).cpu().numpy()
+        oi, ors, _ = O.fixed_radius_search(pts, q, 0.05, rs, qrs)
+        w = int(np.diff(ors).max())
+        assert h[2] == w and d.shape == (len(q), w)
+        assert h[0] == len(oi) and (h[1] > 0) == (w > 64)
+        for i in range(len(q)):
+            row = oi[ors[i]:ors[i + 1]]
+            assert np.array_equal(d[i, :len(row)], row) and (d[i, len(row):] == len(pts)).all()
+    assert kpfcnn._dense_end(e, host[6:9]).shape[0] == 0
