@@ -110,14 +110,49 @@ __global__ void recip_norm_kernel(const float* __restrict__ norm, const float* _
 constexpr int64_t kOrderMinRows = 2048;
 static bool use_order(int64_t n, int K) { return K > 8 && n >= kOrderMinRows; }
 
-__global__ void mask_keys_kernel(const int32_t* __restrict__ map, int64_t n, int K, uint32_t* __restrict__ keys,
-                                 int* __restrict__ flag) {
+// Grids of the GEMM kernels.  O3DML_GEMM_XCD=1: a multiple of 8 workgroups,
+// so xcd_block() hands each XCD one contiguous range of tiles (the extra
+// workgroups exit at once).  OFF by default: same-session A/B on the C4 room
+// (tools/gemm_probe.py, with and without the chunked tile order below) was
+// neutral to 4 % slower at 32->32, 64->32 and 128->128 — the gathers' L2
+// locality is not what bounds these kernels.  Off: an odd grid, so
+// xcd_block() keeps blockIdx.x.
+static int64_t round8(int64_t g) {
+    static const bool on = [] {
+        const char* e = std::getenv("O3DML_GEMM_XCD");
+        return e ? std::atoi(e) != 0 : false;
+    }();
+    if (!on) return g | 1;  // odd: xcd_block() falls back to blockIdx.x
+    return (g + 7) & ~int64_t(7);
+}
+
+// Tile order: rows grouped by their offset mask, globally (default) or inside
+// chunks of O3DML_ORDER_CHUNK consecutive rows (rows come in voxel order, so
+// a chunk is a spatial slab that keeps a tile's or an XCD's gathers local).
+// Chunks measured neutral (4,096 rows) to 10 % slower (1,024) — kept off.
+static int order_chunk_log() {
+    static const int v = [] {
+        const char* e = std::getenv("O3DML_ORDER_CHUNK");
+        const int c = e ? std::atoi(e) : 0;
+        if (c <= 0) return 0;
+        int l = 0;
+        while ((1 << (l + 1)) <= c) ++l;
+        return l;
+    }();
+    return v;
+}
+
+// key = (chunk, hb-bit hash of the offset mask): 16 bits in all while the
+// chunks allow it (two radix passes), never fewer than 10 hash bits
+__global__ void mask_keys_kernel(const int32_t* __restrict__ map, int64_t n, int K, int chunk_log, int hb,
+                                 uint32_t* __restrict__ keys, int* __restrict__ flag) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *flag = 1;  // the sort below completes before any GEMM reads it
     for (int64_t o = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; o < n;
          o += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         uint32_t m = 0u;
         for (int k = 0; k < K; ++k) m |= (map[o * K + k] >= 0 ? 1u : 0u) << k;
-        keys[o] = (m * 0x9E3779B1u) >> 16;
+        const uint32_t chunk = chunk_log ? static_cast<uint32_t>(o >> chunk_log) : 0u;
+        keys[o] = (chunk << hb) | ((m * 0x9E3779B1u) >> (32 - hb));
     }
 }
 
@@ -130,9 +165,14 @@ static void build_order(const int32_t* map, int64_t n, int K, int32_t* order, in
     if (!use_order(n, K)) return;
     uint32_t* kin = scratch.take<uint32_t>(n);
     uint32_t* kout = scratch.take<uint32_t>(n);
-    mask_keys_kernel<<<stream_grid(n, 256), 256, 0, st>>>(map, n, K, kin, flag);
+    const int cl = order_chunk_log();
+    const int cb = cl ? prim::bits_needed(static_cast<uint64_t>((n - 1) >> cl)) : 0;
+    const int hb = std::max(10, 16 - cb);
+    mask_keys_kernel<<<stream_grid(n, 256), 256, 0, st>>>(map, n, K, cl, hb, kin, flag);
     O3DML_LAUNCH_CHECK();
-    prim::radix_sort_pairs<uint32_t>(kin, nullptr, kout, reinterpret_cast<uint32_t*>(order), n, 16, scratch, st);
+    const int bits = hb + cb;
+    O3DML_REQUIRE(bits <= 32, "tile order: too many row chunks");
+    prim::radix_sort_pairs<uint32_t>(kin, nullptr, kout, reinterpret_cast<uint32_t*>(order), n, bits, scratch, st);
 }
 
 // W [K][Cin][Cout] -> Wt [K][Cout][Cin]
@@ -470,17 +510,61 @@ __device__ __forceinline__ void glds16(const float* g, float* lds_wave_base) {
 // into st.b instead of through LDS — half the LDS per wave, so more waves.
 // SC: row / pair scales present (importance, normalisation); without them the
 // factors are 1 and no per-stage scale loads are issued
-template <bool BREG, bool SC = true>
+// BUF (cin % 32 == 0, operands < 2 GiB, no scales, BREG): the rows and the
+// filters through buffer resources with 32-bit offsets — a missing row or
+// column gets an offset past the resource's range, which the buffer unit
+// answers with zeros (no zero-page select, no 64-bit address arithmetic:
+// ~40 % of the loop's VALU went to addresses)
+constexpr uint32_t kNoRow = 0x7FFFFFF0u;  // >= num_records of every operand resource
+struct GemmRsrc {
+    __amdgpu_buffer_rsrc_t src, w;
+};
+__device__ __forceinline__ GemmRsrc gemm_rsrc(const float* src, const float* Wt) {
+    return {__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), static_cast<short>(0),
+                                              static_cast<int>(kNoRow), kBufferFlags),
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Wt), static_cast<short>(0),
+                                              static_cast<int>(kNoRow), kBufferFlags)};
+}
+
+template <bool BREG, bool SC = true, bool BUF = false>
 __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_t* mtile, int K, int k, int c0,
                                           int lane, int64_t o, int i, int col0, const float* __restrict__ src,
                                           const float* __restrict__ sscale, const float* __restrict__ pscale,
-                                          const float* __restrict__ Wt, int cin, int cout, bool live, GemmStage& st) {
+                                          const float* __restrict__ Wt, int cin, int cout, bool live, GemmStage& st,
+                                          const GemmRsrc* rs = nullptr) {
     const int sl = lane & 7;
     // all LDS reads of the map first (a DMA in between would order after them)
     int32_t mq[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) mq[q] = live ? mtile[(8 * q + (lane >> 3)) * K + k] : -1;
     const int32_t mi = live ? mtile[i * K + k] : -1;
+    if constexpr (BUF) {
+        static_assert(BREG && !SC, "buffer addressing: filters in registers, no scales");
+        const uint32_t row_bytes = static_cast<uint32_t>(cin) * 4u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int r = 8 * q + (lane >> 3);
+            const uint32_t cb = static_cast<uint32_t>(c0 + 4 * (sl ^ (r & 7))) * 4u;
+            const uint32_t off = mq[q] >= 0 ? static_cast<uint32_t>(mq[q]) * row_bytes + cb : kNoRow;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs->src, (lds_void_ptr)(abuf + 256 * q), 16, off, 0, 0, 0);
+        }
+        const int col = col0 + i;
+        const uint32_t boff = (live && col < cout)
+                                      ? (static_cast<uint32_t>(k * cout + col) * static_cast<uint32_t>(cin) +
+                                         static_cast<uint32_t>(c0 + 16 * (lane >> 5))) * 4u
+                                      : kNoRow;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs->w, boff + 16u * q, 0, 0));
+            st.b[4 * q] = v.x;
+            st.b[4 * q + 1] = v.y;
+            st.b[4 * q + 2] = v.z;
+            st.b[4 * q + 3] = v.w;
+        }
+        st.s1 = st.s2 = 1.f;
+        st.v = mi >= 0 ? 1.f : 0.f;
+        return;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int r = 8 * q + (lane >> 3);
@@ -595,7 +679,11 @@ __device__ __forceinline__ void mfma_stage(const Stage& cu, f32x16& acc) {
     }
 }
 
-template <bool PRE, bool BREG, int NT = 0, bool SC = true>
+// DEPTH 2 (BUF only, O3DML_GEMM_DEPTH=2): two stages in flight per wave —
+// stage j+2's DMA is issued while stage j is multiplied.  Off by default:
+// 12 instead of 16 waves per CU (136 registers, 49 KiB LDS per workgroup), and
+// same-session A/B 3-8 % slower at 32->32 / 64->32 (tools/gemm_probe.py)
+template <bool PRE, bool BREG, int NT = 0, bool SC = true, bool BUF = false, int DEPTH = 1>
 __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order,
                          const int* order_flag, int K, int64_t n_out,
@@ -605,7 +693,7 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
                          float* __restrict__ out, int nsplit, float* __restrict__ part, GemmPrologue pre,
                          const float* __restrict__ residual, uint32_t* __restrict__ counters) {
     __shared__ float lpre[PRE ? 2 * (kPreMax + 32) : 1];
-    __shared__ __attribute__((aligned(16))) float stage_all[kGemmThreads / 64][BREG ? 1 : 2][32 * 32];
+    __shared__ __attribute__((aligned(16))) float stage_all[kGemmThreads / 64][BREG && DEPTH == 1 ? 1 : 2][32 * 32];
     __shared__ int32_t mtile_all[kGemmThreads / 64][32 * 32];
     __shared__ int32_t orow_all[kGemmThreads / 64][32];
     float* lps = lpre;
@@ -619,7 +707,10 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     }
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    const int64_t o0 = (static_cast<int64_t>(blockIdx.x) * (kGemmThreads / 64) + w) * 32;
+    // XCD-contiguous tiles (grid a multiple of 8): XCD x takes one contiguous
+    // eighth of the (spatially chunked) tile order, so its L2 holds the input
+    // rows that eighth gathers
+    const int64_t o0 = (xcd_block() * (kGemmThreads / 64) + w) * 32;
     if (o0 >= n_out) return;  // whole wave; no barriers below
     const int i = lane & 31, h = lane >> 5;
     const int col0 = blockIdx.y * 32;
@@ -658,13 +749,76 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     const int s = blockIdx.z;
     const int j0 = split_stage(used, nch, K, s, nsplit);
     const int j1 = split_stage(used, nch, K, s + 1, nsplit);
-    if (j0 < j1) {
+    if (DEPTH == 2 && j0 < j1) {
+        static_assert(DEPTH == 1 || (BUF && BREG && !SC), "two stages in flight: buffer path only");
+        unsigned u = used;
+        for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
+        int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
+        auto advance = [&]() {
+            c0 += 32;
+            if (c0 >= cin) {
+                c0 = 0;
+                u &= u - 1u;
+                k = u ? __builtin_ctz(u) : 0;
+            }
+        };
+        const GemmRsrc rs = gemm_rsrc(src, Wt);
+        float* buf1 = stage_all[w][1];
+        GemmStage s0, s1, cu;
+        int c00 = c0;
+        lds_issue<true, false, true>(abuf, nullptr, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin,
+                                     cout, true, s0, &rs);
+        advance();
+        int c01 = c0;
+        lds_issue<true, false, true>(buf1, nullptr, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin,
+                                     cout, j0 + 1 < j1, s1, &rs);
+        advance();
+        // every stage issues exactly 8 vector-memory ops (4 row DMAs, 4 filter
+        // loads; dead stages read zeros), so vmcnt(8) = the older stage landed
+        for (int j = j0; j < j1; j += 2) {
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            lds_read<true>(abuf, nullptr, i, h, cu);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cu.b[r] = s0.b[r];
+            cu.s1 = s0.s1;
+            cu.s2 = s0.s2;
+            cu.v = s0.v;  // the prologue zeroes a missing row (relu(0 * s + b) != 0)
+            int cj = c00;
+            c00 = c0;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_issue<true, false, true>(abuf, nullptr, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt,
+                                         cin, cout, j + 2 < j1, s0, &rs);
+            advance();
+            __builtin_amdgcn_sched_barrier(0);
+            gemm_finish<PRE, false>(cu, cj, h, lps, lpb);
+            mfma_stage<NT>(cu, acc);
+            if (j + 1 >= j1) break;
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            lds_read<true>(buf1, nullptr, i, h, cu);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cu.b[r] = s1.b[r];
+            cu.s1 = s1.s1;
+            cu.s2 = s1.s2;
+            cu.v = s1.v;  // the prologue zeroes a missing row (relu(0 * s + b) != 0)
+            cj = c01;
+            c01 = c0;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_issue<true, false, true>(buf1, nullptr, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt,
+                                         cin, cout, j + 3 < j1, s1, &rs);
+            advance();
+            __builtin_amdgcn_sched_barrier(0);
+            gemm_finish<PRE, false>(cu, cj, h, lps, lpb);
+            mfma_stage<NT>(cu, acc);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead DMAs have landed before the wave exits
+    } else if (j0 < j1) {
         unsigned u = used;
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
         int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
         GemmStage nx, cu;
-        lds_issue<BREG, SC>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout, true,
-                            nx);
+        const GemmRsrc rs = gemm_rsrc(src, Wt);
+        lds_issue<BREG, SC, BUF>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout,
+                                 true, nx, &rs);
         for (int j = j0; j < j1; ++j) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage j in LDS, its row factors in nx
             lds_read<BREG>(abuf, bbuf, i, h, cu);
@@ -683,8 +837,8 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
                 k = u ? __builtin_ctz(u) : 0;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffer read out before the next DMA
-            lds_issue<BREG, SC>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout,
-                            j + 1 < j1, nx);
+            lds_issue<BREG, SC, BUF>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin,
+                                     cout, j + 1 < j1, nx, &rs);
             __builtin_amdgcn_sched_barrier(0);
             (void)kj;
             gemm_finish<PRE, SC>(cu, cj, h, lps, lpb);
@@ -830,7 +984,7 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
     __shared__ __attribute__((aligned(16))) float abuf[2][R * 32];
     __shared__ int32_t mtile[R * 32];
     __shared__ int32_t orow[R];
-    const int64_t o0 = static_cast<int64_t>(blockIdx.x) * R;
+    const int64_t o0 = xcd_block() * R;  // XCD-contiguous tiles, as implicit_gemm_lds_kernel
     if (o0 >= n_out) return;  // whole workgroup, before any barrier
     float* lps = lpre;
     float* lpb = lpre + (PRE ? kPreMax + 32 : 0);
@@ -1568,7 +1722,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
         if (ws.base && ws.used + pb <= ws.size) part = ws.take<float>(static_cast<int64_t>(ns) * n_out * cout);
         else ns = 1;
     }
-    const dim3 g(static_cast<unsigned>(ceil_div(n_out, 32 * (kGemmThreads / 64))),
+    const dim3 g(static_cast<unsigned>(round8(ceil_div(n_out, 32 * (kGemmThreads / 64)))),
                  static_cast<unsigned>(ceil_div(cout, 32)), static_cast<unsigned>(ns));
     O3DML_REQUIRE(pre.scale == nullptr || cin <= kPreMax, "sparse_conv: prologue needs cin <= %d", kPreMax);
     // split-K finished by each tile's last wave (split_store_finish); the wave
@@ -1671,8 +1825,8 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
             const char* e = std::getenv("O3DML_GEMM_RB");  // 2 row blocks per wave: measured slower
             return (e && std::atoi(e) == 2) ? 2 : 1;
         }();
-        const dim3 gs(static_cast<unsigned>(ceil_div(n_out, 32 * rb)), static_cast<unsigned>(ceil_div(cout, 32 * nw)),
-                      static_cast<unsigned>(ns));
+        const dim3 gs(static_cast<unsigned>(round8(ceil_div(n_out, 32 * rb))),
+                      static_cast<unsigned>(ceil_div(cout, 32 * nw)), static_cast<unsigned>(ns));
 #define O3DML_GEMM_SH_SC(P, X, W, B, SCL)                                                                      \
     implicit_gemm_shared_kernel<P, X, W, B, SCL><<<gs, W * 64, 0, st>>>(map, order, order_flag, K, n_out, src,   \
                                                                         sscale, pscale, Wt, cin, cout, oscale,   \
@@ -1709,8 +1863,31 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #define O3DML_GEMM_LDS(P, BR, X)                                      \
     do {                                                              \
         if (sscale || pscale) O3DML_GEMM_LDS_SC(P, BR, X, true);      \
+        else if (BR && buf_ok) O3DML_GEMM_LDS_BUF(P, X);              \
         else O3DML_GEMM_LDS_SC(P, BR, X, false);                      \
     } while (0)
+#define O3DML_GEMM_LDS_BUF2(P, X, D)                                                                             \
+    implicit_gemm_lds_kernel<P, true, X, false, true, D><<<g, kGemmThreads, 0, st>>>(                            \
+            map, order, order_flag, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, bias, out, ns, part, pre, \
+            residual, counters)
+#define O3DML_GEMM_LDS_BUF(P, X)                                 \
+    do {                                                         \
+        if (depth2) O3DML_GEMM_LDS_BUF2(P, X, 2);                \
+        else O3DML_GEMM_LDS_BUF2(P, X, 1);                       \
+    } while (0)
+        // buffer addressing: whole 32-channel stages, every byte offset of the
+        // operands below the resources' out-of-range sentinel
+        static const bool buf_path = [] {
+            const char* e = std::getenv("O3DML_GEMM_BUF");
+            return e ? std::atoi(e) != 0 : true;
+        }();
+        static const bool depth2 = [] {
+            const char* e = std::getenv("O3DML_GEMM_DEPTH");
+            return e ? std::atoi(e) == 2 : false;
+        }();
+        const bool buf_ok = buf_path && cin % 32 == 0 &&
+                            static_cast<uint64_t>(n_src) * cin * 4 < kNoRow &&
+                            static_cast<uint64_t>(K) * cout * cin * 4 < kNoRow - 64;
         const int nt = gemm_nt();
         if (nt == 6) {
             if (pre.scale) O3DML_GEMM_LDS(true, true, 6); else O3DML_GEMM_LDS(false, true, 6);
@@ -1723,6 +1900,8 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
         }
 #undef O3DML_GEMM_LDS
 #undef O3DML_GEMM_LDS_SC
+#undef O3DML_GEMM_LDS_BUF
+#undef O3DML_GEMM_LDS_BUF2
     } else if (pre.scale) {
         if (vec4) O3DML_GEMM_LAUNCH(true, true); else O3DML_GEMM_LAUNCH(false, true);
     } else {

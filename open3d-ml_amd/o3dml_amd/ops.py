@@ -259,10 +259,10 @@ def _splits_key(rs, n):
     return a.tobytes(), a
 
 
-def _layer_plan(dev, n, m, points_row_splits, queries_row_splits, factor, max_table):
+def _layer_plan(dev, st, n, m, points_row_splits, queries_row_splits, factor, max_table):
     pkey, prs = _splits_key(points_row_splits, n)
     qkey, qrs = (pkey, prs) if queries_row_splits is points_row_splits else _splits_key(queries_row_splits, m)
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream, n, m, pkey, qkey, float(factor), int(max_table))
+    key = (dev.index, st, n, m, pkey, qkey, float(factor), int(max_table))
     plan = _LAYER_PLANS.get(key)
     if plan is not None:
         _LAYER_PLANS.move_to_end(key)
@@ -311,12 +311,12 @@ def _layer_count(points, queries, radius, points_row_splits, queries_row_splits,
     if not r > 0:
         raise RuntimeError("radius must be > 0")
     n, m = points.shape[0], queries.shape[0]
-    prs, _qrs, splits, T, prs_d, qrs_d, hts_d, same_splits, ws_bytes = _layer_plan(
-        dev, n, m, points_row_splits, queries_row_splits, hash_table_size_factor, max_hash_table_size)
-    pts = to_dev(points, dev)
-    same = same_splits and points.data_ptr() == queries.data_ptr() and n == m
-    qry = pts if same else to_dev(queries, dev)
     st = stream_handle(dev)
+    prs, _qrs, splits, T, prs_d, qrs_d, hts_d, same_splits, ws_bytes = _layer_plan(
+        dev, st, n, m, points_row_splits, queries_row_splits, hash_table_size_factor, max_hash_table_size)
+    pts = points if points.device == dev and points.is_contiguous() else to_dev(points, dev)
+    same = same_splits and points.data_ptr() == queries.data_ptr() and n == m
+    qry = pts if same else (queries if queries.device == dev and queries.is_contiguous() else to_dev(queries, dev))
     x = _LayerSearch()
     x.ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     x.ws_bytes = ws_bytes

@@ -230,6 +230,47 @@ def test_bf16_split_products_match_exact_f32(cuda, cin, cout):
         assert e6 <= 3 * e1 + 1e-7, (errs[0], errs[1])
 
 
+def test_bf16_split_large_and_nonfinite_inputs(cuda):
+    """The bf16x6 split's range (DESIGN §5 "Product precision"): features up to
+    1e30 stay within the f32 tolerance of float64 (hi carries the exponent,
+    so magnitude costs no bits); a non-finite feature makes exactly the
+    outputs that gather its row non-finite (inf - inf in the split turns the
+    exact path's +-inf into NaN there — the documented deviation; exact mode,
+    o3dml_sparse_conv_set_exact(1), keeps IEEE infinities), every other output
+    stays equal to the exact kernel's within its rounding."""
+    from o3dml_amd import _lib, ops
+    lib = _lib.load()
+    pos = _voxels(2000, 16, 5)
+    oi, ors, _ = O.fixed_radius_search(pos, pos, 1.5, metric="Linf")
+    ok = O.kernel_index(pos, pos, oi, ors, [3, 3, 3], 1.0)
+    gen = torch.Generator().manual_seed(3)
+    W = torch.randn(3, 3, 3, 32, 32, dtype=torch.float64, generator=gen) * 0.1
+    x = torch.randn(len(pos), 32, dtype=torch.float64, generator=gen) * 1e30
+    ref = _csr_conv64(W, x, torch.from_numpy(oi), torch.from_numpy(ok), torch.from_numpy(ors)).numpy()
+    args = (torch.empty(0), torch.from_numpy(oi), torch.from_numpy(ok), torch.empty(0), torch.from_numpy(ors))
+    prev = lib.o3dml_sparse_conv_set_exact(-1)
+    try:
+        lib.o3dml_sparse_conv_set_exact(0)
+        got = ops.sparse_conv(W.float().to(cuda), x.float().to(cuda), *args).cpu().numpy()
+        _close(got, ref)
+        xi = x.float().clone()
+        xi[7, 3], xi[100, 0] = float("inf"), float("-inf")
+        res = {}
+        for mode in (0, 1):
+            lib.o3dml_sparse_conv_set_exact(mode)
+            res[mode] = ops.sparse_conv(W.float().to(cuda), xi.to(cuda), *args).cpu().numpy()
+    finally:
+        lib.o3dml_sparse_conv_set_exact(prev)
+    hit = np.zeros(len(pos), bool)
+    for q in range(len(pos)):
+        hit[q] = np.isin(oi[ors[q]:ors[q + 1]], [7, 100]).any()
+    assert hit.any()
+    assert not np.isfinite(res[0][hit]).all(axis=1).any() and not np.isfinite(res[1][hit]).all(axis=1).any()
+    assert np.isfinite(res[0][~hit]).all() and np.isfinite(res[1][~hit]).all()
+    scale = np.abs(res[1][~hit]).max()
+    assert np.abs(res[0][~hit] - res[1][~hit]).max() <= 1e-6 * scale
+
+
 @pytest.mark.parametrize("normalize,importance", [(False, False), (True, False), (True, True)])
 def test_duplicate_kernel_indices(cuda, normalize, importance):
     """Off-lattice positions: several neighbours of one output share a kernel
