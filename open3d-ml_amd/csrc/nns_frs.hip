@@ -79,7 +79,11 @@ __global__ void __launch_bounds__(256) gather_sorted_points_kernel(const float* 
     }
 }
 
-constexpr int kRowCap = 64;  // neighbours kept per query in the temp rows
+#ifndef O3DML_FRS_ROWCAP
+#define O3DML_FRS_ROWCAP 64
+#endif
+constexpr int kRowCap = O3DML_FRS_ROWCAP;  // neighbours kept per query in the temp rows (<= 64)
+static_assert(kRowCap >= 1 && kRowCap <= 64, "the row copy takes one row per wave instruction");
 // voxel-class directory per bucket (bucket_classes_kernel): sizes of classes
 // 0 and 1, 2 spare words, then per class 0-2 the box min x, y, z, max x, y, z
 constexpr int kDirWords = 24;
@@ -1369,7 +1373,10 @@ static void frs_fill_impl(const float* queries, int64_t n_points, int64_t n_quer
     O3DML_CHECK_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
     const hipStream_t st_main = st;
     st = side->s;
-    const unsigned go = static_cast<unsigned>(std::min<int64_t>(n_queries, 256));
+#ifndef O3DML_FRS_OVER_GRID
+#define O3DML_FRS_OVER_GRID 256
+#endif
+    const unsigned go = static_cast<unsigned>(std::min<int64_t>(n_queries, O3DML_FRS_OVER_GRID));
     const float4* qraw = reinterpret_cast<const float4*>(queries);  // MODE 1 reads [M, 3] via the over list
     if (index_bits == 32)
         launch_group<1, int32_t>(metric, ignore_query_point != 0, dist != nullptr, false, st, go, pl.pts,
