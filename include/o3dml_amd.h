@@ -125,8 +125,10 @@ int o3dml_fixed_radius_search_fill_bounded(const float* points, int64_t n_points
  * rows longer than 64, widest row) on the device (nullable), count_done
  * (nullable hipEvent_t) recorded, and — when capacity >= 0 — the row copy into
  * buffers of `capacity` entries (as _fill_bounded parts 1; nothing written
- * when the total exceeds it).  stage 1..3: _fill_bounded with parts = stage
- * (the re-run of long rows; exact buffers after a short capacity). */
+ * when the total exceeds it); stage 4 = stage 0 with the re-run of rows
+ * longer than 64 queued beside that copy too (it reads the overflow count on
+ * the device).  stage 1..3: _fill_bounded with parts = stage (the re-run of
+ * long rows; exact buffers after a short capacity). */
 size_t o3dml_fixed_radius_search_layer_workspace_size(int64_t n_points, int64_t n_queries, int64_t n_batch,
                                                       int64_t total_bins);
 int o3dml_fixed_radius_search_layer(const float* points, int64_t n_points, const float* queries,

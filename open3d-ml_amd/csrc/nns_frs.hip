@@ -1462,11 +1462,11 @@ O3DML_API int o3dml_fixed_radius_search_layer(
         void* neighbors_index, float* neighbors_distance, int64_t capacity, int stage, void* count_done,
         void* workspace, size_t workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
-    O3DML_REQUIRE(stage >= 0 && stage <= 3, "stage must be 0 (build + count [+ copy]) or fill parts 1..3");
+    O3DML_REQUIRE(stage >= 0 && stage <= 4, "stage must be 0 / 4 (build + count [+ copy]) or fill parts 1..3");
     const size_t need = layer_search_bytes(n_points, n_queries, n_batch, total_bins);
     O3DML_REQUIRE(workspace_bytes >= need, "layer workspace too small");
     hipStream_t st = as_stream(stream);
-    if (stage > 0) {
+    if (stage > 0 && stage < 4) {
         frs_fill_impl(queries, n_points, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
                       points_row_splits_host, hash_table_splits, hash_table_cell_splits, metric, ignore_query_point,
                       with_distances, neighbors_row_splits, index_bits, neighbors_index, neighbors_distance,
@@ -1491,10 +1491,12 @@ O3DML_API int o3dml_fixed_radius_search_layer(
     }
     // the host waits for the totals only, not for the row copy queued next
     if (count_done) O3DML_CHECK_HIP(hipEventRecord(static_cast<hipEvent_t>(count_done), st));
+    // stage 4: the re-run of long rows queued beside the copy as well (it
+    // reads the overflow count on the device: nothing to do when it is 0)
     if (capacity >= 0)
         frs_fill_impl(queries, n_points, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
                       points_row_splits_host, hash_table_splits, hash_table_cell_splits, metric, ignore_query_point,
                       with_distances, neighbors_row_splits, index_bits, neighbors_index, neighbors_distance,
-                      capacity, 1, 0, 0, workspace, need, st);
+                      capacity, stage == 4 ? 3 : 1, 0, 0, workspace, need, st);
     O3DML_GUARD_END
 }

@@ -148,6 +148,7 @@ def _pinned_slot(device, n):
 # total first instead, and a result far below its capacity is returned as a
 # compact copy (a view would keep the whole speculative buffer alive).
 _FRS_DENSITY = {}
+_FRS_HAD_OVER = {}  # call shapes whose last search had rows longer than 64
 _FRS_GUESS_MAX_BYTES = 1 << 30
 _FRS_SLACK = 1.25
 
@@ -298,7 +299,7 @@ class _LayerSearch:
 def _layer_count(points, queries, radius, points_row_splits, queries_row_splits, hash_table_size_factor=1 / 64,
                  max_hash_table_size=33554432, metric="L2", ignore_query_point=False, return_distances=False,
                  table=None, totals=None, sizes=None, count_done=None, index_bits_=32, idx=None, dist=None,
-                 capacity=-1):
+                 capacity=-1, stage=0):
     """Stage 0 of o3dml_fixed_radius_search_layer: the table build (or
     ``table``, a previous _LayerSearch over the same points at this radius),
     the count, totals (pinned) and/or sizes (device) and, with capacity >= 0,
@@ -330,7 +331,7 @@ def _layer_count(points, queries, radius, points_row_splits, queries_row_splits,
     x.n, x.m, x.dev, x.st = n, m, dev, st
     _lib.call("o3dml_fixed_radius_search_layer", *x.head, int(build), *x.tail, None if totals is None else
               totals.data_ptr(), None if sizes is None else ptr(sizes), index_bits_, ptr(idx), ptr(dist), capacity,
-              0, count_done, ptr(x.ws), ws_bytes, st)
+              stage, count_done, ptr(x.ws), ws_bytes, st)
     return x
 
 
@@ -362,6 +363,9 @@ def _fixed_radius_search_layer(points, queries, radius, points_row_splits, queri
     m = queries.shape[0]
     key = (r, metric_code(metric), points.shape[0], m)
     guess = _FRS_DENSITY.get(key)
+    # the previous call of this shape had rows longer than 64: their re-run is
+    # queued with the copy (stage 4) so it runs beside it on the side stream
+    early_over = key in _FRS_HAD_OVER
     elem = (4 if bits == 32 else 8) + (4 if return_distances else 0)
     cap = -1 if guess is None else int(m * guess * 1.0625) + 1024
     if cap * elem > _FRS_GUESS_MAX_BYTES:
@@ -377,15 +381,21 @@ def _fixed_radius_search_layer(points, queries, radius, points_row_splits, queri
     x = _layer_count(points, queries, r, points_row_splits, queries_row_splits, hash_table_size_factor,
                      max_hash_table_size, metric, ignore_query_point, return_distances, totals=host,
                      count_done=ev.cuda_event, index_bits_=bits, idx=idx,
-                     dist=dist if return_distances else None, capacity=cap)
+                     dist=dist if return_distances else None, capacity=cap, stage=4 if early_over else 0)
     ev.synchronize()
     total, n_over = host.tolist()
+    if n_over:
+        _FRS_HAD_OVER[key] = True
+        if len(_FRS_HAD_OVER) > 64:
+            _FRS_HAD_OVER.pop(next(iter(_FRS_HAD_OVER)))
+    else:
+        _FRS_HAD_OVER.pop(key, None)
     if cap < 0 or total > cap:  # no guess, or it was short: exact buffers, both parts
         idx = torch.empty(total, dtype=itype, device=dev)
         dist = torch.empty(total if return_distances else 0, dtype=torch.float32, device=dev)
         _layer_fill(x, idx, dist if return_distances else None, -1, 1 | (2 if n_over else 0), bits)
     else:
-        if n_over:
+        if n_over and not early_over:
             _layer_fill(x, idx, dist if return_distances else None, cap, 2, bits)
         compact = cap > _FRS_SLACK * total + 1024
         idx = idx[:total].clone() if compact else idx[:total]
