@@ -13,6 +13,7 @@
 // the same bins in L1/L2.  Neighbour order per query = ascending bin, then
 // ascending point id (the canonical order of oracle/o3d_oracle.c).
 #include <algorithm>
+#include <cstdlib>
 
 #include "primitives.hpp"
 #include "spatial_hash.hpp"
@@ -357,7 +358,7 @@ O3DML_API size_t o3dml_build_spatial_hash_table_workspace_size(int64_t n_points,
     const size_t radix = ws_bytes<uint32_t>(n_points) * 2 + prim::radix_sort_workspace_bytes<uint32_t>(n_points);
     // chunks of 1024 (small calls): sum_b (N_b / 1024 + 1) T_b <= 4 N + T
     const int64_t nb_ub = total_bins;  // every batch item has >= 1 bin
-    const int64_t hist_ub = (ceil_div(n_points, kHashChunk) < 512 ? 4 * n_points : n_points) + total_bins;
+    const int64_t hist_ub = 4 * n_points + total_bins;  // chunks of 1024 at most 4x the 4096 ones
     const size_t small = ws_bytes<uint32_t>(n_points) + ws_bytes<uint32_t>(hist_ub) +
                          ws_bytes<uint32_t>(total_bins) + 2 * ws_bytes<int64_t>(nb_ub + 1);
     return std::max(radix, small);
@@ -385,9 +386,15 @@ O3DML_API int o3dml_build_spatial_hash_table(const float* points, int64_t n_poin
     }
     if (small) {
         uint32_t* bins = ws.take<uint32_t>(n_points);
-        // small calls (fewer than 512 chunks of 4096) take chunks of 1024
-        const int chunk = ceil_div(n_points, kHashChunk) < 512 ? kHashChunkSmall : kHashChunk;
-        uint32_t* hist = ws.take<uint32_t>((chunk == kHashChunkSmall ? 4 * n_points : n_points) + total_bins);
+        // small calls (fewer than 512 chunks of 4096) take chunks of 1024;
+        // O3DML_HASH_CHUNK (1024, 2048, 4096) forces one size (A/B)
+        static const int forced = [] {
+            const char* e = std::getenv("O3DML_HASH_CHUNK");
+            const int v = e ? std::atoi(e) : 0;
+            return (v == 1024 || v == 2048 || v == 4096) ? v : 0;
+        }();
+        const int chunk = forced ? forced : (ceil_div(n_points, kHashChunk) < 512 ? kHashChunkSmall : kHashChunk);
+        uint32_t* hist = ws.take<uint32_t>((kHashChunk / chunk) * n_points + total_bins);
         uint32_t* bin_tot = ws.take<uint32_t>(total_bins);
         int64_t* chunk_start = ws.take<int64_t>(n_batch + 1);
         int64_t* hist_off = ws.take<int64_t>(n_batch + 1);
@@ -406,6 +413,10 @@ O3DML_API int o3dml_build_spatial_hash_table(const float* points, int64_t n_poin
         const size_t lds = sizeof(uint32_t) * (kHashWaves + 1) * max_bins;
         if (chunk == kHashChunkSmall)
             hash_chunk_scatter_kernel<kHashChunkSmall><<<grid, 256, lds, st>>>(
+                    (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist, bin_tot,
+                    hash_table_cell_splits, hash_table_index, static_cast<int>(max_bins));
+        else if (chunk == 2048)
+            hash_chunk_scatter_kernel<2048><<<grid, 256, lds, st>>>(
                     (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist, bin_tot,
                     hash_table_cell_splits, hash_table_index, static_cast<int>(max_bins));
         else

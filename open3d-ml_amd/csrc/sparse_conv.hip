@@ -879,14 +879,27 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
 // DMA of this wave's share of one stage: row groups q = w, w + NW, ... of the
 // tile's 4*RB groups of 8 rows (lane-linear LDS destination, swizzled source
 // as in lds_issue)
-template <int NW, int RB>
+template <int NW, int RB, bool BUF = false>
 __device__ __forceinline__ void shared_issue(float* abuf, const int32_t* mtile, int K, int k, int c0, int lane, int w,
-                                             const float* __restrict__ src, int cin, bool live) {
+                                             const float* __restrict__ src, int cin, bool live,
+                                             const GemmRsrc* rs = nullptr) {
     constexpr int NQ = 4 * RB / NW;
     const int sl = lane & 7;
     int32_t mq[NQ];
 #pragma unroll
     for (int t = 0; t < NQ; ++t) mq[t] = live ? mtile[(8 * (w + NW * t) + (lane >> 3)) * K + k] : -1;
+    if constexpr (BUF) {  // buffer addressing as lds_issue (cin % 32 == 0)
+        const uint32_t row_bytes = static_cast<uint32_t>(cin) * 4u;
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) {
+            const int q = w + NW * t;
+            const int r = 8 * q + (lane >> 3);
+            const uint32_t cb = static_cast<uint32_t>(c0 + 4 * (sl ^ (r & 7))) * 4u;
+            const uint32_t off = mq[t] >= 0 ? static_cast<uint32_t>(mq[t]) * row_bytes + cb : kNoRow;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs->src, (lds_void_ptr)(abuf + 256 * q), 16, off, 0, 0, 0);
+        }
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < NQ; ++t) {
         const int q = w + NW * t;
@@ -903,14 +916,34 @@ struct SharedStage {
     float sc[RB];  // row factor (importance x pair scale, 0 for a missing row)
 };
 
-template <int RB, bool SC = true>
+template <int RB, bool SC = true, bool BUF = false>
 __device__ __forceinline__ void shared_regs(const int32_t* mtile, int K, int k, int c0, int lane, const int64_t* o,
                                             int i, int col, const float* __restrict__ sscale,
                                             const float* __restrict__ pscale, const float* __restrict__ Wt, int cin,
                                             int cout, bool live, SharedStage<RB>& st, float (&s1)[RB],
-                                            float (&s2)[RB], bool (&v)[RB]) {
+                                            float (&s2)[RB], bool (&v)[RB], const GemmRsrc* rs = nullptr) {
     const int cb = c0 + 16 * (lane >> 5);
     const bool colv = live && col < cout;
+    if constexpr (BUF) {
+        static_assert(!SC, "buffer addressing: no scales");
+        const uint32_t boff =
+                colv ? (static_cast<uint32_t>(k * cout + col) * static_cast<uint32_t>(cin) + static_cast<uint32_t>(cb)) * 4u
+                     : kNoRow;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 x = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs->w, boff + 16u * q, 0, 0));
+            st.b[4 * q] = x.x;
+            st.b[4 * q + 1] = x.y;
+            st.b[4 * q + 2] = x.z;
+            st.b[4 * q + 3] = x.w;
+        }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            v[rb] = live && mtile[(32 * rb + i) * K + k] >= 0;
+            s1[rb] = s2[rb] = 1.f;
+        }
+        return;
+    }
     const float* wr = Wt + (static_cast<int64_t>(k) * cout + (colv ? col : 0)) * cin;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -970,7 +1003,7 @@ __device__ __forceinline__ void mfma_stage_rb(const SharedStage<RB>& cu, f32x16 
 // The tile: 32*RB output rows (RB row blocks) x NW column blocks; wave w owns
 // column block w for all RB row blocks, so each stage's B fragment (the
 // filters, read by every wave of every tile) feeds RB accumulators.
-template <bool PRE, int NT, int NW, int RB, bool SC = true>
+template <bool PRE, int NT, int NW, int RB, bool SC = true, bool BUF = false>
 __global__ void __launch_bounds__(NW * 64)
 implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order,
                             const int* order_flag, int K, int64_t n_out,
@@ -1038,8 +1071,10 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
         SharedStage<RB> nx, cu;
         float s1[RB], s2[RB];
         bool vv[RB];
-        shared_issue<NW, RB>(abuf[0], mtile, K, k, c0, lane, w, src, cin, true);
-        shared_regs<RB, SC>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, true, nx, s1, s2, vv);
+        const GemmRsrc rs = gemm_rsrc(src, Wt);
+        shared_issue<NW, RB, BUF>(abuf[0], mtile, K, k, c0, lane, w, src, cin, true, &rs);
+        shared_regs<RB, SC, BUF>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, true, nx, s1, s2, vv,
+                                 &rs);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         for (int j = j0; j < j1; ++j) {
@@ -1063,9 +1098,9 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
             }
             const bool live = j + 1 < j1;
             // the other buffer was last read in stage j-1, before that stage's barrier
-            shared_issue<NW, RB>(abuf[b ^ 1], mtile, K, k, c0, lane, w, src, cin, live);
-            shared_regs<RB, SC>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, live, nx, s1, s2,
-                                vv);
+            shared_issue<NW, RB, BUF>(abuf[b ^ 1], mtile, K, k, c0, lane, w, src, cin, live, &rs);
+            shared_regs<RB, SC, BUF>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, live, nx, s1, s2,
+                                     vv, &rs);
             __builtin_amdgcn_sched_barrier(0);
             const int cbb = cj + 16 * h;
             if constexpr (PRE || SC) {  // without both the factor is 1 and missing rows are zero already
@@ -1818,6 +1853,22 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
         const char* e = std::getenv("O3DML_GEMM_SHARED");
         return e ? std::atoi(e) != 0 : true;
     }();
+    // buffer addressing (rows and filters through buffer resources): whole
+    // 32-channel stages, every byte offset of the operands below the
+    // resources' out-of-range sentinel
+    static const bool buf_path = [] {
+        const char* e = std::getenv("O3DML_GEMM_BUF");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    const bool buf_ok = buf_path && cin % 32 == 0 && static_cast<uint64_t>(n_src) * cin * 4 < kNoRow &&
+                        static_cast<uint64_t>(K) * cout * cin * 4 < kNoRow - 64;
+    // the shared-A kernel with buffer addressing: neutral in the same-session
+    // A/B (64->96 -3 %, 128->128 +1-2 %: its row addresses are split over the
+    // NW waves already) — off unless O3DML_GEMM_SHARED_BUF=1
+    static const bool shared_buf = [] {
+        const char* e = std::getenv("O3DML_GEMM_SHARED_BUF");
+        return e ? std::atoi(e) != 0 : false;
+    }();
     if (vec4 && lds_path && shared_path && cout >= 64) {
         // A tile shared by NW column-block waves (implicit_gemm_shared_kernel)
         const int nw = (cout % 128 == 0) ? 4 : 2;
@@ -1832,9 +1883,14 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
                                                                         sscale, pscale, Wt, cin, cout, oscale,   \
                                                                         bias, out, ns, part, pre, residual,      \
                                                                         counters)
+#define O3DML_GEMM_SH_BUF(P, X, W, B)                                                                          \
+    implicit_gemm_shared_kernel<P, X, W, B, false, true><<<gs, W * 64, 0, st>>>(                               \
+            map, order, order_flag, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, bias, out, ns, part, pre, \
+            residual, counters)
 #define O3DML_GEMM_SH(P, X, W, B)                                     \
     do {                                                              \
         if (sscale || pscale) O3DML_GEMM_SH_SC(P, X, W, B, true);     \
+        else if (buf_ok && shared_buf) O3DML_GEMM_SH_BUF(P, X, W, B); \
         else O3DML_GEMM_SH_SC(P, X, W, B, false);                     \
     } while (0)
 #define O3DML_GEMM_SH_RB(P, X, W) \
@@ -1854,6 +1910,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #undef O3DML_GEMM_SH_NT
 #undef O3DML_GEMM_SH
 #undef O3DML_GEMM_SH_SC
+#undef O3DML_GEMM_SH_BUF
     } else if (vec4 && lds_path) {
 #define O3DML_GEMM_LDS_SC(P, BR, X, SCL)                                                                          \
     implicit_gemm_lds_kernel<P, BR, X, SCL><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src,    \
@@ -1875,19 +1932,10 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
         if (depth2) O3DML_GEMM_LDS_BUF2(P, X, 2);                \
         else O3DML_GEMM_LDS_BUF2(P, X, 1);                       \
     } while (0)
-        // buffer addressing: whole 32-channel stages, every byte offset of the
-        // operands below the resources' out-of-range sentinel
-        static const bool buf_path = [] {
-            const char* e = std::getenv("O3DML_GEMM_BUF");
-            return e ? std::atoi(e) != 0 : true;
-        }();
         static const bool depth2 = [] {
             const char* e = std::getenv("O3DML_GEMM_DEPTH");
             return e ? std::atoi(e) == 2 : false;
         }();
-        const bool buf_ok = buf_path && cin % 32 == 0 &&
-                            static_cast<uint64_t>(n_src) * cin * 4 < kNoRow &&
-                            static_cast<uint64_t>(K) * cout * cin * 4 < kNoRow - 64;
         const int nt = gemm_nt();
         if (nt == 6) {
             if (pre.scale) O3DML_GEMM_LDS(true, true, 6); else O3DML_GEMM_LDS(false, true, 6);
