@@ -580,7 +580,6 @@ def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_len
     stacked_points = stacked_points.to(dev).float().contiguous()
     stack_lengths = np.asarray(stack_lengths, np.int64)
     r_normal = cfg.first_subsampling_dl * cfg.conv_radius
-    layer_blocks = []
     points, neighbors, pools, upsamples, lengths = [], [], [], [], []
     empty = torch.zeros((0, 1), dtype=torch.int32, device=dev)
     sub_i = 0
@@ -588,44 +587,70 @@ def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_len
     def limit(nb, layer):
         return nb[:, :neighborhood_limits[layer]] if len(neighborhood_limits) > 0 else nb
 
+    # the architecture as layers: (the layer's conv blocks, the block that ends it)
+    layers, layer_blocks = [], []
     for block in cfg.architecture:
         if not any(t in block for t in ("pool", "strided", "global", "upsample")):
             layer_blocks.append(block)
             continue
-        deform = any("deformable" in b for b in layer_blocks)
-        # stage 1: the conv search count and the subsampling count, one read;
-        # the conv search's hash table (this layer's points at its radius) is
-        # shared with the pool search when the radii agree
-        conv_b = sub_b = None
-        r_conv = None
-        reads = _Reads(dev)
-        if layer_blocks:
-            r_conv = r_normal * cfg.deform_radius / cfg.conv_radius if deform else r_normal
-            conv_b = _dense_begin(reads, stacked_points, stacked_points, stack_lengths, stack_lengths, r_conv)
-        pooling = "pool" in block or "strided" in block
-        if pooling:
-            dl = 2 * r_normal / cfg.conv_radius
+        layers.append((layer_blocks, block))
+        layer_blocks = []
+        if "global" in block or "upsample" in block:
+            break
+
+    def stage1(reads, li, pts, lens, r_norm, table=None, r_table=None):
+        """Layer li's conv search count and subsampling count into `reads`
+        (the conv search reuses `table` when it was built over `pts` at the
+        same radius).  Returns (conv handle, subsample handle, conv radius)."""
+        nonlocal sub_i
+        lblocks, block = layers[li]
+        conv_b = sub_b = r_conv = None
+        if lblocks:
+            deform = any("deformable" in b for b in lblocks)
+            r_conv = r_norm * cfg.deform_radius / cfg.conv_radius if deform else r_norm
+            conv_b = _dense_begin(reads, pts, pts, lens, lens, r_conv, table if r_table == r_conv else None)
+        if "pool" in block or "strided" in block:
             rot = None if rotations is None else rotations[sub_i]
             sub_i += 1
-            sub_b = _subsample_begin(reads, stacked_points, stack_lengths, dl, rotations=rot)
-        host = reads.read()
-        conv_i = _dense_end(conv_b, host[:3]) if conv_b else empty
+            sub_b = _subsample_begin(reads, pts, lens, 2 * r_norm / cfg.conv_radius, rotations=rot)
+        return conv_b, sub_b, r_conv
+
+    # Host reads: layer 0's stage 1 alone, then per pooling layer ONE read
+    # for its pool / up-sampling search counts together with the next layer's
+    # conv search and subsampling counts (the reference reads each size
+    # separately: ~9 round trips per layer); the up-sampling search's table
+    # (the subsampled points at twice the radius) serves the next layer's conv
+    # search when the radii agree.
+    reads = _Reads(dev)
+    conv_b, sub_b, r_conv = stage1(reads, 0, stacked_points, stack_lengths, r_normal) if layers else (None,) * 3
+    host, off = (reads.read(), 0) if layers else (None, 0)
+    for li, (lblocks, block) in enumerate(layers):
+        conv_i = _dense_end(conv_b, host[off:off + 3]) if conv_b else empty
+        off += 3 if conv_b else 0
+        pooling = "pool" in block or "strided" in block
         if pooling:
-            pool_p, pool_b = _subsample_end(sub_b, host[3:] if conv_b else host)
+            pool_p, pool_b = _subsample_end(sub_b, host[off:])
             r = r_normal * cfg.deform_radius / cfg.conv_radius if "deformable" in block else r_normal
-            # stage 2: the pool and up-sampling search counts, one read
             reads = _Reads(dev)
             pb = _dense_begin(reads, pool_p, stacked_points, pool_b, stack_lengths, r,
                               conv_b if r == r_conv else None)
             ub = _dense_begin(reads, stacked_points, pool_p, stack_lengths, pool_b, 2 * r)
-            host = reads.read()
-            pool_i = _dense_end(pb, host[:3])
-            up_i = _dense_end(ub, host[3:])
+            nxt = (None,) * 3
+            if li + 1 < len(layers):
+                nxt = stage1(reads, li + 1, pool_p, pool_b, 2 * r_normal, table=ub, r_table=2 * r)
+            host, off = reads.read(), 6
+            pool_i = _dense_end(pb, host[0:3])
+            up_i = _dense_end(ub, host[3:6])
+            conv_b, sub_b, r_conv = nxt
         else:
             pool_i = empty
             pool_p = torch.zeros((0, 3), dtype=torch.float32, device=dev)
             pool_b = np.zeros((0,), np.int64)
             up_i = empty
+            if li + 1 < len(layers):  # (not produced by the reference architectures)
+                reads = _Reads(dev)
+                conv_b, sub_b, r_conv = stage1(reads, li + 1, pool_p, pool_b, 2 * r_normal)
+                host, off = reads.read(), 0
         conv_i = limit(conv_i, len(points))
         pool_i = limit(pool_i, len(points))
         if up_i.shape[0] > 0:
@@ -637,9 +662,6 @@ def segmentation_inputs(cfg, stacked_points, stacked_features, labels, stack_len
         lengths.append(torch.from_numpy(stack_lengths.astype(np.int32)))
         stacked_points, stack_lengths = pool_p, pool_b
         r_normal *= 2
-        layer_blocks = []
-        if "global" in block or "upsample" in block:
-            break
     feats = stacked_features.to(dev).float().contiguous()
     lab = None if labels is None else torch.as_tensor(labels).to(dev).long()
     return KPConvBatch(points, neighbors, pools, upsamples, lengths, feats, lab)
