@@ -278,9 +278,12 @@ def _layer_plan(dev, st, n, m, points_row_splits, queries_row_splits, factor, ma
     splits = np.zeros(B + 1, np.uint32)
     T = lib.o3dml_hash_table_splits(B, prs.ctypes.data, float(factor), int(max_table), splits.ctypes.data)
     same_splits = np.array_equal(prs, qrs)
-    prs_d = torch.from_numpy(prs).to(dev)
-    qrs_d = prs_d if same_splits else torch.from_numpy(qrs).to(dev)
-    hts_d = torch.from_numpy(splits.view(np.int32)).to(dev)
+    # pinned, non-blocking uploads (a pageable copy would wait for the stream
+    # to drain: KPFCNN's collate meets a new layout in every layer, its
+    # subsampled sizes follow the random grid orientation)
+    prs_d = to_dev(prs, dev)
+    qrs_d = prs_d if same_splits else to_dev(qrs, dev)
+    hts_d = to_dev(splits.view(np.int32), dev)
     plan = (prs, qrs, splits, T, prs_d, qrs_d, hts_d, same_splits,
             lib.o3dml_fixed_radius_search_layer_workspace_size(n, m, B, T))
     _LAYER_PLANS[key] = plan

@@ -32,6 +32,13 @@ for _ in range(reps):
     segmentation_inputs(model.cfg, pts, feat, lab, lengths)
 torch.cuda.synchronize()
 print("ms per collate", (time.perf_counter() - t) / reps * 1e3, flush=True)
+each = []
+for _ in range(30):  # one by one (synchronised): median and min are robust to host jitter
+    t = time.perf_counter()
+    segmentation_inputs(model.cfg, pts, feat, lab, lengths)
+    torch.cuda.synchronize()
+    each.append((time.perf_counter() - t) * 1e3)
+print("ms per collate median %.3f min %.3f" % (float(np.median(each)), min(each)), flush=True)
 if os.environ.get("PROFILE", "1") == "1":
     pr = cProfile.Profile()
     pr.enable()
