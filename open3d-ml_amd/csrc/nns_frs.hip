@@ -1313,7 +1313,8 @@ static void frs_fill_impl(const float* queries, int64_t n_points, int64_t n_quer
                           const uint32_t* hash_table_cell_splits, int metric, int ignore_query_point,
                           int with_distances, const int64_t* neighbors_row_splits, int index_bits,
                           void* neighbors_index, float* neighbors_distance, int64_t capacity, int parts,
-                          int64_t dense_w, int32_t pad, void* workspace, size_t workspace_bytes, hipStream_t st) {
+                          int64_t dense_w, int32_t pad, void* workspace, size_t workspace_bytes, hipStream_t st,
+                          hipEvent_t fork_at = nullptr) {
     O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
     O3DML_REQUIRE(!with_distances || neighbors_distance, "with_distances needs a distance buffer");
     O3DML_REQUIRE(dense_w == 0 || (index_bits == 32 && !with_distances && capacity < 0),
@@ -1333,7 +1334,9 @@ static void frs_fill_impl(const float* queries, int64_t n_points, int64_t n_quer
     if (parts & 2) {  // fork before the row copy is queued: the re-run runs beside it
         side = &frs_side(dev);
         side_lock = std::unique_lock<std::mutex>(side->mu);
-        O3DML_CHECK_HIP(hipEventRecord(side->fork, st));
+        // fork_at: an event the caller just recorded at this point of the
+        // stream (one event record fewer between the count and the copy)
+        if (!fork_at) O3DML_CHECK_HIP(hipEventRecord(side->fork, st));
     }
     if ((parts & 1) && dense_w > 0) {
         const unsigned gd = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(ceil_div(n_queries, 4), 1 << 16)));
@@ -1370,7 +1373,7 @@ static void frs_fill_impl(const float* queries, int64_t n_points, int64_t n_quer
     // rows; the overflow count stays on the device (no host round trip), so a
     // fixed grid strides over however many there are (usually none)
     if (!(parts & 2)) return;  // the caller read a zero overflow count
-    O3DML_CHECK_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
+    O3DML_CHECK_HIP(hipStreamWaitEvent(side->s, fork_at ? fork_at : side->fork, 0));
     const hipStream_t st_main = st;
     st = side->s;
 #ifndef O3DML_FRS_OVER_GRID
@@ -1497,6 +1500,7 @@ O3DML_API int o3dml_fixed_radius_search_layer(
         frs_fill_impl(queries, n_points, n_queries, radius, n_batch, points_row_splits, queries_row_splits,
                       points_row_splits_host, hash_table_splits, hash_table_cell_splits, metric, ignore_query_point,
                       with_distances, neighbors_row_splits, index_bits, neighbors_index, neighbors_distance,
-                      capacity, stage == 4 ? 3 : 1, 0, 0, workspace, need, st);
+                      capacity, stage == 4 ? 3 : 1, 0, 0, workspace, need, st,
+                      static_cast<hipEvent_t>(count_done));
     O3DML_GUARD_END
 }

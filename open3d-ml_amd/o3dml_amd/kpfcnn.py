@@ -18,6 +18,8 @@ ml3d/torch/dataloaders/concat_batcher.py segmentation_inputs :186-283).
   (csrc/kpconv.hip ``pool_max_kernel``); KPConv itself is the fused
   neighbourhood aggregation + dense GEMM of ``o3dml_amd.kpconv``.
 """
+import threading
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -496,9 +498,10 @@ class _Reads:
 
     def __init__(self, dev):
         self.dev = dev
-        buf = _Reads._bufs.get(dev)
+        key = (dev, threading.get_ident())  # per host thread (collates may run in threads)
+        buf = _Reads._bufs.get(key)
         if buf is None:
-            buf = _Reads._bufs[dev] = torch.empty(256, dtype=torch.int64, device=dev)
+            buf = _Reads._bufs[key] = torch.empty(256, dtype=torch.int64, device=dev)
         self.buf, self.used = buf, 0
 
     def take(self, k):

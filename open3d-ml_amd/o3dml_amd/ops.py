@@ -7,6 +7,7 @@ reference calls some ops from DataLoader workers on CPU tensors); they are then
 staged to the GPU and the results returned on the CPU.  There is no CPU
 compute path.
 """
+import threading
 from collections import OrderedDict, namedtuple
 
 import numpy as np
@@ -124,18 +125,19 @@ def _frs_launch_fill(rs, state, idx, dist, capacity, parts):
               ptr(dist) if with_dist else None, capacity, parts, ptr(ws), ws.numel(), st)
 
 
-# One pinned host buffer per device for the totals read (a fresh pinned
-# allocation per call can block the host until the device is idle, which
-# would delay the fill launch behind the search); the host reads it before
-# the next call writes it.
+# One pinned host buffer per (device, host thread) for the totals read (a
+# fresh pinned allocation per call can block the host until the device is
+# idle, which would delay the fill launch behind the search); a thread reads
+# its buffer before its next call writes it, and threads never share one.
 _PINNED = {}
 
 
 def _pinned_slot(device, n):
-    buf = _PINNED.get(device)
+    key = (device, threading.get_ident())
+    buf = _PINNED.get(key)
     if buf is None or buf.numel() < n:
         buf = torch.empty(max(n, 8), dtype=torch.int64, pin_memory=True)
-        _PINNED[device] = buf
+        _PINNED[key] = buf
     return buf[:n]
 
 
@@ -377,9 +379,10 @@ def _fixed_radius_search_layer(points, queries, radius, points_row_splits, queri
     idx = torch.empty(max(cap, 0), dtype=itype, device=dev)
     dist = torch.empty(max(cap, 0) if return_distances else 0, dtype=torch.float32, device=dev)
     host = _pinned_slot(dev, 2)
-    ev = _LAYER_EVENTS.get(dev)
+    ekey = (dev, threading.get_ident())  # per host thread, like the pinned totals
+    ev = _LAYER_EVENTS.get(ekey)
     if ev is None:  # recorded by the library after the count, before the row copy
-        ev = _LAYER_EVENTS[dev] = torch.cuda.Event()
+        ev = _LAYER_EVENTS[ekey] = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dev))  # creates the HIP event on this device
     x = _layer_count(points, queries, r, points_row_splits, queries_row_splits, hash_table_size_factor,
                      max_hash_table_size, metric, ignore_query_point, return_distances, totals=host,
