@@ -91,10 +91,12 @@ constexpr int kHashChunk = 4096;
 constexpr int kHashChunkSmall = 1024;
 constexpr int kHashWaves = 4;
 
-__global__ void __launch_bounds__(256) hash_plan_kernel(const int64_t* __restrict__ prs, int nb,
-                                                        const uint32_t* __restrict__ hts,
-                                                        int64_t* __restrict__ chunk_start,
-                                                        int64_t* __restrict__ hist_off, int chunk) {
+// The plan, computed by one 256-thread workgroup into cs / ho (global or LDS):
+// chunk_start[b] (chunks of items < b, at least one per item) and
+// hist_off[b] (offset of item b's chunk histograms), [nb] the totals.
+__device__ __forceinline__ void hash_plan_block(const int64_t* __restrict__ prs, int nb,
+                                                const uint32_t* __restrict__ hts, int chunk, int64_t* cs,
+                                                int64_t* ho) {
     __shared__ int64_t wsum[2][4];
     int64_t carry_c = 0, carry_h = 0;
     for (int b0 = 0; b0 < nb; b0 += 256) {
@@ -121,18 +123,31 @@ __global__ void __launch_bounds__(256) hash_plan_kernel(const int64_t* __restric
             th += wsum[1][w];
         }
         if (b < nb) {
-            chunk_start[b] = bc + ic - c;
-            hist_off[b] = bh + ih - h;
+            cs[b] = bc + ic - c;
+            ho[b] = bh + ih - h;
         }
         carry_c += tc;
         carry_h += th;
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        chunk_start[nb] = carry_c;
-        hist_off[nb] = carry_h;
+        cs[nb] = carry_c;
+        ho[nb] = carry_h;
     }
+    __syncthreads();
 }
+
+__global__ void __launch_bounds__(256) hash_plan_kernel(const int64_t* __restrict__ prs, int nb,
+                                                        const uint32_t* __restrict__ hts,
+                                                        int64_t* __restrict__ chunk_start,
+                                                        int64_t* __restrict__ hist_off, int chunk) {
+    hash_plan_block(prs, nb, hts, chunk, chunk_start, hist_off);
+}
+
+// Batches of up to kPlanLds - 1 items: every histogram workgroup computes the
+// plan itself in LDS (a few hundred cycles) and workgroup 0 publishes it for
+// the later kernels — no plan launch
+constexpr int kPlanLds = 512;
 
 // Batch item and chunk of workgroup blockIdx.x (false: past the last chunk).
 __device__ __forceinline__ bool hash_chunk_of(const int64_t* __restrict__ chunk_start, int nb, int& b, int64_t& c) {
@@ -148,17 +163,32 @@ __device__ __forceinline__ bool hash_chunk_of(const int64_t* __restrict__ chunk_
     return true;
 }
 
+template <bool PLAN>
 __global__ void __launch_bounds__(256) hash_chunk_hist_kernel(const float* __restrict__ points, float inv, int nb,
                                                               const int64_t* __restrict__ prs,
                                                               const uint32_t* __restrict__ hts,
-                                                              const int64_t* __restrict__ chunk_start,
-                                                              const int64_t* __restrict__ hist_off,
+                                                              int64_t* __restrict__ chunk_start,
+                                                              int64_t* __restrict__ hist_off,
                                                               uint32_t* __restrict__ bins, uint32_t* __restrict__ hist,
                                                               int chunk) {
     extern __shared__ uint32_t h[];  // [max bins per item]
+    __shared__ int64_t s_plan[PLAN ? 2 * kPlanLds : 1];
+    const int64_t* cs = chunk_start;
+    const int64_t* ho = hist_off;
+    if constexpr (PLAN) {  // nb < kPlanLds: the plan in LDS, published by workgroup 0
+        hash_plan_block(prs, nb, hts, chunk, s_plan, s_plan + kPlanLds);
+        if (blockIdx.x == 0)
+            for (int i = threadIdx.x; i <= nb; i += 256) {
+                chunk_start[i] = s_plan[i];
+                hist_off[i] = s_plan[kPlanLds + i];
+            }
+        cs = s_plan;
+        ho = s_plan + kPlanLds;
+    }
     int b;
     int64_t c;
-    if (!hash_chunk_of(chunk_start, nb, b, c)) return;
+    if (!hash_chunk_of(cs, nb, b, c)) return;
+    const int64_t* hist_off_ = ho;
     const uint32_t tsize = hts[b + 1] - hts[b];
     const uint32_t k64 = pow64_mod(tsize);
     for (uint32_t i = threadIdx.x; i < tsize; i += 256) h[i] = 0;
@@ -170,7 +200,7 @@ __global__ void __launch_bounds__(256) hash_chunk_hist_kernel(const float* __res
         atomicAdd(&h[bin], 1u);
     }
     __syncthreads();
-    uint32_t* out = hist + hist_off[b] + c * tsize;
+    uint32_t* out = hist + hist_off_[b] + c * tsize;
     for (uint32_t i = threadIdx.x; i < tsize; i += 256) out[i] = h[i];
 }
 
@@ -398,13 +428,19 @@ O3DML_API int o3dml_build_spatial_hash_table(const float* points, int64_t n_poin
         uint32_t* bin_tot = ws.take<uint32_t>(total_bins);
         int64_t* chunk_start = ws.take<int64_t>(n_batch + 1);
         int64_t* hist_off = ws.take<int64_t>(n_batch + 1);
-        hash_plan_kernel<<<1, 256, 0, st>>>(points_row_splits, (int)n_batch, hash_table_splits, chunk_start,
-                                            hist_off, chunk);
-        O3DML_LAUNCH_CHECK();
         const unsigned grid = static_cast<unsigned>(ceil_div(n_points, chunk) + n_batch);  // >= chunk count
-        hash_chunk_hist_kernel<<<grid, 256, sizeof(uint32_t) * max_bins, st>>>(
-                points, inv, (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist,
-                chunk);
+        if (n_batch < kPlanLds) {  // the plan inside the histogram kernel
+            hash_chunk_hist_kernel<true><<<grid, 256, sizeof(uint32_t) * max_bins, st>>>(
+                    points, inv, (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins,
+                    hist, chunk);
+        } else {
+            hash_plan_kernel<<<1, 256, 0, st>>>(points_row_splits, (int)n_batch, hash_table_splits, chunk_start,
+                                                hist_off, chunk);
+            O3DML_LAUNCH_CHECK();
+            hash_chunk_hist_kernel<false><<<grid, 256, sizeof(uint32_t) * max_bins, st>>>(
+                    points, inv, (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins,
+                    hist, chunk);
+        }
         O3DML_LAUNCH_CHECK();
         const int nslices = static_cast<int>(ceil_div(max_bins, kColBins));
         hash_hist_colscan_kernel<<<static_cast<unsigned>(n_batch * nslices), 256, 0, st>>>(

@@ -59,9 +59,13 @@ __global__ void __launch_bounds__(kScanBlock) scan_tile_apply(const TIn* in, TOu
     __shared__ int64_t carry_in[kScanBlock / 64];
     const int64_t base = static_cast<int64_t>(blockIdx.x) * kScanTile;
     const int t = threadIdx.x;
-    if (raw_sums) {  // (uniform branch) carry = sum of the earlier tiles' sums
+    if (raw_sums) {  // (uniform branch) carry = sum of the earlier tiles' sums, 4 loads in flight
         int64_t c = 0;
-        for (int64_t j = t; j < static_cast<int64_t>(blockIdx.x); j += kScanBlock) c += raw_sums[j];
+        const int64_t nb = blockIdx.x;
+        int64_t j = t;
+        for (; j + 3 * kScanBlock < nb; j += 4 * kScanBlock)
+            c += (raw_sums[j] + raw_sums[j + kScanBlock]) + (raw_sums[j + 2 * kScanBlock] + raw_sums[j + 3 * kScanBlock]);
+        for (; j < nb; j += kScanBlock) c += raw_sums[j];
         c = wave_sum(c);
         if (lane_id() == 0) carry_in[wave_id()] = c;
     }
@@ -119,7 +123,7 @@ inline size_t scan_workspace_bytes(int64_t n) {
 
 // Tiles up to which every tile sums its predecessors' sums itself (two
 // launches: sums, apply); more tiles scan the sums recursively (three+).
-constexpr int64_t kScanDirectTiles = 1024;
+constexpr int64_t kScanDirectTiles = 4096;
 
 // out[i] = sum_{j<=i} in[j] (inclusive) or sum_{j<i} in[j] (exclusive).
 // in == out is allowed.  tail (nullable): total -> tail[0] (and tail_src[0]
