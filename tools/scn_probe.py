@@ -40,6 +40,16 @@ for _ in range(reps):
     step()
 torch.cuda.synchronize()
 print("ms/frame", (time.perf_counter() - t) / reps * 1e3, "train" if train else "eval")
+if os.environ.get("CPROFILE"):  # host-side split of one eval frame
+    import cProfile
+    import pstats
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    pr.disable()
+    pstats.Stats(pr).sort_stats("tottime").print_stats(30)
 if os.environ.get("TORCHPROF"):
     from torch.profiler import profile, ProfilerActivity
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as p:
