@@ -48,3 +48,27 @@ def test_ops_fail_loudly_without_gpu():
     from o3dml_amd import ops
     with pytest.raises(RuntimeError, match="no ROCm GPU"):
         ops.fixed_radius_search(torch.zeros(4, 3), torch.zeros(4, 3), 0.1)
+
+
+def test_layer_paths_fail_loudly_without_gpu():
+    """The one-call layer path and the collate's dense path have no CPU
+    fallback either."""
+    import pytest
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from o3dml_amd import layers
+    with pytest.raises(RuntimeError, match="no ROCm GPU"):
+        layers.FixedRadiusSearch()(torch.zeros(4, 3), torch.zeros(4, 3), 0.1)
+
+
+def test_layer_workspace_sizes():
+    """o3dml_fixed_radius_search_layer_workspace_size covers the count
+    workspace and the table build's scratch (host-only helper)."""
+    from o3dml_amd import _lib
+    lib = _lib.load()
+    for n, m, b in ((65536, 65536, 1), (4194304, 4194304, 64), (1000, 10, 3)):
+        t = max(b, n // 64)
+        lay = lib.o3dml_fixed_radius_search_layer_workspace_size(n, m, b, t)
+        assert lay >= lib.o3dml_fixed_radius_search_workspace_size(n, m, b)
+        assert lay >= lib.o3dml_build_spatial_hash_table_workspace_size(n, t)
