@@ -86,6 +86,15 @@ struct TimedRegion {
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Pinned host scratch for the few int64 sizes a count phase reads back (a
+// pageable destination goes through a staging copy): 8 slots per host
+// thread, allocated on first use, never freed.
+inline int64_t* pinned_scratch() {
+    thread_local int64_t* p = nullptr;
+    if (!p) O3DML_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&p), 8 * sizeof(int64_t), 0));
+    return p;
+}
+
 // Grid size for grid-stride streaming kernels: enough workgroups to fill the
 // 256 CUs several times over, capped (cdna_hip_programming.md Guideline 11).
 inline unsigned stream_grid(int64_t n, int block, int64_t cap = 256 * 8) {

@@ -418,8 +418,8 @@ O3DML_API int o3dml_voxelize_count(const float* points, int64_t n_points, int nd
     }
     vox_totals_kernel<<<1, 64, 0, st>>>(s.incl, n_points, s.keep_incl, s.npts_incl, s.scalars + 1);
     O3DML_LAUNCH_CHECK();
-    int64_t tot[3];
-    O3DML_CHECK_HIP(hipMemcpyAsync(tot, s.scalars + 1, sizeof(tot), hipMemcpyDeviceToHost, st));
+    int64_t* tot = pinned_scratch();
+    O3DML_CHECK_HIP(hipMemcpyAsync(tot, s.scalars + 1, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
     counts_host[0] = tot[1];
     counts_host[1] = tot[2];
@@ -549,8 +549,8 @@ O3DML_API int o3dml_grid_subsample_count(const float* points, int64_t n_points, 
     const int rc = o3dml_grid_subsample_count_async(points, n_points, n_batch, row_splits, dl, max_p, out, workspace,
                                                     front, stream);
     if (rc != 0) return rc;
-    int64_t tot[2];
-    O3DML_CHECK_HIP(hipMemcpyAsync(tot, out, sizeof(tot), hipMemcpyDeviceToHost, st));
+    int64_t* tot = pinned_scratch();
+    O3DML_CHECK_HIP(hipMemcpyAsync(tot, out, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
     O3DML_REQUIRE(tot[1] == 0, "grid_subsample: grid too large");
     *n_out_host = tot[0];
@@ -656,7 +656,7 @@ inline GridState take_grid_state(Workspace& ws, int64_t n) {
     g.sidx = ws.take<uint32_t>(n);
     g.head = ws.take<int64_t>(n);
     g.incl = ws.take<int64_t>(n);
-    g.flags = ws.take<int64_t>(2);
+    g.flags = ws.take<int64_t>(4);  // [0] range flag, [2..3] (count, flag) for the host read
     return g;
 }
 
@@ -665,7 +665,7 @@ inline GridState take_grid_state(Workspace& ws, int64_t n) {
 
 O3DML_API size_t o3dml_calculate_grid_workspace_size(int64_t n_points) {
     return 2 * ws_bytes<uint64_t>(n_points) + ws_bytes<uint32_t>(n_points) + 2 * ws_bytes<int64_t>(n_points) +
-           ws_bytes<int64_t>(2) +
+           ws_bytes<int64_t>(4) +
            std::max(prim::radix_sort_workspace_bytes<uint64_t>(n_points), prim::scan_workspace_bytes(n_points));
 }
 
@@ -686,10 +686,14 @@ O3DML_API int o3dml_calculate_grid_count(const float* positions, int64_t n_point
         grid_unique_heads_kernel<<<gr, 256, 0, st>>>(g.sk, n_points, g.head);
         O3DML_LAUNCH_CHECK();
         sws = ws;
-        prim::scan<int64_t, int64_t>(g.head, g.incl, n_points, true, sws, st);
-        O3DML_CHECK_HIP(hipMemcpyAsync(&host[0], g.flags, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-        O3DML_CHECK_HIP(hipMemcpyAsync(&host[1], g.incl + n_points - 1, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        // the scan's last tile writes (count, range flag) next to each other:
+        // one 16-B read into pinned memory instead of two pageable ones
+        prim::scan<int64_t, int64_t>(g.head, g.incl, n_points, true, sws, st, g.flags + 2, g.flags);
+        int64_t* pinned = pinned_scratch();
+        O3DML_CHECK_HIP(hipMemcpyAsync(pinned, g.flags + 2, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
         O3DML_CHECK_HIP(hipStreamSynchronize(st));
+        host[0] = pinned[1];
+        host[1] = pinned[0];
     }
     O3DML_REQUIRE(host[0] == 0, "calculate_grid: positions must be < %lld", (long long)kGridMax);
     *n_out_host = host[1];
