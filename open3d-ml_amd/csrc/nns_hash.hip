@@ -267,8 +267,10 @@ __global__ void __launch_bounds__(256) hash_hist_colscan_kernel(int nslices, con
 // first slot per bin = the bin's start inside the item (exclusive scan of the
 // item's bin totals, done here in LDS; chunk 0 also writes the item's
 // cell_splits) + the chunk's offset from hash_hist_colscan_kernel.
-template <int CHUNK>
-__global__ void __launch_bounds__(256) hash_chunk_scatter_kernel(int nb, const int64_t* __restrict__ prs,
+// NWV waves per chunk (4, or 8: half the rows per wave, so half the
+// ranking chain per wave for the same chunk)
+template <int CHUNK, int NWV = kHashWaves>
+__global__ void __launch_bounds__(NWV * 64) hash_chunk_scatter_kernel(int nb, const int64_t* __restrict__ prs,
                                                                  const uint32_t* __restrict__ hts,
                                                                  const int64_t* __restrict__ chunk_start,
                                                                  const int64_t* __restrict__ hist_off,
@@ -277,10 +279,10 @@ __global__ void __launch_bounds__(256) hash_chunk_scatter_kernel(int nb, const i
                                                                  const uint32_t* __restrict__ bin_tot,
                                                                  uint32_t* __restrict__ cell_splits,
                                                                  uint32_t* __restrict__ hti, int max_bins) {
-    constexpr int kRows = CHUNK / 64 / kHashWaves;  // rows of 64 per wave
-    // [kHashWaves][max_bins]: counts, then bases; then [max_bins] bin starts
+    constexpr int kRows = CHUNK / 64 / NWV;  // rows of 64 per wave
+    // [NWV][max_bins]: counts, then bases; then [max_bins] bin starts
     extern __shared__ uint32_t wc_all[];
-    __shared__ uint32_t wsum[kHashWaves];
+    __shared__ uint32_t wsum[NWV];
     int b;
     int64_t c;
     if (!hash_chunk_of(chunk_start, nb, b, c)) return;
@@ -289,13 +291,13 @@ __global__ void __launch_bounds__(256) hash_chunk_scatter_kernel(int nb, const i
     const int64_t item0 = prs[b], item_end = prs[b + 1];
     const uint32_t* base = hist + hist_off[b] + c * tsize;
     uint32_t* wc = wc_all + w * max_bins;
-    uint32_t* bstart = wc_all + kHashWaves * max_bins;
-    for (uint32_t i = t; i < tsize; i += 256)
+    uint32_t* bstart = wc_all + NWV * max_bins;
+    for (uint32_t i = t; i < tsize; i += NWV * 64)
 #pragma unroll
-        for (int ww = 0; ww < kHashWaves; ++ww) wc_all[ww * max_bins + i] = 0;
-    {  // bin starts: exclusive scan of the item's bin totals, 256-bin rounds
+        for (int ww = 0; ww < NWV; ++ww) wc_all[ww * max_bins + i] = 0;
+    {  // bin starts: exclusive scan of the item's bin totals, (NWV * 64)-bin rounds
         uint32_t carry = 0;
-        for (uint32_t b0 = 0; b0 < tsize; b0 += 256) {
+        for (uint32_t b0 = 0; b0 < tsize; b0 += NWV * 64) {
             const uint32_t i = b0 + t;
             const uint32_t v = i < tsize ? bin_tot[first + i] : 0u;
             const uint32_t inc = wave_inclusive_scan(v);
@@ -303,7 +305,7 @@ __global__ void __launch_bounds__(256) hash_chunk_scatter_kernel(int nb, const i
             __syncthreads();
             uint32_t st = carry + inc - v, all = 0;
 #pragma unroll
-            for (int ww = 0; ww < kHashWaves; ++ww) {
+            for (int ww = 0; ww < NWV; ++ww) {
                 st += ww < w ? wsum[ww] : 0u;
                 all += wsum[ww];
             }
@@ -344,10 +346,10 @@ __global__ void __launch_bounds__(256) hash_chunk_scatter_kernel(int nb, const i
     }
     __syncthreads();
     // per-wave bases: chunk base + counts of the earlier waves (stable)
-    for (uint32_t i = t; i < tsize; i += 256) {
+    for (uint32_t i = t; i < tsize; i += NWV * 64) {
         uint32_t a = bstart[i] + base[i];
 #pragma unroll
-        for (int ww = 0; ww < kHashWaves; ++ww) {
+        for (int ww = 0; ww < NWV; ++ww) {
             const uint32_t cw = wc_all[ww * max_bins + i];
             wc_all[ww * max_bins + i] = a;
             a += cw;
@@ -447,12 +449,22 @@ O3DML_API int o3dml_build_spatial_hash_table(const float* points, int64_t n_poin
                 nslices, hash_table_splits, chunk_start, hist_off, hist, bin_tot);
         O3DML_LAUNCH_CHECK();
         const size_t lds = sizeof(uint32_t) * (kHashWaves + 1) * max_bins;
+        // 8 waves per 4,096-point chunk (O3DML_HASH_WAVES=8) while their LDS fits 64 KiB
+        static const int hw = [] {
+            const char* e = std::getenv("O3DML_HASH_WAVES");
+            return e ? std::atoi(e) : 4;
+        }();
+        const size_t lds8 = sizeof(uint32_t) * 9 * max_bins;
         if (chunk == kHashChunkSmall)
             hash_chunk_scatter_kernel<kHashChunkSmall><<<grid, 256, lds, st>>>(
                     (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist, bin_tot,
                     hash_table_cell_splits, hash_table_index, static_cast<int>(max_bins));
         else if (chunk == 2048)
             hash_chunk_scatter_kernel<2048><<<grid, 256, lds, st>>>(
+                    (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist, bin_tot,
+                    hash_table_cell_splits, hash_table_index, static_cast<int>(max_bins));
+        else if (hw == 8 && lds8 <= 65536)
+            hash_chunk_scatter_kernel<kHashChunk, 8><<<grid, 512, lds8, st>>>(
                     (int)n_batch, points_row_splits, hash_table_splits, chunk_start, hist_off, bins, hist, bin_tot,
                     hash_table_cell_splits, hash_table_index, static_cast<int>(max_bins));
         else
