@@ -714,7 +714,17 @@ __device__ __forceinline__ int32_t wave_ext_i(int32_t v) {
 __device__ __forceinline__ int32_t wave_min_i(int32_t v) { return wave_ext_i<false>(v); }
 __device__ __forceinline__ int32_t wave_max_i(int32_t v) { return wave_ext_i<true>(v); }
 
-__global__ void __launch_bounds__(256) bucket_classes_kernel(const float* __restrict__ points,
+// O3DML_BC_WAVES: waves per SIMD asked of the register allocator (A/B
+// builds; 0 = the compiler's choice, 90 VGPRs -> 5 waves per SIMD)
+#ifndef O3DML_BC_WAVES
+#define O3DML_BC_WAVES 0
+#endif
+#if O3DML_BC_WAVES > 0
+#define O3DML_BC_ATTR __attribute__((amdgpu_waves_per_eu(O3DML_BC_WAVES, 8)))
+#else
+#define O3DML_BC_ATTR
+#endif
+__global__ void __launch_bounds__(256) O3DML_BC_ATTR bucket_classes_kernel(const float* __restrict__ points,
                                                              const uint32_t* __restrict__ hti,
                                                              float4* __restrict__ pts, int64_t n_pts,
                                                              const uint32_t* __restrict__ cs,
