@@ -25,7 +25,8 @@ the stream each kernel is launched on, o3dml_timing_*); the dominant kernel's
 achieved = SURVEY §8d algorithmic bytes (12+12+4+8+4m per query) x queries /
 its average duration.  traffic: HBM bytes per launch
 from the committed rocprofv3 PMC summary (profiles/), if present.
-cpu_baseline: the C oracle (oracle/, OpenMP) on a bounded sample, rank 0, N=1.
+cpu_baseline: oracle/cpu_frs.c (optimised CPU search of the same semantics, OpenMP,
+all host threads and 1 thread) on the bench batch, rank 0, N=1.
 """
 import argparse
 import json
@@ -167,20 +168,43 @@ def issue_bound(kernel):
             "source": "profiles/*/pmc_%s.json (PMC pass duration %.1f us)" % (kernel, c["dur_us_mean"])}
 
 
-def cpu_baseline():
+def cpu_baseline(scenes=64):
+    """C1 on the host cores, same semantics and output as the GPU step.
+    value: oracle/cpu_frs.c (parallel hash build, points in bucket order,
+    ONE search pass with AVX2 + FMA candidate tests, block-local outputs
+    concatenated) on the bench batch itself (`scenes` x 65,536 points), all
+    threads; plus the same code on 1 thread (one scene) and the plain test
+    oracle (serial hash build, count + fill passes) for comparison."""
     import oracle as O
     threads = O.default_threads()
-    pts = np.random.default_rng(0).random((N_POINTS, 3), dtype=np.float32)
-    O.fixed_radius_search(pts, pts, RADIUS, nthreads=threads)  # warm (builds the oracle if needed)
-    times = []
-    for _ in range(3):
-        t = time.perf_counter()
-        O.fixed_radius_search(pts, pts, RADIUS, nthreads=threads)
-        times.append(time.perf_counter() - t)
-    return {"value": round(N_POINTS / float(np.median(times)) / 1e6, 4), "unit": "Mpoints/s", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle fixed_radius_search (hash build + count + fill), one 65,536-pt C1 scene, "
-                      f"median of 3, {threads} OpenMP threads"}
+    pts, rs = make_batch(0, scenes, "cpu")
+    pts, rs = pts.numpy(), rs.numpy()
+    one = pts[:N_POINTS]
+
+    def median_rate(fn, n, reps=3):
+        fn()  # warm (first touch, the oracle build if needed)
+        times = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            fn()
+            times.append(time.perf_counter() - t)
+        return round(n / float(np.median(times)) / 1e6, 4)
+
+    cap = [None, None]
+
+    def fast(p, r, nt, slot):
+        idx, _ = O.fixed_radius_search_fast(p, RADIUS, r, nthreads=nt, capacity=cap[slot])
+        cap[slot] = len(idx)
+
+    n_thr = median_rate(lambda: fast(pts, rs, threads, 0), len(pts))
+    one_thr = median_rate(lambda: fast(one, None, 1, 1), N_POINTS)
+    plain = median_rate(lambda: O.fixed_radius_search(one, one, RADIUS, nthreads=threads), N_POINTS)
+    return {"value": n_thr, "unit": "Mpoints/s", "cores": threads, "kind": "port",
+            "value_1_thread": one_thr, "plain_oracle_value": plain,
+            "sample": f"oracle/cpu_frs.c (parallel hash build + one-pass search, AVX2/FMA when the host has "
+                      f"them) on the bench batch ({scenes} x 65,536-pt C1 scenes), median of 3, {threads} OpenMP "
+                      f"threads; value_1_thread: same code, 1 thread, one scene; plain_oracle_value: the test "
+                      f"oracle (serial build, count + fill passes), one scene, {threads} threads"}
 
 
 def make_scan(seed):

@@ -358,7 +358,8 @@ int o3dml_nms(const float* boxes, const float* scores, int64_t n, float nms_over
  * filters [k,k,k,Cin,Cout] per load_unet_wts :660-677).
  * 1) o3dml_sparse_conv_build_map: CSR pairs (over OUTPUT points) -> dense
  *    kernel map [n_out*K] (+ inverse map for the input gradient) in
- *    `workspace`; status_host[0] bit0 = duplicate (o,k), bit1 = bad index.
+ *    `workspace`; status_host[0] bit0 = duplicate (o,k), bit1 = kernel index
+ *    out of [0, K), bit3 = neighbour index out of [0, n_in) (pair dropped).
  * 2) o3dml_sparse_conv_forward: implicit GEMM on MFMA (f32-accurate bf16x6
  *    products by default, see o3dml_sparse_conv_set_exact).
  * 3) o3dml_sparse_conv_backward: grad_inp (inverse map, W^T) and

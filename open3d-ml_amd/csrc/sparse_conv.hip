@@ -47,7 +47,7 @@ constexpr int kGemmThreads = O3DML_GEMM_THREADS;  // 4 waves
 // --------------------------------------------------------------------------
 __global__ void build_kernel_map_kernel(const int32_t* __restrict__ nbr, const int32_t* __restrict__ kidx,
                                         const float* __restrict__ nimp, const int64_t* __restrict__ rs, int64_t n_out,
-                                        int K, int32_t* __restrict__ map, float* __restrict__ pscale,
+                                        int64_t n_in, int K, int32_t* __restrict__ map, float* __restrict__ pscale,
                                         float* __restrict__ norm, int* __restrict__ dup) {
     for (int64_t o = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; o < n_out;
          o += static_cast<int64_t>(gridDim.x) * blockDim.x) {
@@ -58,12 +58,17 @@ __global__ void build_kernel_map_kernel(const int32_t* __restrict__ nbr, const i
                 atomicOr(dup, 2);
                 continue;
             }
+            const int32_t nb = nbr[e];
+            if (nb < 0 || nb >= n_in) {  // would address past the features (and the inverse map)
+                atomicOr(dup, 8);
+                continue;
+            }
             int32_t* slot = map + o * K + k;
             if (*slot >= 0) {
                 atomicOr(dup, 1);  // two pairs share (o, k): dense map impossible
                 continue;
             }
-            *slot = nbr[e];
+            *slot = nb;
             const float w = nimp ? nimp[e] : 1.f;
             if (pscale) pscale[o * K + k] = w;
             s += w;
@@ -210,6 +215,10 @@ struct GemmStage {
 struct GemmPrologue {
     const float* scale;  // [cin] or null
     const float* shift;  // [cin]
+    // byte sizes of the gathered rows and of the filters: the num_records of
+    // the buffer resources (BUF kernels), so a row index past the operand
+    // reads zeros, never foreign memory (set by the launcher)
+    uint32_t src_bytes = 0, w_bytes = 0;
 };
 constexpr int kPreMax = 1024;  // max cin with a prologue (LDS staging)
 
@@ -515,15 +524,15 @@ __device__ __forceinline__ void glds16(const float* g, float* lds_wave_base) {
 // column gets an offset past the resource's range, which the buffer unit
 // answers with zeros (no zero-page select, no 64-bit address arithmetic:
 // ~40 % of the loop's VALU went to addresses)
-constexpr uint32_t kNoRow = 0x7FFFFFF0u;  // >= num_records of every operand resource
+constexpr uint32_t kNoRow = 0x7FFFFFF0u;  // > num_records of every operand resource (its true byte size)
 struct GemmRsrc {
     __amdgpu_buffer_rsrc_t src, w;
 };
-__device__ __forceinline__ GemmRsrc gemm_rsrc(const float* src, const float* Wt) {
+__device__ __forceinline__ GemmRsrc gemm_rsrc(const float* src, const float* Wt, const GemmPrologue& pre) {
     return {__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), static_cast<short>(0),
-                                              static_cast<int>(kNoRow), kBufferFlags),
+                                              static_cast<int>(pre.src_bytes), kBufferFlags),
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Wt), static_cast<short>(0),
-                                              static_cast<int>(kNoRow), kBufferFlags)};
+                                              static_cast<int>(pre.w_bytes), kBufferFlags)};
 }
 
 template <bool BREG, bool SC = true, bool BUF = false>
@@ -762,7 +771,7 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
                 k = u ? __builtin_ctz(u) : 0;
             }
         };
-        const GemmRsrc rs = gemm_rsrc(src, Wt);
+        const GemmRsrc rs = gemm_rsrc(src, Wt, pre);
         float* buf1 = stage_all[w][1];
         GemmStage s0, s1, cu;
         int c00 = c0;
@@ -816,7 +825,7 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
         int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
         GemmStage nx, cu;
-        const GemmRsrc rs = gemm_rsrc(src, Wt);
+        const GemmRsrc rs = gemm_rsrc(src, Wt, pre);
         lds_issue<BREG, SC, BUF>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout,
                                  true, nx, &rs);
         for (int j = j0; j < j1; ++j) {
@@ -1071,7 +1080,7 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
         SharedStage<RB> nx, cu;
         float s1[RB], s2[RB];
         bool vv[RB];
-        const GemmRsrc rs = gemm_rsrc(src, Wt);
+        const GemmRsrc rs = gemm_rsrc(src, Wt, pre);
         shared_issue<NW, RB, BUF>(abuf[0], mtile, K, k, c0, lane, w, src, cin, true, &rs);
         shared_regs<RB, SC, BUF>(mtile, K, k, c0, lane, o, i, col, sscale, pscale, Wt, cin, cout, true, nx, s1, s2, vv,
                                  &rs);
@@ -1862,6 +1871,10 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
     }();
     const bool buf_ok = buf_path && cin % 32 == 0 && static_cast<uint64_t>(n_src) * cin * 4 < kNoRow &&
                         static_cast<uint64_t>(K) * cout * cin * 4 < kNoRow - 64;
+    if (buf_ok) {  // the resources cover exactly the operands
+        pre.src_bytes = static_cast<uint32_t>(static_cast<uint64_t>(n_src) * cin * 4);
+        pre.w_bytes = static_cast<uint32_t>(static_cast<uint64_t>(K) * cout * cin * 4);
+    }
     // the shared-A kernel with buffer addressing: neutral in the same-session
     // A/B (64->96 -3 %, 128->128 +1-2 %: its row addresses are split over the
     // NW waves already) — off unless O3DML_GEMM_SHARED_BUF=1
@@ -2243,14 +2256,14 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
     if (n_out > 0) {
         O3DML_CHECK_HIP(hipMemsetAsync(map, 0xff, sizeof(int32_t) * n_out * K, st));
         build_kernel_map_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(
-                neighbors_index, neighbors_kernel_index, neighbors_importance, neighbors_row_splits, n_out, K, map,
-                neighbors_importance ? pscale : nullptr, norm, status);
+                neighbors_index, neighbors_kernel_index, neighbors_importance, neighbors_row_splits, n_out, n_in, K,
+                map, neighbors_importance ? pscale : nullptr, norm, status);
         O3DML_LAUNCH_CHECK();
         recip_norm_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(normalize ? norm : nullptr, out_importance, n_out,
                                                                   oscale);
         O3DML_LAUNCH_CHECK();
     }
-    if (want_inverse && n_in > 0) {
+    if (want_inverse && n_in > 0) {  // map entries are < n_in (out-of-range pairs were dropped, status 8)
         O3DML_CHECK_HIP(hipMemsetAsync(inv, 0xff, sizeof(int32_t) * n_in * K, st));
         if (n_out > 0) {
             build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(

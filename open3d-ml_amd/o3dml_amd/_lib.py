@@ -196,6 +196,26 @@ def check(status, what):
         raise RuntimeError(f"o3dml_amd.{what} failed: {msg}")
 
 
+def _stream_device(args):
+    """Device of the StreamHandle among args (the stream is usually last)."""
+    from ._util import StreamHandle
+    if args and isinstance(args[-1], StreamHandle):
+        return args[-1].dev
+    for a in args:
+        if isinstance(a, StreamHandle):
+            return a.dev
+    return None
+
+
 def call(name, *args):
-    """Call a status-returning entry point and raise on failure."""
-    check(getattr(load(), name)(*args), name)
+    """Call a status-returning entry point and raise on failure.  A call given
+    a stream of a device other than the current one runs under a restoring
+    device guard (the caller's current device is unchanged afterwards)."""
+    fn = getattr(load(), name)
+    dev = _stream_device(args)
+    if dev is not None and dev != torch.cuda.current_device():
+        with torch.cuda.device(dev):
+            rc = fn(*args)
+    else:
+        rc = fn(*args)
+    check(rc, name)

@@ -25,16 +25,20 @@ def gpu_device(*tensors):
     return torch.device("cuda", torch.cuda.current_device())
 
 
+class StreamHandle(int):
+    """A hipStream_t (an int for ctypes) that remembers its device: _lib.call
+    runs a call given one under a restoring device guard when that device is
+    not the current one, so the library's launches, scratch streams and events
+    (and torch's default stream handle, the null stream) belong to the device
+    that holds the tensors, and the caller's current device is left as it was."""
+
+
 def stream_handle(device):
-    """The current torch stream of `device`.  The op's device is made the
-    current one first: the library's launches, scratch streams and events then
-    belong to the device that holds the tensors even when the caller's current
-    device is another GPU (and torch's default stream handle, the null stream,
-    resolves to that device)."""
+    """The current torch stream of `device` (see StreamHandle)."""
     device = torch.device(device)
-    if device.index is not None and torch.cuda.current_device() != device.index:
-        torch.cuda.set_device(device)
-    return torch.cuda.current_stream(device).cuda_stream
+    h = StreamHandle(torch.cuda.current_stream(device).cuda_stream)
+    h.dev = device.index
+    return h
 
 
 def ptr(t):

@@ -36,6 +36,8 @@ def _build_map(nidx, kidx, nimp, rs, n_in, K, normalize, out_importance, want_in
               mws.numel(), st)
     if status[0] & 2:
         raise RuntimeError("sparse_conv: neighbors_kernel_index out of range for the filter")
+    if status[0] & 8:
+        raise RuntimeError(f"sparse_conv: neighbors_index out of range [0, {n_in})")
     if status[0] & 1:  # handled by _conv_layers
         raise _DuplicateKernelIndex()
     if tile_order:
@@ -113,8 +115,16 @@ def conv_grads(filters, inp_features, grad_out, neighbors_index, neighbors_kerne
     oimp = _opt(out_importance, dev)
     K = int(np.prod(W.shape[:-2]))
     cin, cout = int(W.shape[-2]), int(W.shape[-1])
-    mws, n_out = _build_map(nidx, kidx, nimp, rs, x.shape[0], K, normalize, oimp, True,
-                            cin * cout >= TILE_ORDER_MIN_CHANNELS, dev, stream_handle(dev))
+    try:
+        mws, n_out = _build_map(nidx, kidx, nimp, rs, x.shape[0], K, normalize, oimp, True,
+                                cin * cout >= TILE_ORDER_MIN_CHANNELS, dev, stream_handle(dev))
+    except _DuplicateKernelIndex:
+        # off-lattice rulebook (pairs sharing an (output, k) or (input, k)):
+        # the forward split the pairs into layers (_conv_layers), so does this
+        # backward — the layered forward re-run on detached leaves and
+        # differentiated by autograd (each layer's backward is the HIP kernel)
+        return _layered_grads(W, x, grad_out.to(dev), nidx, kidx, nimp, rs, sscale, normalize, oimp, K,
+                              need_w, need_x)
     use_os = int(bool(normalize) or oimp is not None)
     meta = (K, cin, cout, x.shape[0], n_out, nimp is not None, use_os, sscale is not None)
     ss = sscale if sscale is not None else torch.empty(0, device=dev)
@@ -123,6 +133,27 @@ def conv_grads(filters, inp_features, grad_out, neighbors_index, neighbors_kerne
 
 class _DuplicateKernelIndex(Exception):
     """Two neighbours of one output share a kernel index (see _conv_layers)."""
+
+
+def _layered_grads(W, x, grad_out, nidx, kidx, nimp, rs, sscale, normalize, oimp, K, need_w, need_x):
+    """(dW, dIn) of _conv_layers' output: its forward on fresh leaves, then
+    torch.autograd.grad (every layer's backward runs the HIP dW / dIn kernels)."""
+    if not (need_w or need_x):
+        return None, None
+    wl = W.detach().requires_grad_(need_w)
+    xl = x.detach().requires_grad_(need_x)
+    with torch.enable_grad():
+        out = _conv_layers(wl, xl, None, nidx, kidx, nimp, rs, sscale, bool(normalize), oimp, K)
+        leaves = [t for t, need in ((wl, need_w), (xl, need_x)) if need]
+        grads = torch.autograd.grad(out, leaves, grad_out.float(), allow_unused=True)
+    it = iter(grads)
+    gw = next(it) if need_w else None
+    gx = next(it) if need_x else None
+    if need_w and gw is None:
+        gw = torch.zeros_like(W)
+    if need_x and gx is None:
+        gx = torch.zeros_like(x)
+    return gw, gx
 
 
 def _conv_layers(f, x, b, nidx, kidx, nimp, rs, sscale, normalize, oimp, K):
@@ -225,18 +256,24 @@ def sparse_conv_transpose(filters, out_importance, inp_features, inp_neighbors_i
     inp_neighbors_* is the same relation per INPUT point and, with normalize,
     each input's contribution is divided by its importance sum (or neighbour
     count).  out_importance scales the outputs."""
-    ss = transpose_scale(inp_features, filters, inp_neighbors_importance_sum, inp_neighbors_row_splits, normalize)
+    ss = transpose_scale(inp_features, filters, inp_neighbors_importance_sum, inp_neighbors_row_splits, normalize,
+                         neighbors_importance)
     return _conv(filters, inp_features, None, neighbors_index, neighbors_kernel_index, neighbors_importance,
                  neighbors_row_splits, ss, False, out_importance)
 
 
-def transpose_scale(inp_features, filters, inp_neighbors_importance_sum, inp_neighbors_row_splits, normalize):
+def transpose_scale(inp_features, filters, inp_neighbors_importance_sum, inp_neighbors_row_splits, normalize,
+                    neighbors_importance=None):
     """Per-input scale of sparse_conv_transpose(normalize=True): 1 / (importance
-    sum or neighbour count), 1 where that is 0; None without normalize."""
+    sum or neighbour count), 1 where that is 0; None without normalize.  The
+    importance sum counts only when per-pair importances are given (Open3D's
+    NEIGHBOR_IMPORTANCE switch is neighbors_importance being non-empty †);
+    otherwise the neighbour count divides, whatever sum the caller passes."""
     if not normalize:
         return None
     dev = gpu_device(inp_features, filters)
-    s = _opt(inp_neighbors_importance_sum, dev)
+    has_imp = neighbors_importance is not None and neighbors_importance.numel() > 0
+    s = _opt(inp_neighbors_importance_sum, dev) if has_imp else None
     if s is None:
         irs = to_dev(inp_neighbors_row_splits, dev, torch.int64)
         s = (irs[1:] - irs[:-1]).float()

@@ -285,7 +285,7 @@ def _sct_setup(ctx, inputs, output):
 
 def _sct_backward(ctx, grad):
     filters, out_imp, x, inp_nimp_sum, inp_rs, nidx, kidx, nimp, rs = ctx.saved_tensors
-    ss = sc.transpose_scale(x, filters, inp_nimp_sum, inp_rs, ctx.normalize)
+    ss = sc.transpose_scale(x, filters, inp_nimp_sum, inp_rs, ctx.normalize, nimp)
     gw, gx = sc.conv_grads(filters, x, grad, nidx, kidx, nimp, rs, ss, False, out_imp,
                            ctx.needs_input_grad[0], ctx.needs_input_grad[2])
     if gw is not None and not filters.is_cuda:

@@ -113,6 +113,30 @@ def fixed_radius_search(points, queries, radius, points_row_splits=None,
     return idx, rs, dist
 
 
+def fixed_radius_search_fast(points, radius, points_row_splits=None, nthreads=None, capacity=None,
+                             hash_table_size_factor=1 / 64, max_hash_table_size=33554432, simd=True):
+    """cpu_frs.c: the optimised CPU self search (parallel hash build + one
+    search pass, AVX2 + FMA candidate tests when the host has them and simd),
+    L2, int32 — the bench's C1 CPU baseline.  Same result as
+    fixed_radius_search(points, points, radius, rs, rs).  Returns (idx, rs)."""
+    points = _f32(points)
+    prs = _splits(points_row_splits, len(points))
+    n = len(points)
+    rs = np.zeros(n + 1, np.int64)
+    nt = default_threads() if nthreads is None else nthreads
+    cap = int(capacity) if capacity is not None else 48 * n
+    f = lib().orc_frs_fast
+    f.restype = ctypes.c_int64
+    while True:
+        idx = np.empty(cap, np.int32)
+        total = f(_p(points), ctypes.c_int64(n), ctypes.c_float(radius), ctypes.c_int64(len(prs) - 1), _p(prs),
+                  ctypes.c_double(hash_table_size_factor), ctypes.c_int64(max_hash_table_size), ctypes.c_int(nt),
+                  ctypes.c_int(int(simd)), _p(rs), _p(idx), ctypes.c_int64(cap))
+        if total <= cap:
+            return idx[:total], rs
+        cap = int(total)
+
+
 def knn_search(points, queries, k, points_row_splits=None, queries_row_splits=None,
                metric="L2", ignore_query_point=False, return_distances=False,
                index_dtype=np.int32, nthreads=None):

@@ -358,3 +358,35 @@ def test_frs_dense_one_call(cuda):
             row = oi[ors[i]:ors[i + 1]]
             assert np.array_equal(d[i, :len(row)], row) and (d[i, len(row):] == len(pts)).all()
     assert kpfcnn._dense_end(e, host[6:9]).shape[0] == 0
+
+
+def test_frs_bench_batch_bit_exact(cuda):
+    """The exact batch bench.py times (64 scenes x 65,536 points, one call,
+    u16 temp rows across 64 batch items) through layers.FixedRadiusSearch,
+    twice (the second call takes the speculative capacity of the first), vs
+    the oracle's fixed_radius_search on the same batch: bit-exact."""
+    import bench
+    from o3dml_amd import layers
+    pts, rs = bench.make_batch(0, 64, cuda)
+    nns = layers.FixedRadiusSearch()
+    for _ in range(2):
+        res = nns(pts, pts, bench.RADIUS, rs, rs)
+    p = pts.cpu().numpy()
+    oi, ors, _ = O.fixed_radius_search(p, p, bench.RADIUS, rs.numpy(), rs.numpy())
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+
+
+@pytest.mark.parametrize("lg", [18, 20, 22])
+def test_frs_large_item_bit_exact(cuda, lg):
+    """One batch item of more than 65,536 points (the c1_sweep shapes of
+    bench.py: N = 2^lg at the C1 density) vs the oracle, bit-exact."""
+    from o3dml_amd import layers
+    n = 1 << lg
+    pts = np.random.default_rng(lg).random((n, 3), dtype=np.float32)
+    r = 0.05 * (65536.0 / n) ** (1.0 / 3.0)
+    t = torch.from_numpy(pts).to(cuda)
+    res = layers.FixedRadiusSearch()(t, t, r)
+    oi, ors, _ = O.fixed_radius_search(pts, pts, r)
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)

@@ -450,3 +450,44 @@ def test_transposed_conv_normalize(cuda):
     r = torch.zeros((vox.shape[0], 24), dtype=torch.float64).index_add_(0, o, contrib)
     gx64, = torch.autograd.grad(r, x64r, go.double().cpu())
     _close(gx.cpu().numpy(), gx64.numpy())
+
+
+def test_out_of_range_neighbour_index_and_map_entry(cuda):
+    """A neighbour index past the input features raises RuntimeError (the
+    map build drops the pair and flags it, status bit 3) instead of reading
+    past the features; and a map entry corrupted past the operand (the
+    buffer-resource GEMM, cin % 32 == 0) reads zeros: its output row equals
+    the row with that pair removed (num_records = the operand's true size)."""
+    from o3dml_amd import _lib, layers, sparse_conv as sc
+    from o3dml_amd._util import ptr, stream_handle, workspace
+    vox = torch.from_numpy(_voxels(3000, 16, 4)).to(cuda)
+    conv = layers.SparseConv(32, 32, [3, 3, 3], use_bias=False).to(cuda)
+    conv.lattice_rulebook = False
+    nb, kidx = conv._rulebook(vox, vox, 1.0, None, False, 1.0)
+    n = vox.shape[0]
+    x = torch.randn((n, 32), device=cuda)
+    bad = nb.neighbors_index.clone()
+    bad[5] = n + 7
+    with pytest.raises(RuntimeError, match="neighbors_index out of range"):
+        sc.sparse_conv(conv.kernel, x, None, bad, kidx, None, nb.neighbors_row_splits)
+    lib = _lib.load()
+    dev = x.device
+    st = stream_handle(dev)
+    W = conv.kernel.detach().contiguous()
+    K = 27
+    outs = []
+    for corrupt in (None, n + 100000, -1):
+        mws, n_out = sc._build_map(nb.neighbors_index, kidx, None, nb.neighbors_row_splits, n, K, False, None,
+                                   False, False, dev, st)
+        m = mws[:n_out * K * 4].view(torch.int32)
+        o = 11
+        k = int(torch.nonzero(m[o * K:(o + 1) * K] >= 0)[0])
+        if corrupt is not None:
+            m[o * K + k] = corrupt
+        out = torch.empty((n_out, 32), device=dev)
+        fws = workspace(lib.o3dml_sparse_conv_forward_workspace_size(n_out, n, K, 32, 32), dev)
+        _lib.call("o3dml_sparse_conv_forward", ptr(W), K, 32, 32, ptr(x), n, None, 0, 0, None, n_out, ptr(out),
+                  ptr(mws), mws.numel(), ptr(fws), fws.numel(), st)
+        outs.append(out)
+    assert torch.equal(outs[1], outs[2])  # past the operand == absent
+    assert not torch.equal(outs[0][11], outs[2][11]) and torch.equal(outs[0][12:], outs[2][12:])

@@ -130,3 +130,86 @@ def test_three_interpolate_autograd(cuda):
     (gf,) = torch.autograd.grad(out, (feats,), go)
     ref = ops.three_interpolate_grad(go, idx, w, 50)
     assert torch.allclose(gf, ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_registered_sparse_conv_backward_duplicate_kernel_indices(cuda):
+    """Off-lattice positions (several neighbours of one output share a kernel
+    index): the registered op's backward splits the pairs like the forward
+    (sparse_conv._layered_grads) and equals sc.sparse_conv's gradients."""
+    from o3dml_amd import layers, sparse_conv as sc
+    rng = np.random.default_rng(5)
+    pos = torch.from_numpy((rng.random((900, 3)) * 10).astype(np.float32)).to(cuda)
+    conv = layers.SparseConv(8, 16, [3, 3, 3], use_bias=False).to(cuda)
+    conv.lattice_rulebook = False
+    nb, kidx = conv._rulebook(pos, pos, 1.0, None, False, 1.0)
+    rs = nb.neighbors_row_splits.cpu()
+    o = torch.repeat_interleave(torch.arange(rs.shape[0] - 1), rs[1:] - rs[:-1])
+    assert torch.unique(o * 27 + kidx.long().cpu()).numel() < kidx.numel()  # duplicates present
+    for normalize in (False, True):
+        x = torch.randn((pos.shape[0], 8), device=cuda, requires_grad=True)
+        w = conv.kernel.detach().clone().requires_grad_(True)
+        out = torch.ops.open3d.sparse_conv(w, x, None, nb.neighbors_index, kidx, None, nb.neighbors_row_splits,
+                                           normalize)
+        go = torch.randn_like(out)
+        gw, gx = torch.autograd.grad(out, (w, x), go)
+        x2 = x.detach().clone().requires_grad_(True)
+        w2 = w.detach().clone().requires_grad_(True)
+        out2 = sc.sparse_conv(w2, x2, None, nb.neighbors_index, kidx, None, nb.neighbors_row_splits, normalize)
+        gw2, gx2 = torch.autograd.grad(out2, (w2, x2), go)
+        assert torch.equal(out, out2)
+        assert torch.allclose(gw, gw2, rtol=1e-5, atol=1e-5) and torch.allclose(gx, gx2, rtol=1e-5, atol=1e-5)
+        outT = torch.ops.open3d.sparse_conv_transpose(w, None, x, nb.neighbors_index, None, nb.neighbors_row_splits,
+                                                      nb.neighbors_index, kidx, None, nb.neighbors_row_splits)
+        gwT, gxT = torch.autograd.grad(outT, (w, x), go)
+        assert torch.isfinite(gwT).all() and torch.isfinite(gxT).all()
+
+
+@pytest.mark.gpu
+def test_transpose_importance_sum_needs_pair_importance(cuda):
+    """sparse_conv_transpose(normalize=True) divides by the importance sum only
+    when per-pair importances are given (Open3D's NEIGHBOR_IMPORTANCE †);
+    without them by the neighbour count, whatever sum is passed (float64
+    restatement)."""
+    from o3dml_amd import layers, sparse_conv as sc
+    g = torch.Generator().manual_seed(3)
+    pos = torch.unique(torch.randint(0, 10, (500, 3), generator=g), dim=0).float().add(0.5).to(cuda)
+    conv = layers.SparseConv(4, 6, [3, 3, 3], use_bias=False).to(cuda)
+    conv.lattice_rulebook = False
+    nb, kidx = conv._rulebook(pos, pos, 1.0, None, False, 1.0)
+    n = pos.shape[0]
+    x = torch.randn((n, 4), device=cuda)
+    W = conv.kernel.detach()
+    idx = nb.neighbors_index.long().cpu()
+    rs = nb.neighbors_row_splits.cpu()
+    o = torch.repeat_interleave(torch.arange(n), rs[1:] - rs[:-1])
+    bogus_sum = torch.full((n,), 7.0, device=cuda)
+    pair_imp = torch.rand(idx.numel(), device=cuda) + 0.5
+    inp_sum = torch.zeros(n, dtype=torch.float64).index_add_(0, idx, pair_imp.double().cpu())
+    cnt = torch.bincount(idx, minlength=n).double()
+    W64 = W.double().cpu().reshape(27, 4, 6)
+    x64 = x.double().cpu()
+    for imp, den in ((None, cnt), (pair_imp, inp_sum)):
+        s = bogus_sum if imp is None else inp_sum.float().to(cuda)
+        out = sc.sparse_conv_transpose(W, None, x, idx.to(cuda).int(), s, rs, nb.neighbors_index, kidx, imp,
+                                       nb.neighbors_row_splits, normalize=True)
+        contrib = torch.einsum("pc,pcd->pd", x64[idx] / den[idx][:, None], W64[kidx.long().cpu()])
+        if imp is not None:
+            contrib = contrib * imp.double().cpu()[:, None]
+        ref = torch.zeros((n, 6), dtype=torch.float64).index_add_(0, o, contrib)
+        err = (out.double().cpu() - ref).abs().max() / ref.abs().max()
+        assert err <= 1e-4, err
+
+
+@pytest.mark.gpu
+def test_ops_leave_current_device_unchanged(cuda):
+    """An op on tensors of another GPU runs there under a restoring guard: the
+    caller's current device is the same afterwards (needs 2 GPUs)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two visible GPUs")
+    from o3dml_amd import ops
+    torch.cuda.set_device(0)
+    pts = torch.rand((2000, 3), device="cuda:1")
+    res = ops.fixed_radius_search(pts, pts, 0.1)
+    assert res.neighbors_index.device == pts.device
+    assert torch.cuda.current_device() == 0
