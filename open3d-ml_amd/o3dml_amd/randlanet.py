@@ -449,9 +449,14 @@ class _PatchStep:
     between patches, so it is captured once as a HIP graph and replayed per
     patch (SemSegInference.run).  The cloud lives in a buffer of ``cap``
     points (sub-sampled cloud + far padding with possibility +inf: never a
-    centre, never in a crop), so clouds of similar size reuse the graph."""
+    centre, never in a crop), so clouds of similar size reuse the graph.
 
-    def __init__(self, inf, cap):
+    replay (tests): the shuffle takes a positional permutation from the
+    device buffer ``perm`` (idxs = crop[perm], refreshed by the host before
+    each replay) instead of the keyed bijection, so a recorded reference run
+    can be replayed through this exact (captured) path."""
+
+    def __init__(self, inf, cap, replay=False):
         model, dev = inf.model, inf.device
         cfg = model.cfg
         lib = _lib.load()
@@ -500,6 +505,7 @@ class _PatchStep:
         self.up = torch.empty(total, dtype=torch.int64, device=dev)
         self.up_ws = torch.empty(max(lib.o3dml_randla_up_workspace_size(total), 1), dtype=torch.uint8, device=dev)
         self.plan = (sizes, self.rs, self.srs)
+        self.perm = torch.empty(n_pts, dtype=torch.int64, device=dev) if replay else None
         self.graph = None
 
     def begin(self, sub, poss0, base_seed):
@@ -530,8 +536,12 @@ class _PatchStep:
         _lib.call("o3dml_knn_search_fill", ptr(self.sub), self.cap, ptr(self.center), 1, n_pts, 1,
                   ptr(self.crop_qrs_d), self.crop_prs.ctypes.data, self.crop_qrs.ctypes.data, l2, 0,
                   ptr(self.crop_rs), 64, ptr(self.crop), None, ptr(self.crop_ws), self.crop_ws.numel(), st)
-        # the shuffle (random.shuffle, semseg_spatially_regular.py:100): keyed bijection
-        _lib.call("o3dml_random_permute_dev", ptr(self.crop), n_pts, ptr(self.seeds), ptr(self.idxs), st)
+        # the shuffle (random.shuffle, semseg_spatially_regular.py:100): keyed
+        # bijection, or (replay) the injected positional permutation
+        if self.perm is not None:
+            torch.index_select(self.crop, 0, self.perm, out=self.idxs)
+        else:
+            _lib.call("o3dml_random_permute_dev", ptr(self.crop), n_pts, ptr(self.seeds), ptr(self.idxs), st)
         # pc = sub[idxs], possibilities += delta, x / y recentred
         _lib.call("o3dml_randla_patch_update", ptr(self.sub), ptr(self.idxs), n_pts, ptr(self.center), None,
                   ptr(self.poss), ptr(self.pc), ptr(self.patch_ws), self.patch_ws.numel(), st)
@@ -588,7 +598,11 @@ class SemSegInference:
     fancy-index assignment does.  ``run(points, patch_hook=f,
     init_possibility=p0)`` replays a recorded patch order: f(patch_number,
     centre_id) returns the patch's (already shuffled) indices in place of the
-    GPU kNN crop + shuffle (tests/test_gpu_pipeline.py)."""
+    GPU kNN crop + shuffle (tests/test_gpu_pipeline.py).  ``run(points,
+    perm_hook=g, init_possibility=p0)`` replays one through the timed path
+    itself (the captured whole-patch step): g(patch_number, centre_id)
+    returns the positional permutation of the GPU crop that gives the
+    recorded patch; the centres and each patch's indices land in ``stats``."""
 
     def __init__(self, model, device=None, seed=0, test_smooth=0.95, use_graph=None, probs_dtype=torch.float16):
         self.model = model
@@ -721,21 +735,21 @@ class SemSegInference:
         graph.replay()
         return out
 
-    def _patch_step(self, n_sub):
+    def _patch_step(self, n_sub, replay=False):
         """The patch-step state (and its graph) for a cloud of n_sub points,
-        kept on the model per (device, capacity, dtype, smooth)."""
+        kept on the model per (device, capacity, dtype, smooth, replay)."""
         cap = -(-n_sub // _CAP_STEP) * _CAP_STEP
-        key = (str(self.device), cap, self.probs_dtype, self.test_smooth)
+        key = (str(self.device), cap, self.probs_dtype, self.test_smooth, bool(replay))
         cur = self.model.__dict__.get("_o3dml_patch_step")
         if cur is None or cur[0] != key:
-            cur = (key, _PatchStep(self, cap))
+            cur = (key, _PatchStep(self, cap, replay))
             self.model.__dict__["_o3dml_patch_step"] = cur
         step = cur[1]
         step.inf = self
         return step
 
     @torch.no_grad()
-    def run(self, points, patch_hook=None, init_possibility=None):
+    def run(self, points, patch_hook=None, init_possibility=None, perm_hook=None):
         self.model.eval()
         points = points.to(self.device).float().contiguous()
         C = self.model.cfg["num_classes"]
@@ -747,18 +761,26 @@ class SemSegInference:
             possibility = torch.rand(n_sub, generator=self.gen, device=self.device, dtype=torch.float64) * 1e-3
         if patch_hook is None and n_sub >= self.model.cfg["num_points"]:
             # the whole patch as one replayed graph (or the same launches eagerly)
-            step = self._patch_step(n_sub)
+            step = self._patch_step(n_sub, replay=perm_hook is not None)
             step.begin(sub, possibility, int(self.rng.integers(0, 2**63)))
-            patches = 0
+            patches, centers, patch_idxs = 0, [], []
             ready = torch.cuda.Event()
             while True:
                 ready.record(torch.cuda.current_stream(self.device))
                 ready.synchronize()
                 if float(step.host_min[0]) > 0.5:
                     break
+                if perm_hook is not None:  # replay (tests): the recorded shuffle, the centre on the host
+                    cid = int(step.arg.item())
+                    centers.append(cid)
+                    step.perm.copy_(torch.as_tensor(np.asarray(perm_hook(patches, cid), np.int64)))
                 step.run_step(self.use_graph)
+                if perm_hook is not None:
+                    patch_idxs.append(step.idxs.clone())
                 patches += 1
-            self.stats = {"patches": patches, "sub_points": n_sub, "centers": []}
+            self.stats = {"patches": patches, "sub_points": n_sub, "centers": centers}
+            if perm_hook is not None:
+                self.stats["patch_idxs"] = patch_idxs
             probs = step.probs[:n_sub][proj]
             return probs.argmax(1), probs
         test_probs = torch.zeros((n_sub, C), dtype=self.probs_dtype, device=self.device)

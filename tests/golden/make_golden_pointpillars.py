@@ -11,7 +11,19 @@ outputs, and for one forward + get_loss + backward in eval mode (running
 batch-norm statistics: well conditioned, the reference in fp32 and fp64
 agree to <1e-6) and in training mode (batch statistics over 32 x 32 .. 8 x 8
 maps: fp32 and fp64 differ by up to 0.7% in the backbone gradients) the
-three losses and a few parameter gradients."""
+three losses and a few parameter gradients.
+
+`--full` writes tests/golden/pointpillars_full.npz instead: the reference
+config itself (ml3d/configs/pointpillars_kitti.yml model section: 432 x 496
+pillars over [0, 69.12] x [-39.68, 39.68], max_voxels 16000 / 40000) on the
+two KITTI-shaped scenes bench.py's C5 leg times on rank 0
+(bench.make_kitti_scene(1000), (1001)): scene 0's voxelization, eval-mode
+head outputs (float64 per-channel sums plus 4,096 sampled entries per
+output, the full maps are ~30 MB), and per mode the losses and GRAD_KEYS
+gradients.  The same forward / loss / backward is also run on the
+reference in float64 (model, points and the decorated pillars in double)
+and the fp32-vs-fp64 spread of every stored value is recorded, so the test
+tolerances are the reference's own precision at this size."""
 import os
 import sys
 import types
@@ -66,6 +78,102 @@ def scene(seed, n=3000, n_boxes=5):
     return pts[rng.permutation(len(pts))], np.array(boxes, np.float32), np.array(labels, np.int64)
 
 
+def full_cfg():
+    """The model section of the reference's pointpillars_kitti.yml (no augmentation)."""
+    import yaml
+    with open("/root/reference/ml3d/configs/pointpillars_kitti.yml") as f:
+        m = yaml.safe_load(f)["model"]
+    keep = ("point_cloud_range", "classes", "loss", "voxelize", "voxel_encoder", "scatter", "backbone", "neck",
+            "head")
+    return {k: m[k] for k in keep}
+
+
+SAMPLE = 4096  # sampled entries per head output in the full fixture
+
+
+def main_full():
+    import ref_loader
+    ref_loader.install()
+    sys.path.insert(0, ROOT)
+    import bench
+    from ml3d.torch.models.point_pillars import PointPillars
+
+    cfg = full_cfg()
+    scenes = [bench.make_kitti_scene(1000 + i) for i in range(2)]
+    torch.manual_seed(0)
+    model = PointPillars(device="cpu", augment={}, **cfg)
+    sd = model.state_dict()
+    model.load_state_dict(randla_weights.state_dict_for([(k, tuple(v.shape)) for k, v in sd.items()], sd))
+    sd0 = {k: v.clone() for k, v in model.state_dict().items()}
+    inputs = types.SimpleNamespace(point=[torch.from_numpy(s[0]) for s in scenes],
+                                   bboxes=[torch.from_numpy(s[1]) for s in scenes],
+                                   labels=[torch.from_numpy(s[2]) for s in scenes])
+    out = {}
+    for i, (p, b, l) in enumerate(scenes):
+        out[f"points_{i}"], out[f"bboxes_{i}"], out[f"labels_{i}"] = p, b, l
+    rng = np.random.default_rng(0)
+
+    def run(m, dtype):
+        """eval head outputs, then per mode losses + GRAD_KEYS grads, in dtype."""
+        res = {}
+        m.load_state_dict(sd0)  # the train-mode pass below moves the BN running statistics
+        m = m.to(dtype)
+        if dtype == torch.float64:  # decorated pillars in double too (the voxelizer's ids are exact)
+            enc = m.voxel_encoder
+            f32_fwd = enc.forward
+
+            def fwd(features, num_points, coors):
+                return f32_fwd(features.double(), num_points, coors)
+            enc.forward = fwd
+        m.eval()
+        with torch.no_grad():
+            heads = m(inputs)
+        for name, t in zip(("cls", "reg", "dir"), heads):
+            res[f"eval_{name}"] = t.double().numpy()
+        params = dict(m.named_parameters())
+        for mode in ("eval", "train"):
+            m.zero_grad()
+            m.train(mode == "train")
+            r = m(inputs)
+            losses = m.get_loss(r, inputs)
+            sum(losses.values()).backward()
+            for k, val in losses.items():
+                res[f"{mode}_{k}"] = float(val.item())
+            for k in GRAD_KEYS:
+                res[f"{mode}_grad_{k}"] = params[k].grad.double().numpy()
+        return res
+
+    m32 = run(model, torch.float32)
+    model.eval()
+    with torch.no_grad():
+        v, c, n = model.voxel_layer(inputs.point[0])
+    out["vox_coords_0"], out["vox_num_0"] = c.numpy(), n.numpy()
+    out["vox_sum_0"] = v.double().sum(dim=(1, 2)).numpy()
+    m64 = run(model, torch.float64)
+    spread = {}
+    for k, a in m32.items():
+        b = m64[k]
+        if k.startswith("eval_") and isinstance(a, np.ndarray) and a.ndim == 4:
+            flat = a.reshape(-1)
+            sel = rng.choice(flat.size, SAMPLE, replace=False)
+            out[f"{k}_shape"] = np.array(a.shape)
+            out[f"{k}_sel"] = sel.astype(np.int64)
+            out[f"{k}_val"] = flat[sel].astype(np.float32)
+            out[f"{k}_chsum"] = a.sum(axis=(0, 2, 3))
+            out[f"{k}_chabs"] = np.abs(a).sum(axis=(0, 2, 3))
+            spread[k] = float(np.abs(a - b).max() / (np.abs(b).max() + 1e-30))
+        elif isinstance(a, np.ndarray):
+            out[k] = a.astype(np.float32)
+            spread[k] = float(np.abs(a - b).max() / (np.abs(b).max() + 1e-30))
+        else:
+            out[k] = np.float64(a)
+            spread[k] = abs(a - b) / (abs(b) + 1e-30)
+    out["spread_keys"] = np.array(list(spread))
+    out["spread_vals"] = np.array([spread[k] for k in spread], np.float64)
+    print("voxels", v.shape, {k: f"{x:.2e}" for k, x in spread.items()})
+    np.savez_compressed(os.path.join(HERE, "pointpillars_full.npz"), **out)
+
+
 def main():
     import ref_loader
     ref_loader.install()
@@ -108,4 +216,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--full" in sys.argv[1:]:
+        main_full()
+    else:
+        main()

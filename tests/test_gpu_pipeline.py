@@ -94,3 +94,67 @@ def test_randla_pipeline_replays_reference(cuda):
         top2 = np.sort(got[diff].astype(np.float32), 1)[:, -2:]
         assert (top2[:, 1] - top2[:, 0] < 2e-3).all(), len(diff)
     assert len(diff) < 1e-3 * len(lab)
+
+
+@pytest.mark.parametrize("use_graph", [True, False])
+def test_randla_timed_path_replays_reference(cuda, use_graph):
+    """The path bench.py times — the whole patch as one captured HIP graph
+    (randlanet._PatchStep: GPU kNN crop, shuffle, float64 possibility update,
+    level kNN, up-sampling ids, network, float16 EMA, next centre by first
+    argmin) — replays the reference run: the shuffle takes an injected
+    positional permutation of the GPU crop (perm_hook) that reproduces the
+    reference's shuffled sklearn crop, which exists only if the GPU crop has
+    sklearn's set.  Centres, patch count, every patch (sha) and the final
+    float16 scores as in the hook-path test above; use_graph=False runs the
+    same launches eagerly."""
+    import bench
+    from sklearn.neighbors import KDTree
+
+    from o3dml_amd import ops
+    from o3dml_amd.randlanet import RandLANet, SemSegInference
+    k = int(P["num_points"])
+    scan, _ = bench.make_scan(int(P["scan_seed"]))
+    scan_t = torch.from_numpy(scan).to(cuda)
+    m = RandLANet(num_points=k, num_classes=19)
+    sd = m.state_dict()
+    m.load_state_dict(randla_weights.state_dict_for([(key, tuple(v.shape)) for key, v in sd.items()]))
+    m = m.to(cuda).eval()
+    inf = SemSegInference(m, seed=0, use_graph=use_graph)
+    sub_t, _ = inf.preprocess(scan_t)
+    sub = sub_t.cpu().numpy()
+    n_sub = int(P["n_sub"])
+    np.random.seed(int(P["np_seed"]))
+    p0 = np.random.rand(n_sub) * 1e-3
+    tree = KDTree(sub)
+    random.seed(int(P["py_seed"]))
+    centers = P["centers"].tolist()
+
+    def perm_hook(i, cid):
+        assert i < len(centers) and cid == centers[i], (i, cid)
+        ref = tree.query(sub[cid:cid + 1], k=k)[1][0]
+        random.shuffle(ref)  # the reference's patch
+        crop = ops.knn_search(sub_t, sub_t[cid:cid + 1].contiguous(), k).neighbors_index.long().cpu().numpy()
+        pos = np.full(n_sub, -1, np.int64)
+        pos[crop] = np.arange(k)
+        perm = pos[np.asarray(ref, np.int64)]
+        assert (perm >= 0).all(), "GPU crop set differs from sklearn's"
+        return perm
+
+    labels, probs = inf.run(scan_t, perm_hook=perm_hook, init_possibility=p0)
+    assert inf.stats["centers"] == centers
+    assert inf.stats["patches"] == len(centers)
+    for i, idxs in enumerate(inf.stats["patch_idxs"]):
+        assert sha(idxs.cpu().numpy().astype(np.int64)) == str(P["patch_sha"][i]), i
+    assert probs.dtype == torch.float16
+    got = probs.cpu().numpy()
+    rows = got[::7].astype(np.float32)
+    ref = P["score_rows"].astype(np.float32)
+    assert np.abs(rows - ref).max() <= 1e-3
+    assert (rows == ref).mean() >= 0.99
+    np.testing.assert_allclose(got.astype(np.float64).sum(0), P["score_colsum"], rtol=0, atol=2e-4 * len(got))
+    lab = labels.cpu().numpy()
+    diff = np.flatnonzero(lab != P["labels"].astype(np.int64))
+    if len(diff):
+        top2 = np.sort(got[diff].astype(np.float32), 1)[:, -2:]
+        assert (top2[:, 1] - top2[:, 0] < 2e-3).all(), len(diff)
+    assert len(diff) < 1e-3 * len(lab)
