@@ -153,7 +153,7 @@ def main_full():
     spread = {}
     for k, a in m32.items():
         b = m64[k]
-        if k.startswith("eval_") and isinstance(a, np.ndarray) and a.ndim == 4:
+        if k in ("eval_cls", "eval_reg", "eval_dir"):
             flat = a.reshape(-1)
             sel = rng.choice(flat.size, SAMPLE, replace=False)
             out[f"{k}_shape"] = np.array(a.shape)
