@@ -177,6 +177,16 @@ int o3dml_knn_search_fill(const float* points, int64_t n_points, const float* qu
                           const int64_t* queries_row_splits_host, int metric, int ignore_query_point,
                           const int64_t* neighbors_row_splits, int index_bits, void* neighbors_index,
                           float* neighbors_distance, void* workspace, size_t workspace_bytes, void* stream);
+/* The patch crop of the spatially-regular sampler (KDTree.query(center,
+ * k=num_points) then random.shuffle, ml3d/datasets/samplers/
+ * semseg_spatially_regular.py:94-100, randlanet.py:175-180): the SET of the
+ * k nearest points of `center` (device float[3]) among points[0, n) by
+ * (distance, index), written as int64 ids in INDEX order (the caller shuffles
+ * it; knn_search's distance order is not needed).  Radix selection in one
+ * workgroup, no host synchronisation (graph-capturable); k <= n_points. */
+size_t o3dml_knn_select_workspace_size(int64_t n_points);
+int o3dml_knn_select(const float* points, int64_t n_points, const float* center, int64_t k, int metric,
+                     int64_t* out_index, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- radius search: replaces open3d.ml.torch.ops.radius_search /
  * layers.RadiusSearch (Open3D ml ops API; SURVEY.md §2.2, no reference model

@@ -385,56 +385,6 @@ __global__ void __launch_bounds__(256) bigk_counts_ignore_kernel(const float* __
     }
 }
 
-// distance bits of every point of the query's batch item; with ignore, the
-// points at the query's position get the largest key (sorted past the row)
-template <int METRIC>
-__global__ void dist_keys_kernel(const float* __restrict__ pts, int64_t s, int64_t n, const float* __restrict__ q,
-                                 int ignore, uint32_t* __restrict__ keys) {
-    const float qx = q[0], qy = q[1], qz = q[2];
-    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < n;
-         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t i = s + j;
-        const float px = pts[3 * i], py = pts[3 * i + 1], pz = pts[3 * i + 2];
-        keys[j] = ignore && px == qx && py == qy && pz == qz
-                          ? 0xffffffffu
-                          : __float_as_uint(dist_metric<METRIC>(px, py, pz, qx, qy, qz));
-    }
-}
-
-// the first rs[q+1] - rs[q] sorted entries into the row at rs[q]
-__global__ void write_bigk_kernel(const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ sidx,
-                                  const int64_t* __restrict__ rs, int64_t q, int64_t base_id, int bits,
-                                  void* __restrict__ out_idx, float* __restrict__ out_dist) {
-    const int64_t out_off = rs[q], cnt = rs[q + 1] - out_off;
-    for (int64_t j = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; j < cnt;
-         j += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t id = base_id + sidx[j];
-        if (bits == 32)
-            static_cast<int32_t*>(out_idx)[out_off + j] = static_cast<int32_t>(id);
-        else
-            static_cast<int64_t*>(out_idx)[out_off + j] = id;
-        if (out_dist) out_dist[out_off + j] = __uint_as_float(skeys[j]);
-    }
-}
-
-// One query of the per-query path (host-side loop driver).
-static void bigk_one(const float* points, const float* queries, int64_t q, int64_t ps, int64_t pn, int64_t k,
-                     int metric, int ignore, const int64_t* rs, int bits, void* oi, float* od, uint32_t* keys,
-                     uint32_t* skeys, uint32_t* sidx, Workspace ws, hipStream_t st) {
-    if (pn == 0) return;
-    const unsigned g = stream_grid(pn, 256);
-    if (metric == kL2)
-        dist_keys_kernel<kL2><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, ignore, keys);
-    else if (metric == kL1)
-        dist_keys_kernel<kL1><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, ignore, keys);
-    else
-        dist_keys_kernel<kLinf><<<g, 256, 0, st>>>(points, ps, pn, queries + 3 * q, ignore, keys);
-    O3DML_LAUNCH_CHECK();
-    prim::radix_sort_pairs<uint32_t>(keys, nullptr, skeys, sidx, pn, 32, ws, st);
-    write_bigk_kernel<<<stream_grid(std::min(k, pn), 256), 256, 0, st>>>(skeys, sidx, rs, q, ps, bits, oi, od);
-    O3DML_LAUNCH_CHECK();
-}
-
 // nns_many.hip: batched 64 < k <= kManyKnnMaxK
 constexpr int64_t kManyKnnMaxK = 2048;
 size_t knn_many_workspace_bytes(int64_t n, int64_t m, int64_t k, int64_t nb);
@@ -442,7 +392,12 @@ void knn_many_count(const float* pts, int64_t n, const float* queries, int64_t m
                     const int64_t* prs, const int64_t* qrs, int ignore, int64_t* rs, Workspace ws, hipStream_t st);
 void knn_many_fill(const float* pts, int64_t n, const float* queries, int64_t m, int64_t k, int nb,
                    const int64_t* qrs, int metric, int ignore, const int64_t* rs, int bits, void* oi, float* od,
-                   Workspace ws, hipStream_t st, uint32_t** over, int64_t** n_over);
+                   Workspace ws, hipStream_t st);
+// nns_topk.hip: k > kManyKnnMaxK, one query by radix selection + a sort of the k selected
+size_t topk_bigk_workspace_bytes(int64_t n_points, int64_t k);
+void topk_bigk_one(const float* pts, int64_t ps, int64_t pn, const float* queries, int64_t q, int64_t k,
+                   int metric, int ignore, const int64_t* rs, int bits, void* oi, float* od, Workspace ws,
+                   hipStream_t st);
 
 }  // namespace o3dml
 
@@ -471,9 +426,9 @@ static double knn_min_target() {
 
 O3DML_API size_t o3dml_knn_search_workspace_size(int64_t n_points, int64_t n_queries, int64_t k, int64_t n_batch) {
     if (knn_bucket(k) == 0) {
-        const size_t one = 3 * ws_bytes<uint32_t>(n_points) + prim::radix_sort_workspace_bytes<uint32_t>(n_points);
-        if (k <= kManyKnnMaxK) return knn_many_workspace_bytes(n_points, n_queries, k, n_batch) + one;
-        return std::max(one, ws_bytes<int64_t>(n_queries) + prim::scan_workspace_bytes(n_queries));
+        if (k <= kManyKnnMaxK) return knn_many_workspace_bytes(n_points, n_queries, k, n_batch);
+        return std::max(topk_bigk_workspace_bytes(n_points, k),
+                        ws_bytes<int64_t>(n_queries) + prim::scan_workspace_bytes(n_queries));
     }
     return grid_workspace_bytes(n_points, static_cast<int>(n_batch), kKnnCapFactor) +
            3 * ws_bytes<uint32_t>(n_queries) + prim::radix_sort_workspace_bytes<uint32_t>(n_queries) +
@@ -573,39 +528,20 @@ O3DML_API int o3dml_knn_search_fill(const float* points, int64_t n_points, const
     const int K = knn_bucket(k);
     if (n_queries == 0) return 0;
     if (K == 0) {
-        const bool many = k <= kManyKnnMaxK;
-        std::vector<uint32_t> qlist;
-        if (many) {  // batched; queries whose candidates overflow the LDS list come back listed
-            uint32_t* over = nullptr;
-            int64_t* n_over = nullptr;
+        if (k <= kManyKnnMaxK) {  // batched; overflowing queries by radix selection on the device
             knn_many_fill(points, n_points, queries, n_queries, k, nb, queries_row_splits, metric,
                           ignore_query_point, neighbors_row_splits, index_bits, neighbors_index, neighbors_distance,
-                          ws, st, &over, &n_over);
-            int64_t nov = 0;
-            O3DML_CHECK_HIP(hipMemcpyAsync(&nov, n_over, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-            O3DML_CHECK_HIP(hipStreamSynchronize(st));
-            if (nov > 0) {
-                qlist.resize(static_cast<size_t>(nov));
-                O3DML_CHECK_HIP(hipMemcpyAsync(qlist.data(), over, sizeof(uint32_t) * nov, hipMemcpyDeviceToHost, st));
-                O3DML_CHECK_HIP(hipStreamSynchronize(st));
-                std::sort(qlist.begin(), qlist.end());
-            }
-            ws.take<uint8_t>(static_cast<int64_t>(knn_many_workspace_bytes(n_points, n_queries, k, n_batch)));
+                          ws, st);
+            return 0;
         }
-        uint32_t* keys = ws.take<uint32_t>(n_points);
-        uint32_t* skeys = ws.take<uint32_t>(n_points);
-        uint32_t* sidx = ws.take<uint32_t>(n_points);
-        auto run = [&](int64_t q) {
-            int b = 0;
+        // k > 2048: per query a radix selection + a sort of the k selected,
+        // queued without any host synchronisation
+        int b = 0;
+        for (int64_t q = 0; q < n_queries; ++q) {
             while (b + 1 < nb && queries_row_splits_host[b + 1] <= q) ++b;
             const int64_t ps = points_row_splits_host[b], pn = points_row_splits_host[b + 1] - ps;
-            bigk_one(points, queries, q, ps, pn, k, metric, ignore_query_point, neighbors_row_splits, index_bits,
-                     neighbors_index, neighbors_distance, keys, skeys, sidx, ws, st);
-        };
-        if (many) {
-            for (uint32_t q : qlist) run(q);
-        } else {
-            for (int64_t q = 0; q < n_queries; ++q) run(q);
+            topk_bigk_one(points, ps, pn, queries, q, k, metric, ignore_query_point, neighbors_row_splits,
+                          index_bits, neighbors_index, neighbors_distance, ws, st);
         }
         return 0;
     }

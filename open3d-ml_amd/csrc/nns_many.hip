@@ -428,8 +428,8 @@ static size_t radius_plan_bytes(int64_t n, int64_t m, int64_t nb) {
 
 // ---- batched kNN, 64 < k <= 2048 (kManyKnnMaxK, called from nns_knn.hip) ----
 size_t knn_many_workspace_bytes(int64_t n, int64_t m, int64_t k, int64_t nb) {
-    return ws_bytes<int64_t>(4) + ws_bytes<uint32_t>(m) + ws_bytes<int64_t>(m) + prim::scan_workspace_bytes(m) +
-           grid_workspace_bytes(n, static_cast<int>(nb), kManyCapFactor);
+    return ws_bytes<int64_t>(4) + ws_bytes<uint32_t>(m) + ws_bytes<int64_t>(m) + ws_bytes<int64_t>(nb + 1) +
+           prim::scan_workspace_bytes(m) + grid_workspace_bytes(n, static_cast<int>(nb), kManyCapFactor);
 }
 
 static double knn_many_target(int64_t k) { return std::max(2.0, static_cast<double>(k) / 8.0); }
@@ -438,6 +438,7 @@ struct KnnManyPlan {
     int64_t* scalars;  // [0] overflow count
     uint32_t* over;    // [M]
     int64_t* counts;   // [M]
+    int64_t* prs;      // [B + 1] device copy of the point row splits (the overflow path of the fill)
     GridIndex gi;
 };
 
@@ -447,6 +448,7 @@ static KnnManyPlan take_knn_many(Workspace& ws, const float* pts, int64_t n, int
     p.scalars = ws.take<int64_t>(4);
     p.over = ws.take<uint32_t>(m);
     p.counts = ws.take<int64_t>(m);
+    p.prs = ws.take<int64_t>(nb + 1);
     if (build) {
         p.gi = build_grid(pts, n, prs, nb, knn_many_target(k), kManyCapFactor, ws, st);
     } else {
@@ -464,6 +466,7 @@ void knn_many_count(const float* pts, int64_t n, const float* queries, int64_t m
     KnnManyPlan p = take_knn_many(ws, pts, n, m, k, prs, nb, st, true);
     O3DML_CHECK_HIP(hipMemsetAsync(p.scalars, 0, 4 * sizeof(int64_t), st));
     O3DML_CHECK_HIP(hipMemsetAsync(rs, 0, sizeof(int64_t), st));
+    O3DML_CHECK_HIP(hipMemcpyAsync(p.prs, prs, sizeof(int64_t) * (nb + 1), hipMemcpyDeviceToDevice, st));
     if (m == 0) return;
     many_knn_counts_kernel<<<stream_grid(m, 256), 256, 0, st>>>(p.gi.sorted, p.gi.splits, p.gi.params, queries, m,
                                                                prs, qrs, nb, k, ignore, p.counts);
@@ -471,14 +474,17 @@ void knn_many_count(const float* pts, int64_t n, const float* queries, int64_t m
     prim::scan<int64_t, int64_t>(p.counts, rs + 1, m, true, ws, st);
 }
 
-// Fills the rows; returns the device pointers of the overflow list (queries
-// for the per-query path) and its count.
+void topk_overflow(const float* pts, const float* queries, const int64_t* prs, const int64_t* qrs, int nb,
+                   int metric, int ignore, const uint32_t* over, const int64_t* n_over, const int64_t* rs, int bits,
+                   void* oi, float* od, int64_t max_over, hipStream_t st);
+
+// Fills the rows; the queries whose candidates overflow the LDS list are
+// listed on the device and done by nns_topk.hip's radix selection over their
+// whole batch item, queued right behind (no host read of the count).
 void knn_many_fill(const float* pts, int64_t n, const float* queries, int64_t m, int64_t k, int nb,
                    const int64_t* qrs, int metric, int ignore, const int64_t* rs, int bits, void* oi, float* od,
-                   Workspace ws, hipStream_t st, uint32_t** over, int64_t** n_over) {
+                   Workspace ws, hipStream_t st) {
     KnnManyPlan p = take_knn_many(ws, pts, n, m, k, nullptr, nb, st, false);
-    *over = p.over;
-    *n_over = p.scalars;
     if (m == 0) return;
     const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(m, 1 << 20)));
 #define O3DML_KM(M, I)                                                                                        \
@@ -494,6 +500,7 @@ void knn_many_fill(const float* pts, int64_t n, const float* queries, int64_t m,
     }
 #undef O3DML_KM
     O3DML_LAUNCH_CHECK();
+    topk_overflow(pts, queries, p.prs, qrs, nb, metric, ignore, p.over, p.scalars, rs, bits, oi, od, m, st);
 }
 
 }  // namespace o3dml

@@ -58,6 +58,8 @@ SIGNATURES = {
                                        c_i32, c_p, c_p, c_sz, c_p]),
     "o3dml_knn_search_fill": (c_i32, [c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i32, c_i32, c_p,
                                       c_i32, c_p, c_p, c_p, c_sz, c_p]),
+    "o3dml_knn_select_workspace_size": (c_sz, [c_i64]),
+    "o3dml_knn_select": (c_i32, [c_p, c_i64, c_p, c_i64, c_i32, c_p, c_p, c_sz, c_p]),
     # nns_many.hip
     "o3dml_radius_search_workspace_size": (c_sz, [c_i64, c_i64, c_i64]),
     "o3dml_radius_search_count": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i32, c_i32, c_p, c_p,

@@ -451,6 +451,9 @@ class _PatchStep:
     points (sub-sampled cloud + far padding with possibility +inf: never a
     centre, never in a crop), so clouds of similar size reuse the graph.
 
+    The crop is the SET of the num_points nearest points in index order
+    (o3dml_knn_select: radix selection, no sort — it is shuffled next).
+
     replay (tests): the shuffle takes a positional permutation from the
     device buffer ``perm`` (idxs = crop[perm], refreshed by the host before
     each replay) instead of the keyed bijection, so a recorded reference run
@@ -473,13 +476,7 @@ class _PatchStep:
         self.min_ws = torch.empty(max(lib.o3dml_randla_possibility_min_workspace_size(), 1), dtype=torch.uint8,
                                   device=dev)
         # crop: one query (the centre) against the padded cloud
-        self.crop_prs = np.array([0, cap], np.int64)
-        self.crop_qrs = np.array([0, 1], np.int64)
-        self.crop_prs_d = torch.from_numpy(self.crop_prs).to(dev)
-        self.crop_qrs_d = torch.from_numpy(self.crop_qrs).to(dev)
-        self.crop_rs = torch.empty(2, dtype=torch.int64, device=dev)
-        self.crop_ws = torch.empty(max(lib.o3dml_knn_search_workspace_size(cap, 1, n_pts, 1), 1),
-                                   dtype=torch.uint8, device=dev)
+        self.crop_ws = torch.empty(max(lib.o3dml_knn_select_workspace_size(cap), 1), dtype=torch.uint8, device=dev)
         self.crop = torch.empty(n_pts, dtype=torch.int64, device=dev)
         self.idxs = torch.empty(n_pts, dtype=torch.int64, device=dev)
         self.pc = torch.empty((n_pts, 3), dtype=torch.float32, device=dev)
@@ -528,14 +525,11 @@ class _PatchStep:
         """The launches of one patch (graph-capturable)."""
         inf, st, n_pts = self.inf, stream_handle(self.dev), self.n_pts
         k, L = self.k, len(self.nxt)
-        # crop: the num_points nearest sub-points of the centre, (distance, index) order
+        # crop: the SET of the num_points nearest sub-points of the centre, in
+        # index order (radix selection, nns_topk.hip; shuffled next)
         l2 = metric_code("L2")
-        _lib.call("o3dml_knn_search_count", ptr(self.sub), self.cap, ptr(self.center), 1, n_pts, 1,
-                  ptr(self.crop_prs_d), ptr(self.crop_qrs_d), self.crop_prs.ctypes.data, self.crop_qrs.ctypes.data,
-                  l2, 0, 0, ptr(self.crop_rs), ptr(self.crop_ws), self.crop_ws.numel(), st)
-        _lib.call("o3dml_knn_search_fill", ptr(self.sub), self.cap, ptr(self.center), 1, n_pts, 1,
-                  ptr(self.crop_qrs_d), self.crop_prs.ctypes.data, self.crop_qrs.ctypes.data, l2, 0,
-                  ptr(self.crop_rs), 64, ptr(self.crop), None, ptr(self.crop_ws), self.crop_ws.numel(), st)
+        _lib.call("o3dml_knn_select", ptr(self.sub), self.cap, ptr(self.center), n_pts, l2, ptr(self.crop),
+                  ptr(self.crop_ws), self.crop_ws.numel(), st)
         # the shuffle (random.shuffle, semseg_spatially_regular.py:100): keyed
         # bijection, or (replay) the injected positional permutation
         if self.perm is not None:
@@ -601,8 +595,9 @@ class SemSegInference:
     GPU kNN crop + shuffle (tests/test_gpu_pipeline.py).  ``run(points,
     perm_hook=g, init_possibility=p0)`` replays one through the timed path
     itself (the captured whole-patch step): g(patch_number, centre_id)
-    returns the positional permutation of the GPU crop that gives the
-    recorded patch; the centres and each patch's indices land in ``stats``."""
+    returns the positional permutation of the GPU crop (the crop set in
+    index order) that gives the recorded patch; the centres and each patch's
+    indices land in ``stats``."""
 
     def __init__(self, model, device=None, seed=0, test_smooth=0.95, use_graph=None, probs_dtype=torch.float16):
         self.model = model

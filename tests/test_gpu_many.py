@@ -131,3 +131,84 @@ def test_knn_large_k_ignore_query_point(cuda, k, metric):
     res = ops.knn_search(torch.from_numpy(pts).to(cuda), torch.from_numpy(qry).to(cuda), k, metric=metric,
                          ignore_query_point=True, return_distances=True)
     _check(res, O.knn_search(pts, qry, k, metric=metric, ignore_query_point=True, return_distances=True))
+
+
+# ------------------------------------------------------------------ radix selection (nns_topk.hip)
+@pytest.mark.parametrize("mode", ["straddle", "whole_item"])
+def test_knn_huge_k_ties_at_the_boundary(cuda, mode):
+    """k > 2048 (radix selection + a sort of the k selected): 500 copies of
+    one point make 500 keys equal; k is chosen so that the k-th neighbour
+    falls inside that block (the selection must take the lowest indices among
+    the ties), or exceeds batch item 0 (whole item); two queries in two
+    batch items, int64 ids, distances."""
+    from o3dml_amd import ops
+    pts = _cloud(60000, 21, 4.0)
+    pts[30000:30500] = pts[7]  # 500 copies of one point
+    qry = np.stack([pts[7] + np.float32(0.9), pts[40000]])
+    prs = np.array([0, 45000, 60000], np.int64)
+    qrs = np.array([0, 1, 2], np.int64)
+    oi, _, od = O.knn_search(pts[:45000], qry[:1], 45000, return_distances=True)
+    first = int(np.flatnonzero(oi == 7)[0])
+    k = first + 250 if mode == "straddle" else 45056
+    assert k > 2048 and (mode != "straddle" or od[first + 250] == od[first])
+    res = ops.knn_search(torch.from_numpy(pts).to(cuda), torch.from_numpy(qry).to(cuda), k, torch.from_numpy(prs),
+                         torch.from_numpy(qrs), return_distances=True, index_dtype=torch.int64)
+    _check(res, O.knn_search(pts, qry, k, prs, qrs, return_distances=True, index_dtype=np.int64))
+
+
+def test_knn_select_set_index_order(cuda):
+    """o3dml_knn_select (the captured RandLA crop): the k-nearest SET of the
+    oracle's kNN in index order, with a block of duplicates at the k-th
+    distance (lowest indices taken) and the whole cloud (k = n)."""
+    from o3dml_amd import _lib
+    from o3dml_amd._util import ptr, stream_handle
+    lib = _lib.load()
+    pts = _cloud(70000, 23, 10.0)
+    pts[100:400] = pts[5000]
+    c = pts[5000] + np.float32(0.37)
+    t = torch.from_numpy(pts).to(cuda)
+    ct = torch.from_numpy(c).to(cuda)
+    oi, _, od = O.knn_search(pts, c[None], 70000, return_distances=True)
+    pos = np.flatnonzero(od == od[oi == 100][0])  # the duplicates' distance in the oracle's order
+    for k in (int(pos[len(pos) // 2]) + 1, 45056, 70000):
+        out = torch.empty(k, dtype=torch.int64, device=cuda)
+        ws = torch.empty(lib.o3dml_knn_select_workspace_size(70000), dtype=torch.uint8, device=cuda)
+        _lib.call("o3dml_knn_select", ptr(t), 70000, ptr(ct), k, 1, ptr(out), ptr(ws), ws.numel(), stream_handle(cuda))
+        assert np.array_equal(out.cpu().numpy(), np.sort(oi[:k])), k
+
+
+def test_knn_many_path_is_capturable(cuda):
+    """64 < k <= 2048 count + fill (incl. the overflow queries' radix
+    selection) inside a HIP graph capture, replayed: no host synchronisation
+    in the library; the replay equals the oracle."""
+    import bench
+    from o3dml_amd import _lib
+    from o3dml_amd._util import ptr
+    lib = _lib.load()
+    scan, _ = bench.make_scan(5)
+    pts = np.ascontiguousarray(scan[:30000])
+    qry = np.ascontiguousarray(scan[:400])  # dense ground: candidate lists overflow -> radix selection
+    k = 1500
+    prs = np.array([0, 30000], np.int64)
+    qrs = np.array([0, 400], np.int64)
+    pt, qt = torch.from_numpy(pts).to(cuda), torch.from_numpy(qry).to(cuda)
+    prs_d, qrs_d = torch.from_numpy(prs).to(cuda), torch.from_numpy(qrs).to(cuda)
+    rs = torch.empty(401, dtype=torch.int64, device=cuda)
+    idx = torch.empty(400 * k, dtype=torch.int32, device=cuda)
+    dist = torch.empty(400 * k, dtype=torch.float32, device=cuda)
+    ws = torch.empty(lib.o3dml_knn_search_workspace_size(30000, 400, k, 1), dtype=torch.uint8, device=cuda)
+    side = torch.cuda.Stream(cuda)
+    side.wait_stream(torch.cuda.current_stream(cuda))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        st = side.cuda_stream
+        _lib.call("o3dml_knn_search_count", ptr(pt), 30000, ptr(qt), 400, k, 1, ptr(prs_d), ptr(qrs_d),
+                  prs.ctypes.data, qrs.ctypes.data, 1, 0, 0, ptr(rs), ptr(ws), ws.numel(), st)
+        _lib.call("o3dml_knn_search_fill", ptr(pt), 30000, ptr(qt), 400, k, 1, ptr(qrs_d), prs.ctypes.data,
+                  qrs.ctypes.data, 1, 0, ptr(rs), 32, ptr(idx), ptr(dist), ptr(ws), ws.numel(), st)
+    g.replay()
+    torch.cuda.synchronize(cuda)
+    assert int(ws[:8].view(torch.int64)[0]) > 0  # some queries took the overflow path
+    oi, ors, od = O.knn_search(pts, qry, k, prs, qrs, return_distances=True)
+    assert np.array_equal(rs.cpu().numpy(), ors)
+    assert np.array_equal(idx.cpu().numpy(), oi) and np.array_equal(dist.cpu().numpy(), od)

@@ -104,7 +104,9 @@ def test_randla_timed_path_replays_reference(cuda, use_graph):
     argmin) — replays the reference run: the shuffle takes an injected
     positional permutation of the GPU crop (perm_hook) that reproduces the
     reference's shuffled sklearn crop, which exists only if the GPU crop has
-    sklearn's set.  Centres, patch count, every patch (sha) and the final
+    sklearn's set (and the step's own crop — radix selection, index order —
+    must be that set, or the patch hashes differ).  Centres, patch count,
+    every patch (sha) and the final
     float16 scores as in the hook-path test above; use_graph=False runs the
     same launches eagerly."""
     import bench
@@ -133,7 +135,9 @@ def test_randla_timed_path_replays_reference(cuda, use_graph):
         assert i < len(centers) and cid == centers[i], (i, cid)
         ref = tree.query(sub[cid:cid + 1], k=k)[1][0]
         random.shuffle(ref)  # the reference's patch
-        crop = ops.knn_search(sub_t, sub_t[cid:cid + 1].contiguous(), k).neighbors_index.long().cpu().numpy()
+        # the step's crop: the GPU k-nearest set in index order; the GPU kNN
+        # of the same centre must have sklearn's set
+        crop = np.sort(ops.knn_search(sub_t, sub_t[cid:cid + 1].contiguous(), k).neighbors_index.long().cpu().numpy())
         pos = np.full(n_sub, -1, np.int64)
         pos[crop] = np.arange(k)
         perm = pos[np.asarray(ref, np.int64)]
