@@ -242,8 +242,9 @@ def test_dense_fused_split_reduce_bitwise(cuda):
 def test_patch_step_equals_ops(cuda):
     """The capturable patch step (SemSegInference._patch_step, direct ABI
     calls over padded static buffers) produces exactly what the op-level
-    pipeline would: the crop = ops.knn_search(sub, centre, num_points) (L2,
-    (distance, index) order), the shuffled indices a permutation of it, the
+    pipeline would: the crop = the set of ops.knn_search(sub, centre,
+    num_points) (L2) in index order (radix selection, o3dml_knn_select), the
+    shuffled indices a permutation of it, the
     per-level k-lists = ops.knn_search on the levels, the up-sampling ids =
     a second 1-NN search, and the possibility update of the crop."""
     from o3dml_amd import ops
@@ -264,7 +265,7 @@ def test_patch_step_equals_ops(cuda):
     with torch.no_grad():
         step.step()
     crop = ops.knn_search(sub, center.view(1, 3), 4096, index_dtype=torch.int64).neighbors_index
-    assert torch.equal(step.crop, crop)
+    assert torch.equal(step.crop, torch.sort(crop).values)
     assert torch.equal(torch.sort(step.idxs).values, torch.sort(crop).values)
     sizes, rs, _ = step.plan
     cat = step.cat
