@@ -108,6 +108,13 @@ __constant__ constexpr LaneSplitTab kLaneSplitTab{};
 #ifndef O3DML_STREAM_U
 #define O3DML_STREAM_U 2
 #endif
+#ifndef O3DML_FRS_DMA
+#define O3DML_FRS_DMA 0  // stream rounds by LDS DMA into the candidate list (A/B switch)
+#endif
+typedef __attribute__((address_space(3))) void* frs_lds_ptr;
+#ifndef O3DML_FRS_OOBST
+#define O3DML_FRS_OOBST 0  // branch-free temp-row stores (A/B switch)
+#endif
 constexpr int kStreamU = O3DML_STREAM_U;  // 64-point loads in flight per lane while streaming buckets
 // LDS candidate list per wave (float4), incl. the padding of the last slice:
 // 4 KiB + 1 KiB of query slots keeps 32 waves per CU (LDS no tighter than the
@@ -116,30 +123,64 @@ constexpr int kCandCap = 256;
 
 // Wave-wide float min / max: DPP within rows of 16 lanes, then the 4 row
 // results through v_readlane (uniform result, no LDS round trip).
+// O3DML_FRS_DPPMIN (default): each step is ONE v_min_f32_dpp / v_max_f32_dpp
+// (the DPP source folded into the VOP2 min/max); fminf through a
+// v_mov_b32_dpp costs that mov plus two canonicalising v_max_f32 (fminf's
+// signalling-NaN rule) per step — 5 instructions instead of 1.  The s_nop
+// covers the VALU-write -> DPP-read hazard inside the asm block.
+#ifndef O3DML_FRS_DPPMIN
+#define O3DML_FRS_DPPMIN 1
+#endif
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
+#define O3DML_DPP_STEP(NAME, OP, CTRL)                                                                   \
+    __device__ __forceinline__ float NAME(float v) {                                                    \
+        float r;                                                                                        \
+        asm volatile("s_nop 1\n\t" OP "_dpp %0, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf"            \
+                     : "=v"(r)                                                                          \
+                     : "v"(v));                                                                         \
+        return r;                                                                                       \
+    }
+O3DML_DPP_STEP(dmin_q1, "v_min_f32", "quad_perm:[1,0,3,2]")
+O3DML_DPP_STEP(dmin_q2, "v_min_f32", "quad_perm:[2,3,0,1]")
+O3DML_DPP_STEP(dmin_hm, "v_min_f32", "row_half_mirror")
+O3DML_DPP_STEP(dmin_rm, "v_min_f32", "row_mirror")
+O3DML_DPP_STEP(dmax_q1, "v_max_f32", "quad_perm:[1,0,3,2]")
+O3DML_DPP_STEP(dmax_q2, "v_max_f32", "quad_perm:[2,3,0,1]")
+O3DML_DPP_STEP(dmax_hm, "v_max_f32", "row_half_mirror")
+O3DML_DPP_STEP(dmax_rm, "v_max_f32", "row_mirror")
+#undef O3DML_DPP_STEP
+// min (MAX: max) over each row of 16 lanes, in every lane of the row
+template <bool MAX>
+__device__ __forceinline__ float row_ext_f(float v) {
+#if O3DML_FRS_DPPMIN
+    if constexpr (MAX) return dmax_rm(dmax_hm(dmax_q2(dmax_q1(v))));
+    return dmin_rm(dmin_hm(dmin_q2(dmin_q1(v))));
+#else
+    auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : fminf(a, b); };
+    v = op(v, dpp_f<0xB1>(v));   // quad_perm(1,0,3,2)
+    v = op(v, dpp_f<0x4E>(v));   // quad_perm(2,3,0,1)
+    v = op(v, dpp_f<0x141>(v));  // row_half_mirror
+    v = op(v, dpp_f<0x140>(v));  // row_mirror
+    return v;
+#endif
+}
+__device__ __forceinline__ float rdlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 __device__ __forceinline__ float wave_min_f(float v) {
-    v = fminf(v, dpp_f<0xB1>(v));   // quad_perm(1,0,3,2)
-    v = fminf(v, dpp_f<0x4E>(v));   // quad_perm(2,3,0,1)
-    v = fminf(v, dpp_f<0x141>(v));  // row_half_mirror
-    v = fminf(v, dpp_f<0x140>(v));  // row_mirror
-    const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-    const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-    const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-    const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-    return fminf(fminf(a, b), fminf(c, d));
+    v = row_ext_f<false>(v);
+    return fminf(fminf(rdlane_f(v, 0), rdlane_f(v, 16)), fminf(rdlane_f(v, 32), rdlane_f(v, 48)));
 }
-__device__ __forceinline__ float wave_max_f(float v) { return -wave_min_f(-v); }
-// min over lanes 0-15 (DPP within row 0), read from lane 0
-__device__ __forceinline__ float row0_min_f(float v) {
-    v = fminf(v, dpp_f<0xB1>(v));   // quad_perm(1,0,3,2)
-    v = fminf(v, dpp_f<0x4E>(v));   // quad_perm(2,3,0,1)
-    v = fminf(v, dpp_f<0x141>(v));  // row_half_mirror
-    v = fminf(v, dpp_f<0x140>(v));  // row_mirror
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+__device__ __forceinline__ float wave_max_f(float v) {
+    v = row_ext_f<true>(v);
+    return fmaxf(fmaxf(rdlane_f(v, 0), rdlane_f(v, 16)), fmaxf(rdlane_f(v, 32), rdlane_f(v, 48)));
 }
+// min / max over lanes 0-15 (DPP within row 0), read from lane 0
+__device__ __forceinline__ float row0_min_f(float v) { return rdlane_f(row_ext_f<false>(v), 0); }
+__device__ __forceinline__ float row0_max_f(float v) { return rdlane_f(row_ext_f<true>(v), 0); }
 
 // Distance of p to the box [lo, hi] with the metric's own operation order;
 // every operand is <= the corresponding one of dist_metric(p, q) for any q in
@@ -319,7 +360,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 const float4 v = lane < ng ? qsh[lane & 15] : far;
                 const float4 w = lane < ng ? v : make_float4(-inf, -inf, -inf, 0.f);
                 lx = row0_min_f(v.x), ly = row0_min_f(v.y), lz = row0_min_f(v.z);
-                hx = -row0_min_f(-w.x), hy = -row0_min_f(-w.y), hz = -row0_min_f(-w.z);
+                hx = row0_max_f(w.x), hy = row0_max_f(w.y), hz = row0_max_f(w.z);
             } else {
                 lx = wave_min_f(same ? q4.x : inf), ly = wave_min_f(same ? q4.y : inf),
                 lz = wave_min_f(same ? q4.z : inf);
@@ -455,7 +496,40 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 // 1. fill the LDS list: steps of kStreamU x 64 loads, all in flight
                 //    (a software-pipelined variant that issued the next step before
                 //    filtering this one measured 8 % slower: more VGPRs, fewer waves)
+#if O3DML_FRS_DMA
+                // LDS-DMA variant (buffer path): the kStreamU rounds land in the
+                // list itself at nc + 64 u (no VGPRs held by loads in flight),
+                // then each round is read back, filtered and compacted in place
+                // (round u's targets end below round u + 1's landing zone)
+                if constexpr (decltype(buf)::value) {
+                    while (bk < nbk && nc <= fill_lim) {
+                        uint32_t src[kStreamU];
+#pragma unroll
+                        for (int u = 0; u < kStreamU; ++u) src[u] = round_src();
+                        const int nc0 = nc;
+#pragma unroll
+                        for (int u = 0; u < kStreamU; ++u)
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(pts_rsrc, (frs_lds_ptr)(cand + nc0 + 64 * u), 16,
+                                                                     src[u] * 16u, 0, 0, 0);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                        for (int u = 0; u < kStreamU; ++u) {
+                            float4 c = cand[nc0 + 64 * u + lane];
+                            const bool keep = box_dist<METRIC>(c, lx, ly, lz, hx, hy, hz) <= thr;
+                            const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
+                            if constexpr (REL16) c.w = __uint_as_float(__float_as_uint(c.w) - gbase);
+                            if (keep)
+                                cand[__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(km >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(km),
+                                                                                         static_cast<uint32_t>(nc)))] = c;
+                            nc += __popcll(km);
+                        }
+                    }
+                }
+                while (!decltype(buf)::value && bk < nbk && nc <= fill_lim) {
+#else
                 while (bk < nbk && nc <= fill_lim) {
+#endif
                     float4 c[kStreamU];
                     load_step(c, buf);
 #pragma unroll
@@ -491,6 +565,20 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                     const uint64_t bal = __builtin_amdgcn_ballot_w64(hit);
                     const uint32_t mlo = static_cast<uint32_t>(bal) & gm_lo;
                     const uint32_t mhi = static_cast<uint32_t>(bal >> 32) & gm_hi;
+#if O3DML_FRS_OOBST
+                    if constexpr (MODE == 0 && REL16 && !DIST) {
+                        // every lane stores: a miss gets an offset past the rows'
+                        // buffer resource, which the buffer unit drops (no exec
+                        // mask save / restore and branch per test)
+                        const uint32_t pos = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cnt));
+                        const uint32_t ps = min(pos, static_cast<uint32_t>(kRowCap - 1));
+                        __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(__float_as_uint(p.w)),
+                                                              rows_rsrc, hit ? row_b + (ps << 1) : 0x80000000u, 0,
+                                                              0);
+                        cnt = bcnt_add(mhi, bcnt_add(mlo, cnt));
+                        return;
+                    }
+#endif
                     if (hit) {
                         // mbcnt's accumulator operand adds the running count for free
                         const uint32_t pos = __builtin_amdgcn_mbcnt_hi(mhi, __builtin_amdgcn_mbcnt_lo(mlo, cnt));
