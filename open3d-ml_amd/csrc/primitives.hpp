@@ -7,6 +7,8 @@
 // Header-only templates, instantiated per translation unit (no -fgpu-rdc).
 #pragma once
 
+#include <cstdlib>
+
 #include <type_traits>
 
 #include "common.hpp"
@@ -442,6 +444,16 @@ __global__ void __launch_bounds__(kBsThreads) block_sort_pairs(const K* __restri
     }
 }
 
+// Largest n sorted in one workgroup (bitonic): O3DML_BS_MAX (A/B), default kBsMax
+inline int64_t block_sort_max() {
+    static const int64_t v = [] {
+        const char* e = std::getenv("O3DML_BS_MAX");
+        const int64_t x = e ? std::atoll(e) : kBsMax;
+        return x < 0 ? 0 : (x > kBsMax ? kBsMax : x);
+    }();
+    return v;
+}
+
 inline int bits_needed(uint64_t max_key) {
     int b = 0;
     while (b < 64 && (max_key >> b) != 0) ++b;
@@ -467,7 +479,7 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
         O3DML_LAUNCH_CHECK();
         return;
     }
-    if (n <= kBsMax) {
+    if (n <= block_sort_max()) {
         const K mask = end_bit >= static_cast<int>(8 * sizeof(K)) ? ~K(0) : ((K(1) << end_bit) - 1);
         // (a merge-path merge sort of packed (key, position) words measured
         // slower: 46 vs 37 us at ~4k keys — dependent LDS latency of the

@@ -22,4 +22,5 @@ done
     -- python3 "$R/tools/frs_single.py" 24 5 > "$R/gpurun_out/r4s1/single24.log" 2>&1) || exit 1
 f=$(find gpurun_out/r4s1/single24 -name '*kernel_stats.csv' | head -1); python3 tools/kstats.py "$f" 25 > gpurun_out/r4s1/single24_top.txt
 cat gpurun_out/r4s1/single24_top.txt
+bash tools/ab_env_scn.sh "O3DML_BS_MAX=8192" "O3DML_BS_MAX=1024" "O3DML_BS_MAX=0" || exit 1
 exit 0
