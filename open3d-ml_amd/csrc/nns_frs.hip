@@ -317,7 +317,17 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
         uint32_t pbase = 0;  // REL16: first point id of the query's batch item
         if (valid) {
             if constexpr (MODE == 0) {
-                q4 = qsel ? pts[qsel[t]] : qpts[t];  // self search: the queries are points
+                if (qsel) {
+                    const uint32_t qs = qsel[t];
+                    if (qpts) {  // the raw [M, 3] queries read through the (batch, Morton) order
+                        const float* qp = reinterpret_cast<const float*>(qpts) + 3 * static_cast<int64_t>(qs);
+                        q4 = make_float4(qp[0], qp[1], qp[2], __uint_as_float(qs));
+                    } else {
+                        q4 = pts[qs];  // self search in bucket order: the queries are points
+                    }
+                } else {
+                    q4 = qpts[t];
+                }
             } else {  // qpts = the raw query array [M, 3], over = the listed query ids
                 const uint32_t id = over[t];
                 const float* qp = reinterpret_cast<const float*>(qpts) + 3 * static_cast<int64_t>(id);
@@ -1061,6 +1071,19 @@ static bool frs_self_order(int64_t n_batch, const int64_t* prs_host, int64_t n_p
     return mx < O3DML_FRS_SELF_ORDER_MAX;
 }
 
+// Morton-ordered queries (items of >= 2^22 points, or queries != points):
+// the search reads the raw [M, 3] queries through the sorted order (default)
+// instead of a gathered float4 copy — the gather cost 0.38 ms at 2^24 points
+// and the search hides the scattered 12-B query reads.  O3DML_FRS_QGATHER=1:
+// the gathered copy (A/B).
+static bool frs_query_gather() {
+    static const bool v = [] {
+        const char* e = std::getenv("O3DML_FRS_QGATHER");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 // log2 of the queries per wave of the MODE 0 search: 64 while that still
 // gives >= 4096 waves (4 per SIMD), else 32 / 16 — a small call (one C1 scene,
 // 65,536 queries: 1,024 waves of 64) is latency-bound on one wave per SIMD.
@@ -1323,9 +1346,11 @@ static void frs_count_impl(const float* points, int64_t n_points, const float* q
             prim::radix_sort_pairs<uint32_t>(pl.keys, nullptr, pl.skeys, pl.qorder, n_queries,
                                              batch_bits + 3 * cell_bits, sws, st);
         }
-        gather_sorted_points_kernel<<<xcd_grid(n_queries, 256), 256, 0, st>>>(queries, pl.qorder, n_queries,
-                                                                             pl.qpts, 0, nullptr, 0, nullptr);
-        O3DML_LAUNCH_CHECK();
+        if (frs_query_gather()) {
+            gather_sorted_points_kernel<<<xcd_grid(n_queries, 256), 256, 0, st>>>(queries, pl.qorder, n_queries,
+                                                                                 pl.qpts, 0, nullptr, 0, nullptr);
+            O3DML_LAUNCH_CHECK();
+        }
         qkeys = pl.skeys;
         bshift = batch_bits == 0 ? 32 : 3 * cell_bits;
     }
@@ -1335,8 +1360,9 @@ static void frs_count_impl(const float* points, int64_t n_points, const float* q
         launch_group<0, int32_t>(metric, ignore_query_point != 0, with_distances != 0,
                                  rel16_rows(n_batch, points_row_splits_host, n_queries), st,
                                  group_grid(n_queries, 1 << qlog), pl.pts,
-                                 static_cast<uint32_t>(n_points), hash_table_cell_splits, pl.qpts,
-                                 self_order ? pl.qorder : nullptr, qkeys, bshift,
+                                 static_cast<uint32_t>(n_points), hash_table_cell_splits,
+                                 self_order ? nullptr : (frs_query_gather() ? pl.qpts : reinterpret_cast<const float4*>(queries)),
+                                 self_order || !frs_query_gather() ? pl.qorder : nullptr, qkeys, bshift,
                                  n_queries, nullptr, radius, inv, thr, (int)n_batch, queries_row_splits,
                                  hash_table_splits, points_row_splits, pl.counts, pl.tidx, pl.tdist, pl.over,
                                  pl.scalars, nullptr, nullptr, nullptr, pl.dir, pl.dir_cap, nullptr, -1, qlog);
