@@ -323,7 +323,8 @@ class RandLANet(nn.Module):
                 self._fc0_cache = (w, b)
         return self._fc0_cache
 
-    # folded eval weights are invalidated whenever parameters may change
+    # folded eval weights are invalidated whenever parameters may change; the
+    # captured patch graphs hold raw pointers to them, so they go too
     def _invalidate(self):
         self._fc0_cache = None
         for m in self.modules():
@@ -331,9 +332,14 @@ class RandLANet(nn.Module):
                 m._folded = None
             if isinstance(m, LocalFeatureAggregation):
                 m.__dict__.pop("_t_cache", None)
+        self.__dict__.pop("_o3dml_patch_step", None)
+        self.__dict__.pop("_o3dml_patch_graph", None)
 
     def train(self, mode=True):
-        self._invalidate()
+        # eval() on a model already in eval mode keeps the folded weights and
+        # the graphs built on them (SemSegInference.run calls it per frame)
+        if mode or self.training:
+            self._invalidate()
         return super().train(mode)
 
     def load_state_dict(self, *a, **kw):

@@ -281,3 +281,75 @@ def test_patch_step_equals_ops(cuda):
     untouched = torch.ones(n, dtype=torch.bool, device=cuda)
     untouched[crop] = False
     assert torch.equal(step.poss[:n][untouched], p0[untouched])
+
+
+def test_patch_graph_survives_frames_and_drops_with_weights(cuda):
+    """The captured patch step holds raw pointers to the folded eval weights:
+    a second frame on the same model reuses the graph AND the folded weights
+    (run() calls eval() per frame, which must not free them), its result equals
+    the eager launches on the same frame; a mode switch or a state_dict load
+    drops the graphs with the weights they point at."""
+    from o3dml_amd.randlanet import RandLANet, SemSegInference
+    torch.manual_seed(0)
+    m = RandLANet(num_points=4096).to(cuda).eval()
+    rng = np.random.default_rng(4)
+
+    def cloud():
+        p = np.stack([rng.uniform(-20, 20, 20000), rng.uniform(-20, 20, 20000), rng.uniform(-2, 2, 20000)], 1)
+        return torch.from_numpy(p.astype(np.float32)).to(cuda)
+
+    a, b = cloud(), cloud()
+    SemSegInference(m, seed=1, use_graph=True, probs_dtype=torch.float32).run(a)
+    step = m.__dict__["_o3dml_patch_step"][1]
+    folded = m.encoder[0].mlp1.folded()[0]
+    lg, pg = SemSegInference(m, seed=2, use_graph=True, probs_dtype=torch.float32).run(b)
+    assert m.__dict__["_o3dml_patch_step"][1] is step and step.graph is not None
+    assert m.encoder[0].mlp1.folded()[0] is folded
+    le, pe = SemSegInference(m, seed=2, use_graph=False, probs_dtype=torch.float32).run(b)
+    torch.testing.assert_close(pg, pe, rtol=0, atol=1e-6)
+    assert torch.equal(lg, le)
+    m.train()
+    assert "_o3dml_patch_step" not in m.__dict__
+    m.eval()
+    SemSegInference(m, seed=1, use_graph=True).run(a)
+    m.load_state_dict(m.state_dict())
+    assert "_o3dml_patch_step" not in m.__dict__
+
+
+def test_knn_select_in_graph_equals_eager(cuda):
+    """o3dml_knn_select (zero + three histogram + count + write launches)
+    captured in a HIP graph and replayed for a moving centre gives the eager
+    call's set."""
+    from o3dml_amd import _lib
+    from o3dml_amd._util import ptr, stream_handle
+    lib = _lib.load()
+    rng = np.random.default_rng(6)
+    n, k = 98304, 45056
+    pts = torch.from_numpy(rng.uniform(-30, 30, (n, 3)).astype(np.float32)).to(cuda)
+    center = torch.zeros(3, dtype=torch.float32, device=cuda)
+    ws = torch.empty(lib.o3dml_knn_select_workspace_size(n), dtype=torch.uint8, device=cuda)
+    out = torch.empty(k, dtype=torch.int64, device=cuda)
+
+    def call():
+        _lib.call("o3dml_knn_select", ptr(pts), n, ptr(center), k, 1, ptr(out), ptr(ws), ws.numel(),
+                  stream_handle(cuda))
+
+    side = torch.cuda.Stream(cuda)
+    side.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(side):
+        call()
+    torch.cuda.current_stream(cuda).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        call()
+    for i in range(4):
+        center.copy_(pts[i * 1000])
+        g.replay()
+        got = out.clone()
+        call()
+        assert torch.equal(got, out), i
+        assert torch.all(got[1:] > got[:-1]), i  # a set, in index order
+        d = ((pts - pts[i * 1000]) ** 2).sum(1)
+        rest = torch.ones(n, dtype=torch.bool, device=cuda)
+        rest[got] = False
+        assert float(d[got].max()) <= float(d[rest].min()) * (1 + 1e-5), i
