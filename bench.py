@@ -352,6 +352,9 @@ def kpconv_bench(dev, steps):
     neighbour searches + grid subsampling per layer) + forward + cross entropy
     + backward + SGD step, ~40k stacked input points per step."""
     from o3dml_amd.kpfcnn import KPFCNN, S3DIS, segmentation_inputs
+    blas = os.environ.get("O3DML_BLAS")  # A/B of torch's GEMM backend ("cublas" = rocBLAS, "cublaslt" = hipBLASLt)
+    if blas:
+        torch.backends.cuda.preferred_blas_library(blas)
     torch.manual_seed(0)
     np.random.seed(0)
     model = KPFCNN(**S3DIS).to(dev).train()

@@ -516,6 +516,42 @@ int o3dml_kpconv_pool_max_backward_det(const float* grad_out, const int32_t* arg
                                        int64_t ld, int64_t n, int nb, int c, int64_t n_support, float* grad_x,
                                        void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- fp32 GEMM through rocBLAS (the KPFCNN Linear / KPConv GEMMs, forward
+ * and backward; replaces torch.matmul in UnaryBlock.mlp and KPConv.forward,
+ * ml3d/torch/models/kpconv.py:1155-1159, 1290).  Row-major C[m, n] = alpha
+ * op(A) op(B) + beta C; trans_a: A stored [k, m], trans_b: B stored [n, k];
+ * leading dimensions of the stored matrices, in elements. */
+int o3dml_sgemm(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k, float alpha, const float* a, int64_t lda,
+                const float* b, int64_t ldb, float beta, float* c, int64_t ldc, void* stream);
+
+/* o3dml_sgemm (alpha 1, beta 0) for a long reduction k with few output tiles
+ * (weight gradients; deep-layer WF @ W): k split into up to 64 parts of >=
+ * 2,048 (strided-batched rocBLAS), the parts summed in order (deterministic).
+ * Workspace: _workspace_size(m, n, k). */
+size_t o3dml_sgemm_splitk_workspace_size(int64_t m, int64_t n, int64_t k);
+int o3dml_sgemm_splitk(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k, const float* a, int64_t lda,
+                       const float* b, int64_t ldb, float* c, int64_t ldc, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
+/* ---- KPFCNN BatchNorm1d (+ LeakyReLU) over [N, C] rows (replaces
+ * nn.BatchNorm1d + nn.LeakyReLU of BatchNormBlock / UnaryBlock / SimpleBlock /
+ * ResnetBottleneckBlock, ml3d/torch/models/kpconv.py:1213-1464).
+ * forward: training -> batch statistics (biased variance for y; running_mean /
+ * running_var updated with the unbiased one, momentum as torch; num_batches_tracked
+ * += 1; any of the three may be NULL), eval -> running statistics.  y = act((x -
+ * mean) * weight * invstd + bias), act = LeakyReLU(slope) when act != 0; weight /
+ * bias may be NULL (1 / 0).  save [4C] = (mean, invstd, weight * invstd, bias)
+ * is the backward's input.  backward: grad_x / grad_weight / grad_bias (each
+ * NULLable).  Workspace: o3dml_batch_norm_workspace_size(n, c). */
+size_t o3dml_batch_norm_workspace_size(int64_t n, int c);
+int o3dml_batch_norm_forward(const float* x, int64_t n, int c, const float* weight, const float* bias,
+                             float* running_mean, float* running_var, int64_t* num_batches_tracked, float momentum,
+                             float eps, int training, int act, float slope, float* y, float* save, void* workspace,
+                             size_t workspace_bytes, void* stream);
+int o3dml_batch_norm_backward(const float* grad_y, const float* x, int64_t n, int c, const float* save, int training,
+                              int act, float slope, float* grad_x, float* grad_weight, float* grad_bias,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- PointPillars pillars (point_pillars.py:352-380,
  * 509-552, 567-601).
  * pillar_features: points f32 [n_points, cdim] (x, y, z, features...), the

@@ -16,6 +16,7 @@
 // exp(-d^2 / (2 sigma^2)), sigma = 0.3 extent (kpconv.py radius_gaussian);
 // closest: only the nearest kernel point of each neighbour contributes.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "primitives.hpp"
@@ -128,6 +129,214 @@ __global__ void __launch_bounds__(256) kpconv_wf_kernel(const float* __restrict_
             }
         }
     }
+}
+
+// ---- MFMA aggregation (rigid kernel points, K <= 16, no closest mode) ----
+// The kernels above give one wave one query and walk its channels 64 at a
+// time, re-reading K influences from LDS per (neighbour, channel): the deep
+// layers (150 queries x 512 channels at C3 layer 4) fill 38 workgroups of
+// the 256 CUs, and layer 0 is LDS-bound.  Here a wave owns one (query,
+// 16T-channel tile) — n x ceil(Cin / 16T) waves — and the aggregation is the
+// per-query product
+//     WF_q [16 kernel points x 16T channels] = A_q [16 x nb] X_q [nb x 16T]
+// on v_mfma_f32_16x16x4_f32 (exact f32, cdna_hip_programming.md): lane l
+// computes the influence of neighbour 4s + (l >> 4) on kernel point l & 15
+// (its A element) and gathers x[nbr][c0 + 16t + (l & 15)] (its B elements,
+// 64 contiguous bytes per 16 lanes); the neighbours' relative positions and
+// ids are staged 64 at a time in LDS (one coalesced load per lane).  The
+// backward scatters dX_q [nb x 16T] = A_q^T dWF_q with the same influences
+// (dWF_q read once per wave as the B operand), one fp32 atomic per
+// (neighbour, channel) as before.
+constexpr int kKpMfmaK = 16;
+
+typedef float kp_f32x4 __attribute__((ext_vector_type(4)));
+
+template <int INFL>
+__device__ __forceinline__ float kp_influence(float ex, float ey, float ez, float extent) {
+    const float d2 = ex * ex + ey * ey + ez * ez;
+    if constexpr (INFL == 0) return 1.f;
+    else if constexpr (INFL == 1) return fmaxf(1.f - sqrtf(d2) / extent, 0.f);
+    else return __expf(-d2 / kp_gauss_den(extent));
+}
+
+// lane l of the wave: neighbour j0 + l of query q -> LDS (p - q, id or -1)
+template <class TI>
+__device__ __forceinline__ void kp_stage_neighbours(const float* __restrict__ s_pts, int64_t n_support,
+                                                    const TI* __restrict__ nbr, int64_t q, int nb, int j0, float qx,
+                                                    float qy, float qz, float4* __restrict__ sh) {
+    const int lane = threadIdx.x & 63;
+    float4 e = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+    if (j0 + lane < nb) {
+        const int64_t v = static_cast<int64_t>(nbr[q * nb + j0 + lane]);
+        if (v >= 0 && v < n_support)
+            e = make_float4(s_pts[3 * v] - qx, s_pts[3 * v + 1] - qy, s_pts[3 * v + 2] - qz,
+                            __int_as_float(static_cast<int>(v)));
+    }
+    sh[lane] = e;
+}
+
+__device__ __forceinline__ void kp_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int INFL, int T, class TI>
+__global__ void __launch_bounds__(256) kpconv_wf_mfma_kernel(const float* __restrict__ q_pts,
+                                                             const float* __restrict__ s_pts, int64_t n_support,
+                                                             const TI* __restrict__ nbr, int64_t n, int nb,
+                                                             const float* __restrict__ x, int cin,
+                                                             const float* __restrict__ kp, int K, float extent,
+                                                             int ctiles, float* __restrict__ wf) {
+    __shared__ float4 sh_all[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t wave = static_cast<int64_t>(blockIdx.x) * 4 + wv;
+    if (wave >= n * ctiles) return;  // wave-uniform
+    float4* sh = sh_all[wv];
+    const int64_t q = wave / ctiles;
+    const int c0 = static_cast<int>(wave - q * ctiles) * 16 * T;
+    const int kk = lane & 15, jr = lane >> 4;
+    const bool kval = kk < K;
+    const float kx = kval ? kp[3 * kk] : 0.f, ky = kval ? kp[3 * kk + 1] : 0.f, kz = kval ? kp[3 * kk + 2] : 0.f;
+    const float qx = q_pts[3 * q], qy = q_pts[3 * q + 1], qz = q_pts[3 * q + 2];
+    kp_f32x4 acc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] = kp_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j0 = 0; j0 < nb; j0 += 64) {
+        kp_wave_sync();
+        kp_stage_neighbours(s_pts, n_support, nbr, q, nb, j0, qx, qy, qz, sh);
+        kp_wave_sync();
+        // groups of 4 steps (16 neighbours; staged entries past nb are id -1)
+        const int groups = (min(64, nb - j0) + 15) >> 4;
+        for (int gi = 0; gi < groups; ++gi)
+#pragma unroll
+        for (int st = 4 * gi; st < 4 * gi + 4; ++st) {
+            const float4 p = sh[4 * st + jr];
+            const int id = __float_as_int(p.w);
+            const float a = (id >= 0 && kval) ? kp_influence<INFL>(p.x - kx, p.y - ky, p.z - kz, extent) : 0.f;
+            const float* xr = x + static_cast<int64_t>(id) * cin + c0 + kk;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const float b = (id >= 0 && c0 + 16 * t + kk < cin) ? xr[16 * t] : 0.f;
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+            }
+        }
+    }
+    // acc[t][r] = WF[q][k = 4 jr + r][c0 + 16 t + kk]
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int c = c0 + 16 * t + kk;
+        if (c >= cin) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int k = 4 * jr + r;
+            if (k < K) wf[(q * K + k) * static_cast<int64_t>(cin) + c] = acc[t][r];
+        }
+    }
+}
+
+template <int INFL, int T, class TI>
+__global__ void __launch_bounds__(256) kpconv_wf_backward_mfma_kernel(const float* __restrict__ q_pts,
+                                                                      const float* __restrict__ s_pts,
+                                                                      int64_t n_support, const TI* __restrict__ nbr,
+                                                                      int64_t n, int nb,
+                                                                      const float* __restrict__ dwf, int cin,
+                                                                      const float* __restrict__ kp, int K,
+                                                                      float extent, int ctiles,
+                                                                      float* __restrict__ dx) {
+    __shared__ float4 sh_all[4][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t wave = static_cast<int64_t>(blockIdx.x) * 4 + wv;
+    if (wave >= n * ctiles) return;  // wave-uniform
+    float4* sh = sh_all[wv];
+    const int64_t q = wave / ctiles;
+    const int c0 = static_cast<int>(wave - q * ctiles) * 16 * T;
+    const int jl = lane & 15, kr = lane >> 4;
+    const float qx = q_pts[3 * q], qy = q_pts[3 * q + 1], qz = q_pts[3 * q + 2];
+    // B operands: dWF[q][k = 4 s + kr][c0 + 16 t + jl]; this lane's kernel points 4 s + kr
+    float gb[4][T], kx[4], ky[4], kz[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int k = 4 * s + kr;
+        const bool kv = k < K;
+        kx[s] = kv ? kp[3 * k] : 0.f;
+        ky[s] = kv ? kp[3 * k + 1] : 0.f;
+        kz[s] = kv ? kp[3 * k + 2] : 0.f;
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int c = c0 + 16 * t + jl;
+            gb[s][t] = (kv && c < cin) ? dwf[(q * K + k) * static_cast<int64_t>(cin) + c] : 0.f;
+        }
+    }
+    for (int j0 = 0; j0 < nb; j0 += 64) {
+        kp_wave_sync();
+        kp_stage_neighbours(s_pts, n_support, nbr, q, nb, j0, qx, qy, qz, sh);
+        kp_wave_sync();
+        const int jn = min(64, nb - j0);
+        for (int jt = 0; jt < jn; jt += 16) {
+            // A operand: influence of kernel point 4 s + kr on neighbour jt + jl
+            const float4 p = sh[jt + jl];
+            const bool live = __float_as_int(p.w) >= 0;
+            kp_f32x4 acc[T];
+#pragma unroll
+            for (int t = 0; t < T; ++t) acc[t] = kp_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const float a = (live && 4 * s + kr < K)
+                                        ? kp_influence<INFL>(p.x - kx[s], p.y - ky[s], p.z - kz[s], extent)
+                                        : 0.f;
+#pragma unroll
+                for (int t = 0; t < T; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, gb[s][t], acc[t], 0, 0, 0);
+            }
+            // acc[t][r] = dX[neighbour jt + 4 kr + r][c0 + 16 t + jl]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int id = __float_as_int(sh[jt + 4 * kr + r].w);
+                if (id < 0) continue;
+                float* d = dx + static_cast<int64_t>(id) * cin + c0 + jl;
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+                    if (c0 + 16 * t + jl < cin) atomicAdd(d + 16 * t, acc[t][r]);
+            }
+        }
+    }
+}
+
+static bool kp_mfma_enabled() {
+    const char* e = std::getenv("O3DML_KPCONV_MFMA");
+    return !e || std::atoi(e) != 0;
+}
+
+// the MFMA path: rigid shared kernel points, K <= 16, no closest / modulations
+template <bool BWD, class TI>
+static void launch_kp_mfma(int influence, hipStream_t st, const float* qp, const float* sp, int64_t ns,
+                           const void* nbr, int64_t n, int nb, const float* in, int cin, const float* kp, int K,
+                           float extent, float* out) {
+    const int T = cin <= 16 ? 1 : (cin <= 32 ? 2 : 4);
+    const int ctiles = static_cast<int>(ceil_div(cin, 16 * T));
+    const unsigned g = static_cast<unsigned>(ceil_div(n * ctiles, 4));
+    const TI* nb_ = static_cast<const TI*>(nbr);
+#define O3DML_KPM(I, TT)                                                                                           \
+    do {                                                                                                           \
+        if constexpr (BWD)                                                                                         \
+            kpconv_wf_backward_mfma_kernel<I, TT, TI><<<g, 256, 0, st>>>(qp, sp, ns, nb_, n, nb, in, cin, kp, K,   \
+                                                                         extent, ctiles, out);                     \
+        else                                                                                                       \
+            kpconv_wf_mfma_kernel<I, TT, TI><<<g, 256, 0, st>>>(qp, sp, ns, nb_, n, nb, in, cin, kp, K, extent,    \
+                                                                ctiles, out);                                      \
+    } while (0)
+#define O3DML_KPM_T(I)                          \
+    do {                                        \
+        if (T == 1) O3DML_KPM(I, 1);            \
+        else if (T == 2) O3DML_KPM(I, 2);       \
+        else O3DML_KPM(I, 4);                   \
+    } while (0)
+    if (influence == 0) O3DML_KPM_T(0);
+    else if (influence == 1) O3DML_KPM_T(1);
+    else O3DML_KPM_T(2);
+#undef O3DML_KPM_T
+#undef O3DML_KPM
+    O3DML_LAUNCH_CHECK();
 }
 
 // Backward of the aggregation for the features: dx[ids[j]][c] += sum_k
@@ -529,6 +738,15 @@ O3DML_API int o3dml_kpconv_weighted_features(const float* q_pts, int64_t n, cons
     O3DML_REQUIRE(influence >= 0 && influence <= 2, "KPConv: influence must be constant, linear or gaussian");
     O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
     if (n == 0) return 0;
+    if (!closest && !kp_per_query && !modulations && K <= kKpMfmaK && kp_mfma_enabled()) {
+        if (index_bits == 32)
+            launch_kp_mfma<false, int32_t>(influence, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
+                                           features, cin, kernel_points, K, extent, out);
+        else
+            launch_kp_mfma<false, int64_t>(influence, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
+                                           features, cin, kernel_points, K, extent, out);
+        return 0;
+    }
     const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n, 4), 1 << 20));
     if (index_bits == 32)
         launch_kp<false, int32_t>(influence, closest, g, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
@@ -548,6 +766,15 @@ O3DML_API int o3dml_kpconv_weighted_features_backward(const float* q_pts, int64_
     O3DML_REQUIRE(K >= 1 && K <= kKpMaxK, "KPConv: kernel points must be in [1, %d]", kKpMaxK);
     O3DML_REQUIRE(index_bits == 32 || index_bits == 64, "index_bits must be 32 or 64");
     if (n == 0) return 0;
+    if (!closest && !kp_per_query && K <= kKpMfmaK && kp_mfma_enabled()) {
+        if (index_bits == 32)
+            launch_kp_mfma<true, int32_t>(influence, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
+                                          grad_wf, cin, kernel_points, K, extent, grad_features);
+        else
+            launch_kp_mfma<true, int64_t>(influence, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,
+                                          grad_wf, cin, kernel_points, K, extent, grad_features);
+        return 0;
+    }
     const unsigned g = static_cast<unsigned>(std::min<int64_t>(ceil_div(n, 4), 1 << 20));
     if (index_bits == 32)
         launch_kp<true, int32_t>(influence, closest, g, as_stream(stream), q_pts, s_pts, n_support, neighbors, n, nb,

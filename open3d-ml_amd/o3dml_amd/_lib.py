@@ -89,6 +89,15 @@ SIGNATURES = {
     "o3dml_kpconv_kernel_point_grad": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p,
                                                c_i32, c_f32, c_i32, c_i32, c_p, c_p, c_p, c_p]),
     "o3dml_kpconv_min_d2_columns": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_p]),
+    "o3dml_sgemm": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_f32, c_p, c_i64, c_p, c_i64, c_f32, c_p, c_i64, c_p]),
+    "o3dml_sgemm_splitk_workspace_size": (c_sz, [c_i64, c_i64, c_i64]),
+    "o3dml_sgemm_splitk": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_sz,
+                                   c_p]),
+    "o3dml_batch_norm_workspace_size": (c_sz, [c_i64, c_i32]),
+    "o3dml_batch_norm_forward": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_f32, c_f32, c_i32, c_i32, c_f32,
+                                         c_p, c_p, c_p, c_sz, c_p]),
+    "o3dml_batch_norm_backward": (c_i32, [c_p, c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_f32, c_p, c_p, c_p, c_p, c_sz,
+                                          c_p]),
     "o3dml_kpconv_pool_max": (c_i32, [c_p, c_i64, c_i32, c_p, c_i32, c_i64, c_i64, c_i32, c_p, c_p, c_p]),
     "o3dml_kpconv_pool_max_backward": (c_i32, [c_p, c_p, c_i64, c_i32, c_i64, c_p, c_p]),
     "o3dml_kpconv_pool_max_backward_det": (c_i32, [c_p, c_p, c_p, c_i32, c_i64, c_i64, c_i32, c_i32, c_i64, c_p, c_p,

@@ -34,15 +34,37 @@ class StreamHandle(int):
 
 
 def stream_handle(device):
-    """The current torch stream of `device` (see StreamHandle)."""
-    device = torch.device(device)
-    h = StreamHandle(torch.cuda.current_stream(device).cuda_stream)
-    h.dev = device.index
+    """The current torch stream of `device` (see StreamHandle); the raw handle
+    straight from torch's stream registry (no Stream object per call)."""
+    if not isinstance(device, torch.device):
+        device = torch.device(device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    h = StreamHandle(torch._C._cuda_getCurrentRawStream(idx))
+    h.dev = idx
     return h
 
 
 def ptr(t):
     return None if t is None else t.data_ptr()
+
+
+def mm(a, b, ta=False, tb=False):
+    """op(a) @ op(b) for contiguous row-major float32 CUDA matrices through
+    rocBLAS (csrc/gemm.cpp o3dml_sgemm); ta / tb: use a.T / b.T."""
+    from . import _lib
+    m, k = (a.shape[1], a.shape[0]) if ta else a.shape
+    n = b.shape[0] if tb else b.shape[1]
+    c = torch.empty((m, n), dtype=torch.float32, device=a.device)
+    if k >= 4096 and m * n <= (1 << 20):  # long reduction, few output tiles: split-K
+        lib = _lib.load()
+        ws = torch.empty(max(int(lib.o3dml_sgemm_splitk_workspace_size(m, n, k)), 1), dtype=torch.uint8,
+                         device=a.device)
+        _lib.call("o3dml_sgemm_splitk", int(ta), int(tb), m, n, k, a.data_ptr(), a.shape[1], b.data_ptr(),
+                  b.shape[1], c.data_ptr(), n, ws.data_ptr(), ws.numel(), stream_handle(a.device))
+        return c
+    _lib.call("o3dml_sgemm", int(ta), int(tb), m, n, k, 1.0, a.data_ptr(), a.shape[1], b.data_ptr(), b.shape[1], 0.0,
+              c.data_ptr(), n, stream_handle(a.device))
+    return c
 
 
 _SMALL_CACHE = OrderedDict()  # (device, stream, dtype, shape, bytes) -> device tensor

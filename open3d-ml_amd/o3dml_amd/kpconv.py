@@ -21,25 +21,49 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from ._util import gpu_device, index_bits, ptr, stream_handle, to_dev, workspace
+from ._util import gpu_device, index_bits, mm, ptr, stream_handle, to_dev, workspace
 
 _INFLUENCE = {"constant": 0, "linear": 1, "gaussian": 2}
+
+
+def _wf_forward(x, q_pts, s_pts, nbr, kp, kp_per_query, extent, influence, closest, mod):
+    n, nb = nbr.shape
+    K = kp.shape[-2]
+    cin = x.shape[1]
+    out = torch.empty((n, K, cin), dtype=torch.float32, device=x.device)
+    _lib.call("o3dml_kpconv_weighted_features", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr),
+              index_bits(nbr.dtype), nb, ptr(x), cin, ptr(kp), K, int(kp_per_query), float(extent), influence,
+              int(closest), ptr(mod), ptr(out), stream_handle(x.device))
+    return out
+
+
+def _wf_backward_x(gm, q_pts, s_pts, nbr, kp, kp_per_query, extent, influence, closest, n_s, cin):
+    """dX of the aggregation for dWF gm (modulations already folded in)."""
+    n, nb = nbr.shape
+    K = kp.shape[-2]
+    if torch.are_deterministic_algorithms_enabled():
+        # fixed-order gather over the inverse neighbour lists (no fp32 atomics)
+        dx = torch.empty((n_s, cin), dtype=torch.float32, device=gm.device)
+        ws = workspace(_lib.load().o3dml_kpconv_inverse_workspace_size(n, nb, n_s), gm.device)
+        _lib.call("o3dml_kpconv_weighted_features_backward_det", ptr(q_pts), n, ptr(s_pts), n_s, ptr(nbr),
+                  index_bits(nbr.dtype), nb, ptr(gm), cin, ptr(kp), K, int(kp_per_query), float(extent),
+                  influence, int(closest), ptr(dx), ptr(ws), ws.numel(), stream_handle(gm.device))
+    else:
+        dx = torch.zeros((n_s, cin), dtype=torch.float32, device=gm.device)
+        _lib.call("o3dml_kpconv_weighted_features_backward", ptr(q_pts), n, ptr(s_pts), n_s, ptr(nbr),
+                  index_bits(nbr.dtype), nb, ptr(gm), cin, ptr(kp), K, int(kp_per_query), float(extent),
+                  influence, int(closest), ptr(dx), stream_handle(gm.device))
+    return dx
 
 
 class _WeightedFeatures(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, q_pts, s_pts, nbr, kp, kp_per_query, extent, influence, closest, modulations):
-        n, nb = nbr.shape
-        K = kp.shape[-2]
-        cin = x.shape[1]
-        out = torch.empty((n, K, cin), dtype=torch.float32, device=x.device)
         kpd = kp.detach().contiguous()
         mod = None if modulations is None else modulations.detach().contiguous()
-        _lib.call("o3dml_kpconv_weighted_features", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr),
-                  index_bits(nbr.dtype), nb, ptr(x), cin, ptr(kpd), K, int(kp_per_query), float(extent), influence,
-                  int(closest), ptr(mod), ptr(out), stream_handle(x.device))
+        out = _wf_forward(x, q_pts, s_pts, nbr, kpd, kp_per_query, extent, influence, closest, mod)
         ctx.save_for_backward(x, q_pts, s_pts, nbr, kpd, mod if mod is not None else torch.empty(0, device=x.device))
-        ctx.meta = (kp_per_query, extent, influence, closest, x.shape[0], cin, mod is not None)
+        ctx.meta = (kp_per_query, extent, influence, closest, x.shape[0], x.shape[1], mod is not None)
         return out
 
     @staticmethod
@@ -52,19 +76,8 @@ class _WeightedFeatures(torch.autograd.Function):
         dx = dkp = dmod = None
         if ctx.needs_input_grad[0]:
             gm = g * mod[:, :, None] if has_mod else g  # the modulation scales dWF (kpconv.py:1149-1150)
-            gm = gm.contiguous()
-            if torch.are_deterministic_algorithms_enabled():
-                # fixed-order gather over the inverse neighbour lists (no fp32 atomics)
-                dx = torch.empty((n_s, cin), dtype=torch.float32, device=g.device)
-                ws = workspace(_lib.load().o3dml_kpconv_inverse_workspace_size(n, nb, n_s), g.device)
-                _lib.call("o3dml_kpconv_weighted_features_backward_det", ptr(q_pts), n, ptr(s_pts), n_s, ptr(nbr),
-                          index_bits(nbr.dtype), nb, ptr(gm), cin, ptr(kp), K, int(kp_per_query), float(extent),
-                          influence, int(closest), ptr(dx), ptr(ws), ws.numel(), stream_handle(g.device))
-            else:
-                dx = torch.zeros((n_s, cin), dtype=torch.float32, device=g.device)
-                _lib.call("o3dml_kpconv_weighted_features_backward", ptr(q_pts), n, ptr(s_pts), n_s, ptr(nbr),
-                          index_bits(nbr.dtype), nb, ptr(gm), cin, ptr(kp), K, int(kp_per_query), float(extent),
-                          influence, int(closest), ptr(dx), stream_handle(g.device))
+            dx = _wf_backward_x(gm.contiguous(), q_pts, s_pts, nbr, kp, kp_per_query, extent, influence, closest,
+                                n_s, cin)
         if ctx.needs_input_grad[4] or (has_mod and ctx.needs_input_grad[9]):
             if not kp_per_query:
                 raise NotImplementedError("KPConv: gradients w.r.t. shared (non-deformed) kernel points")
@@ -75,6 +88,38 @@ class _WeightedFeatures(torch.autograd.Function):
                       int(closest), ptr(mod) if has_mod else None, ptr(dkp), ptr(dm), stream_handle(g.device))
             dmod = dm
         return dx, None, None, None, dkp, None, None, None, None, dmod
+
+
+class _KPConvRigid(torch.autograd.Function):
+    """Rigid KPConv as ONE autograd node: the HIP aggregation WF [n, K, Cin]
+    and the GEMM out = WF.view(n, K Cin) @ W.view(K Cin, Cout) in the forward;
+    dWF = g W^T, dW = WF^T g and the aggregation backward in the backward
+    (the matmul / view nodes of the unfused form cost host time per call)."""
+
+    @staticmethod
+    def forward(ctx, x, w, q_pts, s_pts, nbr, kp, extent, influence, closest):
+        kpd = kp.detach().contiguous()
+        wf = _wf_forward(x, q_pts, s_pts, nbr, kpd, False, extent, influence, closest, None)
+        n, K, cin = wf.shape
+        out = mm(wf.view(n, K * cin), w.detach().reshape(K * cin, -1).contiguous())
+        ctx.save_for_backward(w, wf, q_pts, s_pts, nbr, kpd)
+        ctx.meta = (extent, influence, closest, x.shape[0])
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        w, wf, q_pts, s_pts, nbr, kp = ctx.saved_tensors
+        extent, influence, closest, n_s = ctx.meta
+        n, K, cin = wf.shape
+        g = g.contiguous()
+        w2 = w.detach().reshape(K * cin, -1).contiguous()
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            dw = mm(wf.view(n, K * cin), g, ta=True).view_as(w)
+        if ctx.needs_input_grad[0]:
+            gwf = mm(g, w2, tb=True)
+            dx = _wf_backward_x(gwf, q_pts, s_pts, nbr, kp, False, extent, influence, closest, n_s, cin)
+        return dx, dw, None, None, None, None, None, None, None
 
 
 def min_d2(q_pts, s_pts, neighb_inds, kernel_points):
@@ -124,6 +169,30 @@ def weighted_features(q_pts, s_pts, neighb_inds, x, kernel_points, extent, influ
     xx = x if x.is_cuda else x.to(dev)
     return _WeightedFeatures.apply(xx.float().contiguous(), qp, sp, nbr.contiguous(), kp, kp.dim() == 3,
                                    float(extent), _INFLUENCE[influence], aggregation_mode == "closest", mod)
+
+
+def kpconv_rigid(q_pts, s_pts, neighb_inds, x, kernel_points, weights, extent, influence="linear",
+                 aggregation_mode="sum"):
+    """KPConv.forward for rigid kernel points: sum_k WF[:, k] @ W[k] with WF
+    the weighted neighbour features (kpconv.py:1046-1159), one autograd node
+    (_KPConvRigid)."""
+    dev = gpu_device(x)
+    if influence not in _INFLUENCE:
+        raise ValueError("Unknown influence function type (config.KP_influence)")
+    if aggregation_mode not in ("sum", "closest"):
+        raise ValueError("Unknown convolution mode. Should be 'closest' or 'sum'")
+    if kernel_points.requires_grad:
+        raise NotImplementedError("KPConv: gradients w.r.t. shared (non-deformed) kernel points are not supported")
+    qp = to_dev(q_pts, dev, torch.float32)
+    sp = to_dev(s_pts, dev, torch.float32)
+    nbr = to_dev(neighb_inds, dev)
+    if nbr.dtype not in (torch.int32, torch.int64):
+        nbr = nbr.long()
+    kp = kernel_points if kernel_points.is_cuda and kernel_points.dtype == torch.float32 else \
+        kernel_points.to(dev).float()
+    xx = x if x.is_cuda else x.to(dev)
+    return _KPConvRigid.apply(xx.float().contiguous(), weights, qp, sp, nbr.contiguous(), kp, float(extent),
+                              _INFLUENCE[influence], aggregation_mode == "closest")
 
 
 def _sphere_points(radius, K, fixed):
@@ -196,6 +265,9 @@ class KPConv(nn.Module):
             kp = self.deformed_KP
             # distances kept for p2p_fitting_regularizer (kpconv.py:1071)
             self.min_d2 = min_d2(q_pts, s_pts, neighb_inds, kp)
+        if not self.deformable and self.weights.dtype == torch.float32:
+            return kpconv_rigid(q_pts, s_pts, neighb_inds, x, kp, self.weights, self.KP_extent, self.KP_influence,
+                                self.aggregation_mode)
         wf = weighted_features(q_pts, s_pts, neighb_inds, x, kp, self.KP_extent, self.KP_influence,
                                self.aggregation_mode, modulations)
         n = wf.shape[0]

@@ -27,6 +27,7 @@ import torch.nn.functional as F
 
 from . import _lib, ops
 from ._util import index_bits, ptr, stream_handle, to_dev, workspace
+from .batchnorm import bn_act, linear_bn_act
 from .kpconv import KPConv
 
 
@@ -115,8 +116,13 @@ class BatchNormBlock(nn.Module):
         else:
             self.bias = nn.Parameter(torch.zeros(in_dim, dtype=torch.float32))
 
-    def forward(self, x):
-        return self.batch_norm(x) if self.use_bn else x + self.bias
+    def forward(self, x, slope=None):
+        """BN (+ LeakyReLU(slope) when slope is not None: the activation the
+        enclosing block applies next, fused into the BN launches, csrc/bn.hip)."""
+        if self.use_bn:
+            return bn_act(x, self.batch_norm, slope)
+        x = x + self.bias
+        return x if slope is None else F.leaky_relu(x, slope)
 
 
 class UnaryBlock(nn.Module):
@@ -135,8 +141,10 @@ class UnaryBlock(nn.Module):
             self.leaky_relu = nn.LeakyReLU(l_relu)
 
     def forward(self, x, batch=None):
-        x = self.batch_norm(self.mlp(x))
-        return x if self.no_relu else self.leaky_relu(x)
+        slope = None if self.no_relu else self.leaky_relu.negative_slope
+        if self.use_bn:  # Linear + BN (+ LeakyReLU) as one autograd node (batchnorm.linear_bn_act)
+            return linear_bn_act(x, self.mlp.weight, self.batch_norm.batch_norm, slope)
+        return self.batch_norm(self.mlp(x), slope)
 
 
 def _conv_inputs(block_name, layer_ind, batch):
@@ -170,7 +178,7 @@ class SimpleBlock(nn.Module):
 
     def forward(self, x, batch):
         q, s, nb = _conv_inputs(self.block_name, self.layer_ind, batch)
-        return self.leaky_relu(self.batch_norm(self.KPConv(q, s, nb, x)))
+        return self.batch_norm(self.KPConv(q, s, nb, x), self.leaky_relu.negative_slope)
 
 
 class ResnetBottleneckBlock(nn.Module):
@@ -203,7 +211,7 @@ class ResnetBottleneckBlock(nn.Module):
     def forward(self, features, batch):
         q, s, nb = _conv_inputs(self.block_name, self.layer_ind, batch)
         x = self.unary1(features)
-        x = self.leaky_relu(self.batch_norm_conv(self.KPConv(q, s, nb, x)))
+        x = self.batch_norm_conv(self.KPConv(q, s, nb, x), self.leaky_relu.negative_slope)
         x = self.unary2(x)
         shortcut = max_pool(features, nb) if "strided" in self.block_name else features
         return self.leaky_relu(x + self.unary_shortcut(shortcut))

@@ -186,3 +186,40 @@ def test_deformable_kpconv_training(cuda, influence, mode, modulated):
     _close(conv.weights.grad, W.grad)
     _close(conv.offset_conv.weights.grad, Wo.grad, rtol=1e-3)
     _close(conv.offset_bias.grad, bo.grad, rtol=1e-3)
+
+
+@pytest.mark.parametrize("cin,nb,influence", [(1, 40, "linear"), (5, 80, "linear"), (16, 20, "gaussian"),
+                                              (33, 70, "constant"), (64, 58, "linear"), (512, 61, "linear")])
+def test_mfma_aggregation_matches_wave_kernels(cuda, monkeypatch, cin, nb, influence):
+    """The MFMA aggregation (one wave per (query, channel tile), csrc/kpconv.hip
+    kpconv_wf_mfma_kernel / _backward_) against the per-query wave kernels
+    (O3DML_KPCONV_MFMA=0) and the float64 restatement: WF and the feature
+    gradient, channel counts off and on the 16-lane tiles, > 64 neighbours,
+    shadow entries."""
+    from o3dml_amd import _lib
+    from o3dml_amd._util import ptr, stream_handle
+    from o3dml_amd.kpconv import KPConv
+    q, s, nbr, x = _data(n=300, ns=500, nb=nb, cin=cin, seed=cin)
+    conv = KPConv(15, 3, cin, 8, KP_extent=0.07, radius=0.1, KP_influence=influence).to(cuda)
+    qd, sd, nd, xd = q.float().to(cuda), s.float().to(cuda), nbr.int().to(cuda), x.float().to(cuda)
+    kp = conv.kernel_points.detach().float().contiguous()
+    code = {"constant": 0, "linear": 1, "gaussian": 2}[influence]
+    g = torch.randn((300, 15, cin), device=cuda)
+
+    def run(flag):
+        monkeypatch.setenv("O3DML_KPCONV_MFMA", flag)
+        wf = torch.empty((300, 15, cin), device=cuda)
+        _lib.call("o3dml_kpconv_weighted_features", ptr(qd), 300, ptr(sd), 500, ptr(nd), 32, nb, ptr(xd), cin,
+                  ptr(kp), 15, 0, 0.07, code, 0, None, ptr(wf), stream_handle(cuda))
+        dx = torch.zeros((500, cin), device=cuda)
+        _lib.call("o3dml_kpconv_weighted_features_backward", ptr(qd), 300, ptr(sd), 500, ptr(nd), 32, nb, ptr(g),
+                  cin, ptr(kp), 15, 0, 0.07, code, 0, ptr(dx), stream_handle(cuda))
+        return wf, dx
+
+    wf1, dx1 = run("1")
+    wf0, dx0 = run("0")
+    torch.testing.assert_close(wf1, wf0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dx1, dx0, rtol=1e-5, atol=1e-5)
+    out = torch.matmul(wf1.view(300, -1), conv.weights.detach().view(-1, 8))
+    ref = _ref(q, s, nbr, x, kp.double().cpu(), 0.07, conv.weights.detach().double().cpu(), influence)
+    _close(out, ref)

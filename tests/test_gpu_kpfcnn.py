@@ -73,6 +73,12 @@ def test_segmentation_inputs_match_reference(cuda):
 
 @pytest.mark.parametrize("mode", ["eval", "train"])
 def test_step_matches_reference(cuda, mode):
+    """Logits and loss in both modes, parameter gradients in eval mode at the
+    tight bar.  Training-mode gradients (batch statistics) are discontinuous
+    in the activations on this fixture — a 1e-7 relative perturbation of
+    torch's own BN outputs moves them by ~1e-2 (max-pool argmax ties /
+    LeakyReLU kinks, tools/bn_diag3.py) — so they are pinned against that
+    rounding envelope by test_step_fused_bn_within_rounding_envelope."""
     m = _model(cuda)
     m.train(mode == "train")
     b = _ref_batch(cuda)
@@ -82,13 +88,58 @@ def test_step_matches_reference(cuda, mode):
     assert logits.shape == G[f"{mode}_logits"].shape
     assert _rel(logits.detach().cpu().numpy(), G[f"{mode}_logits"]) < 1e-4
     assert abs(loss.item() - float(G[f"{mode}_loss"])) < 1e-5 * abs(float(G[f"{mode}_loss"]))
+    if mode == "train":
+        return
     params = dict(m.named_parameters())
-    pre = "grad_" if mode == "eval" else "tgrad_"
+    pre = "grad_"
     keys = [k[len(pre):] for k in G.files if k.startswith(pre)]
     assert keys
     for k in keys:
         err = _rel(params[k].grad.cpu().numpy(), G[pre + k])
         assert err < 1e-4, (k, err)
+
+
+def _train_grads(cuda, bn_act=None):
+    from o3dml_amd import kpfcnn
+    if bn_act is not None:
+        kpfcnn.bn_act = bn_act
+        kpfcnn.linear_bn_act = lambda x, w, bn, slope=None: bn_act(torch.nn.functional.linear(x, w), bn, slope)
+    m = _model(cuda)
+    m.train(True)
+    b = _ref_batch(cuda)
+    logits = m(b)
+    loss = torch.nn.functional.cross_entropy(logits, b.labels)
+    loss.backward()
+    params = dict(m.named_parameters())
+    keys = [k[6:] for k in G.files if k.startswith("tgrad_")]
+    return logits, loss, max(_rel(params[k].grad.cpu().numpy(), G["tgrad_" + k]) for k in keys)
+
+
+def test_step_fused_bn_within_rounding_envelope(cuda, monkeypatch):
+    """Training step with the fused BN (csrc/bn.hip): logits and loss at the
+    tight bars; the worst parameter-gradient error no larger than twice what
+    a 1e-7 relative perturbation of torch's own BN outputs produces on this
+    fixture (measured ~1e-2: max-pool argmax / LeakyReLU kinks), i.e. the
+    fused BN moves the gradients no more than fp32 rounding of the
+    reference's activations does."""
+    from o3dml_amd import batchnorm, kpfcnn
+    monkeypatch.setattr(kpfcnn, "bn_act", kpfcnn.bn_act)
+    monkeypatch.setattr(kpfcnn, "linear_bn_act", kpfcnn.linear_bn_act)
+    logits, loss, err = _train_grads(cuda)
+    assert _rel(logits.detach().cpu().numpy(), G["train_logits"]) < 1e-4
+    assert abs(loss.item() - float(G["train_loss"])) < 1e-5 * abs(float(G["train_loss"]))
+    monkeypatch.setenv("O3DML_FUSED_BN", "0")
+    env = 0.0
+    for sign in (1.0, -1.0):
+        gen = torch.Generator(device=cuda).manual_seed(1)
+
+        def noisy(x, bn, slope=None, sign=sign, gen=gen):
+            y = batchnorm.bn_act(x, bn, slope)
+            return y * (1 + sign * 1e-7 * torch.randn(y.shape, generator=gen, device=y.device))
+
+        env = max(env, _train_grads(cuda, noisy)[2])
+    assert env > 1e-4  # the fixture is kink-sensitive (else this test's premise is void)
+    assert err <= 2 * env, (err, env)
 
 
 @pytest.mark.parametrize("dtype", [torch.int32, torch.int64])
