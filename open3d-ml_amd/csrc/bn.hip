@@ -18,6 +18,7 @@
 // save [4C] = (mean, invstd, k = weight * invstd, bias): forward output,
 // backward input.  y = (x - mean) * k + bias, then LeakyReLU when act.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "counters.hpp"
@@ -277,7 +278,13 @@ static void bn_reduce(BnArgs& a, hipStream_t st) {
     const int64_t G = bn_blocks(a.n, a.c);
     a.rows_per_block = ceil_div(a.n, G);
     const int g = static_cast<int>(ceil_div(a.n, a.rows_per_block));
-    uint32_t* counter = tile_counters(st, 1);
+    // O3DML_BN_LAST_BLOCK=0: a separate finalize launch instead of the
+    // last-arriving block (A/B: the arrival chain's latency vs one more launch)
+    static const bool last_block = [] {
+        const char* e = std::getenv("O3DML_BN_LAST_BLOCK");
+        return !e || std::atoi(e) != 0;
+    }();
+    uint32_t* counter = last_block ? tile_counters(st, 1) : nullptr;
     bn_reduce_kernel<MODE><<<g, kBnThreads, 0, st>>>(a, counter);
     O3DML_LAUNCH_CHECK();
     if (!counter) {
