@@ -61,8 +61,8 @@ def parse():
     ap.add_argument("--scenes", type=int, default=64, help="C1-shaped scenes per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
-    ap.add_argument("--randla-frames", type=int, default=3, help="RandLA-Net frames timed (0: skip)")
-    ap.add_argument("--kpconv-steps", type=int, default=5, help="C3 KPFCNN training steps timed (0: skip)")
+    ap.add_argument("--randla-frames", type=int, default=6, help="RandLA-Net frames timed (0: skip)")
+    ap.add_argument("--kpconv-steps", type=int, default=10, help="C3 KPFCNN training steps timed (0: skip)")
     ap.add_argument("--pointpillars-steps", type=int, default=5,
                     help="C5 PointPillars DDP training steps timed on every rank (0: skip)")
     ap.add_argument("--sparse-conv-reps", type=int, default=10, help="C4 sparse-conv forwards timed (0: skip)")
@@ -372,7 +372,7 @@ def kpconv_bench(dev, steps):
         opt.step()
         return batch
 
-    for _ in range(2):
+    for _ in range(3):
         step()
     torch.cuda.synchronize(dev)
     t = time.perf_counter()

@@ -45,7 +45,8 @@ struct BnArgs {
     float* coef;          // [2C] backward dx coefficients
     float* grad_weight;   // nullable
     float* grad_bias;     // nullable
-    double* part;         // [2][G][C]
+    double* part;         // [2][G][C] ([2][C][G] when part_t)
+    int part_t;           // tree finalize: channel-major partials
 };
 
 // accumulate (s, q) of one element for channel ch: forward x, x^2;
@@ -119,8 +120,21 @@ __device__ __forceinline__ void bn_finish(const BnArgs& a, int ch, double S, dou
     }
 }
 
-__device__ __forceinline__ double bn_load(const double* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// index of partial (which: 0 = S, 1 = Q) of block b, channel ch
+__device__ __forceinline__ int64_t bn_pidx(const BnArgs& a, int G, int which, int b, int ch) {
+    return a.part_t ? (static_cast<int64_t>(which) * a.c + ch) * G + b
+                    : (static_cast<int64_t>(which) * G + b) * a.c + ch;
+}
+
+// partial store: agent scope when the last-arriving block reads it in this
+// launch, plain when a separate finalize launch does
+__device__ __forceinline__ void bn_store(double* p, double v, bool agent) {
+    if (agent) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
+__device__ __forceinline__ double bn_load(const double* p, bool agent) {
+    return agent ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
 }
 
 // the totals of the G partials, every thread busy (packed: 256 / C threads
@@ -128,7 +142,7 @@ __device__ __forceinline__ double bn_load(const double* p) {
 // through LDS; wide C: a thread per channel), 8 agent-scope loads in flight
 // per thread; fixed order throughout (deterministic)
 template <int MODE>
-__device__ void bn_finalize_block(const BnArgs& a, int G) {
+__device__ void bn_finalize_block(const BnArgs& a, int G, bool agent) {
     __shared__ double fs[kBnThreads], fq[kBnThreads];
     const int tid = threadIdx.x, c = a.c;
     const int per = c <= kBnThreads ? kBnThreads / c : 1;
@@ -141,8 +155,8 @@ __device__ void bn_finalize_block(const BnArgs& a, int G) {
                 double vs[8], vq[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
-                    vs[u] = bn_load(a.part + static_cast<int64_t>(b + u * per) * c + ch);
-                    vq[u] = bn_load(a.part + (static_cast<int64_t>(G) + b + u * per) * c + ch);
+                    vs[u] = bn_load(a.part + static_cast<int64_t>(b + u * per) * c + ch, agent);
+                    vq[u] = bn_load(a.part + (static_cast<int64_t>(G) + b + u * per) * c + ch, agent);
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
@@ -151,8 +165,8 @@ __device__ void bn_finalize_block(const BnArgs& a, int G) {
                 }
             }
             for (; b < G; b += per) {
-                S += bn_load(a.part + static_cast<int64_t>(b) * c + ch);
-                Q += bn_load(a.part + (static_cast<int64_t>(G) + b) * c + ch);
+                S += bn_load(a.part + static_cast<int64_t>(b) * c + ch, agent);
+                Q += bn_load(a.part + (static_cast<int64_t>(G) + b) * c + ch, agent);
             }
         }
         if (c <= kBnThreads) {
@@ -198,10 +212,8 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(BnArgs a, uint32_
                 S += sh_s[k * c + tid];
                 Q += sh_q[k * c + tid];
             }
-            __hip_atomic_store(a.part + static_cast<int64_t>(blockIdx.x) * c + tid, S, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.part + (static_cast<int64_t>(G) + blockIdx.x) * c + tid, Q, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            bn_store(a.part + bn_pidx(a, G, 0, blockIdx.x, tid), S, counter != nullptr);
+            bn_store(a.part + bn_pidx(a, G, 1, blockIdx.x, tid), Q, counter != nullptr);
         }
     } else {
         // channel blocks of 256: thread -> channel cb + tid over every row
@@ -210,10 +222,8 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(BnArgs a, uint32_
             if (ch >= c) break;
             double s = 0.0, q = 0.0;
             bn_rows<MODE>(a, r0, r1, 1, ch, s, q);
-            __hip_atomic_store(a.part + static_cast<int64_t>(blockIdx.x) * c + ch, s, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.part + (static_cast<int64_t>(G) + blockIdx.x) * c + ch, q, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            bn_store(a.part + bn_pidx(a, G, 0, blockIdx.x, ch), s, counter != nullptr);
+            bn_store(a.part + bn_pidx(a, G, 1, blockIdx.x, ch), q, counter != nullptr);
         }
     }
     if (!counter) return;  // bn_finalize_kernel finishes
@@ -225,13 +235,47 @@ __global__ void __launch_bounds__(kBnThreads) bn_reduce_kernel(BnArgs a, uint32_
     if (tid == 0) s_last = atomicAdd(counter, 1u) == static_cast<uint32_t>(G) - 1;
     __syncthreads();
     if (!s_last) return;
-    bn_finalize_block<MODE>(a, G);
+    bn_finalize_block<MODE>(a, G, true);
     if (tid == 0) atomicExch(counter, 0u);  // ready for the next launch
 }
 
 template <int MODE>
 __global__ void __launch_bounds__(kBnThreads) bn_finalize_kernel(BnArgs a, int G) {
-    bn_finalize_block<MODE>(a, G);
+    bn_finalize_block<MODE>(a, G, false);
+}
+
+// tree finalize: one workgroup per channel sums its G (<= 1,024) channel-major
+// partials (coalesced, <= 4 loads per thread, all in flight) and reduces them
+// through LDS in a fixed order (deterministic)
+template <int MODE>
+__global__ void __launch_bounds__(kBnThreads) bn_finalize_tree_kernel(BnArgs a, int G) {
+    __shared__ double fs[kBnThreads], fq[kBnThreads];
+    const int ch = blockIdx.x, tid = threadIdx.x;
+    const double* ps = a.part + static_cast<int64_t>(ch) * G;
+    const double* pq = a.part + (static_cast<int64_t>(a.c) + ch) * G;
+    double S = 0.0, Q = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int b = tid + u * kBnThreads;
+        if (b < G) {
+            S += ps[b];
+            Q += pq[b];
+        }
+    }
+    fs[tid] = S;
+    fq[tid] = Q;
+    __syncthreads();
+    for (int h = kBnThreads / 2; h > 0; h >>= 1) {
+        if (tid < h) {
+            fs[tid] += fs[tid + h];
+            fq[tid] += fq[tid + h];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        bn_finish<MODE>(a, ch, fs[0], fq[0]);
+        if (MODE == 0 && ch == 0 && a.training && a.num_batches) a.num_batches[0] += 1;
+    }
 }
 
 // eval forward: save from the running statistics
@@ -269,8 +313,23 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_kernel(BnArgs a, float* _
     }
 }
 
+// finalize of the partial sums (O3DML_BN_FINALIZE, A/B): 0 = the
+// last-arriving block of the reduce launch (<= 128 partials, 64 elements per
+// thread), 1 = a separate one-workgroup launch (same partials), 2 = tree:
+// <= 1,024 partials (8 elements per thread: one round of loads) and a
+// workgroup per channel
+static int bn_finalize_mode() {
+    static const int m = [] {
+        const char* e = std::getenv("O3DML_BN_FINALIZE");
+        return e ? std::atoi(e) : 0;
+    }();
+    return m;
+}
+
 static int64_t bn_blocks(int64_t n, int c) {
-    return std::max<int64_t>(1, std::min<int64_t>(kBnMaxBlocks, ceil_div(n * c, kBnThreads * 64)));
+    const bool tree = bn_finalize_mode() == 2;
+    return std::max<int64_t>(1, std::min<int64_t>(tree ? 1024 : kBnMaxBlocks,
+                                                  ceil_div(n * c, kBnThreads * (tree ? 8 : 64))));
 }
 
 template <int MODE>
@@ -278,16 +337,15 @@ static void bn_reduce(BnArgs& a, hipStream_t st) {
     const int64_t G = bn_blocks(a.n, a.c);
     a.rows_per_block = ceil_div(a.n, G);
     const int g = static_cast<int>(ceil_div(a.n, a.rows_per_block));
-    // O3DML_BN_LAST_BLOCK=0: a separate finalize launch instead of the
-    // last-arriving block (A/B: the arrival chain's latency vs one more launch)
-    static const bool last_block = [] {
-        const char* e = std::getenv("O3DML_BN_LAST_BLOCK");
-        return !e || std::atoi(e) != 0;
-    }();
-    uint32_t* counter = last_block ? tile_counters(st, 1) : nullptr;
+    const int fm = bn_finalize_mode();
+    a.part_t = fm == 2;
+    uint32_t* counter = fm == 0 ? tile_counters(st, 1) : nullptr;
     bn_reduce_kernel<MODE><<<g, kBnThreads, 0, st>>>(a, counter);
     O3DML_LAUNCH_CHECK();
-    if (!counter) {
+    if (fm == 2) {
+        bn_finalize_tree_kernel<MODE><<<a.c, kBnThreads, 0, st>>>(a, g);
+        O3DML_LAUNCH_CHECK();
+    } else if (!counter) {
         bn_finalize_kernel<MODE><<<1, kBnThreads, 0, st>>>(a, g);
         O3DML_LAUNCH_CHECK();
     }
