@@ -533,6 +533,36 @@ int o3dml_sgemm_splitk(int trans_a, int trans_b, int64_t m, int64_t n, int64_t k
                        const float* b, int64_t ldb, float* c, int64_t ldc, void* workspace, size_t workspace_bytes,
                        void* stream);
 
+/* ---- KPFCNN layers as one call per direction (UnaryBlock: Linear without
+ * bias + BatchNorm1d + LeakyReLU, kpconv.py:1255-1295; rigid KPConv:
+ * aggregation + WF @ W, kpconv.py:1005-1159), composed from o3dml_sgemm*,
+ * o3dml_batch_norm_* and o3dml_kpconv_weighted_features* on one stream.
+ * linear_bn: w [cout, cin]; z [n, cout] = x w^T (kept for the backward); y =
+ * act(bn(z)); backward: dz scratch [n, cout], dx / dw / dgamma / dbeta nullable.
+ * kpconv_rigid: w [K cin, cout]; wf [n, K, cin] kept for the backward; gwf
+ * scratch [n, K cin]; dx [n_support, cin] zeroed by the call. */
+size_t o3dml_linear_bn_workspace_size(int64_t n, int cin, int cout);
+int o3dml_linear_bn_forward(const float* x, int64_t n, int cin, const float* w, int cout, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                            float momentum, float eps, int training, int act, float slope, float* z, float* y,
+                            float* save, void* workspace, size_t workspace_bytes, void* stream);
+int o3dml_linear_bn_backward(const float* gy, const float* x, int64_t n, int cin, const float* w, int cout,
+                             const float* z, const float* save, int training, int act, float slope, float* dz,
+                             float* dx, float* dw, float* dgamma, float* dbeta, void* workspace,
+                             size_t workspace_bytes, void* stream);
+size_t o3dml_kpconv_rigid_workspace_size(int64_t n, int nb, int64_t n_support, int K, int cin, int cout,
+                                         int deterministic);
+int o3dml_kpconv_rigid_forward(const float* q_pts, int64_t n, const float* s_pts, int64_t n_support,
+                               const void* neighbors, int index_bits, int nb, const float* x, int cin,
+                               const float* kernel_points, int K, float extent, int influence, int closest,
+                               const float* w, int cout, float* wf, float* out, void* workspace,
+                               size_t workspace_bytes, void* stream);
+int o3dml_kpconv_rigid_backward(const float* q_pts, int64_t n, const float* s_pts, int64_t n_support,
+                                const void* neighbors, int index_bits, int nb, const float* g, int cin,
+                                const float* kernel_points, int K, float extent, int influence, int closest,
+                                const float* w, int cout, const float* wf, float* gwf, float* dx, float* dw,
+                                int deterministic, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- KPFCNN BatchNorm1d (+ LeakyReLU) over [N, C] rows (replaces
  * nn.BatchNorm1d + nn.LeakyReLU of BatchNormBlock / UnaryBlock / SimpleBlock /
  * ResnetBottleneckBlock, ml3d/torch/models/kpconv.py:1213-1464).

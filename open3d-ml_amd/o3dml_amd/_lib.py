@@ -93,6 +93,16 @@ SIGNATURES = {
     "o3dml_sgemm_splitk_workspace_size": (c_sz, [c_i64, c_i64, c_i64]),
     "o3dml_sgemm_splitk": (c_i32, [c_i32, c_i32, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_sz,
                                    c_p]),
+    "o3dml_linear_bn_workspace_size": (c_sz, [c_i64, c_i32, c_i32]),
+    "o3dml_linear_bn_forward": (c_i32, [c_p, c_i64, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_f32, c_f32, c_i32,
+                                        c_i32, c_f32, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "o3dml_linear_bn_backward": (c_i32, [c_p, c_p, c_i64, c_i32, c_p, c_i32, c_p, c_p, c_i32, c_i32, c_f32, c_p, c_p,
+                                         c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "o3dml_kpconv_rigid_workspace_size": (c_sz, [c_i64, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32]),
+    "o3dml_kpconv_rigid_forward": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_i32, c_f32,
+                                           c_i32, c_i32, c_p, c_i32, c_p, c_p, c_p, c_sz, c_p]),
+    "o3dml_kpconv_rigid_backward": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_i32, c_f32,
+                                            c_i32, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_i32, c_p, c_sz, c_p]),
     "o3dml_batch_norm_workspace_size": (c_sz, [c_i64, c_i32]),
     "o3dml_batch_norm_forward": (c_i32, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_f32, c_f32, c_i32, c_i32, c_f32,
                                          c_p, c_p, c_p, c_sz, c_p]),

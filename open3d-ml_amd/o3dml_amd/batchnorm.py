@@ -20,7 +20,7 @@ import os
 import torch
 
 from . import _lib
-from ._util import mm, ptr, stream_handle
+from ._util import ptr, stream_handle
 
 _WS = {}  # (n, c) -> workspace bytes
 
@@ -79,12 +79,40 @@ class _BnAct(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
+_LWS = {}  # (n, cin, cout) -> workspace bytes of the one-call Linear + BN
+
+
+def _lws(n, cin, cout, dev):
+    b = _LWS.get((n, cin, cout))
+    if b is None:
+        b = _LWS[(n, cin, cout)] = max(int(_lib.load().o3dml_linear_bn_workspace_size(n, cin, cout)), 1)
+    return torch.empty(b, dtype=torch.uint8, device=dev)
+
+
 class _LinearBnAct(torch.autograd.Function):
+    """One C call per direction (csrc/kpfcnn_ops.cpp o3dml_linear_bn_*):
+    z = x W^T (rocBLAS), then the BN launches; backward the BN launches then
+    dX = dZ W and dW = dZ^T x."""
+
     @staticmethod
     def forward(ctx, x, w, weight, bias, bn, training, slope):
         x = x.contiguous()
-        z = mm(x, w.contiguous(), tb=True)
-        y, save = _bn_forward(z, weight, bias, bn, training, slope)
+        w = w.detach().contiguous()
+        n, cin = x.shape
+        cout = w.shape[0]
+        z = torch.empty((n, cout), dtype=torch.float32, device=x.device)
+        y = torch.empty_like(z)
+        save = torch.empty(4 * cout, dtype=torch.float32, device=x.device)
+        ws = _lws(n, cin, cout, x.device)
+        track = training and bn.track_running_stats and bn.running_mean is not None
+        if training and bn.momentum is None:
+            raise NotImplementedError("bn_act: cumulative moving average (momentum=None)")
+        use_running = track or not training
+        _lib.call("o3dml_linear_bn_forward", ptr(x), n, cin, ptr(w), cout, ptr(weight), ptr(bias),
+                  ptr(bn.running_mean) if use_running else None, ptr(bn.running_var) if use_running else None,
+                  ptr(bn.num_batches_tracked) if track else None, float(bn.momentum or 0.0), float(bn.eps),
+                  int(training), int(slope is not None), float(slope or 0.0), ptr(z), ptr(y), ptr(save), ptr(ws),
+                  ws.numel(), stream_handle(x.device))
         ctx.save_for_backward(x, w, z, save)
         ctx.meta = (training, slope, weight is not None, bias is not None)
         return y
@@ -93,10 +121,19 @@ class _LinearBnAct(torch.autograd.Function):
     def backward(ctx, g):
         x, w, z, save = ctx.saved_tensors
         training, slope, has_w, has_b = ctx.meta
-        dz, dwt, db = _bn_backward(g.contiguous(), z, save, training, slope, True,
-                                   has_w and ctx.needs_input_grad[2], has_b and ctx.needs_input_grad[3])
-        dx = mm(dz, w) if ctx.needs_input_grad[0] else None
-        dW = mm(dz, x, ta=True) if ctx.needs_input_grad[1] else None
+        g = g.contiguous()
+        n, cin = x.shape
+        cout = w.shape[0]
+        dev = x.device
+        dz = torch.empty((n, cout), dtype=torch.float32, device=dev)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dW = torch.empty_like(w) if ctx.needs_input_grad[1] else None
+        dwt = torch.empty(cout, dtype=torch.float32, device=dev) if has_w and ctx.needs_input_grad[2] else None
+        db = torch.empty(cout, dtype=torch.float32, device=dev) if has_b and ctx.needs_input_grad[3] else None
+        ws = _lws(n, cin, cout, dev)
+        _lib.call("o3dml_linear_bn_backward", ptr(g), ptr(x), n, cin, ptr(w), cout, ptr(z), ptr(save), int(training),
+                  int(slope is not None), float(slope or 0.0), ptr(dz), ptr(dx), ptr(dW), ptr(dwt), ptr(db), ptr(ws),
+                  ws.numel(), stream_handle(dev))
         return dx, dW, dwt, db, None, None, None
 
 

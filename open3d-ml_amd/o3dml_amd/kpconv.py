@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from ._util import gpu_device, index_bits, mm, ptr, stream_handle, to_dev, workspace
+from ._util import gpu_device, index_bits, ptr, stream_handle, to_dev, workspace
 
 _INFLUENCE = {"constant": 0, "linear": 1, "gaussian": 2}
 
@@ -90,35 +90,57 @@ class _WeightedFeatures(torch.autograd.Function):
         return dx, None, None, None, dkp, None, None, None, None, dmod
 
 
+_KWS = {}  # (n, nb, n_support, K, cin, cout, deterministic) -> workspace bytes
+
+
 class _KPConvRigid(torch.autograd.Function):
-    """Rigid KPConv as ONE autograd node: the HIP aggregation WF [n, K, Cin]
-    and the GEMM out = WF.view(n, K Cin) @ W.view(K Cin, Cout) in the forward;
-    dWF = g W^T, dW = WF^T g and the aggregation backward in the backward
-    (the matmul / view nodes of the unfused form cost host time per call)."""
+    """Rigid KPConv as ONE autograd node and one C call per direction
+    (csrc/kpfcnn_ops.cpp o3dml_kpconv_rigid_*): the HIP aggregation WF [n, K,
+    Cin] and out = WF.view(n, K Cin) @ W.view(K Cin, Cout) (rocBLAS) forward;
+    dW = WF^T g, dWF = g W^T and the aggregation backward backward."""
+
+    @staticmethod
+    def _ws(n, nb, ns, K, cin, cout, det, dev):
+        key = (n, nb, ns, K, cin, cout, det)
+        b = _KWS.get(key)
+        if b is None:
+            b = _KWS[key] = max(int(_lib.load().o3dml_kpconv_rigid_workspace_size(n, nb, ns, K, cin, cout, det)), 1)
+        return torch.empty(b, dtype=torch.uint8, device=dev)
 
     @staticmethod
     def forward(ctx, x, w, q_pts, s_pts, nbr, kp, extent, influence, closest):
         kpd = kp.detach().contiguous()
-        wf = _wf_forward(x, q_pts, s_pts, nbr, kpd, False, extent, influence, closest, None)
-        n, K, cin = wf.shape
-        out = mm(wf.view(n, K * cin), w.detach().reshape(K * cin, -1).contiguous())
-        ctx.save_for_backward(w, wf, q_pts, s_pts, nbr, kpd)
-        ctx.meta = (extent, influence, closest, x.shape[0])
+        w2 = w.detach().reshape(-1, w.shape[-1]).contiguous()
+        n, nb = nbr.shape
+        K, cin, cout = kpd.shape[-2], x.shape[1], w2.shape[1]
+        wf = torch.empty((n, K, cin), dtype=torch.float32, device=x.device)
+        out = torch.empty((n, cout), dtype=torch.float32, device=x.device)
+        ws = _KPConvRigid._ws(n, nb, s_pts.shape[0], K, cin, cout, 0, x.device)
+        _lib.call("o3dml_kpconv_rigid_forward", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr),
+                  index_bits(nbr.dtype), nb, ptr(x), cin, ptr(kpd), K, float(extent), influence, int(closest),
+                  ptr(w2), cout, ptr(wf), ptr(out), ptr(ws), ws.numel(), stream_handle(x.device))
+        ctx.save_for_backward(w2, wf, q_pts, s_pts, nbr, kpd)
+        ctx.meta = (extent, influence, closest, x.shape[0], tuple(w.shape))
         return out
 
     @staticmethod
     def backward(ctx, g):
-        w, wf, q_pts, s_pts, nbr, kp = ctx.saved_tensors
-        extent, influence, closest, n_s = ctx.meta
+        w2, wf, q_pts, s_pts, nbr, kp = ctx.saved_tensors
+        extent, influence, closest, n_s, wshape = ctx.meta
         n, K, cin = wf.shape
+        nb = nbr.shape[1]
+        cout = w2.shape[1]
+        dev = wf.device
         g = g.contiguous()
-        w2 = w.detach().reshape(K * cin, -1).contiguous()
-        dx = dw = None
-        if ctx.needs_input_grad[1]:
-            dw = mm(wf.view(n, K * cin), g, ta=True).view_as(w)
-        if ctx.needs_input_grad[0]:
-            gwf = mm(g, w2, tb=True)
-            dx = _wf_backward_x(gwf, q_pts, s_pts, nbr, kp, False, extent, influence, closest, n_s, cin)
+        dw = torch.empty(wshape, dtype=torch.float32, device=dev) if ctx.needs_input_grad[1] else None
+        need_x = ctx.needs_input_grad[0]
+        det = int(need_x and torch.are_deterministic_algorithms_enabled())
+        dx = torch.empty((n_s, cin), dtype=torch.float32, device=dev) if need_x else None
+        gwf = torch.empty((n, K * cin), dtype=torch.float32, device=dev) if need_x else None
+        ws = _KPConvRigid._ws(n, nb, n_s, K, cin, cout, det, dev)
+        _lib.call("o3dml_kpconv_rigid_backward", ptr(q_pts), n, ptr(s_pts), n_s, ptr(nbr), index_bits(nbr.dtype), nb,
+                  ptr(g), cin, ptr(kp), K, float(extent), influence, int(closest), ptr(w2), cout, ptr(wf), ptr(gwf),
+                  ptr(dx), ptr(dw), det, ptr(ws), ws.numel(), stream_handle(dev))
         return dx, dw, None, None, None, None, None, None, None
 
 
