@@ -6,13 +6,13 @@
 // torch runs a BN + LeakyReLU pair as 4 launches forward (statistics, running
 // update, transform, activation) and 3 backward (activation, reduce,
 // element-wise), and its channels-last statistics kernel reads a 40,000 x 128
-// layer at ~0.25 TB/s.  Here: forward = one reduce launch (per-block partial
-// sums of x and x^2 in double, the last-arriving block sums the partials in
-// block order — deterministic — and finalises mean, invstd, the running
-// statistics and num_batches_tracked) + one apply launch (normalise, affine,
-// LeakyReLU); backward = one reduce launch (sum dz and dz * xhat with dz the
-// activation's gradient, recomputed from x; finalised into grad_weight,
-// grad_bias and the dx coefficients) + one apply launch.  The statistics are
+// layer at ~0.25 TB/s.  Here: forward = a reduce launch (per-block partial
+// sums of x and x^2 in double), a finalize launch (a workgroup per channel
+// sums the partials in a fixed order — deterministic — and finalises mean,
+// invstd, the running statistics and num_batches_tracked) and an apply launch
+// (normalise, affine, LeakyReLU); backward = the same three for sum dz and
+// dz * xhat (dz the activation's gradient, recomputed from x; finalised into
+// grad_weight, grad_bias and the dx coefficients).  The statistics are
 // accumulated in double (closer to the fp64 reference than fp32 Welford).
 //
 // save [4C] = (mean, invstd, k = weight * invstd, bias): forward output,
@@ -313,15 +313,19 @@ __global__ void __launch_bounds__(kBnThreads) bn_apply_kernel(BnArgs a, float* _
     }
 }
 
-// finalize of the partial sums (O3DML_BN_FINALIZE, A/B): 0 = the
-// last-arriving block of the reduce launch (<= 128 partials, 64 elements per
-// thread), 1 = a separate one-workgroup launch (same partials), 2 = tree:
-// <= 1,024 partials (8 elements per thread: one round of loads) and a
-// workgroup per channel
+// finalize of the partial sums (O3DML_BN_FINALIZE): 2 (default) = tree:
+// <= 1,024 partials (8 elements per thread: one round of loads in flight) and
+// a separate launch with a workgroup per channel; 0 = the last-arriving block
+// of the reduce launch (<= 128 partials, 64 elements per thread); 1 = a
+// separate one-workgroup launch over those.  Measured on the C3 step (kernel
+// trace, last 5 steps, gpurun_out/r4s10): reduce + finalize 22.3 -> 10.2 +
+// 4.8 us backward, 17.5 -> 7.4 + 5.1 us forward; 9.74 -> 9.19 ms of kernel
+// time per step for 92 more launches.  Per-channel sums in a fixed order in
+// every mode (deterministic).
 static int bn_finalize_mode() {
     static const int m = [] {
         const char* e = std::getenv("O3DML_BN_FINALIZE");
-        return e ? std::atoi(e) : 0;
+        return e ? std::atoi(e) : 2;
     }();
     return m;
 }

@@ -15,6 +15,12 @@ for rep in 1 2 3; do
     echo "$lib | frs $f | $s | c3 $k"
   done
 done
+for m in 0 2; do
+  (cd /tmp && O3DML_BN_FINALIZE=$m timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/bn$m" -o run --output-format csv \
+      -- python3 "$R/bench.py" $A > "$OUT/bn$m.log" 2>&1) || { echo "bn$m prof rc=$?"; exit 1; }
+  f=$(find $OUT/bn$m -name '*kernel_trace.csv' | head -1)
+  echo "BN_FINALIZE=$m: $(python3 tools/trace_window_stats.py $f nll_loss_forward 5 60 | grep -E 'window|bn_' | tr -s ' ' | tr '\n' ';')"
+done
 SECTION=randla TAG=r4s10 bash tools/prof_section.sh || exit 1
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/single24" -o run --output-format csv \
     -- python3 "$R/tools/frs_single.py" 24 5 > "$OUT/single24.log" 2>&1) || { echo "single24 rc=$?"; exit 1; }
