@@ -591,6 +591,8 @@ class PointPillars(nn.Module):
                 list(points), decorate=self.voxel_encoder.decoration())
         x = self.voxel_encoder.forward_decorated(voxels, num_points)
         x = self.middle_encoder(x, coors, len(points))
+        if next(self.backbone.parameters()).is_contiguous(memory_format=torch.channels_last) and x.dim() == 4:
+            x = x.contiguous(memory_format=torch.channels_last)  # a channels-last model: NHWC BEV canvas
         return self.neck(self.backbone(x))
 
     def forward(self, inputs):
