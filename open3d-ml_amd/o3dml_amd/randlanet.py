@@ -736,16 +736,22 @@ class SemSegInference:
         graph.replay()
         return out
 
+    _MAX_STEPS = 4  # patch-step states (and graphs) kept per model
+
     def _patch_step(self, n_sub, replay=False):
         """The patch-step state (and its graph) for a cloud of n_sub points,
-        kept on the model per (device, capacity, dtype, smooth, replay)."""
+        kept on the model per (device, capacity, dtype, smooth, replay): up to
+        _MAX_STEPS of them, so scans whose sub-clouds fall into a few
+        capacity classes do not re-capture the graph when they alternate."""
         cap = -(-n_sub // _CAP_STEP) * _CAP_STEP
         key = (str(self.device), cap, self.probs_dtype, self.test_smooth, bool(replay))
-        cur = self.model.__dict__.get("_o3dml_patch_step")
-        if cur is None or cur[0] != key:
-            cur = (key, _PatchStep(self, cap, replay))
-            self.model.__dict__["_o3dml_patch_step"] = cur
-        step = cur[1]
+        steps = self.model.__dict__.setdefault("_o3dml_patch_step", {})
+        step = steps.pop(key, None)
+        if step is None:
+            step = _PatchStep(self, cap, replay)
+            while len(steps) >= self._MAX_STEPS:
+                steps.pop(next(iter(steps)))  # least recently used first
+        steps[key] = step  # most recently used last
         step.inf = self
         return step
 

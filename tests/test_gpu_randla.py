@@ -300,10 +300,12 @@ def test_patch_graph_survives_frames_and_drops_with_weights(cuda):
 
     a, b = cloud(), cloud()
     SemSegInference(m, seed=1, use_graph=True, probs_dtype=torch.float32).run(a)
-    step = m.__dict__["_o3dml_patch_step"][1]
+    steps = m.__dict__["_o3dml_patch_step"]
+    assert len(steps) == 1
+    step = next(iter(steps.values()))
     folded = m.encoder[0].mlp1.folded()[0]
     lg, pg = SemSegInference(m, seed=2, use_graph=True, probs_dtype=torch.float32).run(b)
-    assert m.__dict__["_o3dml_patch_step"][1] is step and step.graph is not None
+    assert step in m.__dict__["_o3dml_patch_step"].values() and step.graph is not None
     assert m.encoder[0].mlp1.folded()[0] is folded
     le, pe = SemSegInference(m, seed=2, use_graph=False, probs_dtype=torch.float32).run(b)
     torch.testing.assert_close(pg, pe, rtol=0, atol=1e-6)
@@ -353,3 +355,26 @@ def test_knn_select_in_graph_equals_eager(cuda):
         rest = torch.ones(n, dtype=torch.bool, device=cuda)
         rest[got] = False
         assert float(d[got].max()) <= float(d[rest].min()) * (1 + 1e-5), i
+
+
+def test_patch_steps_kept_per_capacity(cuda):
+    """Scans whose sub-clouds fall into different capacity classes keep one
+    captured patch step each (up to _MAX_STEPS): alternating between them
+    replays the existing graphs instead of re-capturing."""
+    from o3dml_amd.randlanet import RandLANet, SemSegInference
+    torch.manual_seed(0)
+    m = RandLANet(num_points=4096).to(cuda).eval()
+    rng = np.random.default_rng(7)
+
+    def cloud(n):
+        p = np.stack([rng.uniform(-20, 20, n), rng.uniform(-20, 20, n), rng.uniform(-2, 2, n)], 1)
+        return torch.from_numpy(p.astype(np.float32)).to(cuda)
+
+    small, large = cloud(20000), cloud(40000)
+    SemSegInference(m, seed=1, use_graph=True).run(small)
+    SemSegInference(m, seed=1, use_graph=True).run(large)
+    steps = dict(m.__dict__["_o3dml_patch_step"])
+    assert len(steps) == 2 and all(s.graph is not None for s in steps.values())
+    SemSegInference(m, seed=2, use_graph=True).run(small)
+    after = m.__dict__["_o3dml_patch_step"]
+    assert set(after) == set(steps) and all(after[k] is steps[k] for k in steps)
