@@ -184,8 +184,17 @@ static DensePlan dense_plan(int64_t n, int k, int m) {
     p.tr = ceil_div(n, 64) * p.gy < 1024 ? 2 : 4;
     p.gx = static_cast<unsigned>(ceil_div(n, 16 * p.tr));
     // split K until ~4 blocks per CU (1024), each split >= 2 chunks
+    // (O3DML_DENSE_TARGET / O3DML_DENSE_MIN_CHUNKS: A/B of the split plan)
+    static const int64_t target = [] {
+        const char* e = std::getenv("O3DML_DENSE_TARGET");
+        return e ? std::atoll(e) : 1024;
+    }();
+    static const int min_chunks = [] {
+        const char* e = std::getenv("O3DML_DENSE_MIN_CHUNKS");
+        return e ? std::max(1, std::atoi(e)) : 2;
+    }();
     const int64_t blocks = static_cast<int64_t>(p.gx) * p.gy;
-    int s = static_cast<int>(std::min<int64_t>(ceil_div(1024, blocks), ceil_div(k, 2 * kDenseKC)));
+    int s = static_cast<int>(std::min<int64_t>(ceil_div(target, blocks), ceil_div(k, min_chunks * kDenseKC)));
     s = std::max(1, std::min(s, 16));
     p.k_per_split = static_cast<int>(ceil_div(ceil_div(k, s), kDenseKC) * kDenseKC);
     p.splits = static_cast<int>(ceil_div(k, p.k_per_split));
