@@ -163,7 +163,8 @@ __device__ void topk_compact(KeyFn key, int64_t n, uint32_t T, uint32_t take_eq,
 // ---------------------------------------------------------------------------
 constexpr int kSelThreads = 256;
 constexpr int kSelMaxWgs = 256;
-constexpr int kSelChunkMin = 4096;  // keys per workgroup at least (fewer global histogram atomics)
+constexpr int kSelChunkMin = 4096;  // histogram passes: keys per workgroup at least (fewer global atomics)
+constexpr int kSelChunkOut = 1024;  // count / ordered write: keys per workgroup at least (tiles walked in order)
 
 struct SelGlobal {
     uint32_t hist[3][kTopkBins];  // zeroed per call (one memset)
@@ -414,6 +415,11 @@ static void sel_run(const float* pts, int64_t n, const float* query, int metric,
     const int64_t G = std::max<int64_t>(1, std::min<int64_t>(kSelMaxWgs, ceil_div(n, kSelChunkMin)));
     const int64_t chunk = ceil_div(n, G);
     const unsigned grid = static_cast<unsigned>(G);
+    // the count / write launches walk their chunk tile by tile (two barriers
+    // per 256 keys): smaller chunks, more workgroups
+    const int64_t Gw = std::max<int64_t>(1, std::min<int64_t>(kSelMaxWgs, ceil_div(n, kSelChunkOut)));
+    const int64_t chunk_w = ceil_div(n, Gw);
+    const unsigned grid_w = static_cast<unsigned>(ceil_div(n, chunk_w));
 #define O3DML_SELH(M, P) \
     sel_hist_kernel<M, P><<<grid, kSelThreads, 0, st>>>(pts, n, query, ignore, rs, q, k, chunk, keys, g)
 #define O3DML_SELH3(M) \
@@ -426,9 +432,10 @@ static void sel_run(const float* pts, int64_t n, const float* query, int metric,
 #undef O3DML_SELH3
 #undef O3DML_SELH
     O3DML_LAUNCH_CHECK();
-    sel_count_kernel<<<grid, kSelThreads, 0, st>>>(n, rs, q, k, chunk, keys, g);
+    sel_count_kernel<<<grid_w, kSelThreads, 0, st>>>(n, rs, q, k, chunk_w, keys, g);
     O3DML_LAUNCH_CHECK();
-    sel_write_kernel<SINK><<<grid, kSelThreads, 0, st>>>(n, rs, q, k, chunk, keys, g, out_ids, kcap, sel_key, sel_idx);
+    sel_write_kernel<SINK><<<grid_w, kSelThreads, 0, st>>>(n, rs, q, k, chunk_w, keys, g, out_ids, kcap, sel_key,
+                                                           sel_idx);
     O3DML_LAUNCH_CHECK();
 }
 

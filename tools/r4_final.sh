@@ -5,6 +5,8 @@
 # and its HBM PMC passes (u32 temp rows).  Stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$(pwd); T=${TAG:-r4fin}; OUT=$R/gpurun_out/$T; mkdir -p "$OUT"; export TMPDIR=/tmp
+( while true; do sleep 45; echo "[hb] $(date +%T)"; done ) & HB=$!
+trap "kill $HB" EXIT
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
     || { echo "pytest rc=$?"; grep -E "^(FAILED|ERROR)|passed|failed" "$OUT/pytest_gpu.log" | tail -20; exit 1; }
 tail -1 "$OUT/pytest_gpu.log"
