@@ -643,6 +643,19 @@ int o3dml_ragged_to_dense(const void* values, const int64_t* row_splits, int64_t
 int o3dml_reduce_subarrays_sum(const float* values, const int64_t* row_splits, int64_t n_rows, float* out,
                                void* stream);
 
+/* ---- stable key sort -----------------------------------------------------
+ * The stable LSD radix sort behind every order the ops define (bins, voxels,
+ * grid cells, tile orders): (keys, vals) sorted by key, ties in input order,
+ * for keys < 2^end_bit (the passes cover only those bits); vals_in NULL =
+ * element index.  key_bytes 4 or 8;
+ * small_kind picks the one-workgroup sort used for n <= 8,192 (-1 default,
+ * 0 LSD radix, 1 bitonic).  No reference entry point: Open3D sorts inside
+ * its C++ ops (e.g. std::stable_sort in the voxelize / grid CPU kernels). */
+size_t o3dml_sort_pairs_workspace_size(int64_t n, int key_bytes);
+int o3dml_sort_pairs(const void* keys_in, const uint32_t* vals_in, void* keys_out, uint32_t* vals_out, int64_t n,
+                     int key_bytes, int end_bit, int small_kind, void* workspace, size_t workspace_bytes,
+                     void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -444,7 +444,138 @@ __global__ void __launch_bounds__(kBsThreads) block_sort_pairs(const K* __restri
     }
 }
 
-// Largest n sorted in one workgroup (bitonic): O3DML_BS_MAX (A/B), default kBsMax
+// Small sorts by LSD radix in ONE workgroup (the default; O3DML_BS_KIND=1 runs
+// the bitonic network above): 4-bit digits, and only the digits in which the
+// keys differ (the OR of key ^ key[0] over the input) — the SparseConvUnet grid
+// keys (three 20-bit fields, a few bits varying in each) take 6 passes, not 16.
+// Each pass is a stable counting pass: digit counters in thread-private LDS
+// columns (u16 pairs packed in a u32), a packed wave scan of the thread's 8
+// counter words, wave totals through LDS, then the ranked scatter into the
+// exchange buffer.  Element i lives in thread i / S, slot i % S (blocked), so
+// counting a thread's slots in order keeps equal digits in input order.
+// Padding slots (pos = ~0) take digit 15 in every pass: they start last and
+// stay last.  N <= 8,192 keeps every rank and packed sum within 16 bits.
+template <class K, int S>
+__global__ void __launch_bounds__(kBsThreads) block_radix_sort_pairs(const K* __restrict__ kin,
+                                                                     const uint32_t* __restrict__ vin,
+                                                                     K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                                     int n, K mask) {
+    constexpr int N = S * kBsThreads;
+    constexpr int kWaves = kBsThreads / 64;
+    static_assert(N <= 8192, "packed 16-bit counters");
+    __shared__ K xk[N];
+    __shared__ uint32_t xp[N];
+    __shared__ uint32_t cnt[8 * kBsThreads];  // [digit pair][thread]
+    __shared__ uint32_t wtot[kWaves][8];
+    __shared__ K wor[kWaves];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {  // coalesced load, blocked read below
+        const int i = s * kBsThreads + t;
+        xk[i] = i < n ? (kin[i] & mask) : K(0);
+    }
+    __syncthreads();
+    const K k0 = xk[0];
+    K key[S];
+    uint32_t pos[S];
+    K vb = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int i = t * S + s;
+        key[s] = xk[i];
+        pos[s] = i < n ? static_cast<uint32_t>(i) : 0xffffffffu;
+        if (i < n) vb |= key[s] ^ k0;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) vb |= __shfl_xor(vb, d, 64);
+    if (lane == 0) wor[w] = vb;
+    __syncthreads();
+    K vbits = 0;
+#pragma unroll
+    for (int v = 0; v < kWaves; ++v) vbits |= wor[v];
+    for (int sh = 0; sh < static_cast<int>(8 * sizeof(K)); sh += 4) {
+        if (((vbits >> sh) & K(15)) == 0) continue;  // uniform: this digit is the same everywhere
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cnt[j * kBsThreads + t] = 0u;
+        uint32_t dg[S], lr[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const uint32_t d = pos[s] != 0xffffffffu ? static_cast<uint32_t>(key[s] >> sh) & 15u : 15u;
+            dg[s] = d;
+            const int a = static_cast<int>(d >> 1) * kBsThreads + t;
+            const int hs = static_cast<int>(d & 1u) * 16;
+            const uint32_t v = cnt[a];
+            lr[s] = (v >> hs) & 0xffffu;
+            cnt[a] = v + (1u << hs);
+        }
+        uint32_t c[8], x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            c[j] = cnt[j * kBsThreads + t];
+            x[j] = wave_inclusive_scan(c[j]);
+        }
+        if (lane == 63) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wtot[w][j] = x[j];
+        }
+        __syncthreads();
+        uint32_t base = 0;  // elements of all digits below 2j
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint32_t wp = 0, tot = 0;
+#pragma unroll
+            for (int v = 0; v < kWaves; ++v) {
+                const uint32_t y = wtot[v][j];
+                wp += v < w ? y : 0u;
+                tot += y;
+            }
+            const uint32_t ex = wp + x[j] - c[j];
+            const uint32_t lo = tot & 0xffffu;
+            const uint32_t p0 = (ex & 0xffffu) + base, p1 = (ex >> 16) + base + lo;
+            cnt[j * kBsThreads + t] = p0 | (p1 << 16);
+            base += lo + (tot >> 16);
+        }
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const uint32_t v = cnt[static_cast<int>(dg[s] >> 1) * kBsThreads + t];
+            const uint32_t r = ((v >> ((dg[s] & 1u) * 16)) & 0xffffu) + lr[s];
+            xk[r] = key[s];
+            xp[r] = pos[s];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            key[s] = xk[t * S + s];
+            pos[s] = xp[t * S + s];
+        }
+        __syncthreads();  // exchange buffer and wave totals free for the next pass
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) xp[t * S + s] = pos[s];
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int i = s * kBsThreads + t;
+        if (i < n) {
+            const uint32_t p = xp[i];
+            kout[i] = kin[p];
+            vout[i] = vin ? vin[p] : p;
+        }
+    }
+}
+
+// Small-sort kind: 0 = LSD radix in one workgroup (default), 1 = bitonic
+// (O3DML_BS_KIND, A/B; o3dml_sort_pairs picks one per call for the tests)
+inline int g_block_sort_kind_override = -1;
+inline int block_sort_kind() {
+    static const int v = [] {
+        const char* e = std::getenv("O3DML_BS_KIND");
+        return e ? std::atoi(e) : 0;
+    }();
+    return g_block_sort_kind_override >= 0 ? g_block_sort_kind_override : v;
+}
+
+// Largest n sorted in one workgroup: O3DML_BS_MAX (A/B), default kBsMax
 inline int64_t block_sort_max() {
     static const int64_t v = [] {
         const char* e = std::getenv("O3DML_BS_MAX");
@@ -485,7 +616,16 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
         // slower: 46 vs 37 us at ~4k keys — dependent LDS latency of the
         // per-round binary searches)
         const int ni = static_cast<int>(n);
-        if (n <= kBsThreads)
+        if (block_sort_kind() == 0) {
+            if (n <= kBsThreads)
+                block_radix_sort_pairs<K, 1><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);
+            else if (n <= 2 * kBsThreads)
+                block_radix_sort_pairs<K, 2><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);
+            else if (n <= 4 * kBsThreads)
+                block_radix_sort_pairs<K, 4><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);
+            else
+                block_radix_sort_pairs<K, 8><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);
+        } else if (n <= kBsThreads)
             block_sort_pairs<K, 1><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);
         else if (n <= 2 * kBsThreads)
             block_sort_pairs<K, 2><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);

@@ -5,6 +5,7 @@
 // left-to-right fp32 summation order (one lane per row) so results are
 // bit-identical to the oracle.
 #include "common.hpp"
+#include "primitives.hpp"
 
 namespace o3dml {
 
@@ -70,5 +71,39 @@ O3DML_API int o3dml_reduce_subarrays_sum(const float* values, const int64_t* row
     reduce_subarrays_sum_kernel<<<stream_grid(n_rows, 256), 256, 0, as_stream(stream)>>>(values, row_splits,
                                                                                          n_rows, out);
     O3DML_LAUNCH_CHECK();
+    O3DML_GUARD_END
+}
+
+// The stable LSD radix sort every op of the path uses (primitives.hpp), as an
+// entry point of its own for tests and callers that sort ids by a key:
+// (keys, vals) sorted by key, ties in input order, for keys < 2^end_bit;
+// vals_in == nullptr means the element index.  key_bytes 4 or 8; small_kind picks the one-workgroup sort
+// for n <= 8,192 (-1 default, 0 LSD radix, 1 bitonic).
+O3DML_API size_t o3dml_sort_pairs_workspace_size(int64_t n, int key_bytes) {
+    return key_bytes == 8 ? prim::radix_sort_workspace_bytes<uint64_t>(n)
+                          : prim::radix_sort_workspace_bytes<uint32_t>(n);
+}
+
+O3DML_API int o3dml_sort_pairs(const void* keys_in, const uint32_t* vals_in, void* keys_out, uint32_t* vals_out,
+                               int64_t n, int key_bytes, int end_bit, int small_kind, void* workspace,
+                               size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(key_bytes == 4 || key_bytes == 8, "sort_pairs: key_bytes must be 4 or 8, got %d", key_bytes);
+    O3DML_REQUIRE(end_bit >= 0 && end_bit <= 8 * key_bytes, "sort_pairs: end_bit %d out of range", end_bit);
+    O3DML_REQUIRE(n < (int64_t(1) << 32), "sort_pairs: %lld keys exceed 32-bit ids", (long long)n);
+    O3DML_REQUIRE(workspace_bytes >= o3dml_sort_pairs_workspace_size(n, key_bytes), "sort_pairs: workspace too small");
+    hipStream_t st = as_stream(stream);
+    Workspace ws(workspace, workspace_bytes);
+    struct KindScope {  // restored on every exit
+        int prev;
+        explicit KindScope(int k) : prev(prim::g_block_sort_kind_override) { prim::g_block_sort_kind_override = k; }
+        ~KindScope() { prim::g_block_sort_kind_override = prev; }
+    } kind_scope(small_kind);
+    if (key_bytes == 8)
+        prim::radix_sort_pairs<uint64_t>(static_cast<const uint64_t*>(keys_in), vals_in,
+                                         static_cast<uint64_t*>(keys_out), vals_out, n, end_bit, ws, st);
+    else
+        prim::radix_sort_pairs<uint32_t>(static_cast<const uint32_t*>(keys_in), vals_in,
+                                         static_cast<uint32_t*>(keys_out), vals_out, n, end_bit, ws, st);
     O3DML_GUARD_END
 }

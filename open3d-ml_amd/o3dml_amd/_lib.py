@@ -173,6 +173,8 @@ SIGNATURES = {
     # ragged.hip
     "o3dml_ragged_to_dense": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p]),
     "o3dml_reduce_subarrays_sum": (c_i32, [c_p, c_p, c_i64, c_p, c_p]),
+    "o3dml_sort_pairs_workspace_size": (c_sz, [c_i64, c_i32]),
+    "o3dml_sort_pairs": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_sz, c_p]),
 }
 
 

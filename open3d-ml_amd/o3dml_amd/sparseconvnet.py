@@ -96,7 +96,8 @@ class InputLayer(nn.Module):
         # voxel of every input point (points outside the range map nowhere, as
         # the reference's zero-initialised reverse map does: voxel 0)
         index_map = torch.zeros(in_positions.shape[0], dtype=torch.int64, device=dev)
-        index_map[pidx] = torch.repeat_interleave(torch.arange(nvox, device=dev), count)
+        index_map[pidx] = torch.repeat_interleave(torch.arange(nvox, device=dev), count,
+                                                  output_size=pidx.shape[0])  # no host read of the sum
         return avg, positions, index_map
 
 
@@ -137,8 +138,9 @@ class Convolution(nn.Module):
         self.net = SparseConv(in_channels=in_channels, filters=filters, kernel_size=kernel_size, use_bias=use_bias,
                               offset=torch.full((3,), offset, dtype=torch.float32), normalize=normalize)
 
-    def forward(self, features_list, in_positions_list, voxel_size=1.0):
-        out_positions_list = [ops.calculate_grid(p) for p in in_positions_list]
+    def forward(self, features_list, in_positions_list, voxel_size=1.0, out_positions_list=None):
+        if out_positions_list is None:  # UNet passes the grids it computed up front
+            out_positions_list = [ops.calculate_grid(p) for p in in_positions_list]
         out_feat = [self.net(f, i, o, voxel_size) for f, i, o in zip(features_list, in_positions_list,
                                                                     out_positions_list)]
         return out_feat, [o / 2 for o in out_positions_list]
@@ -240,10 +242,29 @@ class UNet(nn.Module):
         self.net = nn.ModuleList(_unet_layers(list(nPlanes), residual_blocks, conv_block_reps))
         self.residual_blocks = residual_blocks
 
-    def forward(self, pos_list, feat_list):
+    @staticmethod
+    def _grid_chain(pos_list, n_down):
+        """The stride-2 grids of every level (calculate_grid, then / 2), computed
+        before any convolution is queued: each calculate_grid reads its output
+        size back to the host, and issued here that read waits only for the
+        grid kernels, not for the convolutions of the levels above."""
+        chain = []
+        for _ in range(n_down):
+            outs = [ops.calculate_grid(p) for p in pos_list]
+            pos_list = [o / 2 for o in outs]
+            chain.append((outs, pos_list))
+        return chain
+
+    def n_down(self):
+        return sum(isinstance(m, Convolution) for m in self.net)
+
+    def forward(self, pos_list, feat_list, grid_chain=None):
         conv_pos, concat_feat = [], []
         mods = list(self.net)
         fuse = _fusable(self)
+        if grid_chain is None:
+            grid_chain = self._grid_chain(pos_list, self.n_down())
+        grids = iter(grid_chain)
         pre = None  # pending folded BN + ReLU (eval): applied by the next conv's gather
         for j, m in enumerate(mods):
             if fuse and isinstance(m, BatchNormBlock) and j + 2 < len(mods) and \
@@ -258,10 +279,10 @@ class UNet(nn.Module):
                     feat_list = [m.net.forward_fused(f, p, p, 1.0, pre=pre) for f, p in zip(feat_list, pos_list)]
                 elif isinstance(m, Convolution):
                     conv_pos.append(pos_list)
-                    outs = [ops.calculate_grid(p) for p in pos_list]
+                    outs, half = next(grids)
                     feat_list = [m.net.forward_fused(f, p, o, 1.0, pre=pre)
                                  for f, p, o in zip(feat_list, pos_list, outs)]
-                    pos_list = [o / 2 for o in outs]
+                    pos_list = half
                 else:  # DeConvolution
                     feat_list = [m.net.forward_fused(f, 2 * p, o, 1.0, pre=pre)
                                  for f, p, o in zip(feat_list, pos_list, conv_pos[-1])]
@@ -274,7 +295,9 @@ class UNet(nn.Module):
                 feat_list = m(feat_list, pos_list)
             elif isinstance(m, Convolution):
                 conv_pos.append(pos_list)
-                feat_list, pos_list = m(feat_list, pos_list)
+                outs, half = next(grids)
+                feat_list, _ = m(feat_list, pos_list, out_positions_list=outs)
+                pos_list = half
             elif isinstance(m, DeConvolution):
                 feat_list = m(feat_list, [2 * p for p in pos_list], conv_pos[-1])
                 pos_list = conv_pos.pop()
@@ -324,8 +347,9 @@ class SparseConvUnet(nn.Module):
             pos_list.append(p)
             feat_list.append(f)
             index_maps.append(m)
+        chain = self.unet._grid_chain(pos_list, self.unet.n_down())  # host reads before any convolution
         feat_list = self.sub_sparse_conv(feat_list, pos_list, voxel_size=1.0)
-        feat_list = self.unet(pos_list, feat_list)
+        feat_list = self.unet(pos_list, feat_list, grid_chain=chain)
         feat_list = self.relu(self.batch_norm(feat_list))
         feat_list = self.linear(feat_list)
         return self.output_layer(feat_list, index_maps)

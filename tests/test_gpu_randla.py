@@ -213,7 +213,7 @@ def test_update_probs_matches_reference_float16(cuda):
     assert np.array_equal(t.cpu().numpy(), ref)
 
 
-def test_dense_fused_split_reduce_bitwise(cuda):
+def test_dense_fused_split_reduce_bitwise(cuda, tmp_path):
     """The optional split-K finish in the last-arriving block of each tile
     (O3DML_DENSE_FUSED_REDUCE=1, per-tile counters) against the default
     two-launch form: same split order, so bit-identical (child processes:
@@ -230,8 +230,7 @@ def test_dense_fused_split_reduce_bitwise(cuda):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = []
     for flag in ("1", "0"):
-        path = os.path.join(root, "gpurun_out", f"dense_reduce_{flag}.pt")
-        os.makedirs(os.path.dirname(path), exist_ok=True)
+        path = str(tmp_path / f"dense_reduce_{flag}.pt")
         env = dict(os.environ, O3DML_DENSE_FUSED_REDUCE=flag)
         subprocess.run([sys.executable, "-c", code, path], check=True, env=env, cwd=root, timeout=120)
         outs.append(torch.load(path, weights_only=True))

@@ -382,7 +382,7 @@ def test_presplit_fused_eval_bitwise_equal(cuda):
         lib.o3dml_sparse_conv_set_presplit(prev)
 
 
-def test_split_k_last_wave_finish_bitwise(cuda):
+def test_split_k_last_wave_finish_bitwise(cuda, tmp_path):
     """Split-K GEMMs (deep SparseConvUnet levels) optionally finish in the
     last-arriving wave of each tile (O3DML_GEMM_FUSED_REDUCE=1) instead of a
     split_reduce_kernel launch: same slab order and epilogue, so
@@ -410,8 +410,7 @@ def test_split_k_last_wave_finish_bitwise(cuda):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = []
     for flag in ("1", "0"):
-        path = os.path.join(root, "gpurun_out", f"sc_reduce_{flag}.pt")
-        os.makedirs(os.path.dirname(path), exist_ok=True)
+        path = str(tmp_path / f"sc_reduce_{flag}.pt")
         env = dict(os.environ, O3DML_GEMM_FUSED_REDUCE=flag)
         subprocess.run([sys.executable, "-c", code, path], check=True, env=env, cwd=root, timeout=180)
         outs.append(torch.load(path, weights_only=True))
