@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 evidence session: full GPU suite, smoke, default bench line, FRS
 # kernel stats + PMC (tools/round_profile.sh), the C3 / C5 / RandLA sections
-# under rocprofv3 --kernel-trace --stats, the 2^24-point single scene stats
+# and SparseConvUnet frames under rocprofv3 --kernel-trace --stats, the 2^24-point single scene stats
 # and its HBM PMC passes (u32 temp rows).  Stops at the first failure.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$(pwd); T=${TAG:-r4fin}; OUT=$R/gpurun_out/$T; mkdir -p "$OUT"; export TMPDIR=/tmp
@@ -16,6 +16,9 @@ timeout -k 10 500 python bench.py > "$OUT/full_bench.log" 2>&1 || { echo "bench 
 tail -1 "$OUT/full_bench.log" | cut -c1-300
 TAG=$T/frs bash tools/round_profile.sh || exit 1
 for s in kpconv pp randla; do SECTION=$s TAG=$T bash tools/prof_section.sh || exit 1; done
+(cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/scn" -o run --output-format csv \
+    -- python3 "$R/tools/scn_frames.py" 10 > "$OUT/scn.log" 2>&1) || { echo "scn rc=$?"; exit 1; }
+grep "SCN frame" "$OUT/scn.log"
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/single24" -o run --output-format csv \
     -- python3 "$R/tools/frs_single.py" 24 5 > "$OUT/single24.log" 2>&1) || { echo "single24 rc=$?"; exit 1; }
 i=0
