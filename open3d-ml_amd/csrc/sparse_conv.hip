@@ -354,6 +354,38 @@ __device__ __forceinline__ void split_store_finish(const f32x16& acc, const int3
     if (lane == 0) atomicExch(counters + tile, 0u);  // ready for the next launch
 }
 
+// The map rows of a tile into LDS with every global load in flight at once:
+// thread t of T takes the entries e = t + T * it (K <= 32 bounds their number
+// at compile time), a dead entry's address is clamped to map[0] so that each
+// load is unconditional, and the LDS stores follow.  (The plain loop over e
+// waited for each load before issuing the next: 14 serialised map-load
+// latencies per wave at 32 rows x 27 offsets, ahead of the first gather.)
+template <int ROWS, int T>
+__device__ __forceinline__ void load_map_tile(const int32_t* __restrict__ map, const int32_t* orow, int K, int t,
+                                              int32_t* mtile) {
+    constexpr int kIt = (ROWS * 32 + T - 1) / T;
+    const int tot = ROWS * K;
+    // e / K through a float reciprocal: exact here (e < 2,048, K <= 32, so
+    // (e + 0.5) / K stays >= 1/64 away from an integer)
+    const float invk = 1.0f / static_cast<float>(K);
+    int32_t v[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int e = t + T * it;
+        int rr = static_cast<int>((static_cast<float>(e) + 0.5f) * invk);
+        rr = rr < ROWS ? rr : ROWS - 1;
+        const int32_t orr = e < tot ? orow[rr] : -1;
+        const int64_t a = orr >= 0 ? static_cast<int64_t>(orr) * K + (e - rr * K) : 0;
+        const int32_t m = map[a];
+        v[it] = orr >= 0 ? m : -1;
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int e = t + T * it;
+        if (e < tot) mtile[e] = v[it];
+    }
+}
+
 template <bool VEC4, bool PRE>
 __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, const int* order_flag,
@@ -393,18 +425,7 @@ implicit_gemm_kernel(const int32_t* __restrict__ map, const int32_t* __restrict_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (order) {
-        for (int e = lane; e < 32 * K; e += 64) {
-            const int rr = e / K;
-            const int32_t orr = orow[rr];
-            mtile[e] = orr >= 0 ? map[static_cast<int64_t>(orr) * K + (e - rr * K)] : -1;
-        }
-    } else {
-        for (int e = lane; e < 32 * K; e += 64) {
-            const int64_t oo = o0 + e / K;
-            mtile[e] = oo < n_out ? map[o0 * K + e] : -1;
-        }
-    }
+    load_map_tile<32, 64>(map, orow, K, lane, mtile);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -736,11 +757,7 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int e = lane; e < 32 * K; e += 64) {
-        const int rr = e / K;
-        const int32_t orr = orow[rr];
-        mtile[e] = orr >= 0 ? map[static_cast<int64_t>(orr) * K + (e - rr * K)] : -1;
-    }
+    load_map_tile<32, 64>(map, orow, K, lane, mtile);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1046,11 +1063,7 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
         orow[t] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < R * K; e += NW * 64) {
-        const int rr = e / K;
-        const int32_t orr = orow[rr];
-        mtile[e] = orr >= 0 ? map[static_cast<int64_t>(orr) * K + (e - rr * K)] : -1;
-    }
+    load_map_tile<R, NW * 64>(map, orow, K, threadIdx.x, mtile);
     __syncthreads();
     unsigned used = 0u;  // identical in every wave (same rows)
     for (int k = h; k < K; k += 2) {
@@ -1222,11 +1235,7 @@ implicit_gemm_split_kernel(const int32_t* __restrict__ map, const int32_t* __res
         orow[t] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < R * K; e += NW * 64) {
-        const int rr = e / K;
-        const int32_t orr = orow[rr];
-        mtile[e] = orr >= 0 ? map[static_cast<int64_t>(orr) * K + (e - rr * K)] : -1;
-    }
+    load_map_tile<R, NW * 64>(map, orow, K, threadIdx.x, mtile);
     __syncthreads();
     unsigned used = 0u;  // identical in every wave (same rows)
     for (int k = h; k < K; k += 2) {
