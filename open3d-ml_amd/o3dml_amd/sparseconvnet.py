@@ -139,7 +139,7 @@ class Convolution(nn.Module):
                               offset=torch.full((3,), offset, dtype=torch.float32), normalize=normalize)
 
     def forward(self, features_list, in_positions_list, voxel_size=1.0, out_positions_list=None):
-        if out_positions_list is None:  # UNet passes the grids it computed up front
+        if out_positions_list is None:  # UNet passes the grids it computed on its side stream
             out_positions_list = [ops.calculate_grid(p) for p in in_positions_list]
         out_feat = [self.net(f, i, o, voxel_size) for f, i, o in zip(features_list, in_positions_list,
                                                                     out_positions_list)]
@@ -234,6 +234,62 @@ def _unet_layers(planes, residual, reps):
     return layers
 
 
+def _grid_mode():
+    """O3DML_SCN_GRIDS: "front" (default) computes every level's grid before
+    the first convolution is queued, "side" computes each when its
+    Convolution needs it on a side stream (A/B)."""
+    import os
+    return os.environ.get("O3DML_SCN_GRIDS", "front")
+
+
+class _LevelGrids:
+    """The stride-2 grid of each level (calculate_grid, then / 2) for the
+    UNet's Convolutions.  calculate_grid reads its output size back to the
+    host; issued on the caller's stream between the convolutions, that read
+    waited for every convolution queued above it.  "front": all levels are
+    computed when this object is made (before any convolution: the reads wait
+    only for the grid kernels).  "side": each level when its Convolution needs
+    it, on a side stream, so the read waits only for the grid kernels while
+    the queued convolutions keep the GPU busy; the side stream first waits for
+    the caller's stream as of construction (the input positions), each grid
+    (the next level's input) is then ordered on the side stream itself, and
+    the caller's stream waits for the side stream before it uses a grid."""
+    _streams = {}
+
+    def __init__(self, pos_list, n_down):
+        self.dev = pos_list[0].device if pos_list and pos_list[0].is_cuda else None
+        self.ready = None
+        self.chain = None
+        if _grid_mode() != "side" or self.dev is None:
+            self.chain = []
+            for _ in range(n_down):
+                outs = [ops.calculate_grid(p) for p in pos_list]
+                pos_list = [o / 2 for o in outs]
+                self.chain.append((outs, pos_list))
+            self.chain.reverse()
+        else:
+            self.main = torch.cuda.current_stream(self.dev)
+            self.ready = torch.cuda.Event()
+            self.ready.record(self.main)
+
+    def next(self, pos_list):
+        if self.chain is not None:
+            return self.chain.pop()
+        side = self._streams.get(self.dev)
+        if side is None:
+            side = self._streams[self.dev] = torch.cuda.Stream(self.dev)
+        if self.ready is not None:
+            side.wait_event(self.ready)
+            self.ready = None
+        with torch.cuda.stream(side):
+            outs = [ops.calculate_grid(p) for p in pos_list]
+            half = [o / 2 for o in outs]
+        for t in outs + half:
+            t.record_stream(self.main)  # freed blocks wait for the caller's stream
+        self.main.wait_stream(side)
+        return outs, half
+
+
 class UNet(nn.Module):
     """sparseconvnet.py:568-653."""
 
@@ -242,29 +298,15 @@ class UNet(nn.Module):
         self.net = nn.ModuleList(_unet_layers(list(nPlanes), residual_blocks, conv_block_reps))
         self.residual_blocks = residual_blocks
 
-    @staticmethod
-    def _grid_chain(pos_list, n_down):
-        """The stride-2 grids of every level (calculate_grid, then / 2), computed
-        before any convolution is queued: each calculate_grid reads its output
-        size back to the host, and issued here that read waits only for the
-        grid kernels, not for the convolutions of the levels above."""
-        chain = []
-        for _ in range(n_down):
-            outs = [ops.calculate_grid(p) for p in pos_list]
-            pos_list = [o / 2 for o in outs]
-            chain.append((outs, pos_list))
-        return chain
-
     def n_down(self):
         return sum(isinstance(m, Convolution) for m in self.net)
 
-    def forward(self, pos_list, feat_list, grid_chain=None):
+    def forward(self, pos_list, feat_list, grids=None):
         conv_pos, concat_feat = [], []
         mods = list(self.net)
         fuse = _fusable(self)
-        if grid_chain is None:
-            grid_chain = self._grid_chain(pos_list, self.n_down())
-        grids = iter(grid_chain)
+        if grids is None:
+            grids = _LevelGrids(pos_list, self.n_down())
         pre = None  # pending folded BN + ReLU (eval): applied by the next conv's gather
         for j, m in enumerate(mods):
             if fuse and isinstance(m, BatchNormBlock) and j + 2 < len(mods) and \
@@ -279,7 +321,7 @@ class UNet(nn.Module):
                     feat_list = [m.net.forward_fused(f, p, p, 1.0, pre=pre) for f, p in zip(feat_list, pos_list)]
                 elif isinstance(m, Convolution):
                     conv_pos.append(pos_list)
-                    outs, half = next(grids)
+                    outs, half = grids.next(pos_list)
                     feat_list = [m.net.forward_fused(f, p, o, 1.0, pre=pre)
                                  for f, p, o in zip(feat_list, pos_list, outs)]
                     pos_list = half
@@ -295,7 +337,7 @@ class UNet(nn.Module):
                 feat_list = m(feat_list, pos_list)
             elif isinstance(m, Convolution):
                 conv_pos.append(pos_list)
-                outs, half = next(grids)
+                outs, half = grids.next(pos_list)
                 feat_list, _ = m(feat_list, pos_list, out_positions_list=outs)
                 pos_list = half
             elif isinstance(m, DeConvolution):
@@ -347,9 +389,9 @@ class SparseConvUnet(nn.Module):
             pos_list.append(p)
             feat_list.append(f)
             index_maps.append(m)
-        chain = self.unet._grid_chain(pos_list, self.unet.n_down())  # host reads before any convolution
+        grids = _LevelGrids(pos_list, self.unet.n_down())  # before the first convolution is queued
         feat_list = self.sub_sparse_conv(feat_list, pos_list, voxel_size=1.0)
-        feat_list = self.unet(pos_list, feat_list, grid_chain=chain)
+        feat_list = self.unet(pos_list, feat_list, grids=grids)
         feat_list = self.relu(self.batch_norm(feat_list))
         feat_list = self.linear(feat_list)
         return self.output_layer(feat_list, index_maps)
