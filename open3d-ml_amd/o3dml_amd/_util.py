@@ -85,6 +85,9 @@ def to_dev(t, device, dtype=None):
     the stream its upload was queued on (so every use is ordered after the
     copy), and an evicted block returns to that stream's pool, the only one
     that ever used it."""
+    if isinstance(t, torch.Tensor) and t.is_cuda and (dtype is None or t.dtype == dtype) and \
+            t.device == (device if isinstance(device, torch.device) else torch.device(device)):
+        return t if t.is_contiguous() else t.contiguous()  # already there: no copy, no device object
     if not isinstance(t, torch.Tensor):
         t = torch.as_tensor(np.asarray(t))
     if dtype is not None and t.dtype != dtype:

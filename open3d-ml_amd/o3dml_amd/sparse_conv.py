@@ -408,7 +408,7 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
         res = None if residual is None else residual.contiguous()
         if res is not None and tuple(res.shape) != (n_out, cout):
             raise ValueError("sparse_conv: residual must be [n_out, cout]")
-        fws = workspace(lib.o3dml_sparse_conv_forward_workspace_size(n_out, n_in, K, cin, cout), dev)
+        fws = workspace(_forward_ws_bytes(lib, n_out, n_in, K, cin, cout), dev)
         x_c, b_c = x.detach().contiguous(), None if b is None else b.detach().contiguous()
         _lib.call("o3dml_sparse_conv_forward_fused", ptr(_transposed_filters(f)), K, cin, cout,
                   ptr(x_c), n_in, ptr(ps), ptr(pb), ptr(res),
@@ -421,6 +421,19 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
     if not _late_ok(late):
         return None
     return out if inp_features.is_cuda else out.cpu()
+
+
+_FWS = {}  # (n_out, n_in, K, cin, cout) -> forward workspace bytes (one ctypes query per shape)
+
+
+def _forward_ws_bytes(lib, n_out, n_in, K, cin, cout):
+    key = (n_out, n_in, K, cin, cout)
+    v = _FWS.get(key)
+    if v is None:
+        if len(_FWS) > 4096:
+            _FWS.clear()
+        v = _FWS[key] = int(lib.o3dml_sparse_conv_forward_workspace_size(n_out, n_in, K, cin, cout))
+    return v
 
 
 def _late_ok(status):
