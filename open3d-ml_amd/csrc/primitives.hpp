@@ -463,8 +463,11 @@ __global__ void __launch_bounds__(kBsThreads) block_radix_sort_pairs(const K* __
     constexpr int N = S * kBsThreads;
     constexpr int kWaves = kBsThreads / 64;
     static_assert(N <= 8192, "packed 16-bit counters");
-    __shared__ K xk[N];
-    __shared__ uint32_t xp[N];
+    // exchange buffers padded by one slot per 32 (bpad): a thread's S
+    // consecutive slots no longer start on the same few banks as its neighbours'
+    __shared__ K xk[N + N / 32];
+    __shared__ uint32_t xp[N + N / 32];
+    auto bpad = [](int i) { return i + (i >> 5); };
     __shared__ uint32_t cnt[8 * kBsThreads];  // [digit pair][thread]
     __shared__ uint32_t wtot[kWaves][8];
     __shared__ K wor[kWaves];
@@ -472,17 +475,17 @@ __global__ void __launch_bounds__(kBsThreads) block_radix_sort_pairs(const K* __
 #pragma unroll
     for (int s = 0; s < S; ++s) {  // coalesced load, blocked read below
         const int i = s * kBsThreads + t;
-        xk[i] = i < n ? (kin[i] & mask) : K(0);
+        xk[bpad(i)] = i < n ? (kin[i] & mask) : K(0);
     }
     __syncthreads();
-    const K k0 = xk[0];
+    const K k0 = xk[0];  // bpad(0) = 0
     K key[S];
     uint32_t pos[S];
     K vb = 0;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
         const int i = t * S + s;
-        key[s] = xk[i];
+        key[s] = xk[bpad(i)];
         pos[s] = i < n ? static_cast<uint32_t>(i) : 0xffffffffu;
         if (i < n) vb |= key[s] ^ k0;
     }
@@ -539,25 +542,25 @@ __global__ void __launch_bounds__(kBsThreads) block_radix_sort_pairs(const K* __
         for (int s = 0; s < S; ++s) {
             const uint32_t v = cnt[static_cast<int>(dg[s] >> 1) * kBsThreads + t];
             const uint32_t r = ((v >> ((dg[s] & 1u) * 16)) & 0xffffu) + lr[s];
-            xk[r] = key[s];
-            xp[r] = pos[s];
+            xk[bpad(static_cast<int>(r))] = key[s];
+            xp[bpad(static_cast<int>(r))] = pos[s];
         }
         __syncthreads();
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            key[s] = xk[t * S + s];
-            pos[s] = xp[t * S + s];
+            key[s] = xk[bpad(t * S + s)];
+            pos[s] = xp[bpad(t * S + s)];
         }
         __syncthreads();  // exchange buffer and wave totals free for the next pass
     }
 #pragma unroll
-    for (int s = 0; s < S; ++s) xp[t * S + s] = pos[s];
+    for (int s = 0; s < S; ++s) xp[bpad(t * S + s)] = pos[s];
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < S; ++s) {
         const int i = s * kBsThreads + t;
         if (i < n) {
-            const uint32_t p = xp[i];
+            const uint32_t p = xp[bpad(i)];
             kout[i] = kin[p];
             vout[i] = vin ? vin[p] : p;
         }
