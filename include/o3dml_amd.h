@@ -423,6 +423,10 @@ int o3dml_sparse_conv_set_exact(int exact);
  * loads them; the sums are bit-identical to the in-kernel split.  on = 0 / 1
  * sets, < 0 queries; returns the previous setting. */
 int o3dml_sparse_conv_set_presplit(int on);
+/* Filters split into bf16 hi / mid / lo once per call for the narrow-output
+ * GEMM (default on; same bits either way).  on < 0 only queries; returns the
+ * previous setting. */
+int o3dml_sparse_conv_set_bsplit(int on);
 int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* query_positions,
                                    const int32_t* neighbors_index, const int64_t* neighbors_row_splits,
                                    int64_t n_query, const int32_t* ksize_host, float voxel_size, int mirror,

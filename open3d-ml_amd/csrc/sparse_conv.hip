@@ -204,6 +204,7 @@ __global__ void transpose_filters_kernel(const float* __restrict__ w, int K, int
 // --------------------------------------------------------------------------
 struct GemmStage {
     float a[16], b[16];
+    bf16x8 bs[6];  // filters split once per call (BS kernels): hi, mid, lo of channels 8t.. for t = 0, 1
     float s1, s2;  // row importance, pair scale (1 without them)
     float v;       // 1 for a present neighbour, 0 for a missing one
 };
@@ -219,6 +220,10 @@ struct GemmPrologue {
     // the buffer resources (BUF kernels), so a row index past the operand
     // reads zeros, never foreign memory (set by the launcher)
     uint32_t src_bytes = 0, w_bytes = 0;
+    // the filters split into bf16 hi / mid / lo once per call (split_filters_kernel;
+    // BS kernels) and the byte size of that copy
+    const __bf16* wsplit = nullptr;
+    uint32_t wsplit_bytes = 0;
 };
 constexpr int kPreMax = 1024;  // max cin with a prologue (LDS staging)
 
@@ -547,16 +552,18 @@ __device__ __forceinline__ void glds16(const float* g, float* lds_wave_base) {
 // ~40 % of the loop's VALU went to addresses)
 constexpr uint32_t kNoRow = 0x7FFFFFF0u;  // > num_records of every operand resource (its true byte size)
 struct GemmRsrc {
-    __amdgpu_buffer_rsrc_t src, w;
+    __amdgpu_buffer_rsrc_t src, w, wsp;
 };
 __device__ __forceinline__ GemmRsrc gemm_rsrc(const float* src, const float* Wt, const GemmPrologue& pre) {
     return {__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), static_cast<short>(0),
                                               static_cast<int>(pre.src_bytes), kBufferFlags),
             __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Wt), static_cast<short>(0),
-                                              static_cast<int>(pre.w_bytes), kBufferFlags)};
+                                              static_cast<int>(pre.w_bytes), kBufferFlags),
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(pre.wsplit), static_cast<short>(0),
+                                              static_cast<int>(pre.wsplit_bytes), kBufferFlags)};
 }
 
-template <bool BREG, bool SC = true, bool BUF = false>
+template <bool BREG, bool SC = true, bool BUF = false, bool BS = false>
 __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_t* mtile, int K, int k, int c0,
                                           int lane, int64_t o, int i, int col0, const float* __restrict__ src,
                                           const float* __restrict__ sscale, const float* __restrict__ pscale,
@@ -579,17 +586,27 @@ __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs->src, (lds_void_ptr)(abuf + 256 * q), 16, off, 0, 0, 0);
         }
         const int col = col0 + i;
-        const uint32_t boff = (live && col < cout)
-                                      ? (static_cast<uint32_t>(k * cout + col) * static_cast<uint32_t>(cin) +
-                                         static_cast<uint32_t>(c0 + 16 * (lane >> 5))) * 4u
-                                      : kNoRow;
+        if constexpr (BS) {  // the lane's 16 channels as two 8-channel blocks of 3 x 16 B
+            const uint32_t soff = (live && col < cout)
+                                          ? (static_cast<uint32_t>(k * cout + col) * static_cast<uint32_t>(cin) +
+                                             static_cast<uint32_t>(c0 + 16 * (lane >> 5))) / 8u * 48u
+                                          : kNoRow;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs->w, boff + 16u * q, 0, 0));
-            st.b[4 * q] = v.x;
-            st.b[4 * q + 1] = v.y;
-            st.b[4 * q + 2] = v.z;
-            st.b[4 * q + 3] = v.w;
+            for (int m = 0; m < 6; ++m)
+                st.bs[m] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs->wsp, soff + 16u * m, 0, 0));
+        } else {
+            const uint32_t boff = (live && col < cout)
+                                          ? (static_cast<uint32_t>(k * cout + col) * static_cast<uint32_t>(cin) +
+                                             static_cast<uint32_t>(c0 + 16 * (lane >> 5))) * 4u
+                                          : kNoRow;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs->w, boff + 16u * q, 0, 0));
+                st.b[4 * q] = v.x;
+                st.b[4 * q + 1] = v.y;
+                st.b[4 * q + 2] = v.z;
+                st.b[4 * q + 3] = v.w;
+            }
         }
         st.s1 = st.s2 = 1.f;
         st.v = mi >= 0 ? 1.f : 0.f;
@@ -698,6 +715,41 @@ __device__ __forceinline__ void mfma_stage_split(const Stage& cu, f32x16& acc) {
     }
 }
 
+// bf16x6 products with the B operand split once per call (BS): the same six
+// MFMAs in the same order as mfma_stage_split<6> on the same bf16 terms, so
+// the same bits; only A is split per stage
+template <class Stage>
+__device__ __forceinline__ void mfma_stage_bs(const Stage& cu, f32x16& acc) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        bf16x8 ah, am, al;
+        split_bf16x8<6>(cu.a + 8 * t, ah, am, al);
+        const bf16x8 bh = cu.bs[3 * t], bm = cu.bs[3 * t + 1], bl = cu.bs[3 * t + 2];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+    }
+}
+
+// The filters Wt [K][cout][cin] (cin % 8 == 0) as 8-channel blocks of three
+// bf16x8 (split_bf16x8<6>: hi, mid, lo) for the BS kernels
+__global__ void split_filters_kernel(const float* __restrict__ wt, int64_t nblk, bf16x8* __restrict__ out) {
+    for (int64_t b = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; b < nblk;
+         b += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const float4 p = reinterpret_cast<const float4*>(wt)[2 * b];
+        const float4 q = reinterpret_cast<const float4*>(wt)[2 * b + 1];
+        const float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+        bf16x8 hi, mid, lo;
+        split_bf16x8<6>(v, hi, mid, lo);
+        out[3 * b] = hi;
+        out[3 * b + 1] = mid;
+        out[3 * b + 2] = lo;
+    }
+}
+
 // product precision of a GEMM instantiation: 0 = exact f32 MFMA, 3 / 6 = bf16 split
 template <int NT, class Stage>
 __device__ __forceinline__ void mfma_stage(const Stage& cu, f32x16& acc) {
@@ -713,7 +765,7 @@ __device__ __forceinline__ void mfma_stage(const Stage& cu, f32x16& acc) {
 // stage j+2's DMA is issued while stage j is multiplied.  Off by default:
 // 12 instead of 16 waves per CU (136 registers, 49 KiB LDS per workgroup), and
 // same-session A/B 3-8 % slower at 32->32 / 64->32 (tools/gemm_probe.py)
-template <bool PRE, bool BREG, int NT = 0, bool SC = true, bool BUF = false, int DEPTH = 1>
+template <bool PRE, bool BREG, int NT = 0, bool SC = true, bool BUF = false, int DEPTH = 1, bool BS = false>
 __global__ void __launch_bounds__(kGemmThreads)
 implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order,
                          const int* order_flag, int K, int64_t n_out,
@@ -838,17 +890,21 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead DMAs have landed before the wave exits
     } else if (j0 < j1) {
+        static_assert(!BS || (BUF && BREG && !SC && NT == 6 && DEPTH == 1), "split filters: bf16x6 buffer path");
         unsigned u = used;
         for (int t = j0 / nch; t > 0; --t) u &= u - 1u;
         int k = __builtin_ctz(u), c0 = (j0 % nch) * 32;
         GemmStage nx, cu;
         const GemmRsrc rs = gemm_rsrc(src, Wt, pre);
-        lds_issue<BREG, SC, BUF>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin, cout,
-                                 true, nx, &rs);
+        lds_issue<BREG, SC, BUF, BS>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin,
+                                     cout, true, nx, &rs);
         for (int j = j0; j < j1; ++j) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage j in LDS, its row factors in nx
             lds_read<BREG>(abuf, bbuf, i, h, cu);
-            if constexpr (BREG) {
+            if constexpr (BS) {
+#pragma unroll
+                for (int m = 0; m < 6; ++m) cu.bs[m] = nx.bs[m];
+            } else if constexpr (BREG) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) cu.b[r] = nx.b[r];
             }
@@ -863,12 +919,13 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
                 k = u ? __builtin_ctz(u) : 0;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffer read out before the next DMA
-            lds_issue<BREG, SC, BUF>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin,
-                                     cout, j + 1 < j1, nx, &rs);
+            lds_issue<BREG, SC, BUF, BS>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin,
+                                         cout, j + 1 < j1, nx, &rs);
             __builtin_amdgcn_sched_barrier(0);
             (void)kj;
             gemm_finish<PRE, SC>(cu, cj, h, lps, lpb);
-            mfma_stage<NT>(cu, acc);
+            if constexpr (BS) mfma_stage_bs(cu, acc);
+            else mfma_stage<NT>(cu, acc);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead DMA has landed before the wave exits
     }
@@ -1757,8 +1814,20 @@ static size_t presplit_bytes(int64_t n_src, int K, int cin, int cout) {
 }
 
 // everything run_gemm may take from its workspace
+// Filters split once per call for the per-wave kernel (split_filters_kernel,
+// BS): the B operand's hi / mid / lo come from a 6-B-per-weight copy instead
+// of three roundings per stage in every wave.  O3DML_GEMM_BSPLIT=0 or
+// o3dml_sparse_conv_set_bsplit(0) turns it off (same bits either way).
+static bool g_bsplit = [] {
+    const char* e = std::getenv("O3DML_GEMM_BSPLIT");
+    return e ? std::atoi(e) != 0 : true;
+}();
+static size_t bsplit_bytes(int K, int cin, int cout) {
+    return cin == 32 ? ws_bytes<uint16_t>(3 * static_cast<int64_t>(K) * cout * cin) : 0;
+}
+
 static size_t gemm_ws_bytes(int64_t n_out, int64_t n_src, int K, int cin, int cout) {
-    return gemm_split_bytes(n_out, K, cin, cout) + presplit_bytes(n_src, K, cin, cout);
+    return gemm_split_bytes(n_out, K, cin, cout) + presplit_bytes(n_src, K, cin, cout) + bsplit_bytes(K, cin, cout);
 }
 
 static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, const int* order_flag, int K,
@@ -1959,7 +2028,27 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
             return e ? std::atoi(e) == 2 : false;
         }();
         const int nt = gemm_nt();
-        if (nt == 6) {
+        const int64_t wn = static_cast<int64_t>(K) * cout * cin;
+        // one 32-channel chunk per offset only: at cin 32 the split copy saves
+        // 3 % (32->32, 32->16 layers), at cin 64 it cost 15 % (64->32;
+        // gpurun_out/r4s28, same session)
+        const bool bs = g_bsplit && nt == 6 && buf_ok && !depth2 && !sscale && !pscale && cin == 32 &&
+                        static_cast<uint64_t>(wn) * 6u < kNoRow - 128 && ws.base &&
+                        ws.used + bsplit_bytes(K, cin, cout) <= ws.size;
+        if (bs) {
+            bf16x8* w3 = reinterpret_cast<bf16x8*>(ws.take<uint16_t>(3 * wn));
+            split_filters_kernel<<<stream_grid(wn / 8, 256), 256, 0, st>>>(Wt, wn / 8, w3);
+            O3DML_LAUNCH_CHECK();
+            pre.wsplit = reinterpret_cast<const __bf16*>(w3);
+            pre.wsplit_bytes = static_cast<uint32_t>(wn * 6);
+        }
+#define O3DML_GEMM_LDS_BS(P)                                                                                     \
+    implicit_gemm_lds_kernel<P, true, 6, false, true, 1, true><<<g, kGemmThreads, 0, st>>>(                      \
+            map, order, order_flag, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, bias, out, ns, part, pre, \
+            residual, counters)
+        if (nt == 6 && bs) {
+            if (pre.scale) O3DML_GEMM_LDS_BS(true); else O3DML_GEMM_LDS_BS(false);
+        } else if (nt == 6) {
             if (pre.scale) O3DML_GEMM_LDS(true, true, 6); else O3DML_GEMM_LDS(false, true, 6);
         } else if (nt == 3) {
             if (pre.scale) O3DML_GEMM_LDS(true, true, 3); else O3DML_GEMM_LDS(false, true, 3);
@@ -1972,6 +2061,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #undef O3DML_GEMM_LDS_SC
 #undef O3DML_GEMM_LDS_BUF
 #undef O3DML_GEMM_LDS_BUF2
+#undef O3DML_GEMM_LDS_BS
     } else if (pre.scale) {
         if (vec4) O3DML_GEMM_LAUNCH(true, true); else O3DML_GEMM_LAUNCH(false, true);
     } else {
@@ -2595,6 +2685,12 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
 
 // ksize_host[3] = filter dims (k0,k1,k2) = (z,y,x) extents.
 // presplit operands on (1, default) / off (0); < 0 queries.  Returns the previous setting.
+O3DML_API int o3dml_sparse_conv_set_bsplit(int on) {
+    const int prev = g_bsplit ? 1 : 0;
+    if (on >= 0) g_bsplit = on != 0;
+    return prev;
+}
+
 O3DML_API int o3dml_sparse_conv_set_presplit(int on) {
     const int prev = g_presplit ? 1 : 0;
     if (on >= 0) g_presplit = on != 0;

@@ -161,6 +161,7 @@ SIGNATURES = {
                                             c_sz, c_p]),
     "o3dml_sparse_conv_forward_workspace_size": (c_sz, [c_i64, c_i64, c_i32, c_i32, c_i32]),
     "o3dml_sparse_conv_set_presplit": (c_i32, [c_i32]),
+    "o3dml_sparse_conv_set_bsplit": (c_i32, [c_i32]),
     "o3dml_sparse_conv_forward_fused": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64,
                                                 c_p, c_p, c_sz, c_p, c_sz, c_p]),
     "o3dml_sparse_conv_forward": (c_i32, [c_p, c_i32, c_i32, c_i32, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i64, c_p,

@@ -353,6 +353,38 @@ def test_presplit_operands_bitwise_equal(cuda, cin, cout):
         lib.o3dml_sparse_conv_set_exact(prev_mode)
 
 
+@pytest.mark.parametrize("cin,cout", [(32, 32), (64, 32), (32, 16), (96, 48), (16, 32)])
+def test_split_filters_bitwise_equal(cuda, cin, cout):
+    """Filters split into bf16 hi / mid / lo once per call (split_filters_kernel,
+    the BS form of implicit_gemm_lds_kernel) against the per-stage split: the
+    same bf16 terms in the same MFMA order, so the forward is bitwise
+    identical; the SparseConvUnet eval (prologue + residual) too."""
+    from o3dml_amd import _lib, layers
+    from o3dml_amd.sparseconvnet import SparseConvUnet
+    import types
+    lib = _lib.load()
+    vox = torch.from_numpy(_voxels(30000, 40, 3)).to(cuda)
+    torch.manual_seed(0)
+    conv = layers.SparseConv(cin, cout, [3, 3, 3], use_bias=True).to(cuda)
+    x = torch.randn((vox.shape[0], cin), device=cuda)
+    m = SparseConvUnet(multiplier=16, residual_blocks=True, conv_block_reps=1, num_classes=5).to(cuda).eval()
+    g = torch.Generator().manual_seed(1)
+    pos = (torch.rand((20000, 3), generator=g) * 30).to(cuda)
+    inp = types.SimpleNamespace(point=[pos], feat=[torch.rand((20000, 3), generator=g).to(cuda)],
+                                batch_lengths=[20000])
+    prev = lib.o3dml_sparse_conv_set_bsplit(-1)
+    try:
+        res = []
+        for on in (1, 0):
+            lib.o3dml_sparse_conv_set_bsplit(on)
+            with torch.no_grad():
+                res.append((conv(x, vox, vox, 1.0), m(inp)))
+        for a, b in zip(*res):
+            assert torch.equal(a, b), (cin, cout)
+    finally:
+        lib.o3dml_sparse_conv_set_bsplit(prev)
+
+
 def test_presplit_fused_eval_bitwise_equal(cuda):
     """SparseConvUnet eval (BN + ReLU prologue folded into the presplit
     planes, residual epilogue): presplit on / off give identical logits."""
