@@ -227,37 +227,67 @@ def make_scan(seed):
     return pts, rng.integers(0, 20, pts.shape[0]).astype(np.int32)
 
 
-def randla_frames(dev, frames, cpu=False):
+def shard(n_total, world, rank):
+    """Round-robin assignment of n_total independent units (scans, rooms)
+    to the ranks: rank r takes units r, r + world, ... (scenes
+    shard with no data-path collective)."""
+    return list(range(rank, n_total, world))
+
+
+def frames_over_ranks(frames_local, elapsed_max, world):
+    """(all ranks' frames, frames / s over the max-over-ranks time)."""
+    counts = gather_units(frames_local, world)
+    total = sum(counts)
+    return counts, total, (total / elapsed_max if elapsed_max > 0 else 0.0)
+
+
+def randla_frames(dev, frames, cpu=False, world=1, rank=0):
     """RandLA-Net GPU inference (SemSegInference, randlanet_semantickitti.yml:
     45,056-pt patches, k=16, 4 layers, grid 0.06, random-init weights) on C2
     scans: one frame = the full possibility loop until every sub-point > 0.5.
-    Each scan runs once untimed first (the captured patch graphs exist per
-    sub-cloud capacity class), then the same scans are timed."""
+    `frames` scans per rank (weak scaling), the frames * world scans dealt
+    round-robin over the ranks (shard()); at world 1 the scans are seeds
+    0 .. frames-1.  Cold pass: each rank's scans once on a fresh model (the
+    captured patch graph of every sub-cloud capacity class is built inside
+    it); then the timed pass over the same scans (graphs kept per class,
+    randlanet._patch_step, as in a stream of scans of similar size).  Both
+    passes are bracketed by barrier + device sync, max over ranks."""
     from o3dml_amd.randlanet import RandLANet, SemSegInference
     torch.manual_seed(0)
     model = RandLANet(num_points=45056, num_classes=19).to(dev).eval()
-    scans = [torch.from_numpy(make_scan(s)[0]).to(dev) for s in range(frames)]
-    # warm-up: every scan once (other shuffle seeds), so each sub-cloud
-    # capacity class has its captured patch step before the timed frames, as
-    # in a stream of scans (the graphs are kept per class, randlanet._patch_step)
-    for f in range(frames):
-        SemSegInference(model, seed=100 + f).run(scans[f])
-    torch.cuda.synchronize(dev)
-    patches = 0
-    t = time.perf_counter()
-    for f in range(frames):
-        inf = SemSegInference(model, seed=f)
-        inf.run(scans[f])
-        patches += inf.stats["patches"]
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t
-    out = {"frames_per_s": round(frames / dt, 3), "ms_per_frame": round(dt / frames * 1e3, 2),
-           "patches_per_frame": round(patches / frames, 2), "frames": frames,
-           "config": "C2: 120,000-pt synthetic 64-beam scan, RandLANet semantickitti cfg, fp32, random init",
+    mine = shard(frames * world, world, rank)
+    scans = [torch.from_numpy(make_scan(s)[0]).to(dev) for s in mine]
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+
+    def cold():
+        for f, sc in enumerate(scans):
+            SemSegInference(model, seed=100 + mine[f]).run(sc)
+
+    patches = [0]
+
+    def timed():
+        for f, sc in enumerate(scans):
+            inf = SemSegInference(model, seed=mine[f])
+            inf.run(sc)
+            patches[0] += inf.stats["patches"]
+
+    dt_cold, _ = timed_run(cold, 1, 0, world, sync)
+    dt, _ = timed_run(timed, 1, 0, world, sync)
+    counts, total, fps = frames_over_ranks(len(scans), dt, world)
+    _, _, fps_cold = frames_over_ranks(len(scans), dt_cold, world)
+    out = {"frames_per_s": round(fps, 3), "ms_per_frame": round(dt / max(len(scans), 1) * 1e3, 2),
+           "patches_per_frame": round(patches[0] / max(len(scans), 1), 2), "frames": total, "n_gpus": world,
+           "frames_per_rank": counts,
+           "cold_frames_per_s": round(fps_cold, 3),
+           "cold_ms_per_frame": round(dt_cold / max(len(scans), 1) * 1e3, 2),
+           "note": "frames_per_s: scans whose sub-cloud capacity class already has its captured patch graph "
+                   "(kept per class); cold_*: the same scans first seen by a fresh model, graph captures included",
+           "config": "C2: 120,000-pt synthetic 64-beam scan, RandLANet semantickitti cfg, fp32, random init"
+                     + (f", scans round-robin over {world} GPUs" if world > 1 else ""),
            "cpu_reference_s_per_frame_8cores_survey": 10.6}
-    if cpu:
-        out["cpu_baseline"] = randla_cpu_baseline(model, make_scan(0)[0], patches / frames)
-        out["cpu_baseline"]["gpu_speedup"] = round(out["cpu_baseline"]["value"] / (dt / frames), 1)
+    if cpu and world == 1:
+        out["cpu_baseline"] = randla_cpu_baseline(model, make_scan(0)[0], patches[0] / len(scans))
+        out["cpu_baseline"]["gpu_speedup"] = round(out["cpu_baseline"]["value"] / (dt / len(scans)), 1)
     return out
 
 
@@ -525,6 +555,13 @@ def sparse_conv_bench(dev, reps):
             "unet": scn_bench(dev, pos, reps)}
 
 
+def sparse_conv_ranks(dev, reps, world, rank):
+    """N > 1: the C4 SparseConvUnet frames on every rank (rank r's room =
+    make_room(r)); the single-GPU layer / GEMM probes run at N = 1 only."""
+    pos_np, _ = make_room(rank)
+    return {"unet": scn_bench(dev, torch.from_numpy(pos_np).to(dev), reps, world, rank)}
+
+
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X dense fp32-input MFMA (MI355X_MICROARCH.md)
 MFMA_BF16_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 flop/clk x 2.4 GHz
 # bf16-split products: useful f32 flop peak = bf16 peak / MFMAs per product
@@ -574,10 +611,12 @@ def _gemm_roofline(dev, pos, nb, kidx, pairs, ch, reps, mode):
             "unit": "TFLOP/s", "frac": round(tf / peak, 4)}
 
 
-def scn_bench(dev, pos, reps):
+def scn_bench(dev, pos, reps, world=1, rank=0):
     """C4 whole-network forward: SparseConvUnet with the reference scannet
     config (multiplier 32, residual blocks, 1 rep, 20 classes; random init, eval
-    mode), InputLayer -> 7-level UNet -> per-point logits, one point per voxel."""
+    mode), InputLayer -> 7-level UNet -> per-point logits, one point per voxel.
+    `reps` frames per rank of that rank's room (weak scaling: pos = make_room
+    of the rank's seed), bracketed by barrier + device sync, max over ranks."""
     import types
     from o3dml_amd.sparseconvnet import SparseConvUnet
     torch.manual_seed(0)
@@ -585,15 +624,14 @@ def scn_bench(dev, pos, reps):
     feat = torch.rand((pos.shape[0], 3), device=dev)
     inp = types.SimpleNamespace(point=[pos], feat=[feat], batch_lengths=[pos.shape[0]])
     with torch.no_grad():
-        m(inp)
-        torch.cuda.synchronize(dev)
-        t = time.perf_counter()
-        for _ in range(reps):
-            m(inp)
-        torch.cuda.synchronize(dev)
-        dt = (time.perf_counter() - t) / reps
-    return {"ms_per_frame": round(dt * 1e3, 3), "mvoxels_per_s": round(pos.shape[0] / dt / 1e6, 3),
-            "config": "SparseConvUnet m=32 residual reps=1 (sparseconvunet_scannet.yml), fp32 (bf16x6 MFMA products), eval"}
+        dt, _ = timed_run(lambda: m(inp), reps, 1, world, lambda: torch.cuda.synchronize(dev))
+    counts, total, fps = frames_over_ranks(reps, dt, world)
+    voxels = sum(gather_units(int(pos.shape[0]) * reps, world))
+    return {"ms_per_frame": round(dt / reps * 1e3, 3), "frames_per_s": round(fps, 2),
+            "mvoxels_per_s": round(voxels / dt / 1e6, 3), "n_gpus": world, "frames": total,
+            "frames_per_rank": counts,
+            "config": "SparseConvUnet m=32 residual reps=1 (sparseconvunet_scannet.yml), fp32 (bf16x6 MFMA "
+                      "products), eval" + (f", one room per GPU x {world}" if world > 1 else "")}
 
 
 def timed_run(step, steps, warmup, world, sync):
@@ -663,10 +701,18 @@ def plumbing_test(args, world, rank):
     x = torch.ones(1 << 14)
     elapsed, _ = timed_run(lambda: x.sum(), args.steps, args.warmup, world, lambda: None)
     units = gather_units(args.scenes * N_POINTS * args.steps, world)
+    # the C2 / C4 legs' sharding: each rank's scans (round-robin) and the
+    # frames aggregated over the max-over-ranks time, as randla_frames does
+    frames = max(args.randla_frames, 1)
+    assigned = gather_units(shard(frames * world, world, rank), world)
+    f_elapsed, _ = timed_run(lambda: None, 1, 0, world, lambda: None)
+    f_counts, f_total, f_rate = frames_over_ranks(len(assigned[rank]), f_elapsed, world)
     if rank == 0:
         print(json.dumps({"plumbing_test": True, "n_gpus": world, "ranks_reported": len(units),
                           "units_per_rank": units, "value": sum(units) / elapsed / 1e6,
-                          "elapsed_max_s": elapsed, "steps": args.steps}), flush=True)
+                          "elapsed_max_s": elapsed, "steps": args.steps,
+                          "scan_shards": assigned, "frames_per_rank": f_counts, "frames_total": f_total,
+                          "frames_elapsed_max_s": f_elapsed, "frames_per_s": f_rate}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -692,6 +738,11 @@ def run(args):
     units = gather_units(args.scenes * N_POINTS * args.steps, world)
 
     pp = pointpillars_bench(dev, world, rank, args.pointpillars_steps) if args.pointpillars_steps > 0 else None
+    # the sharding workloads run on every rank at N > 1 (collective timing)
+    sc_multi = sparse_conv_ranks(dev, args.sparse_conv_reps, world, rank) \
+        if world > 1 and args.sparse_conv_reps > 0 else None
+    rl_multi = randla_frames(dev, args.randla_frames, False, world, rank) \
+        if world > 1 and args.randla_frames > 0 else None
     out = None
     if rank == 0:
         queries_total = sum(units)
@@ -737,12 +788,16 @@ def run(args):
             out["c1_sweep"] = c1_sweep(dev, args.sweep_reps)
         if world == 1 and args.sparse_conv_reps > 0:
             out["sparse_conv"] = sparse_conv_bench(dev, args.sparse_conv_reps)
+        if sc_multi is not None:
+            out["sparse_conv"] = sc_multi
         if pp is not None:
             out["pointpillars"] = pp
         if world == 1 and args.kpconv_steps > 0:
             out["kpconv"] = kpconv_bench(dev, args.kpconv_steps)
         if world == 1 and args.randla_frames > 0:
             out["randlanet"] = randla_frames(dev, args.randla_frames, cpu=not args.no_cpu_baseline)
+        if rl_multi is not None:
+            out["randlanet"] = rl_multi
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

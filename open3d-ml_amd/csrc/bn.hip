@@ -424,8 +424,8 @@ O3DML_API int o3dml_batch_norm_backward(const float* grad_y, const float* x, int
     a.part = ws.take<double>(2 * bn_blocks(n, c) * static_cast<int64_t>(c));
     a.coef = ws.take<float>(2 * c);
     if (n == 0) {
-        if (grad_weight) O3DML_CHECK_HIP(hipMemsetAsync(grad_weight, 0, sizeof(float) * c, st));
-        if (grad_bias) O3DML_CHECK_HIP(hipMemsetAsync(grad_bias, 0, sizeof(float) * c, st));
+        if (grad_weight) fill_async(grad_weight, 0, sizeof(float) * c, st);
+        if (grad_bias) fill_async(grad_bias, 0, sizeof(float) * c, st);
         return 0;
     }
     bn_reduce<1>(a, st);

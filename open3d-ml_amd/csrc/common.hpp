@@ -86,6 +86,13 @@ struct TimedRegion {
 
 __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Set `bytes` of device memory at dst to the byte `value` on st with a
+// kernel (fill.hip): capture-safe, unlike a hipMemsetAsync node (>= 16 bytes
+// re-applied on the first graph replay only).  Throws Error on launch failure.
+void fill_async(void* dst, int value, size_t bytes, hipStream_t st);
+// Device-to-device copy by a kernel (no memcpy node in captured graphs).
+void copy_async(void* dst, const void* src, size_t bytes, hipStream_t st);
+
 // Pinned host scratch for the few int64 sizes a count phase reads back (a
 // pageable destination goes through a staging copy): 8 slots per host
 // thread, allocated on first use, never freed.

@@ -103,10 +103,10 @@ O3DML_API int o3dml_kpconv_rigid_backward(const float* q_pts, int64_t n, const f
         return o3dml_kpconv_weighted_features_backward_det(q_pts, n, s_pts, n_support, neighbors, index_bits, nb, gwf,
                                                            cin, kernel_points, K, 0, extent, influence, closest, dx,
                                                            workspace, workspace_bytes, stream);
-    if (n_support > 0 && cin > 0 &&
-        hipMemsetAsync(dx, 0, sizeof(float) * n_support * cin, as_stream(stream)) != hipSuccess) {
-        set_error("kpconv_rigid_backward: hipMemsetAsync failed");
-        return 1;
+    try {
+        fill_async(dx, 0, sizeof(float) * n_support * cin, as_stream(stream));
+    } catch (const Error& e) {
+        return e.code;
     }
     return o3dml_kpconv_weighted_features_backward(q_pts, n, s_pts, n_support, neighbors, index_bits, nb, gwf, cin,
                                                    kernel_points, K, 0, extent, influence, closest, dx, stream);

@@ -251,7 +251,7 @@ O3DML_API int o3dml_nms(const float* boxes, const float* scores, int64_t n, floa
                   (long long)kNmsMaxBoxes);
     hipStream_t st = as_stream(stream);
     if (n == 0) {
-        O3DML_CHECK_HIP(hipMemsetAsync(keep_count, 0, sizeof(int64_t), st));
+        fill_async(keep_count, 0, sizeof(int64_t), st);
         return 0;
     }
     const int ni = static_cast<int>(n), words = static_cast<int>(nms_words(n));

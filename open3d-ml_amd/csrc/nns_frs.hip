@@ -1310,8 +1310,8 @@ static void frs_count_impl(const float* points, int64_t n_points, const float* q
     Workspace ws(workspace, workspace_bytes);
     FrsPlan pl = take_plan(ws, n_points, n_queries, n_batch, with_distances != 0);
     if (n_queries == 0 || n_points == 0) {
-        O3DML_CHECK_HIP(hipMemsetAsync(pl.scalars, 0, sizeof(int64_t) * 4, st));
-        O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t) * (n_queries + 1), st));
+        fill_async(pl.scalars, 0, sizeof(int64_t) * 4, st);
+        fill_async(neighbors_row_splits, 0, sizeof(int64_t) * (n_queries + 1), st);
         if (totals) frs_totals_kernel<<<1, 64, 0, st>>>(neighbors_row_splits, n_queries, pl.scalars, totals);
         return;
     }

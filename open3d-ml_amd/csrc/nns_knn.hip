@@ -462,7 +462,7 @@ O3DML_API int o3dml_knn_search_count(const float* points, int64_t n_points, cons
                            ignore_query_point, neighbors_row_splits, ws, st);
             return 0;
         }
-        O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
+        fill_async(neighbors_row_splits, 0, sizeof(int64_t), st);
         if (n_queries == 0) return 0;
         int64_t* cnt = ws.take<int64_t>(n_queries);
         if (ignore_query_point)
@@ -484,7 +484,7 @@ O3DML_API int o3dml_knn_search_count(const float* points, int64_t n_points, cons
     uint32_t* qkeys = ws.take<uint32_t>(n_queries);
     uint32_t* qskeys = ws.take<uint32_t>(n_queries);
     uint32_t* qorder = ws.take<uint32_t>(n_queries);
-    O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
+    fill_async(neighbors_row_splits, 0, sizeof(int64_t), st);
     if (n_queries == 0) return 0;
     const uint32_t* order = nullptr;
     if (self_search) {

@@ -464,9 +464,9 @@ static KnnManyPlan take_knn_many(Workspace& ws, const float* pts, int64_t n, int
 void knn_many_count(const float* pts, int64_t n, const float* queries, int64_t m, int64_t k, int nb,
                     const int64_t* prs, const int64_t* qrs, int ignore, int64_t* rs, Workspace ws, hipStream_t st) {
     KnnManyPlan p = take_knn_many(ws, pts, n, m, k, prs, nb, st, true);
-    O3DML_CHECK_HIP(hipMemsetAsync(p.scalars, 0, 4 * sizeof(int64_t), st));
-    O3DML_CHECK_HIP(hipMemsetAsync(rs, 0, sizeof(int64_t), st));
-    O3DML_CHECK_HIP(hipMemcpyAsync(p.prs, prs, sizeof(int64_t) * (nb + 1), hipMemcpyDeviceToDevice, st));
+    fill_async(p.scalars, 0, 4 * sizeof(int64_t), st);
+    fill_async(rs, 0, sizeof(int64_t), st);
+    copy_async(p.prs, prs, sizeof(int64_t) * (nb + 1), st);
     if (m == 0) return;
     many_knn_counts_kernel<<<stream_grid(m, 256), 256, 0, st>>>(p.gi.sorted, p.gi.splits, p.gi.params, queries, m,
                                                                prs, qrs, nb, k, ignore, p.counts);
@@ -525,11 +525,11 @@ O3DML_API int o3dml_radius_search_count(const float* points, int64_t n_points, c
     Workspace ws(workspace, workspace_bytes);
     RadiusPlan p = take_radius_plan(ws, points, n_points, n_queries, points_row_splits, static_cast<int>(n_batch), st,
                                     true);
-    O3DML_CHECK_HIP(hipMemsetAsync(p.scalars, 0, 4 * sizeof(int64_t), st));
-    O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t), st));
+    fill_async(p.scalars, 0, 4 * sizeof(int64_t), st);
+    fill_async(neighbors_row_splits, 0, sizeof(int64_t), st);
     if (n_queries == 0) return 0;
     if (n_points == 0) {
-        O3DML_CHECK_HIP(hipMemsetAsync(neighbors_row_splits, 0, sizeof(int64_t) * (n_queries + 1), st));
+        fill_async(neighbors_row_splits, 0, sizeof(int64_t) * (n_queries + 1), st);
         return 0;
     }
     launch_radius<1, 0>(metric, ignore_query_point != 0, st, p, queries, radii, n_queries, queries_row_splits,

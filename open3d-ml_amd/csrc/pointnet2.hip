@@ -393,7 +393,7 @@ O3DML_API int o3dml_three_interpolate_grad(const float* grad_out, const int32_t*
                                            int64_t C, int64_t n, int64_t m, float* grad_features, void* stream) {
     O3DML_GUARD_BEGIN
     hipStream_t st = as_stream(stream);
-    if (B * C * m > 0) O3DML_CHECK_HIP(hipMemsetAsync(grad_features, 0, sizeof(float) * B * C * m, st));
+    if (B * C * m > 0) fill_async(grad_features, 0, sizeof(float) * B * C * m, st);
     const int64_t total = B * C * n;
     if (total == 0) return 0;
     three_interpolate_grad_kernel<<<stream_grid(total, 256), 256, 0, st>>>(grad_out, idx, weight, (int)B, (int)C,

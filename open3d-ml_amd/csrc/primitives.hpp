@@ -568,14 +568,15 @@ __global__ void __launch_bounds__(kBsThreads) block_radix_sort_pairs(const K* __
 }
 
 // Small-sort kind: 0 = LSD radix in one workgroup (default), 1 = bitonic
-// (O3DML_BS_KIND, A/B; o3dml_sort_pairs picks one per call for the tests)
-inline int g_block_sort_kind_override = -1;
-inline int block_sort_kind() {
+// (O3DML_BS_KIND, A/B); a call may pick one (small_kind >= 0: o3dml_sort_pairs
+// for the tests) — an argument, not process state, so concurrent host
+// threads never see another call's choice
+inline int block_sort_kind(int small_kind = -1) {
     static const int v = [] {
         const char* e = std::getenv("O3DML_BS_KIND");
         return e ? std::atoi(e) : 0;
     }();
-    return g_block_sort_kind_override >= 0 ? g_block_sort_kind_override : v;
+    return small_kind >= 0 ? small_kind : v;
 }
 
 // Largest n sorted in one workgroup: O3DML_BS_MAX (A/B), default kBsMax
@@ -605,7 +606,7 @@ size_t radix_sort_workspace_bytes(int64_t n) {
 // keys_in must not alias keys_out.
 template <class K>
 void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, uint32_t* vals_out,
-                      int64_t n, int end_bit, Workspace& ws, hipStream_t st) {
+                      int64_t n, int end_bit, Workspace& ws, hipStream_t st, int small_kind = -1) {
     if (n <= 0) return;
     const int passes = (end_bit + 7) / 8;
     if (passes == 0 || n == 1) {
@@ -619,7 +620,7 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
         // slower: 46 vs 37 us at ~4k keys — dependent LDS latency of the
         // per-round binary searches)
         const int ni = static_cast<int>(n);
-        if (block_sort_kind() == 0) {
+        if (block_sort_kind(small_kind) == 0) {
             if (n <= kBsThreads)
                 block_radix_sort_pairs<K, 1><<<1, kBsThreads, 0, st>>>(keys_in, vals_in, keys_out, vals_out, ni, mask);
             else if (n <= 2 * kBsThreads)

@@ -94,16 +94,11 @@ O3DML_API int o3dml_sort_pairs(const void* keys_in, const uint32_t* vals_in, voi
     O3DML_REQUIRE(workspace_bytes >= o3dml_sort_pairs_workspace_size(n, key_bytes), "sort_pairs: workspace too small");
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
-    struct KindScope {  // restored on every exit
-        int prev;
-        explicit KindScope(int k) : prev(prim::g_block_sort_kind_override) { prim::g_block_sort_kind_override = k; }
-        ~KindScope() { prim::g_block_sort_kind_override = prev; }
-    } kind_scope(small_kind);
     if (key_bytes == 8)
         prim::radix_sort_pairs<uint64_t>(static_cast<const uint64_t*>(keys_in), vals_in,
-                                         static_cast<uint64_t*>(keys_out), vals_out, n, end_bit, ws, st);
+                                         static_cast<uint64_t*>(keys_out), vals_out, n, end_bit, ws, st, small_kind);
     else
         prim::radix_sort_pairs<uint32_t>(static_cast<const uint32_t*>(keys_in), vals_in,
-                                         static_cast<uint32_t*>(keys_out), vals_out, n, end_bit, ws, st);
+                                         static_cast<uint32_t*>(keys_out), vals_out, n, end_bit, ws, st, small_kind);
     O3DML_GUARD_END
 }

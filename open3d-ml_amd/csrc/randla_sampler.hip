@@ -424,7 +424,7 @@ O3DML_API int o3dml_randla_up_from_knn(int32_t* nb, int k, const float* cat, int
     Workspace ws(workspace, workspace_bytes);
     uint32_t* cntr = ws.take<uint32_t>(1);
     uint32_t* list = ws.take<uint32_t>(total);
-    O3DML_CHECK_HIP(hipMemsetAsync(cntr, 0, sizeof(uint32_t), st));
+    fill_async(cntr, 0, sizeof(uint32_t), st);
     up_from_knn_kernel<<<stream_grid(total, 256), 256, 0, st>>>(nb, k, total, L, up, list, cntr);
     O3DML_LAUNCH_CHECK();
     up_fallback_kernel<<<512, 256, 0, st>>>(cat, L, list, cntr, up);

@@ -2351,9 +2351,9 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
     int32_t* inv = ws.take<int32_t>(n_in * K);
     float* ipscale = ws.take<float>(n_in * K);
     int* status = ws.take<int>(4);
-    O3DML_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, st));  // [2], [3]: no tile orders yet
+    fill_async(status, 0, sizeof(int) * 4, st);  // [2], [3]: no tile orders yet
     if (n_out > 0) {
-        O3DML_CHECK_HIP(hipMemsetAsync(map, 0xff, sizeof(int32_t) * n_out * K, st));
+        fill_async(map, 0xff, sizeof(int32_t) * n_out * K, st);
         build_kernel_map_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(
                 neighbors_index, neighbors_kernel_index, neighbors_importance, neighbors_row_splits, n_out, n_in, K,
                 map, neighbors_importance ? pscale : nullptr, norm, status);
@@ -2363,7 +2363,7 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
         O3DML_LAUNCH_CHECK();
     }
     if (want_inverse && n_in > 0) {  // map entries are < n_in (out-of-range pairs were dropped, status 8)
-        O3DML_CHECK_HIP(hipMemsetAsync(inv, 0xff, sizeof(int32_t) * n_in * K, st));
+        fill_async(inv, 0xff, sizeof(int32_t) * n_in * K, st);
         if (n_out > 0) {
             build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(
                     map, neighbors_importance ? pscale : nullptr, n_out, K, inv,
@@ -2451,7 +2451,7 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
         O3DML_LAUNCH_CHECK();
     }
     if (want_inverse) {
-        O3DML_CHECK_HIP(hipMemsetAsync(inv, 0xff, sizeof(int32_t) * n_in * K, st));
+        fill_async(inv, 0xff, sizeof(int32_t) * n_in * K, st);
         build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, nullptr, n_out, K, inv, nullptr,
                                                                             status);
         O3DML_LAUNCH_CHECK();
@@ -2623,7 +2623,7 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
     if (grad_filters) {
         const int64_t KC = static_cast<int64_t>(K) * cin * cout;
         if (n_out == 0) {
-            O3DML_CHECK_HIP(hipMemsetAsync(grad_filters, 0, sizeof(float) * KC, st));
+            fill_async(grad_filters, 0, sizeof(float) * KC, st);
             return 0;
         }
         int64_t* flags = ws.take<int64_t>(n_out * K);

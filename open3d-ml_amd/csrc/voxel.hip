@@ -333,7 +333,7 @@ inline size_t seg_state_bytes(int64_t n, int nb) {
 // keys (unsorted) -> sorted segments, heads, starts, batch firsts.
 inline void sort_segments(const uint64_t* keys, int64_t n, int end_bit, uint64_t invalid, int nb, bool batch_shift,
                           uint64_t batch_div, SegState& s, Workspace& ws, hipStream_t st) {
-    O3DML_CHECK_HIP(hipMemsetAsync(s.scalars, 0, sizeof(int64_t) * 8, st));
+    fill_async(s.scalars, 0, sizeof(int64_t) * 8, st);
     const unsigned g = stream_grid(n > 0 ? n : 1, 256);
     if (n > 0) {
         Workspace sws = ws;
@@ -509,7 +509,7 @@ O3DML_API int o3dml_grid_subsample_count_async(const float* points, int64_t n_po
     Workspace ws(workspace, workspace_bytes);
     const int nb = static_cast<int>(n_batch);
     if (n_points == 0) {
-        O3DML_CHECK_HIP(hipMemsetAsync(out, 0, sizeof(int64_t) * (2 + nb), st));
+        fill_async(out, 0, sizeof(int64_t) * (2 + nb), st);
         return 0;
     }
     SegState s = take_seg_state(ws, n_points, nb);
@@ -575,7 +575,7 @@ O3DML_API int o3dml_grid_subsample_fill(const float* points, int64_t n_points, i
         O3DML_LAUNCH_CHECK();
         sub_lengths_kernel<<<1, 256, 0, st>>>(s.bfirst, s.keep_incl, nb, out_lengths);
     } else {
-        O3DML_CHECK_HIP(hipMemsetAsync(out_lengths, 0, sizeof(int64_t) * nb, st));
+        fill_async(out_lengths, 0, sizeof(int64_t) * nb, st);
     }
     O3DML_LAUNCH_CHECK();
     O3DML_GUARD_END
@@ -677,7 +677,7 @@ O3DML_API int o3dml_calculate_grid_count(const float* positions, int64_t n_point
     GridState g = take_grid_state(ws, n_points);
     int64_t host[2] = {0, 0};
     if (n_points > 0) {
-        O3DML_CHECK_HIP(hipMemsetAsync(g.flags, 0, 2 * sizeof(int64_t), st));
+        fill_async(g.flags, 0, 2 * sizeof(int64_t), st);
         const unsigned gr = stream_grid(n_points, 256);
         grid_parent_kernel<<<gr, 256, 0, st>>>(positions, n_points, g.keys, g.flags);
         O3DML_LAUNCH_CHECK();

@@ -111,6 +111,28 @@ def to_dev(t, device, dtype=None):
     return t.to(device, non_blocking=False).contiguous()
 
 
+class SizeCache:
+    """Bounded memo of workspace-size queries (one ctypes call per new
+    shape): keys carry per-batch point counts that change step to step, so
+    the cache is an LRU of at most `cap` entries, not an ever-growing dict."""
+
+    def __init__(self, query, cap=1024):
+        self.query, self.cap, self.d = query, cap, OrderedDict()
+
+    def __call__(self, *key):
+        v = self.d.get(key)
+        if v is None:
+            v = self.d[key] = self.query(*key)
+            if len(self.d) > self.cap:
+                self.d.popitem(last=False)
+        else:
+            self.d.move_to_end(key)
+        return v
+
+    def __len__(self):
+        return len(self.d)
+
+
 def workspace(nbytes, device):
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
 
@@ -169,4 +191,4 @@ def metric_code(metric):
 
 
 __all__ = ["require_gpu", "gpu_device", "stream_handle", "ptr", "to_dev", "workspace",
-           "row_splits_host", "scalar", "back_to", "check_points", "index_bits", "metric_code", "_lib"]
+           "row_splits_host", "scalar", "SizeCache", "back_to", "check_points", "index_bits", "metric_code", "_lib"]

@@ -20,16 +20,13 @@ import os
 import torch
 
 from . import _lib
-from ._util import ptr, stream_handle
+from ._util import SizeCache, ptr, stream_handle
 
-_WS = {}  # (n, c) -> workspace bytes
+_WS = SizeCache(lambda n, c: max(int(_lib.load().o3dml_batch_norm_workspace_size(n, c)), 1))
 
 
 def _ws(n, c, dev):
-    b = _WS.get((n, c))
-    if b is None:
-        b = _WS[(n, c)] = max(int(_lib.load().o3dml_batch_norm_workspace_size(n, c)), 1)
-    return torch.empty(b, dtype=torch.uint8, device=dev)
+    return torch.empty(_WS(n, c), dtype=torch.uint8, device=dev)
 
 
 def _bn_forward(x, weight, bias, bn, training, slope):
@@ -79,14 +76,12 @@ class _BnAct(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
-_LWS = {}  # (n, cin, cout) -> workspace bytes of the one-call Linear + BN
+# workspace bytes of the one-call Linear + BN per (n, cin, cout)
+_LWS = SizeCache(lambda n, cin, cout: max(int(_lib.load().o3dml_linear_bn_workspace_size(n, cin, cout)), 1))
 
 
 def _lws(n, cin, cout, dev):
-    b = _LWS.get((n, cin, cout))
-    if b is None:
-        b = _LWS[(n, cin, cout)] = max(int(_lib.load().o3dml_linear_bn_workspace_size(n, cin, cout)), 1)
-    return torch.empty(b, dtype=torch.uint8, device=dev)
+    return torch.empty(_LWS(n, cin, cout), dtype=torch.uint8, device=dev)
 
 
 class _LinearBnAct(torch.autograd.Function):
@@ -97,7 +92,7 @@ class _LinearBnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, weight, bias, bn, training, slope):
         x = x.contiguous()
-        w = w.detach().contiguous()
+        w_param, w = w, w.detach().contiguous()
         n, cin = x.shape
         cout = w.shape[0]
         z = torch.empty((n, cout), dtype=torch.float32, device=x.device)
@@ -113,13 +108,16 @@ class _LinearBnAct(torch.autograd.Function):
                   ptr(bn.num_batches_tracked) if track else None, float(bn.momentum or 0.0), float(bn.eps),
                   int(training), int(slope is not None), float(slope or 0.0), ptr(z), ptr(y), ptr(save), ptr(ws),
                   ws.numel(), stream_handle(x.device))
-        ctx.save_for_backward(x, w, z, save)
+        # the parameter itself (not a detached view): autograd's version check
+        # then catches an in-place update between forward and backward
+        ctx.save_for_backward(x, w_param, z, save)
         ctx.meta = (training, slope, weight is not None, bias is not None)
         return y
 
     @staticmethod
     def backward(ctx, g):
         x, w, z, save = ctx.saved_tensors
+        w = w.detach().contiguous()
         training, slope, has_w, has_b = ctx.meta
         g = g.contiguous()
         n, cin = x.shape

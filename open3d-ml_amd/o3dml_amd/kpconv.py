@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from ._util import gpu_device, index_bits, ptr, stream_handle, to_dev, workspace
+from ._util import SizeCache, gpu_device, index_bits, ptr, stream_handle, to_dev, workspace
 
 _INFLUENCE = {"constant": 0, "linear": 1, "gaussian": 2}
 
@@ -90,7 +90,8 @@ class _WeightedFeatures(torch.autograd.Function):
         return dx, None, None, None, dkp, None, None, None, None, dmod
 
 
-_KWS = {}  # (n, nb, n_support, K, cin, cout, deterministic) -> workspace bytes
+# (n, nb, n_support, K, cin, cout, deterministic) -> workspace bytes
+_KWS = SizeCache(lambda *key: max(int(_lib.load().o3dml_kpconv_rigid_workspace_size(*key)), 1))
 
 
 class _KPConvRigid(torch.autograd.Function):
@@ -101,11 +102,7 @@ class _KPConvRigid(torch.autograd.Function):
 
     @staticmethod
     def _ws(n, nb, ns, K, cin, cout, det, dev):
-        key = (n, nb, ns, K, cin, cout, det)
-        b = _KWS.get(key)
-        if b is None:
-            b = _KWS[key] = max(int(_lib.load().o3dml_kpconv_rigid_workspace_size(n, nb, ns, K, cin, cout, det)), 1)
-        return torch.empty(b, dtype=torch.uint8, device=dev)
+        return torch.empty(_KWS(n, nb, ns, K, cin, cout, det), dtype=torch.uint8, device=dev)
 
     @staticmethod
     def forward(ctx, x, w, q_pts, s_pts, nbr, kp, extent, influence, closest):
@@ -119,13 +116,16 @@ class _KPConvRigid(torch.autograd.Function):
         _lib.call("o3dml_kpconv_rigid_forward", ptr(q_pts), n, ptr(s_pts), s_pts.shape[0], ptr(nbr),
                   index_bits(nbr.dtype), nb, ptr(x), cin, ptr(kpd), K, float(extent), influence, int(closest),
                   ptr(w2), cout, ptr(wf), ptr(out), ptr(ws), ws.numel(), stream_handle(x.device))
-        ctx.save_for_backward(w2, wf, q_pts, s_pts, nbr, kpd)
+        # the parameter itself (not a detached view): autograd's version check
+        # then catches an in-place update between forward and backward
+        ctx.save_for_backward(w, wf, q_pts, s_pts, nbr, kpd)
         ctx.meta = (extent, influence, closest, x.shape[0], tuple(w.shape))
         return out
 
     @staticmethod
     def backward(ctx, g):
-        w2, wf, q_pts, s_pts, nbr, kp = ctx.saved_tensors
+        w, wf, q_pts, s_pts, nbr, kp = ctx.saved_tensors
+        w2 = w.detach().reshape(-1, w.shape[-1]).contiguous()
         extent, influence, closest, n_s, wshape = ctx.meta
         n, K, cin = wf.shape
         nb = nbr.shape[1]

@@ -19,6 +19,7 @@ is grid-subsampled and projected ONCE, then patches are cropped, recentred,
 searched (kNN k=16 / k=1 per layer), inferred and accumulated on the GPU
 until every sub-point's possibility exceeds 0.5.
 """
+import itertools
 import os
 
 import numpy as np
@@ -346,6 +347,22 @@ class RandLANet(nn.Module):
         self._invalidate()
         return super().load_state_dict(*a, **kw)
 
+    def _apply(self, fn, *a, **kw):
+        # .to() / .half() / .cuda() replace the parameters: the folded copies
+        # (and graphs on them) would keep the old values
+        self._invalidate()
+        return super()._apply(fn, *a, **kw)
+
+    def _sync_folded(self):
+        """Drop the folded eval weights (and the graphs built on them) if any
+        parameter or buffer was modified in place since they were made (an
+        in-place copy_, an optimizer step in eval mode): the tensors' version
+        counters are compared, once per frame / forward call."""
+        v = tuple(t._version for t in itertools.chain(self.parameters(), self.buffers()))
+        if self.__dict__.get("_o3dml_wver") != v:
+            self._invalidate()
+            self.__dict__["_o3dml_wver"] = v
+
     def forward_points(self, feat, coords, nbrs, subs, ups):
         """One or more concatenated patches, channels-last.
         feat [N0,Cin]; coords[i] [Ni,3]; nbrs[i] [Ni,K] int32; subs[i] [N(i+1),K] int32
@@ -388,6 +405,7 @@ class RandLANet(nn.Module):
         """Reference signature (randlanet.py:241-298): inputs['features'] [B,N,Cin],
         'coords'/'neighbor_indices'/'sub_idx'/'interp_idx' lists of [B,...]."""
         dev = next(self.parameters()).device
+        self._sync_folded()
         feats = inputs["features"].to(dev).float()
         B, N, _ = feats.shape
         L = len(self.encoder)
@@ -758,6 +776,7 @@ class SemSegInference:
     @torch.no_grad()
     def run(self, points, patch_hook=None, init_possibility=None, perm_hook=None):
         self.model.eval()
+        self.model._sync_folded()
         points = points.to(self.device).float().contiguous()
         C = self.model.cfg["num_classes"]
         sub, proj = self.preprocess(points)

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._util import gpu_device, ptr, stream_handle, to_dev, workspace
+from ._util import SizeCache, gpu_device, ptr, stream_handle, to_dev, workspace
 
 
 def _opt(t, dev, dtype=torch.float32):
@@ -423,17 +423,12 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
     return out if inp_features.is_cuda else out.cpu()
 
 
-_FWS = {}  # (n_out, n_in, K, cin, cout) -> forward workspace bytes (one ctypes query per shape)
+# (n_out, n_in, K, cin, cout) -> forward workspace bytes (one ctypes query per shape)
+_FWS = SizeCache(lambda *key: int(_lib.load().o3dml_sparse_conv_forward_workspace_size(*key)))
 
 
 def _forward_ws_bytes(lib, n_out, n_in, K, cin, cout):
-    key = (n_out, n_in, K, cin, cout)
-    v = _FWS.get(key)
-    if v is None:
-        if len(_FWS) > 4096:
-            _FWS.clear()
-        v = _FWS[key] = int(lib.o3dml_sparse_conv_forward_workspace_size(n_out, n_in, K, cin, cout))
-    return v
+    return _FWS(n_out, n_in, K, cin, cout)
 
 
 def _late_ok(status):

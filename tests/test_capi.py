@@ -72,3 +72,17 @@ def test_layer_workspace_sizes():
         lay = lib.o3dml_fixed_radius_search_layer_workspace_size(n, m, b, t)
         assert lay >= lib.o3dml_fixed_radius_search_workspace_size(n, m, b)
         assert lay >= lib.o3dml_build_spatial_hash_table_workspace_size(n, t)
+
+
+def test_workspace_size_caches_are_bounded():
+    """The per-shape workspace-size memos (BN, Linear+BN, rigid KPConv,
+    sparse conv) are LRUs of bounded size: KPFCNN's per-step point counts
+    would otherwise grow them for the whole run."""
+    from o3dml_amd import batchnorm, kpconv, sparse_conv
+    from o3dml_amd._util import SizeCache
+    for c in (batchnorm._WS, batchnorm._LWS, kpconv._KWS, sparse_conv._FWS):
+        assert isinstance(c, SizeCache) and c.cap <= 4096
+    for n in range(1, 3000):
+        batchnorm._WS(n, 64)
+    assert len(batchnorm._WS) <= batchnorm._WS.cap
+    assert batchnorm._WS(5, 64) == max(int(__import__("o3dml_amd")._lib.load().o3dml_batch_norm_workspace_size(5, 64)), 1)

@@ -150,7 +150,7 @@ def test_bench_spawns_ranks_without_torchrun():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing-test",
-                          "--steps", "3", "--warmup", "1", "--scenes", "2"], env=env, capture_output=True,
+                          "--steps", "3", "--warmup", "1", "--scenes", "2", "--randla-frames", "3"], env=env, capture_output=True,
                          text=True, timeout=240, check=True).stdout
     lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out  # rank 0 only
@@ -158,3 +158,19 @@ def test_bench_spawns_ranks_without_torchrun():
     assert rec["n_gpus"] == 2 and rec["ranks_reported"] == 2
     assert rec["units_per_rank"] == [2 * 65536 * 3] * 2
     assert abs(rec["value"] - sum(rec["units_per_rank"]) / rec["elapsed_max_s"] / 1e6) < 1e-6 * rec["value"]
+    # C2 / C4 legs: --randla-frames scans per rank dealt round-robin, frames over the max time
+    shards = rec["scan_shards"]
+    assert shards == [[0, 2, 4], [1, 3, 5]]
+    assert sorted(sum(shards, [])) == list(range(6))
+    assert rec["frames_per_rank"] == [3, 3] and rec["frames_total"] == 6
+    if rec["frames_elapsed_max_s"] > 0:
+        assert abs(rec["frames_per_s"] - 6 / rec["frames_elapsed_max_s"]) < 1e-6 * rec["frames_per_s"]
+
+
+def test_shard_round_robin():
+    import bench
+    for world in (1, 2, 3, 8):
+        parts = [bench.shard(13, world, r) for r in range(world)]
+        assert sorted(sum(parts, [])) == list(range(13))
+        assert all(p == list(range(r, 13, world)) for r, p in enumerate(parts))
+    assert bench.shard(6, 1, 0) == list(range(6))  # N = 1: the scans of the single-GPU line

@@ -179,19 +179,23 @@ def test_knn_select_set_index_order(cuda):
 
 def test_knn_many_path_is_capturable(cuda):
     """64 < k <= 2048 count + fill (incl. the overflow queries' radix
-    selection) inside a HIP graph capture, replayed: no host synchronisation
-    in the library; the replay equals the oracle."""
+    selection) inside a HIP graph capture, replayed several times with the
+    queries changed between replays: no host synchronisation in the library,
+    and every replay equals the oracle — the overflow counter and list are
+    re-zeroed by a kernel on each replay (a hipMemsetAsync node of >= 16 bytes
+    is re-applied on the first replay only on this runtime: csrc/fill.hip)."""
     import bench
     from o3dml_amd import _lib
     from o3dml_amd._util import ptr
     lib = _lib.load()
     scan, _ = bench.make_scan(5)
     pts = np.ascontiguousarray(scan[:30000])
-    qry = np.ascontiguousarray(scan[:400])  # dense ground: candidate lists overflow -> radix selection
+    # dense ground: candidate lists overflow -> radix selection
+    query_sets = [np.ascontiguousarray(scan[a:a + 400]) for a in (0, 1000, 0, 5000)]
     k = 1500
     prs = np.array([0, 30000], np.int64)
     qrs = np.array([0, 400], np.int64)
-    pt, qt = torch.from_numpy(pts).to(cuda), torch.from_numpy(qry).to(cuda)
+    pt, qt = torch.from_numpy(pts).to(cuda), torch.from_numpy(query_sets[0]).to(cuda)
     prs_d, qrs_d = torch.from_numpy(prs).to(cuda), torch.from_numpy(qrs).to(cuda)
     rs = torch.empty(401, dtype=torch.int64, device=cuda)
     idx = torch.empty(400 * k, dtype=torch.int32, device=cuda)
@@ -206,9 +210,14 @@ def test_knn_many_path_is_capturable(cuda):
                   prs.ctypes.data, qrs.ctypes.data, 1, 0, 0, ptr(rs), ptr(ws), ws.numel(), st)
         _lib.call("o3dml_knn_search_fill", ptr(pt), 30000, ptr(qt), 400, k, 1, ptr(qrs_d), prs.ctypes.data,
                   qrs.ctypes.data, 1, 0, ptr(rs), 32, ptr(idx), ptr(dist), ptr(ws), ws.numel(), st)
-    g.replay()
-    torch.cuda.synchronize(cuda)
-    assert int(ws[:8].view(torch.int64)[0]) > 0  # some queries took the overflow path
-    oi, ors, od = O.knn_search(pts, qry, k, prs, qrs, return_distances=True)
-    assert np.array_equal(rs.cpu().numpy(), ors)
-    assert np.array_equal(idx.cpu().numpy(), oi) and np.array_equal(dist.cpu().numpy(), od)
+    overflow = []
+    for i, qry in enumerate(query_sets):
+        qt.copy_(torch.from_numpy(qry))
+        g.replay()
+        torch.cuda.synchronize(cuda)
+        overflow.append(int(ws[:8].view(torch.int64)[0]))
+        oi, ors, od = O.knn_search(pts, qry, k, prs, qrs, return_distances=True)
+        assert np.array_equal(rs.cpu().numpy(), ors), i
+        assert np.array_equal(idx.cpu().numpy(), oi) and np.array_equal(dist.cpu().numpy(), od), i
+    assert overflow[0] > 0  # some queries took the overflow path
+    assert overflow[2] == overflow[0]  # the counter starts from zero on every replay
