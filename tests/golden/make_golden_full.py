@@ -263,6 +263,22 @@ def make_c4(out):
     out["c4_n"] = np.int64(len(pos))
     out["c4_logit_rows"] = logits[::11]
     out["c4_logit_colsum"] = logits.astype(np.float64).sum(0)
+    # the same reference model in float64 (same rulebooks; float64 sums): the
+    # truth the per-element C4 check holds fp32 results to, and the
+    # reference's own fp32 error against it
+    import copy
+    model64 = copy.deepcopy(model).double()
+    inp64 = types.SimpleNamespace(point=[torch.from_numpy(pos).double()], feat=[torch.from_numpy(feat).double()],
+                                  batch_lengths=[len(pos)])
+    t0 = time.time()
+    with torch.no_grad():
+        logits64 = model64(inp64).numpy()
+    print("c4 f64", round(time.time() - t0, 1), "s")
+    out["c4_f64_logit_rows"] = logits64[::11]
+    out["c4_ref32_abs_err"] = np.float64(np.abs(logits.astype(np.float64) - logits64).max())
+    out["c4_ref32_rel_err"] = np.float64((np.abs(logits.astype(np.float64) - logits64) /
+                                          np.maximum(np.abs(logits64), 1e-300)).max())
+    print("c4 ref fp32 vs fp64: max abs", float(out["c4_ref32_abs_err"]), "max |f64|", float(np.abs(logits64).max()))
 
 
 def main():

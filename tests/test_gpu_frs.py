@@ -390,3 +390,25 @@ def test_frs_large_item_bit_exact(cuda, lg):
     oi, ors, _ = O.fixed_radius_search(pts, pts, r)
     assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
     assert np.array_equal(res.neighbors_index.cpu().numpy(), oi)
+
+
+def test_frs_2_24_sweep_scene_bit_exact(cuda):
+    """The 2^24-point c1_sweep scene (bench.py c1_sweep: U[0,1)^3, seed 24,
+    r = 0.05 (65536 / N)^(1/3); u32 temp rows, Morton query order) through
+    layers.FixedRadiusSearch, twice as the sweep calls it, vs the optimised
+    CPU search of the same semantics (oracle/cpu_frs.c, bit-identical to the
+    oracle: tests/test_golden.py::test_cpu_frs_fast_equals_oracle): row splits
+    and every neighbour index bit-exact (~560 M pairs, compared on the GPU)."""
+    from o3dml_amd import layers
+    n = 1 << 24
+    pts = np.random.default_rng(24).random((n, 3), dtype=np.float32)
+    r = 0.05 * (65536.0 / n) ** (1.0 / 3.0)
+    t = torch.from_numpy(pts).to(cuda)
+    rs = torch.tensor([0, n], dtype=torch.int64)
+    nns = layers.FixedRadiusSearch()
+    for _ in range(2):
+        res = nns(t, t, r, rs, rs)
+    oi, ors = O.fixed_radius_search_fast(pts, r, rs.numpy())
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert res.neighbors_index.shape[0] == len(oi)
+    assert torch.equal(res.neighbors_index, torch.from_numpy(oi).to(cuda))

@@ -220,5 +220,12 @@ def test_c4_scn_full_room_vs_reference(cuda):
         out = m(inp).cpu().numpy()
     ref = F["c4_logit_rows"]
     assert _rel(out[::11], ref) < 1e-4
+    # per element against the float64 run of the same reference model:
+    # |a - b| <= 1e-4 |b| + floor, floor = 1e-5 max|b| (the reference's own
+    # fp32 logits sit within c4_ref32_abs_err = 2.8e-7 of it)
+    b64 = F["c4_f64_logit_rows"]
+    err = np.abs(out[::11].astype(np.float64) - b64)
+    bound = 1e-4 * np.abs(b64) + 1e-5 * np.abs(b64).max()
+    assert (err <= bound).all(), (float((err / bound).max()), float(err.max()))
     np.testing.assert_allclose(out.astype(np.float64).sum(0), F["c4_logit_colsum"], rtol=0,
                                atol=1e-5 * len(out) * np.abs(ref).max())

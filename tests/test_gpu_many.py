@@ -221,3 +221,46 @@ def test_knn_many_path_is_capturable(cuda):
         assert np.array_equal(idx.cpu().numpy(), oi) and np.array_equal(dist.cpu().numpy(), od), i
     assert overflow[0] > 0  # some queries took the overflow path
     assert overflow[2] == overflow[0]  # the counter starts from zero on every replay
+
+
+def test_knn_search_layer_point_transformer_shapes(cuda):
+    """layers.KNNSearch as PointTransformer's knn_batch calls it
+    (point_transformer.py:700-734: CPU tensors in, return_distances=True,
+    reshape(-1, k)) at the model's shapes (:60 stride [1, 4, 4, 4, 4], nsample
+    [8, 16, 16, 16, 16]) on two S3DIS-like clouds of 20,000 points: per level
+    the self kNN of queryandgroup (k = nsample), the transition-down kNN
+    (level l - 1 points, level l queries, k = 16) and the interpolation 3-NN
+    (level l points, level l - 1 queries) — indices and distances bit-exact
+    vs the oracle, results back on the CPU."""
+    import bench
+    from o3dml_amd import layers
+    pts, _, _, lengths = bench.make_c3(0)
+    rng = np.random.default_rng(9)
+    levels = [(pts, np.array([0, lengths[0], lengths[0] + lengths[1]], np.int64))]
+    for _ in range(4):  # stride 4: a subset of each item (FPS-sized)
+        p, rs = levels[-1]
+        keep, nrs = [], [0]
+        for b in range(len(rs) - 1):
+            nb = (rs[b + 1] - rs[b]) // 4
+            keep.append(rs[b] + np.sort(rng.choice(rs[b + 1] - rs[b], nb, replace=False)))
+            nrs.append(nrs[-1] + nb)
+        levels.append((np.ascontiguousarray(p[np.concatenate(keep)]), np.array(nrs, np.int64)))
+    nsample = [8, 16, 16, 16, 16]
+    knn = layers.KNNSearch(return_distances=True)
+
+    def check(points, prs, queries, qrs, k):
+        ans = knn(torch.from_numpy(points), torch.from_numpy(queries), k, torch.from_numpy(prs),
+                  torch.from_numpy(qrs))
+        assert not ans.neighbors_index.is_cuda  # CPU in -> CPU out, as the caller expects
+        oi, ors, od = O.knn_search(points, queries, k, prs, qrs, return_distances=True)
+        assert np.array_equal(ans.neighbors_row_splits.numpy(), ors)
+        assert np.array_equal(ans.neighbors_index.numpy(), oi), k
+        assert np.array_equal(ans.neighbors_distance.numpy(), od), k
+        assert ans.neighbors_index.reshape(-1, k).shape == (len(queries), k)
+
+    for lvl, (p, rs) in enumerate(levels):
+        check(p, rs, p, rs, nsample[lvl])
+        if lvl > 0:
+            fp, frs = levels[lvl - 1]
+            check(fp, frs, p, rs, 16)  # transition down
+            check(p, rs, fp, frs, 3)   # interpolation

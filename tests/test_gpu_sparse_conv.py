@@ -29,6 +29,31 @@ def _csr_conv64(W, x, nidx, kidx, rs, bias=None):
     return out if bias is None else out + bias
 
 
+def _close_elem(a, b, s, rtol=RTOL, floor=1e-6):
+    """Per element against the float64 truth b: |a - b| <= rtol |b| + floor * s,
+    s = the element's sum of |term| (sum over its pairs of |x| . |W|): the
+    absolute floor only matters where the terms cancel (|b| << s); 1e-6 s is
+    ~16 units of fp32 roundoff of the summed magnitudes."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    s = np.asarray(s, np.float64)
+    err = np.abs(a - b)
+    bound = rtol * np.abs(b) + floor * s
+    assert (err <= bound).all(), f"worst err / bound {float((err / bound).max()):.3e}, max rel {float((err / np.maximum(np.abs(b), 1e-300)).max()):.3e}"
+
+
+def _truth64(W, x, nidx, kidx, rs, bias=None):
+    """(float64 output, per-element term magnitude sum) of the CSR conv."""
+    W = torch.as_tensor(np.asarray(W), dtype=torch.float64)
+    x = torch.as_tensor(np.asarray(x), dtype=torch.float64)
+    nidx, kidx, rs = (torch.as_tensor(np.asarray(t)) for t in (nidx, kidx, rs))
+    out = _csr_conv64(W, x, nidx, kidx, rs, None if bias is None else torch.as_tensor(np.asarray(bias), dtype=torch.float64))
+    mag = _csr_conv64(W.abs(), x.abs(), nidx, kidx, rs)
+    if bias is not None:
+        mag = mag + torch.as_tensor(np.abs(np.asarray(bias)), dtype=torch.float64)
+    return out.numpy(), mag.numpy()
+
+
 def _close(a, b, rtol=RTOL):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
@@ -57,6 +82,9 @@ def test_submanifold_conv_forward(cuda, cin, cout):
     ref = O.sparse_conv(conv.kernel.detach().cpu().numpy(), feat.cpu().numpy(), oi, ok, ors)
     ref = ref + conv.bias.detach().cpu().numpy()
     _close(out.detach().cpu().numpy(), ref)
+    t64, mag = _truth64(conv.kernel.detach().cpu().numpy(), feat.cpu().numpy(), oi, ok, ors,
+                        conv.bias.detach().cpu().numpy())
+    _close_elem(out.detach().cpu().numpy(), t64, mag)
 
 
 def test_strided_and_transposed_conv(cuda):
@@ -81,6 +109,8 @@ def test_strided_and_transposed_conv(cuda):
     assert (np.diff(ors) <= 8).all() and (np.diff(ors) >= 1).all()
     ref = O.sparse_conv(conv.kernel.detach().cpu().numpy(), feat.cpu().numpy(), oi, ok, ors)
     _close(out.detach().cpu().numpy(), ref)
+    _close_elem(out.detach().cpu().numpy(), *_truth64(conv.kernel.detach().cpu().numpy(), feat.cpu().numpy(), oi,
+                                                      ok, ors))
     # transposed: coarse (2*coarse_pos in fine coords) -> fine positions
     coarse = out_pos / 2
     deconv = layers.SparseConvTranspose(32, 16, [2, 2, 2], use_bias=False, offset=torch.full((3,), -0.5)).to(cuda)
@@ -92,6 +122,8 @@ def test_strided_and_transposed_conv(cuda):
     assert (np.diff(trs) == 1).all()  # every fine voxel has exactly one parent
     ref = O.sparse_conv(deconv.kernel.detach().cpu().numpy(), cf.cpu().numpy(), ti, tk, trs)
     _close(fo.detach().cpu().numpy(), ref)
+    _close_elem(fo.detach().cpu().numpy(), *_truth64(deconv.kernel.detach().cpu().numpy(), cf.cpu().numpy(), ti,
+                                                     tk, trs))
     # adjointness: <conv(x), y> == <x, deconv_W(y)> with the same weights
     deconv.kernel.data.copy_(conv.kernel.data.transpose(3, 4))
     lhs = (conv(feat, p, out_pos, 1.0) * cf).sum()
@@ -118,6 +150,15 @@ def test_sparse_conv_backward(cuda, cin, cout):
     ref.backward(g)
     _close(out.detach().cpu().numpy(), ref.detach().numpy())
     _close(xd.grad.cpu().numpy(), x64.grad.numpy())
+    # per element vs float64: the forward, dIn (a conv of g with the
+    # transposed filters over the same pairs) and dW (per filter entry a sum
+    # over pairs of x * g) with their own term-magnitude sums
+    mag = _csr_conv64(W.abs(), x.abs(), torch.from_numpy(oi), torch.from_numpy(ok), torch.from_numpy(ors))
+    _close_elem(out.detach().cpu().numpy(), ref.detach().numpy(), mag.numpy())
+    Wa, xa = W.abs().clone().requires_grad_(), x.abs().clone().requires_grad_()
+    _csr_conv64(Wa, xa, torch.from_numpy(oi), torch.from_numpy(ok), torch.from_numpy(ors)).backward(g.abs())
+    _close_elem(xd.grad.cpu().numpy(), x64.grad.numpy(), xa.grad.numpy())
+    _close_elem(Wd.grad.cpu().numpy(), W64.grad.numpy(), Wa.grad.numpy())
     _close(Wd.grad.cpu().numpy(), W64.grad.numpy())
 
 
