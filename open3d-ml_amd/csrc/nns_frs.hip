@@ -759,6 +759,11 @@ __device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 10 bits -> every t
     return v;
 }
 
+// (batch, Morton r-cell) key of every query.  F4: the queries are the points
+// in Open3D bucket order (pts, float4), so the sorted payload is a position in
+// pts — the search then reads each query from the same lines its group
+// streams (large self searches); else the raw [M, 3] query array.
+template <bool F4>
 __global__ void __launch_bounds__(256) group_query_keys_kernel(const float* __restrict__ queries, int64_t m,
                                                                float inv2, int n_batch,
                                                                const int64_t* __restrict__ qrs, int cell_bits,
@@ -766,12 +771,20 @@ __global__ void __launch_bounds__(256) group_query_keys_kernel(const float* __re
     __shared__ int64_t s_rs[kLdsSplits];
     const int64_t* rsp = stage_splits(s_rs, qrs, n_batch);
     const uint32_t mask = (1u << cell_bits) - 1u;
+    constexpr int W = F4 ? 4 : 3;
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < m;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int b = batch_of(i, rsp, n_batch);
-        const uint32_t cx = static_cast<uint32_t>(static_cast<int32_t>(floorf(queries[3 * i] * inv2))) & mask;
-        const uint32_t cy = static_cast<uint32_t>(static_cast<int32_t>(floorf(queries[3 * i + 1] * inv2))) & mask;
-        const uint32_t cz = static_cast<uint32_t>(static_cast<int32_t>(floorf(queries[3 * i + 2] * inv2))) & mask;
+        float x, y, z;
+        if constexpr (F4) {
+            const float4 p = reinterpret_cast<const float4*>(queries)[i];
+            x = p.x, y = p.y, z = p.z;
+        } else {
+            x = queries[W * i], y = queries[W * i + 1], z = queries[W * i + 2];
+        }
+        const uint32_t cx = static_cast<uint32_t>(static_cast<int32_t>(floorf(x * inv2))) & mask;
+        const uint32_t cy = static_cast<uint32_t>(static_cast<int32_t>(floorf(y * inv2))) & mask;
+        const uint32_t cz = static_cast<uint32_t>(static_cast<int32_t>(floorf(z * inv2))) & mask;
         const uint32_t mort = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
         keys[i] = (static_cast<uint32_t>(b) << (3 * cell_bits)) | mort;
     }
@@ -1084,6 +1097,19 @@ static bool frs_query_gather() {
     return v;
 }
 
+// Self searches of large items (Morton query order) sort the POINTS IN
+// BUCKET ORDER by their Morton r-cell, so the search reads each query (16 B,
+// aligned) from pts — lines its group streams anyway — instead of 12 B from
+// the raw array through a random gather (one 128-B line per query that no
+// other access reuses).  O3DML_FRS_SELF_PTS=0: the raw-array order (A/B).
+static bool frs_self_pts_order() {
+    static const bool v = [] {
+        const char* e = std::getenv("O3DML_FRS_SELF_PTS");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // log2 of the queries per wave of the MODE 0 search: 64 while that still
 // gives >= 4096 waves (4 per SIMD), else 32 / 16 — a small call (one C1 scene,
 // 65,536 queries: 1,024 waves of 64) is latency-bound on one wave per SIMD.
@@ -1321,6 +1347,8 @@ static void frs_count_impl(const float* points, int64_t n_points, const float* q
     const uint32_t* qkeys;
     int bshift;
     const bool self_order = self_search && frs_self_order(n_batch, points_row_splits_host, n_points);
+    // large self search: Morton order over the bucket-order points (qsel = positions in pl.pts)
+    const bool self_pts = self_search && !self_order && frs_self_pts_order();
     // the points in Open3D bucket order, class sub-lists + directory; for a
     // self search also the query order: Open3D's bucket order with the
     // (voxel, octant) groups made adjacent inside each bucket — no sort of the
@@ -1338,15 +1366,22 @@ static void frs_count_impl(const float* points, int64_t n_points, const float* q
         // (batch, Morton r-cell) order: <= 24 key bits = 3 radix passes;
         // Morton coordinates wrap modulo 2^cell_bits
         const int cell_bits = std::max(1, std::min(8, (24 - batch_bits) / 3));
-        group_query_keys_kernel<<<stream_grid(n_queries, 256), 256, 0, st>>>(
-                queries, n_queries, 2.0f * inv, (int)n_batch, queries_row_splits, cell_bits, pl.keys);
+        // a self search keys the points in bucket order (positions in pl.pts,
+        // the batch items' ranges unchanged); other queries key themselves
+        if (self_search && frs_self_pts_order())
+            group_query_keys_kernel<true><<<stream_grid(n_queries, 256), 256, 0, st>>>(
+                    reinterpret_cast<const float*>(pl.pts), n_queries, 2.0f * inv, (int)n_batch, queries_row_splits,
+                    cell_bits, pl.keys);
+        else
+            group_query_keys_kernel<false><<<stream_grid(n_queries, 256), 256, 0, st>>>(
+                    queries, n_queries, 2.0f * inv, (int)n_batch, queries_row_splits, cell_bits, pl.keys);
         O3DML_LAUNCH_CHECK();
         {
             Workspace sws = ws;
             prim::radix_sort_pairs<uint32_t>(pl.keys, nullptr, pl.skeys, pl.qorder, n_queries,
                                              batch_bits + 3 * cell_bits, sws, st);
         }
-        if (frs_query_gather()) {
+        if (frs_query_gather() && !self_pts) {
             gather_sorted_points_kernel<<<xcd_grid(n_queries, 256), 256, 0, st>>>(queries, pl.qorder, n_queries,
                                                                                  pl.qpts, 0, nullptr, 0, nullptr);
             O3DML_LAUNCH_CHECK();
@@ -1361,8 +1396,10 @@ static void frs_count_impl(const float* points, int64_t n_points, const float* q
                                  rel16_rows(n_batch, points_row_splits_host, n_queries), st,
                                  group_grid(n_queries, 1 << qlog), pl.pts,
                                  static_cast<uint32_t>(n_points), hash_table_cell_splits,
-                                 self_order ? nullptr : (frs_query_gather() ? pl.qpts : reinterpret_cast<const float4*>(queries)),
-                                 self_order || !frs_query_gather() ? pl.qorder : nullptr, qkeys, bshift,
+                                 self_order || self_pts ? nullptr
+                                                        : (frs_query_gather() ? pl.qpts
+                                                                              : reinterpret_cast<const float4*>(queries)),
+                                 self_order || self_pts || !frs_query_gather() ? pl.qorder : nullptr, qkeys, bshift,
                                  n_queries, nullptr, radius, inv, thr, (int)n_batch, queries_row_splits,
                                  hash_table_splits, points_row_splits, pl.counts, pl.tidx, pl.tdist, pl.over,
                                  pl.scalars, nullptr, nullptr, nullptr, pl.dir, pl.dir_cap, nullptr, -1, qlog);

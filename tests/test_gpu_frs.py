@@ -412,3 +412,20 @@ def test_frs_2_24_sweep_scene_bit_exact(cuda):
     assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
     assert res.neighbors_index.shape[0] == len(oi)
     assert torch.equal(res.neighbors_index, torch.from_numpy(oi).to(cuda))
+
+
+def test_frs_two_large_items_bit_exact(cuda):
+    """Two batch items of ~2^22 points in one call (the Morton query order of
+    large self searches keys the bucket-order points with batch bits), vs
+    the optimised CPU search (= the oracle), bit-exact."""
+    from o3dml_amd import layers
+    sizes = [(1 << 22) + 3, (1 << 22) - 5]
+    rng = np.random.default_rng(23)
+    pts = np.concatenate([rng.random((n, 3), dtype=np.float32) + np.float32(i * 0.25) for i, n in enumerate(sizes)])
+    rs = np.array([0, sizes[0], sizes[0] + sizes[1]], np.int64)
+    r = 0.05 * (65536.0 / sizes[0]) ** (1.0 / 3.0)
+    t = torch.from_numpy(pts).to(cuda)
+    res = layers.FixedRadiusSearch()(t, t, r, torch.from_numpy(rs), torch.from_numpy(rs))
+    oi, ors = O.fixed_radius_search_fast(pts, r, rs)
+    assert np.array_equal(res.neighbors_row_splits.cpu().numpy(), ors)
+    assert torch.equal(res.neighbors_index, torch.from_numpy(oi).to(cuda))
