@@ -458,6 +458,17 @@ int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, const floa
                                   int want_inverse, int defer_status, int* status_host, void* workspace,
                                   size_t workspace_bytes, void* lattice_workspace, size_t lattice_workspace_bytes,
                                   void* stream);
+/* The kernel map of the SparseConvTranspose that undoes a built SparseConv
+ * map (same positions swapped, same kernel size, voxel size and offset: a
+ * pair (coarse c, fine f) of the convolution at kernel index k is the pair
+ * (f, c) of the transpose at the same index — SparseConvUnet's DeConvolution
+ * after its Convolution, sparseconvnet.py:404-482): out_workspace (a map
+ * workspace for n_out = n_fine, n_in = n_coarse) gets the inverse of the
+ * convolution's map (and, with want_inverse, the map itself as its inverse)
+ * and the convolution's status word — no voxel hash, no lookups. */
+int o3dml_sparse_conv_transpose_map(const void* conv_workspace, size_t conv_workspace_bytes, int64_t n_coarse,
+                                    int64_t n_fine, int K, int want_inverse, void* out_workspace,
+                                    size_t out_workspace_bytes, void* stream);
 
 /* ---- KPConv neighbourhood aggregation (ml3d/torch/models/
  * kpconv.py:1005-1159).  q_pts f32 [n,3], s_pts f32 [n_support,3], neighbors

@@ -174,7 +174,10 @@ constexpr int kRsWaves = kRsBlock / 64;
 // digits' global bases are a 256-entry scan the scatter kernel does itself).
 static __global__ void __launch_bounds__(kRsBlock) radix_digit_scan(const uint32_t* __restrict__ hist, int64_t tiles,
                                                              uint32_t* __restrict__ offs,
-                                                             uint32_t* __restrict__ dtot) {
+                                                             uint32_t* __restrict__ dtot,
+                                                             const uint64_t* __restrict__ or_and = nullptr,
+                                                             int pass = 0) {
+    if (or_and && pass > 0 && ((((or_and[0] & or_and[1]) >> (8 * pass)) & 255u) == 0)) return;  // skipped pass
     __shared__ uint32_t wsum[kRsWaves];
     const int64_t row = static_cast<int64_t>(blockIdx.x) * tiles;
     uint32_t carry = 0;
@@ -208,9 +211,56 @@ static __global__ void __launch_bounds__(kRsBlock) radix_digit_scan(const uint32
     if (threadIdx.x == 0) dtot[blockIdx.x] = carry;
 }
 
+// Device-planned passes (radix_sort_pairs with or_and != nullptr): or_and[0]
+// = OR of all keys, or_and[1] = OR of their complements (both start at 0),
+// so the bits that vary among the keys are or_and[0] & or_and[1] and
+// only passes whose 8-bit digit varies run (pass 0 always: it also moves
+// the keys when none varies); the others return at once.  The i-th of the A
+// running passes reads the input (i = 0) or the previous pass's output and
+// writes out when A - 1 - i is even, tmp otherwise, so the last running pass
+// lands in out.  Returns false for a skipped pass.
+template <class K>
+struct PassPlan {
+    const K* src;
+    K* dst;
+    const uint32_t* vsrc;
+    uint32_t* vdst;
+};
+
+template <class K>
+__device__ __forceinline__ bool device_pass(const uint64_t* or_and, int p, int passes, const K* kin,
+                                            const uint32_t* vin, K* ktmp, uint32_t* vtmp, K* kout, uint32_t* vout,
+                                            PassPlan<K>& plan) {
+    const uint64_t vary = or_and[0] & or_and[1];
+    auto act = [&](int q) { return q == 0 || ((vary >> (8 * q)) & 255u) != 0; };
+    if (!act(p)) return false;
+    int A = 0, i = 0;
+    for (int q = 0; q < passes; ++q) {
+        const bool a = act(q);
+        A += a;
+        i += a && q < p;
+    }
+    auto dst_out = [&](int j) { return ((A - 1 - j) & 1) == 0; };
+    plan.src = i == 0 ? kin : (dst_out(i - 1) ? kout : ktmp);
+    plan.vsrc = i == 0 ? vin : (dst_out(i - 1) ? vout : vtmp);
+    plan.dst = dst_out(i) ? kout : ktmp;
+    plan.vdst = dst_out(i) ? vout : vtmp;
+    return true;
+}
+
 template <class K>
 __global__ void __launch_bounds__(kRsBlock) radix_hist(const K* __restrict__ keys, int64_t n, int shift,
-                                                       uint32_t* __restrict__ hist, int64_t tiles) {
+                                                       uint32_t* __restrict__ hist, int64_t tiles,
+                                                       const uint64_t* __restrict__ or_and = nullptr,
+                                                       int passes = 0, const K* kalt = nullptr,
+                                                       const K* kout = nullptr) {
+    if (or_and) {  // device-planned: skip, or read this pass's source (keys = the input)
+        PassPlan<K> pl;
+        if (!device_pass<K>(or_and, shift / 8, passes, keys, nullptr, const_cast<K*>(kalt), nullptr,
+                            const_cast<K*>(kout), nullptr, pl))
+            return;
+        keys = pl.src;
+    }
     __shared__ uint32_t h[256];
     h[threadIdx.x] = 0;
     __syncthreads();
@@ -234,12 +284,23 @@ __global__ void __launch_bounds__(kRsBlock) radix_hist(const K* __restrict__ key
 // write consecutive addresses of each digit run (coalesced).  Four barriers
 // per tile.
 template <class K>
-__global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                          K* __restrict__ kout, uint32_t* __restrict__ vout,
+__global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* kin, const uint32_t* vin, K* kout, uint32_t* vout,
                                                           int64_t n, int shift,
                                                           const uint32_t* __restrict__ offsets,
                                                           const uint32_t* __restrict__ dtot,
-                                                          const uint32_t* __restrict__ hist, int64_t tiles) {
+                                                          const uint32_t* __restrict__ hist, int64_t tiles,
+                                                          const uint64_t* __restrict__ or_and = nullptr,
+                                                          int passes = 0, K* ktmp = nullptr,
+                                                          uint32_t* vtmp = nullptr, K* kfinal = nullptr,
+                                                          uint32_t* vfinal = nullptr) {
+    if (or_and) {  // device-planned: kin / vin = the sort's input, kfinal / vfinal its output
+        PassPlan<K> pl;
+        if (!device_pass<K>(or_and, shift / 8, passes, kin, vin, ktmp, vtmp, kfinal, vfinal, pl)) return;
+        kin = pl.src;
+        vin = pl.vsrc;
+        kout = pl.dst;
+        vout = pl.vdst;
+    }
     constexpr int kRowsPerWave = kRsItems * kRsBlock / 64 / kRsWaves;  // = kRsItems
     __shared__ uint32_t wcnt[kRsWaves][256];
     __shared__ uint32_t wsum[kRsWaves], dsum[kRsWaves];
@@ -604,9 +665,15 @@ size_t radix_sort_workspace_bytes(int64_t n) {
 // Sorts (keys_in, vals_in) by key bits [0, end_bit) into (keys_out, vals_out).
 // vals_in == nullptr means the payload is the element index (iota).
 // keys_in must not alias keys_out.
+// or_and (nullable, device [2]): OR of all n keys and OR of their
+// complements (the bits that vary: both set) — the passes whose
+// digit does not vary then return at once (device-planned, see device_pass):
+// the launches stay, their work goes.  For keys of which the host knows only a
+// generous bit width (packed coordinates).
 template <class K>
 void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, uint32_t* vals_out,
-                      int64_t n, int end_bit, Workspace& ws, hipStream_t st, int small_kind = -1) {
+                      int64_t n, int end_bit, Workspace& ws, hipStream_t st, int small_kind = -1,
+                      const uint64_t* or_and = nullptr) {
     if (n <= 0) return;
     const int passes = (end_bit + 7) / 8;
     if (passes == 0 || n == 1) {
@@ -646,6 +713,21 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
     uint32_t* hist = ws.take<uint32_t>(256 * tiles);
     uint32_t* offs = ws.take<uint32_t>(256 * tiles);
     uint32_t* dtot = ws.take<uint32_t>(256);
+    if (or_and) {
+        for (int p = 0; p < passes; ++p) {
+            const int shift = 8 * p;
+            radix_hist<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(keys_in, n, shift, hist, tiles, or_and,
+                                                                             passes, ktmp, keys_out);
+            O3DML_LAUNCH_CHECK();
+            radix_digit_scan<<<256, kRsBlock, 0, st>>>(hist, tiles, offs, dtot, or_and, p);
+            O3DML_LAUNCH_CHECK();
+            radix_scatter<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(
+                    keys_in, vals_in, nullptr, nullptr, n, shift, offs, dtot, hist, tiles, or_and, passes, ktmp, vtmp,
+                    keys_out, vals_out);
+            O3DML_LAUNCH_CHECK();
+        }
+        return;
+    }
     const K* ksrc = keys_in;
     const uint32_t* vsrc = vals_in;
     for (int p = 0; p < passes; ++p) {

@@ -2122,9 +2122,11 @@ __device__ __forceinline__ int lat_stat_merge(int j, int a, int b) { return (j &
 __global__ void __launch_bounds__(256) lattice_stats_kernel(const float* __restrict__ inp_pos, int64_t n_in,
                                                             const float* __restrict__ qpos, int64_t n_q,
                                                             float inv_vs, int* __restrict__ part,
-                                                            uint64_t* __restrict__ keys, int64_t cap) {
+                                                            uint64_t* __restrict__ keys, int64_t cap,
+                                                            int* __restrict__ status) {
     __shared__ int red[12][256];
-    // the voxel hash's empty keys (lattice_insert_kernel runs after finalize)
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 4) status[threadIdx.x] = 0;  // [2], [3]: no tile orders
+    // the voxel hash's empty keys (lattice_insert_kernel runs next)
     for (int64_t e = (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
          e < cap; e += static_cast<int64_t>(gridDim.x) * gridDim.y * blockDim.x)
         keys[e] = kLatEmpty;
@@ -2165,15 +2167,14 @@ struct LatticeOffsets {
 };
 
 // Reduces the stats partials (nblk per set) and derives the per-axis lattice
-// offsets on the device: the lattice test is "every input shares one fraction
-// per axis, every query shares one, keys within +-2^19, and exactly ksize
-// lattice offsets j + (f_in - f_q) lie in [-ks/2, ks/2] with distinct kernel
-// indices".  status[0] = 4 when the test fails (then nothing else reads lo),
-// else 0; lattice_insert_kernel may still add 4 (two inputs on one voxel).
-__global__ void __launch_bounds__(64) lattice_finalize_kernel(const int* __restrict__ part, int nblk, int ksize,
-                                                              int mirror, LatticeOffsets* __restrict__ lo_out,
-                                                              int* __restrict__ status) {
-    __shared__ int st[24];
+// offsets: the lattice test is "every input shares one fraction per axis,
+// every query shares one, keys within +-2^19, and exactly ksize lattice
+// offsets j + (f_in - f_q) lie in [-ks/2, ks/2] with distinct kernel
+// indices".  Every block of the insert and map kernels runs it on the few
+// partials itself (no separate finalize launch): threads 0-23 reduce, thread 0
+// derives the offsets; the block's copy lands in LDS.  Returns ok (uniform).
+__device__ bool lattice_block_offsets(const int* __restrict__ part, int nblk, int ksize, int mirror,
+                                      LatticeOffsets& lo_sh, int* st, int* ok_sh) {
     const int t = threadIdx.x;
     if (t < 24) {
         const int set = t / 12, j = t % 12;
@@ -2189,43 +2190,54 @@ __global__ void __launch_bounds__(64) lattice_finalize_kernel(const int* __restr
         st[t] = v;
     }
     __syncthreads();
-    if (t != 0) return;
-    LatticeOffsets lo{};
-    const double h = 0.5 * ksize;
-    bool ok = true;
-    for (int d = 0; d < 3 && ok; ++d) {
-        const float fi_lo = __int_as_float(st[4 * d]), fi_hi = __int_as_float(st[4 * d + 1]);
-        const float fq_lo = __int_as_float(st[12 + 4 * d]), fq_hi = __int_as_float(st[12 + 4 * d + 1]);
-        const bool keys_ok = st[4 * d + 2] > -(1 << 19) && st[4 * d + 3] < (1 << 19) &&
-                             st[12 + 4 * d + 2] > -(1 << 19) && st[12 + 4 * d + 3] < (1 << 19);
-        if (fi_lo != fi_hi || fq_lo != fq_hi || !keys_ok) {
-            ok = false;
-            break;
-        }
-        const double dc = static_cast<double>(fi_lo) - static_cast<double>(fq_lo);
-        int n_within = 0;
-        for (int j = -8; j <= 8; ++j) {
-            const double dd = j + dc;
-            if (dd < -h || dd > h) continue;
-            const int kid = mirror ? static_cast<int>(floor(h - dd)) : static_cast<int>(floor(dd + h));
-            if (kid < 0 || kid >= ksize || n_within >= ksize) {
+    if (t == 0) {
+        LatticeOffsets lo{};
+        const double h = 0.5 * ksize;
+        bool ok = true;
+        for (int d = 0; d < 3 && ok; ++d) {
+            const float fi_lo = __int_as_float(st[4 * d]), fi_hi = __int_as_float(st[4 * d + 1]);
+            const float fq_lo = __int_as_float(st[12 + 4 * d]), fq_hi = __int_as_float(st[12 + 4 * d + 1]);
+            const bool keys_ok = st[4 * d + 2] > -(1 << 19) && st[4 * d + 3] < (1 << 19) &&
+                                 st[12 + 4 * d + 2] > -(1 << 19) && st[12 + 4 * d + 3] < (1 << 19);
+            if (fi_lo != fi_hi || fq_lo != fq_hi || !keys_ok) {
                 ok = false;
                 break;
             }
-            lo.off[d][kid] = j;
-            ++n_within;
+            const double dc = static_cast<double>(fi_lo) - static_cast<double>(fq_lo);
+            int n_within = 0;
+            for (int j = -8; j <= 8; ++j) {
+                const double dd = j + dc;
+                if (dd < -h || dd > h) continue;
+                const int kid = mirror ? static_cast<int>(floor(h - dd)) : static_cast<int>(floor(dd + h));
+                if (kid < 0 || kid >= ksize || n_within >= ksize) {
+                    ok = false;
+                    break;
+                }
+                lo.off[d][kid] = j;
+                ++n_within;
+            }
+            if (n_within != ksize) ok = false;
         }
-        if (n_within != ksize) ok = false;
+        lo_sh = lo;
+        *ok_sh = ok ? 1 : 0;
     }
-    *lo_out = lo;
-    status[0] = ok ? 0 : 4;
-    status[2] = 0;  // no tile orders yet (o3dml_sparse_conv_tile_order)
-    status[3] = 0;
+    __syncthreads();
+    return *ok_sh != 0;
 }
 
-__global__ void lattice_insert_kernel(const float* __restrict__ pos, int64_t n, float inv_vs, uint64_t* __restrict__ keys,
-                                      int32_t* __restrict__ vals, uint32_t mask, int* __restrict__ status) {
-    if (*status & 4) return;  // not a lattice set: the map is discarded
+// Hashes the input voxels (keys emptied by lattice_stats_kernel, which also
+// zeroed the status words); block 0 flags a non-lattice set (status 4), any
+// block two inputs on one voxel (4 as well).
+__global__ void __launch_bounds__(256) lattice_insert_kernel(const float* __restrict__ pos, int64_t n, float inv_vs,
+                                                             uint64_t* __restrict__ keys, int32_t* __restrict__ vals,
+                                                             uint32_t mask, const int* __restrict__ part, int nblk,
+                                                             int ksize, int mirror, int* __restrict__ status) {
+    __shared__ LatticeOffsets lo_sh;
+    __shared__ int st_sh[24], ok_sh;
+    if (!lattice_block_offsets(part, nblk, ksize, mirror, lo_sh, st_sh, &ok_sh)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(status, 4);
+        return;  // not a lattice set: the map is discarded
+    }
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const uint64_t k = lat_key(static_cast<int>(floorf(pos[3 * i] * inv_vs)),
@@ -2250,12 +2262,17 @@ __global__ void lattice_insert_kernel(const float* __restrict__ pos, int64_t n, 
 }
 
 // map[o*K + k] for k = (kz*ks + ky)*ks + kx: one thread per (output, offset)
-__global__ void lattice_map_kernel(const float* __restrict__ inp_pos, const float* __restrict__ qpos, int64_t n_out,
-                                   float inv_vs, float radius, int ks, const LatticeOffsets* __restrict__ lop,
-                                   const uint64_t* __restrict__ keys, const int32_t* __restrict__ vals, uint32_t mask,
-                                   const int* __restrict__ status, int32_t* __restrict__ map) {
+__global__ void __launch_bounds__(256) lattice_map_kernel(const float* __restrict__ inp_pos,
+                                                          const float* __restrict__ qpos, int64_t n_out, float inv_vs,
+                                                          float radius, int ks, const int* __restrict__ part, int nblk,
+                                                          int mirror, const uint64_t* __restrict__ keys,
+                                                          const int32_t* __restrict__ vals, uint32_t mask,
+                                                          const int* __restrict__ status, int32_t* __restrict__ map) {
+    __shared__ LatticeOffsets lo_sh;
+    __shared__ int st_sh[24], ok_sh;
+    lattice_block_offsets(part, nblk, ks, mirror, lo_sh, st_sh, &ok_sh);
     const bool skip = (*status & 4) != 0;  // not a lattice set: an all-empty (safe) map
-    const LatticeOffsets lo = skip ? LatticeOffsets{} : *lop;
+    const LatticeOffsets lo = skip ? LatticeOffsets{} : lo_sh;
     const int K = ks * ks * ks;
     const int64_t total = n_out * K;
     for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
@@ -2425,21 +2442,22 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     uint64_t* keys = lws.take<uint64_t>(cap);
     int32_t* vals = lws.take<int32_t>(cap);
     int* part = lws.take<int>(2 * kLatStatBlocks * 12);
-    LatticeOffsets* lo = lws.take<LatticeOffsets>(1);
+    lws.take<LatticeOffsets>(1);
     const float inv_vs = 1.0f / voxel_size;
-    // ---- 1. lattice check + offsets, on the device (no host round trip)
+    // ---- 1. lattice statistics (per-block partials; the offsets are derived
+    // from them by every block of the next two kernels: no host round trip,
+    // no finalize launch), 2. hash the input voxels, 3. K lookups per output
     const int nblk = static_cast<int>(std::min<int64_t>(kLatStatBlocks, ceil_div(std::max(n_in, n_out), 256)));
-    lattice_stats_kernel<<<dim3(nblk, 2), 256, 0, st>>>(inp_pos, n_in, query_pos, n_out, inv_vs, part, keys, cap);
+    lattice_stats_kernel<<<dim3(nblk, 2), 256, 0, st>>>(inp_pos, n_in, query_pos, n_out, inv_vs, part, keys, cap,
+                                                         status);
     O3DML_LAUNCH_CHECK();
-    lattice_finalize_kernel<<<1, 64, 0, st>>>(part, nblk, ksize, mirror, lo, status);
-    O3DML_LAUNCH_CHECK();
-    // ---- 2. hash the input voxels (keys emptied by lattice_stats_kernel), 3. K lookups per output
     lattice_insert_kernel<<<stream_grid(n_in, 256), 256, 0, st>>>(inp_pos, n_in, inv_vs, keys, vals,
-                                                                 static_cast<uint32_t>(cap - 1), status);
+                                                                 static_cast<uint32_t>(cap - 1), part, nblk, ksize,
+                                                                 mirror, status);
     O3DML_LAUNCH_CHECK();
     lattice_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(
-            inp_pos, query_pos, n_out, inv_vs, 0.5f * voxel_size * static_cast<float>(ksize), ksize, lo, keys, vals,
-            static_cast<uint32_t>(cap - 1), status, map);
+            inp_pos, query_pos, n_out, inv_vs, 0.5f * voxel_size * static_cast<float>(ksize), ksize, part, nblk,
+            mirror, keys, vals, static_cast<uint32_t>(cap - 1), status, map);
     O3DML_LAUNCH_CHECK();
     if (normalize) {
         map_count_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(map, n_out, K, norm);
@@ -2459,6 +2477,44 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     if (defer_status) return 0;  // status stays on the device (o3dml_sparse_conv_map_status_offset)
     O3DML_CHECK_HIP(hipMemcpyAsync(status_host, status, sizeof(int), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
+    O3DML_GUARD_END
+}
+
+__global__ void copy_status_kernel(const int* __restrict__ src, int* __restrict__ dst) {
+    if (threadIdx.x < 4) dst[threadIdx.x] = threadIdx.x == 0 ? src[0] : 0;  // [2], [3]: no tile orders yet
+}
+
+O3DML_API int o3dml_sparse_conv_transpose_map(const void* conv_workspace, size_t conv_workspace_bytes,
+                                              int64_t n_coarse, int64_t n_fine, int K, int want_inverse,
+                                              void* out_workspace, size_t out_workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(K >= 1 && K <= 32, "sparse_conv: kernel volume must be in [1, 32] (got %d)", K);
+    hipStream_t st = as_stream(stream);
+    Workspace cw(const_cast<void*>(conv_workspace), conv_workspace_bytes);  // n_out = n_coarse, n_in = n_fine
+    const int32_t* cmap = cw.take<int32_t>(n_coarse * K);
+    cw.take<float>(n_coarse * K);
+    cw.take<float>(n_coarse);
+    cw.take<float>(n_coarse);
+    cw.take<int32_t>(n_fine * K);
+    cw.take<float>(n_fine * K);
+    const int* cstatus = cw.take<int>(4);
+    Workspace ws(out_workspace, out_workspace_bytes);  // n_out = n_fine, n_in = n_coarse
+    int32_t* map = ws.take<int32_t>(n_fine * K);
+    ws.take<float>(n_fine * K);
+    ws.take<float>(n_fine);
+    ws.take<float>(n_fine);
+    int32_t* inv = ws.take<int32_t>(n_coarse * K);
+    ws.take<float>(n_coarse * K);
+    int* status = ws.take<int>(4);
+    copy_status_kernel<<<1, 64, 0, st>>>(cstatus, status);
+    O3DML_LAUNCH_CHECK();
+    if (n_fine > 0) fill_async(map, 0xff, sizeof(int32_t) * n_fine * K, st);
+    if (n_coarse > 0 && n_fine > 0) {
+        build_inverse_map_kernel<<<stream_grid(n_coarse * K, 256), 256, 0, st>>>(cmap, nullptr, n_coarse, K, map,
+                                                                                nullptr, status);
+        O3DML_LAUNCH_CHECK();
+    }
+    if (want_inverse && n_coarse > 0) copy_async(inv, cmap, sizeof(int32_t) * n_coarse * K, st);
     O3DML_GUARD_END
 }
 

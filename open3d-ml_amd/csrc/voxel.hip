@@ -596,8 +596,12 @@ namespace {
 constexpr uint64_t kGridInvalid = uint64_t(1) << 60;
 constexpr int64_t kGridMax = int64_t(1) << 21;
 
+// or_and[0] / [1]: OR of the keys and of their complements (the bits that
+// vary among them, for the device-planned radix passes): one atomic pair per
+// wave.
 __global__ void grid_parent_kernel(const float* __restrict__ pos, int64_t n, uint64_t* __restrict__ keys,
-                                   int64_t* __restrict__ flags) {
+                                   int64_t* __restrict__ flags, unsigned long long* __restrict__ or_and) {
+    uint64_t o1 = 0, o0 = 0;
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         uint64_t key = 0;
@@ -617,6 +621,17 @@ __global__ void grid_parent_kernel(const float* __restrict__ pos, int64_t n, uin
             key = (key << 20) | static_cast<uint64_t>(c >> 1);
         }
         keys[i] = valid ? key : kGridInvalid;
+        o1 |= keys[i];
+        o0 |= ~keys[i];
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        o1 |= static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(o1), d, 64));
+        o0 |= static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(o0), d, 64));
+    }
+    if ((threadIdx.x & 63) == 0 && (o1 | ~o0)) {
+        atomicOr(&or_and[0], static_cast<unsigned long long>(o1));
+        atomicOr(&or_and[1], static_cast<unsigned long long>(o0));
     }
 }
 
@@ -656,7 +671,7 @@ inline GridState take_grid_state(Workspace& ws, int64_t n) {
     g.sidx = ws.take<uint32_t>(n);
     g.head = ws.take<int64_t>(n);
     g.incl = ws.take<int64_t>(n);
-    g.flags = ws.take<int64_t>(4);  // [0] range flag, [2..3] (count, flag) for the host read
+    g.flags = ws.take<int64_t>(6);  // [0] range flag, [2..3] (count, flag) for the host read, [4..5] key OR / ~OR
     return g;
 }
 
@@ -665,7 +680,7 @@ inline GridState take_grid_state(Workspace& ws, int64_t n) {
 
 O3DML_API size_t o3dml_calculate_grid_workspace_size(int64_t n_points) {
     return 2 * ws_bytes<uint64_t>(n_points) + ws_bytes<uint32_t>(n_points) + 2 * ws_bytes<int64_t>(n_points) +
-           ws_bytes<int64_t>(4) +
+           ws_bytes<int64_t>(6) +
            std::max(prim::radix_sort_workspace_bytes<uint64_t>(n_points), prim::scan_workspace_bytes(n_points));
 }
 
@@ -677,12 +692,16 @@ O3DML_API int o3dml_calculate_grid_count(const float* positions, int64_t n_point
     GridState g = take_grid_state(ws, n_points);
     int64_t host[2] = {0, 0};
     if (n_points > 0) {
-        fill_async(g.flags, 0, 2 * sizeof(int64_t), st);
+        fill_async(g.flags, 0, 6 * sizeof(int64_t), st);
         const unsigned gr = stream_grid(n_points, 256);
-        grid_parent_kernel<<<gr, 256, 0, st>>>(positions, n_points, g.keys, g.flags);
+        unsigned long long* or_and = reinterpret_cast<unsigned long long*>(g.flags + 4);
+        grid_parent_kernel<<<gr, 256, 0, st>>>(positions, n_points, g.keys, g.flags, or_and);
         O3DML_LAUNCH_CHECK();
         Workspace sws = ws;
-        prim::radix_sort_pairs<uint64_t>(g.keys, nullptr, g.sk, g.sidx, n_points, 61, sws, st);
+        // three 20-bit fields, 8 passes planned on the host; only the digits
+        // that vary among the keys run (a room's parents: 3-4 of the 8)
+        prim::radix_sort_pairs<uint64_t>(g.keys, nullptr, g.sk, g.sidx, n_points, 61, sws, st, -1,
+                                         reinterpret_cast<const uint64_t*>(or_and));
         grid_unique_heads_kernel<<<gr, 256, 0, st>>>(g.sk, n_points, g.head);
         O3DML_LAUNCH_CHECK();
         sws = ws;

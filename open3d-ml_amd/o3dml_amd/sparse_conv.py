@@ -362,6 +362,8 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
         key = (ks, bool(mirror), bool(normalize), bool(want_grad), float(voxel_size)) + tuple(cache_key[2:])
         key = key + (id(cache_key[0]), cache_key[0]._version, id(cache_key[1]), cache_key[1]._version)
     hit = scope.maps.get(key) if key is not None else None
+    if hit is None and key is not None and mirror:
+        hit = _transpose_of_cached(scope, key, cache_key, ks, n_in, n_out, want_grad, dev)
     late = None  # status word read after the GEMM (standalone call, no scope)
     if hit is not None:
         mws, status0 = hit[0], hit[1]
@@ -380,8 +382,8 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
                   int(bool(mirror)), int(bool(normalize)), ptr(oimp), int(bool(want_grad)), int(defer),
                   status.ctypes.data, ptr(mws), mws.numel(), ptr(lws), lws.numel(), stream_handle(dev))
         status0 = int(status[0])
-        if (scope is not None or int(filters.shape[3]) * int(filters.shape[4]) >= TILE_ORDER_MIN_CHANNELS) \
-                and not status0 & 4:
+        if K > 8 and (scope is not None or int(filters.shape[3]) * int(filters.shape[4]) >= TILE_ORDER_MIN_CHANNELS) \
+                and not status0 & 4:  # (no tile orders for K <= 8, csrc use_order)
             # cached maps serve several convolutions: sort the GEMM tiles by offset mask once
             _lib.call("o3dml_sparse_conv_tile_order", ptr(mws), mws.numel(), n_out, n_in, K, int(bool(want_grad)),
                       stream_handle(dev))
@@ -421,6 +423,33 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
     if not _late_ok(late):
         return None
     return out if inp_features.is_cuda else out.cpu()
+
+
+def _transpose_of_cached(scope, key, cache_key, ks, n_in, n_out, want_grad, dev):
+    """The kernel map of a SparseConvTranspose whose SparseConv partner (same
+    kernel size, voxel size and offset, input and output positions swapped —
+    SparseConvUnet's DeConvolution after its Convolution) is already in the
+    scope: derived from the partner's map (o3dml_sparse_conv_transpose_map:
+    the same pairs at the same kernel indices) instead of a voxel hash and K
+    lookups per output.  None when there is no such partner."""
+    inp, out = cache_key[0], cache_key[1]
+    conv_key = key[:1] + (False,) + key[2:5] + (-key[5],) + key[6:9] + (id(out), out._version, id(inp), inp._version)
+    hit = scope.maps.get(conv_key)
+    if hit is None or hit[1] & 4:
+        return None
+    lib = _lib.load()
+    K = ks ** 3
+    n_coarse, n_fine = n_in, n_out
+    cmws = hit[0]
+    mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_fine, n_coarse, K), dev)
+    _lib.call("o3dml_sparse_conv_transpose_map", ptr(cmws), cmws.numel(), n_coarse, n_fine, K, int(bool(want_grad)),
+              ptr(mws), mws.numel(), stream_handle(dev))
+    if scope.defer:
+        off = lib.o3dml_sparse_conv_map_status_offset(n_fine, n_coarse, K)
+        scope.pending.append(mws[off:off + 4].view(torch.int32))
+    entry = (mws, hit[1], inp, out)
+    scope.maps[key] = entry
+    return entry
 
 
 # (n_out, n_in, K, cin, cout) -> forward workspace bytes (one ctypes query per shape)

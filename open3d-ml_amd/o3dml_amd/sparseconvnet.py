@@ -302,7 +302,11 @@ class UNet(nn.Module):
         return sum(isinstance(m, Convolution) for m in self.net)
 
     def forward(self, pos_list, feat_list, grids=None):
-        conv_pos, concat_feat = [], []
+        # conv_out: each Convolution's output grid in the fine level's units —
+        # the DeConvolution's input positions (= 2 x the coarse positions,
+        # exactly), the same tensor, so the DeConvolution's kernel map is
+        # derived from the Convolution's (sparse_conv._transpose_of_cached)
+        conv_pos, conv_out, concat_feat = [], [], []
         mods = list(self.net)
         fuse = _fusable(self)
         if grids is None:
@@ -322,12 +326,13 @@ class UNet(nn.Module):
                 elif isinstance(m, Convolution):
                     conv_pos.append(pos_list)
                     outs, half = grids.next(pos_list)
+                    conv_out.append(outs)
                     feat_list = [m.net.forward_fused(f, p, o, 1.0, pre=pre)
                                  for f, p, o in zip(feat_list, pos_list, outs)]
                     pos_list = half
                 else:  # DeConvolution
-                    feat_list = [m.net.forward_fused(f, 2 * p, o, 1.0, pre=pre)
-                                 for f, p, o in zip(feat_list, pos_list, conv_pos[-1])]
+                    feat_list = [m.net.forward_fused(f, c, o, 1.0, pre=pre)
+                                 for f, c, o in zip(feat_list, conv_out.pop(), conv_pos[-1])]
                     pos_list = conv_pos.pop()
                 pre = None
                 continue
@@ -338,10 +343,11 @@ class UNet(nn.Module):
             elif isinstance(m, Convolution):
                 conv_pos.append(pos_list)
                 outs, half = grids.next(pos_list)
+                conv_out.append(outs)
                 feat_list, _ = m(feat_list, pos_list, out_positions_list=outs)
                 pos_list = half
             elif isinstance(m, DeConvolution):
-                feat_list = m(feat_list, [2 * p for p in pos_list], conv_pos[-1])
+                feat_list = m(feat_list, conv_out.pop(), conv_pos[-1])
                 pos_list = conv_pos.pop()
             elif isinstance(m, ConcatFeat):
                 concat_feat.append(m(feat_list))

@@ -125,3 +125,29 @@ def test_calculate_grid(cuda):
     assert ops.calculate_grid(_t(np.zeros((0, 3), np.float32), cuda)).shape == (0, 3)
     with pytest.raises(RuntimeError):
         ops.calculate_grid(_t(np.full((4, 3), 3e6, np.float32), cuda))
+
+
+@pytest.mark.parametrize("case", ["room", "flat", "wide", "negative", "one_cell"])
+def test_calculate_grid_large_vs_oracle(cuda, case):
+    """calculate_grid above the one-workgroup sort (n > 8,192: the multi-pass
+    radix sort whose passes run only for the digits that vary among the packed
+    parent keys, planned on the device) vs the oracle, bit-exact: the C4 room,
+    a flat slab (one axis constant), coordinates over the whole 20-bit field
+    range, points with negative coordinates (no parent) and every point in one
+    parent cell (no digit varies)."""
+    import bench
+    from o3dml_amd import ops
+    rng = np.random.default_rng(31)
+    if case == "room":
+        pos = bench.make_room(0)[0]
+    elif case == "flat":
+        pos = (np.stack([rng.integers(0, 300, 40000), rng.integers(0, 300, 40000), np.full(40000, 7)], 1)
+               + 0.5).astype(np.float32)
+    elif case == "wide":
+        pos = (rng.integers(0, (1 << 21) - 2, (30000, 3)) + 0.5).astype(np.float32)
+    elif case == "negative":
+        pos = (rng.integers(-50, 50, (30000, 3)) + 0.5).astype(np.float32)
+    else:
+        pos = (np.full((20000, 3), 10) + rng.integers(0, 2, (20000, 3)) + 0.5).astype(np.float32)
+    out = ops.calculate_grid(_t(pos, cuda)).cpu().numpy()
+    assert np.array_equal(out, O.calculate_grid(pos))

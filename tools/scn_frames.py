@@ -47,3 +47,12 @@ if len(sys.argv) > 2 and sys.argv[2] == "prof":
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(35)
     st.sort_stats("cumtime").print_stats(40)
+
+if len(sys.argv) > 2 and sys.argv[2] == "ops":
+    # every aten op of one frame (count, device time) and where the memcpys come from
+    from torch.profiler import ProfilerActivity, profile
+    with torch.no_grad(), profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        m(inp)
+        torch.cuda.synchronize(dev)
+    print(prof.key_averages().table(sort_by="count", row_limit=45))
+    print(prof.key_averages(group_by_stack_n=6).table(sort_by="count", row_limit=25))
