@@ -2480,15 +2480,16 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     O3DML_GUARD_END
 }
 
-__global__ void copy_status_kernel(const int* __restrict__ src, int* __restrict__ dst) {
-    if (threadIdx.x < 4) dst[threadIdx.x] = threadIdx.x == 0 ? src[0] : 0;  // [2], [3]: no tile orders yet
-}
-
 O3DML_API int o3dml_sparse_conv_transpose_map(const void* conv_workspace, size_t conv_workspace_bytes,
                                               int64_t n_coarse, int64_t n_fine, int K, int want_inverse,
                                               void* out_workspace, size_t out_workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
     O3DML_REQUIRE(K >= 1 && K <= 32, "sparse_conv: kernel volume must be in [1, 32] (got %d)", K);
+    {
+        const hipError_t pending = hipPeekAtLastError();
+        O3DML_REQUIRE(pending == hipSuccess, "sparse_conv_transpose_map: HIP error pending on entry: %s",
+                      hipGetErrorString(pending));
+    }
     hipStream_t st = as_stream(stream);
     Workspace cw(const_cast<void*>(conv_workspace), conv_workspace_bytes);  // n_out = n_coarse, n_in = n_fine
     const int32_t* cmap = cw.take<int32_t>(n_coarse * K);
@@ -2506,8 +2507,8 @@ O3DML_API int o3dml_sparse_conv_transpose_map(const void* conv_workspace, size_t
     int32_t* inv = ws.take<int32_t>(n_coarse * K);
     ws.take<float>(n_coarse * K);
     int* status = ws.take<int>(4);
-    copy_status_kernel<<<1, 64, 0, st>>>(cstatus, status);
-    O3DML_LAUNCH_CHECK();
+    copy_async(status, cstatus, sizeof(int), st);  // the partner's lattice / duplicate status
+    fill_async(status + 1, 0, 3 * sizeof(int), st);  // [2], [3]: no tile orders yet
     if (n_fine > 0) fill_async(map, 0xff, sizeof(int32_t) * n_fine * K, st);
     if (n_coarse > 0 && n_fine > 0) {
         build_inverse_map_kernel<<<stream_grid(n_coarse * K, 256), 256, 0, st>>>(cmap, nullptr, n_coarse, K, map,

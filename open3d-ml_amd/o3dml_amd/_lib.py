@@ -78,6 +78,7 @@ SIGNATURES = {
                                               c_p, c_p, c_sz, c_p, c_sz, c_p]),
     "o3dml_sparse_conv_map_status_offset": (c_sz, [c_i64, c_i64, c_i32]),
     "o3dml_sparse_conv_tile_order": (c_i32, [c_p, c_sz, c_i64, c_i64, c_i32, c_i32, c_p]),
+    "o3dml_sparse_conv_transpose_map": (c_i32, [c_p, c_sz, c_i64, c_i64, c_i32, c_i32, c_p, c_sz, c_p]),
     "o3dml_kpconv_weighted_features": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p, c_i32,
                                                c_i32, c_f32, c_i32, c_i32, c_p, c_p, c_p]),
     "o3dml_kpconv_weighted_features_backward": (c_i32, [c_p, c_i64, c_p, c_i64, c_p, c_i32, c_i32, c_p, c_i32, c_p,
@@ -235,6 +236,8 @@ def call(name, *args):
     """Call a status-returning entry point and raise on failure.  A call given
     a stream of a device other than the current one runs under a restoring
     device guard (the caller's current device is unchanged afterwards)."""
+    if name not in SIGNATURES:  # ctypes would pass untyped ints as 32-bit: pointers truncated
+        raise RuntimeError(f"o3dml_amd: no ctypes signature for {name} (add it to _lib.SIGNATURES)")
     fn = getattr(load(), name)
     dev = _stream_device(args)
     if dev is not None and dev != torch.cuda.current_device():
