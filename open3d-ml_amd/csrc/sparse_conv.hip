@@ -2170,9 +2170,9 @@ struct LatticeOffsets {
 // offsets: the lattice test is "every input shares one fraction per axis,
 // every query shares one, keys within +-2^19, and exactly ksize lattice
 // offsets j + (f_in - f_q) lie in [-ks/2, ks/2] with distinct kernel
-// indices".  Every block of the insert and map kernels runs it on the few
-// partials itself (no separate finalize launch): threads 0-23 reduce, thread 0
-// derives the offsets; the block's copy lands in LDS.  Returns ok (uniform).
+// indices".  Run by the insert kernel's extra block (no separate finalize
+// launch): threads 0-23 reduce, thread 0 derives the offsets into LDS.
+// Returns ok (uniform over the block).
 __device__ bool lattice_block_offsets(const int* __restrict__ part, int nblk, int ksize, int mirror,
                                       LatticeOffsets& lo_sh, int* st, int* ok_sh) {
     const int t = threadIdx.x;
@@ -2226,20 +2226,28 @@ __device__ bool lattice_block_offsets(const int* __restrict__ part, int nblk, in
 }
 
 // Hashes the input voxels (keys emptied by lattice_stats_kernel, which also
-// zeroed the status words); block 0 flags a non-lattice set (status 4), any
-// block two inputs on one voxel (4 as well).
+// zeroed the status words) and, in block 0 (one extra block: the serial part
+// stays off the insert's critical path), derives the lattice offsets into lo
+// and flags a non-lattice set (status 4); any block flags two inputs on one
+// voxel (4 as well).  A non-lattice set inserts anyway: its map is discarded.
 __global__ void __launch_bounds__(256) lattice_insert_kernel(const float* __restrict__ pos, int64_t n, float inv_vs,
                                                              uint64_t* __restrict__ keys, int32_t* __restrict__ vals,
                                                              uint32_t mask, const int* __restrict__ part, int nblk,
-                                                             int ksize, int mirror, int* __restrict__ status) {
-    __shared__ LatticeOffsets lo_sh;
-    __shared__ int st_sh[24], ok_sh;
-    if (!lattice_block_offsets(part, nblk, ksize, mirror, lo_sh, st_sh, &ok_sh)) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(status, 4);
-        return;  // not a lattice set: the map is discarded
+                                                             int ksize, int mirror, LatticeOffsets* __restrict__ lo,
+                                                             int* __restrict__ status) {
+    if (blockIdx.x == gridDim.x - 1) {
+        __shared__ LatticeOffsets lo_sh;
+        __shared__ int st_sh[24], ok_sh;
+        const bool ok = lattice_block_offsets(part, nblk, ksize, mirror, lo_sh, st_sh, &ok_sh);
+        if (threadIdx.x == 0) {
+            *lo = lo_sh;
+            if (!ok) atomicOr(status, 4);
+        }
+        return;
     }
+    const int64_t inserters = gridDim.x - 1;  // the last block derived the offsets
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
-         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+         i += inserters * blockDim.x) {
         const uint64_t k = lat_key(static_cast<int>(floorf(pos[3 * i] * inv_vs)),
                                    static_cast<int>(floorf(pos[3 * i + 1] * inv_vs)),
                                    static_cast<int>(floorf(pos[3 * i + 2] * inv_vs)));
@@ -2264,15 +2272,12 @@ __global__ void __launch_bounds__(256) lattice_insert_kernel(const float* __rest
 // map[o*K + k] for k = (kz*ks + ky)*ks + kx: one thread per (output, offset)
 __global__ void __launch_bounds__(256) lattice_map_kernel(const float* __restrict__ inp_pos,
                                                           const float* __restrict__ qpos, int64_t n_out, float inv_vs,
-                                                          float radius, int ks, const int* __restrict__ part, int nblk,
-                                                          int mirror, const uint64_t* __restrict__ keys,
+                                                          float radius, int ks, const LatticeOffsets* __restrict__ lop,
+                                                          const uint64_t* __restrict__ keys,
                                                           const int32_t* __restrict__ vals, uint32_t mask,
                                                           const int* __restrict__ status, int32_t* __restrict__ map) {
-    __shared__ LatticeOffsets lo_sh;
-    __shared__ int st_sh[24], ok_sh;
-    lattice_block_offsets(part, nblk, ks, mirror, lo_sh, st_sh, &ok_sh);
     const bool skip = (*status & 4) != 0;  // not a lattice set: an all-empty (safe) map
-    const LatticeOffsets lo = skip ? LatticeOffsets{} : lo_sh;
+    const LatticeOffsets lo = skip ? LatticeOffsets{} : *lop;
     const int K = ks * ks * ks;
     const int64_t total = n_out * K;
     for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
@@ -2442,7 +2447,7 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     uint64_t* keys = lws.take<uint64_t>(cap);
     int32_t* vals = lws.take<int32_t>(cap);
     int* part = lws.take<int>(2 * kLatStatBlocks * 12);
-    lws.take<LatticeOffsets>(1);
+    LatticeOffsets* lo = lws.take<LatticeOffsets>(1);
     const float inv_vs = 1.0f / voxel_size;
     // ---- 1. lattice statistics (per-block partials; the offsets are derived
     // from them by every block of the next two kernels: no host round trip,
@@ -2451,13 +2456,13 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     lattice_stats_kernel<<<dim3(nblk, 2), 256, 0, st>>>(inp_pos, n_in, query_pos, n_out, inv_vs, part, keys, cap,
                                                          status);
     O3DML_LAUNCH_CHECK();
-    lattice_insert_kernel<<<stream_grid(n_in, 256), 256, 0, st>>>(inp_pos, n_in, inv_vs, keys, vals,
-                                                                 static_cast<uint32_t>(cap - 1), part, nblk, ksize,
-                                                                 mirror, status);
+    lattice_insert_kernel<<<stream_grid(n_in, 256) + 1, 256, 0, st>>>(inp_pos, n_in, inv_vs, keys, vals,
+                                                                     static_cast<uint32_t>(cap - 1), part, nblk, ksize,
+                                                                     mirror, lo, status);
     O3DML_LAUNCH_CHECK();
     lattice_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(
-            inp_pos, query_pos, n_out, inv_vs, 0.5f * voxel_size * static_cast<float>(ksize), ksize, part, nblk,
-            mirror, keys, vals, static_cast<uint32_t>(cap - 1), status, map);
+            inp_pos, query_pos, n_out, inv_vs, 0.5f * voxel_size * static_cast<float>(ksize), ksize, lo, keys, vals,
+            static_cast<uint32_t>(cap - 1), status, map);
     O3DML_LAUNCH_CHECK();
     if (normalize) {
         map_count_kernel<<<stream_grid(n_out, 256), 256, 0, st>>>(map, n_out, K, norm);

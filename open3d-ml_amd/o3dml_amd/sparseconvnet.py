@@ -178,6 +178,13 @@ class NetworkInNetwork(nn.Module):
         self.linear = nn.Identity() if nIn == nOut else nn.Linear(nIn, nOut, bias=bias)
 
     def forward(self, inputs):
+        if isinstance(self.linear, nn.Linear) and _fusable(self) and inputs and inputs[0].is_cuda:
+            # eval: one HIP dense launch (csrc/dense.hip) instead of torch's
+            # GEMM, whose per-call host cost (library heuristics) was ~50 us
+            from .randlanet import dense_act
+            w = self.linear.weight.detach()
+            b = None if self.linear.bias is None else self.linear.bias.detach()
+            return [dense_act(x.contiguous(), w, b) for x in inputs]
         return [self.linear(x) for x in inputs]
 
 
