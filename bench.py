@@ -550,8 +550,8 @@ def sparse_conv_bench(dev, reps):
             "ms_layer": round(t_layer * 1e3, 4), "ms_gemm": round(t_gemm * 1e3, 4),
             "tflops_gemm": round(flops / t_gemm / 1e12, 3),
             "mfma_roofline": [gemm_roofline(dev, pos, nb, kidx, pairs, c, reps, mode)
-                              for mode in (0, 1) for c in (32, 128)],
-            "config": "C4: ~80k 2 cm room voxels, SparseConv 3^3 32->32 fp32 (bf16x6 MFMA products), rulebook rebuilt per call",
+                              for mode in (1, 0) for c in (32, 128)],
+            "config": "C4: ~80k 2 cm room voxels, SparseConv 3^3 32->32 fp32 (exact f32 MFMA products), rulebook rebuilt per call",
             "unet": scn_bench(dev, pos, reps)}
 
 
@@ -573,9 +573,9 @@ def gemm_roofline(dev, pos, nb, kidx, pairs, ch, reps, mode=0):
     launch inside the library, o3dml_timing_*) on the C4 3^3 map (lattice
     rulebook, cached and tile-ordered as in SparseConvUnet) at ch -> ch
     channels: useful flops 2 * pairs * ch^2 per launch over the kernel time,
-    against the MFMA peak of the product precision in use — bf16x6 (mode 0,
-    the default: each f32 operand as hi + mid + lo bf16 terms, six bf16 MFMAs
-    per f32 product, peak = bf16 peak / 6), exact f32-input MFMA (mode 1) or
+    against the MFMA peak of the product precision in use — exact f32-input
+    MFMA (mode 1, the default), bf16x6 (mode 0: each f32 operand as hi + mid
+    + lo bf16 terms, six bf16 MFMAs per f32 product, peak = bf16 peak / 6) or
     bf16x3 (mode 2, peak = bf16 / 3)."""
     from o3dml_amd import _lib, layers, sparse_conv as sc
     lib = _lib.load()
@@ -630,7 +630,7 @@ def scn_bench(dev, pos, reps, world=1, rank=0):
     return {"ms_per_frame": round(dt / reps * 1e3, 3), "frames_per_s": round(fps, 2),
             "mvoxels_per_s": round(voxels / dt / 1e6, 3), "n_gpus": world, "frames": total,
             "frames_per_rank": counts,
-            "config": "SparseConvUnet m=32 residual reps=1 (sparseconvunet_scannet.yml), fp32 (bf16x6 MFMA "
+            "config": "SparseConvUnet m=32 residual reps=1 (sparseconvunet_scannet.yml), fp32 (exact f32 MFMA "
                       "products), eval" + (f", one room per GPU x {world}" if world > 1 else "")}
 
 

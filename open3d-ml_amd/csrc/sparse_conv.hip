@@ -1758,15 +1758,20 @@ constexpr int64_t kGemmTargetWaves = 4096;
 constexpr int kGemmMinStages = 4;
 constexpr int64_t kGemmSplitBytes = int64_t(64) << 20;
 
-// Product precision of the gather-GEMMs (mfma_stage_split): 0 = bf16x6
-// (default, f32-accurate), 1 = exact f32-input MFMA, 2 = bf16x3.  Env
-// O3DML_SPARSE_CONV_EXACT sets the initial mode; o3dml_sparse_conv_set_exact.
+// Product precision of the gather-GEMMs (mfma_stage_split): 1 = exact
+// f32-input MFMA (default: IEEE f32 products, infinities kept), 0 = bf16x6
+// (f32-accurate for finite inputs, a +-inf input turns the outputs that
+// gather it into NaN), 2 = bf16x3.  bf16x6 was the default until round 5; it
+// measured 1.20x (32 -> 32) / 1.24x (128 -> 128) faster per GEMM and equal on
+// the host-bound SparseConvUnet frame (tools/scn_precision_ab.sh), too little
+// for its non-finite deviation.  Env O3DML_SPARSE_CONV_EXACT sets the initial
+// mode; o3dml_sparse_conv_set_exact.
 static int g_gemm_mode = -1;
 static int gemm_mode() {
     if (g_gemm_mode < 0) {
         const char* e = std::getenv("O3DML_SPARSE_CONV_EXACT");
-        const int v = e ? std::atoi(e) : 0;
-        g_gemm_mode = (v == 1 || v == 2) ? v : 0;
+        const int v = e ? std::atoi(e) : 1;
+        g_gemm_mode = (v == 0 || v == 2) ? v : 1;
     }
     return g_gemm_mode;
 }

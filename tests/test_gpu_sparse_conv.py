@@ -230,8 +230,8 @@ def test_lattice_rulebook_falls_back_off_lattice(cuda):
 @pytest.mark.parametrize("cin,cout", [(32, 32), (64, 128), (3, 48)])
 def test_bf16_split_products_match_exact_f32(cuda, cin, cout):
     """Product precisions of the gather-GEMMs against a float64 reference:
-    the default bf16x6 (each f32 operand as hi + mid + lo bf16, six products)
-    must be as accurate as the exact f32-input MFMA kernel (within a few times
+    bf16x6 (each f32 operand as hi + mid + lo bf16, six products; opt-in)
+    must be as accurate as the exact f32-input MFMA kernel (the default) (within a few times
     its own f32 rounding error); bf16x3 (two terms, three products) within the
     north-star 1e-4.  Forward, input gradient and filter gradient; features
     span six decades of magnitude across channels."""
@@ -269,6 +269,28 @@ def test_bf16_split_products_match_exact_f32(cuda, cin, cout):
         lib.o3dml_sparse_conv_set_exact(prev)
     for e6, e1 in zip(errs[0], errs[1]):
         assert e6 <= 3 * e1 + 1e-7, (errs[0], errs[1])
+
+
+def test_default_precision_is_exact_f32_and_keeps_infinities(cuda):
+    """The default product precision is the exact f32-input MFMA (mode 1):
+    a +-inf feature gives the IEEE result (+-inf, or NaN only where the
+    exact arithmetic itself makes one: inf * 0, inf - inf), and finite
+    outputs are unaffected."""
+    from o3dml_amd import _lib, ops
+    lib = _lib.load()
+    assert lib.o3dml_sparse_conv_set_exact(-1) == 1
+    pos = _voxels(2000, 16, 6)
+    oi, ors, _ = O.fixed_radius_search(pos, pos, 1.5, metric="Linf")
+    ok = O.kernel_index(pos, pos, oi, ors, [3, 3, 3], 1.0)
+    gen = torch.Generator().manual_seed(4)
+    W = torch.rand(3, 3, 3, 32, 32, generator=gen) + 0.05  # positive weights: inf stays inf
+    x = torch.rand(len(pos), 32, generator=gen)
+    x[11, 5] = float("inf")
+    out = ops.sparse_conv(W.to(cuda), x.to(cuda), torch.empty(0), torch.from_numpy(oi), torch.from_numpy(ok),
+                          torch.empty(0), torch.from_numpy(ors)).cpu().numpy()
+    hit = np.array([np.isin(oi[ors[q]:ors[q + 1]], [11]).any() for q in range(len(pos))])
+    assert hit.any() and np.isposinf(out[hit]).all()
+    assert np.isfinite(out[~hit]).all()
 
 
 def test_bf16_split_large_and_nonfinite_inputs(cuda):

@@ -6,6 +6,7 @@
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py [args]
 #   py         python -u tools/<script> [args]
+#   sh         bash tools/<script> [args]
 #   prof       rocprofv3 --kernel-trace --stats over python3 tools/<script> [args]
 # Output under gpurun_out/$TAG/.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -34,6 +35,10 @@ for step in "$@"; do
       timeout -k 10 600 python -u tools/$arg > "$OUT/py_$n.log" 2>&1 \
           || { echo "py rc=$?"; tail -15 "$OUT/py_$n.log"; exit 1; }
       tail -40 "$OUT/py_$n.log";;
+    sh)
+      timeout -k 10 900 bash tools/$arg > "$OUT/sh_$n.log" 2>&1 \
+          || { echo "sh rc=$?"; tail -15 "$OUT/sh_$n.log"; exit 1; }
+      tail -40 "$OUT/sh_$n.log";;
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$n" -o run --output-format csv \
           -- python3 "$R/tools/"$arg > "$OUT/prof_$n.log" 2>&1) \
