@@ -113,7 +113,14 @@ __global__ void recip_norm_kernel(const float* __restrict__ norm, const float* _
 // per-row sums are unchanged.
 // --------------------------------------------------------------------------
 constexpr int64_t kOrderMinRows = 2048;
-static bool use_order(int64_t n, int K) { return K > 8 && n >= kOrderMinRows; }
+// O3DML_TILE_ORDER=0: no tile orders (rows in map order; A/B)
+static bool use_order(int64_t n, int K) {
+    static const bool on = [] {
+        const char* e = std::getenv("O3DML_TILE_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    return on && K > 8 && n >= kOrderMinRows;
+}
 
 // Grids of the GEMM kernels.  O3DML_GEMM_XCD=1: a multiple of 8 workgroups,
 // so xcd_block() hands each XCD one contiguous range of tiles (the extra
