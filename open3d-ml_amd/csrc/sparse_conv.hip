@@ -231,6 +231,10 @@ struct GemmPrologue {
     // BS kernels) and the byte size of that copy
     const __bf16* wsplit = nullptr;
     uint32_t wsplit_bytes = 0;
+    // persistent grid (implicit_gemm_lds_kernel): the column blocks of the
+    // work when the grid holds only the resident waves, each looping over
+    // (tile, split, column block) items; 0 = one wave per item
+    int pcols = 0;
 };
 constexpr int kPreMax = 1024;  // max cin with a prologue (LDS staging)
 
@@ -768,6 +772,29 @@ __device__ __forceinline__ void mfma_stage(const Stage& cu, f32x16& acc) {
     }
 }
 
+// Per-wave timeline of implicit_gemm_lds_kernel (diagnostic builds only:
+// -DO3DML_GEMM_TRACE=1, tools/gemm_trace.py): 100-MHz real-time stamps of
+// each wave's phases, read back with o3dml_gemm_trace_read.  Slots: 0 entry,
+// 1 output rows in LDS, 2 map tile in LDS, 3 offset mask, 4..11 stage j's
+// operands landed (first 8 stages), 12 stages done, 13 results stored,
+// 14 stage count, 15 HW_ID | XCC_ID << 32.
+#ifndef O3DML_GEMM_TRACE
+#define O3DML_GEMM_TRACE 0
+#endif
+#if O3DML_GEMM_TRACE
+constexpr int kTraceSlots = 16;
+constexpr int64_t kTraceWaves = 1 << 16;
+__device__ uint64_t g_gemm_trace[kTraceWaves * kTraceSlots];
+#define O3DML_TRACE_AT(slot, v)                                                            \
+    do {                                                                                   \
+        if (trace_row >= 0 && lane == 0) g_gemm_trace[trace_row * kTraceSlots + (slot)] = (v); \
+    } while (0)
+#define O3DML_TRACE(slot) O3DML_TRACE_AT(slot, __builtin_amdgcn_s_memrealtime())
+#else
+#define O3DML_TRACE_AT(slot, v) do {} while (0)
+#define O3DML_TRACE(slot) do {} while (0)
+#endif
+
 // DEPTH 2 (BUF only, O3DML_GEMM_DEPTH=2): two stages in flight per wave —
 // stage j+2's DMA is issued while stage j is multiplied.  Off by default:
 // 12 instead of 16 waves per CU (136 registers, 49 KiB LDS per workgroup), and
@@ -785,6 +812,9 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     __shared__ __attribute__((aligned(16))) float stage_all[kGemmThreads / 64][BREG && DEPTH == 1 ? 1 : 2][32 * 32];
     __shared__ int32_t mtile_all[kGemmThreads / 64][32 * 32];
     __shared__ int32_t orow_all[kGemmThreads / 64][32];
+#if O3DML_GEMM_TRACE
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+#endif
     float* lps = lpre;
     float* lpb = lpre + (PRE ? kPreMax + 32 : 0);
     if (PRE) {
@@ -794,21 +824,62 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
         }
         __syncthreads();
     }
-    const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
-    // XCD-contiguous tiles (grid a multiple of 8): XCD x takes one contiguous
-    // eighth of the (spatially chunked) tile order, so its L2 holds the input
-    // rows that eighth gathers
-    const int64_t o0 = (xcd_block() * (kGemmThreads / 64) + w) * 32;
-    if (o0 >= n_out) return;  // whole wave; no barriers below
-    const int i = lane & 31, h = lane >> 5;
-    const int col0 = blockIdx.y * 32;
-    const int col = col0 + i;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: item decode in scalars
     int32_t* mtile = mtile_all[w];
     int32_t* orow = orow_all[w];
     float* abuf = stage_all[w][0];
     float* bbuf = stage_all[w][BREG ? 0 : 1];  // unused with BREG
     if (order && *order_flag == 0) order = nullptr;  // map built without a tile order
+    // Work items (32-row tile, column block, split).  Default: one wave per
+    // item, the grid's (x, y, z).  Persistent grid (pre.pcols > 0): only as
+    // many waves as are resident, each looping over items tile-major, so no
+    // partial last round of waves idles most SIMDs (wave-lifetime tail).
+    const bool pers = pre.pcols > 0;
+    const int64_t ntw = (n_out + 31) >> 5;
+    const int64_t per_tile = pers ? static_cast<int64_t>(pre.pcols) * nsplit : 1;
+    const int64_t n_items = pers ? ntw * per_tile : 1;
+    const int64_t it_step = static_cast<int64_t>(gridDim.x) * (kGemmThreads / 64);
+#pragma clang loop unroll(disable)
+    for (int64_t it = pers ? static_cast<int64_t>(blockIdx.x) * (kGemmThreads / 64) + w : 0; it < n_items;
+         it += it_step) {
+    // the lane index made opaque per item: otherwise every lane-derived
+    // address of the body is hoisted out of the item loop and held live
+    // across it (72 -> 161 registers, half the waves)
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    const int i = lane & 31, h = lane >> 5;
+    int64_t tw;
+    int cy, s;
+    if (pers) {
+        tw = it / per_tile;
+        const int r = static_cast<int>(it - tw * per_tile);
+        cy = r % pre.pcols;
+        s = r / pre.pcols;
+    } else {
+        // XCD-contiguous tiles (grid a multiple of 8): XCD x takes one
+        // contiguous eighth of the (spatially chunked) tile order, so its L2
+        // holds the input rows that eighth gathers
+        tw = xcd_block() * (kGemmThreads / 64) + w;
+        cy = blockIdx.y;
+        s = blockIdx.z;
+    }
+    const int64_t o0 = tw * 32;
+    if (o0 >= n_out) continue;  // whole wave; no barriers below
+    const int col0 = cy * 32;
+    const int col = col0 + i;
+#if O3DML_GEMM_TRACE
+    const int64_t trace_wave = pers ? it
+                                    : ((static_cast<int64_t>(blockIdx.z) * gridDim.y + blockIdx.y) * gridDim.x +
+                                       blockIdx.x) * (kGemmThreads / 64) + w;
+    const int64_t trace_row = trace_wave < kTraceWaves ? trace_wave : -1;
+    O3DML_TRACE_AT(0, t_entry);
+    O3DML_TRACE_AT(15, static_cast<uint64_t>(__builtin_amdgcn_s_getreg((31 << 11) | 4)) |
+                           (static_cast<uint64_t>(__builtin_amdgcn_s_getreg((31 << 11) | 20)) << 32));
+#endif
+    // the previous item's LDS reads (orow, mtile, stage) are done
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (lane < 32) {
         const int64_t oo = o0 + lane;
         orow[lane] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
@@ -816,24 +887,27 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    O3DML_TRACE(1);
     load_map_tile<32, 64>(map, orow, K, lane, mtile);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    O3DML_TRACE(2);
     unsigned used = 0u;
     for (int k = h; k < K; k += 2) {
         const uint64_t b = __ballot(mtile[i * K + k] >= 0);
         used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
     }
     used = __builtin_amdgcn_readlane(used, 32) | __builtin_amdgcn_readlane(used, 0);
+    O3DML_TRACE(3);
     const int64_t o = orow[i] >= 0 ? orow[i] : 0;
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     const int nch = (cin + 31) >> 5;
-    const int s = blockIdx.z;
     const int j0 = split_stage(used, nch, K, s, nsplit);
     const int j1 = split_stage(used, nch, K, s + 1, nsplit);
+    O3DML_TRACE_AT(14, static_cast<uint64_t>(j1 - j0));
     if (DEPTH == 2 && j0 < j1) {
         static_assert(DEPTH == 1 || (BUF && BREG && !SC), "two stages in flight: buffer path only");
         unsigned u = used;
@@ -907,6 +981,7 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
                                      cout, true, nx, &rs);
         for (int j = j0; j < j1; ++j) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage j in LDS, its row factors in nx
+            if (j - j0 < 8) O3DML_TRACE(4 + j - j0);
             lds_read<BREG>(abuf, bbuf, i, h, cu);
             if constexpr (BS) {
 #pragma unroll
@@ -936,11 +1011,14 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead DMA has landed before the wave exits
     }
+    O3DML_TRACE(12);
     if (nsplit > 1) {
         split_store_finish(acc, orow, h, col, lane, s, nsplit, n_out, cout, part, counters,
-                           (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * (kGemmThreads / 64) + w,
+                           pers ? cy * ntw + tw
+                                : (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * (kGemmThreads / 64) + w,
                            oscale, bias, residual, out);
-        return;
+        O3DML_TRACE(13);
+        continue;
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -953,7 +1031,23 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
             out[orr * cout + col] = v;
         }
     }
+    O3DML_TRACE(13);
+    }  // work items
 }
+
+#if O3DML_GEMM_TRACE
+// diagnostic builds: copy the per-wave timeline out (kTraceWaves x kTraceSlots
+// u64) after the GEMM of interest has run; o3dml_gemm_trace_clear zeroes it
+O3DML_API int o3dml_gemm_trace_read(void* dst, size_t bytes) {
+    bytes = std::min(bytes, sizeof(g_gemm_trace));
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_gemm_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+O3DML_API int o3dml_gemm_trace_clear() {
+    static std::vector<uint64_t> z(kTraceWaves * kTraceSlots, 0);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_trace), z.data(), sizeof(g_gemm_trace), 0, hipMemcpyHostToDevice) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif
 
 // --------------------------------------------------------------------------
 // implicit GEMM, A tile shared by the workgroup (cout >= 64): NW waves own the
@@ -1800,6 +1894,36 @@ static int gemm_splits(int64_t n_out, int K, int cin, int cout) {
     return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ns, 64)));
 }
 
+// Persistent grid of implicit_gemm_lds_kernel: O3DML_GEMM_PERSIST = v > 0
+// launches v x the resident workgroups (occupancy x CUs) when the work has
+// more waves than that, the waves looping over the items; 0 = one wave per item
+static int gemm_persist() {
+    static const int v = [] {
+        const char* e = std::getenv("O3DML_GEMM_PERSIST");
+        return e ? std::max(0, std::atoi(e)) : 1;
+    }();
+    return v;
+}
+template <auto Kern>
+static int resident_blocks() {  // once per instantiation (one device per process)
+    static const int v = [] {
+        int nb = 0, dev = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, Kern, kGemmThreads, 0) != hipSuccess) nb = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+        return nb * cus;
+    }();
+    return v;
+}
+template <auto Kern>
+static dim3 persist_grid(dim3 g, GemmPrologue& pp) {
+    const int64_t rb = static_cast<int64_t>(resident_blocks<Kern>()) * gemm_persist();
+    if (rb <= 0 || static_cast<int64_t>(g.x) * g.y * g.z <= rb) return g;
+    pp.pcols = static_cast<int>(g.y);
+    return dim3(static_cast<unsigned>(rb), 1, 1);
+}
+
 static size_t gemm_split_bytes(int64_t n_out, int K, int cin, int cout) {
     const int ns = gemm_splits(n_out, K, cin, cout);
     return ns > 1 ? ws_bytes<float>(ns * n_out * cout) : 0;
@@ -2015,21 +2139,21 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #undef O3DML_GEMM_SH_SC
 #undef O3DML_GEMM_SH_BUF
     } else if (vec4 && lds_path) {
-#define O3DML_GEMM_LDS_SC(P, BR, X, SCL)                                                                          \
-    implicit_gemm_lds_kernel<P, BR, X, SCL><<<g, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src,    \
-                                                                        sscale, pscale, Wt, cin, cout, oscale,    \
-                                                                        bias, out, ns, part, pre, residual,       \
-                                                                        counters)
+#define O3DML_GEMM_LDS_GO(...)                                                                                   \
+    do {                                                                                                         \
+        GemmPrologue pp = pre;                                                                                   \
+        const dim3 gg = persist_grid<__VA_ARGS__>(g, pp);                                                        \
+        __VA_ARGS__<<<gg, kGemmThreads, 0, st>>>(map, order, order_flag, K, n_out, src, sscale, pscale, Wt, cin, \
+                                                 cout, oscale, bias, out, ns, part, pp, residual, counters);     \
+    } while (0)
+#define O3DML_GEMM_LDS_SC(P, BR, X, SCL) O3DML_GEMM_LDS_GO(implicit_gemm_lds_kernel<P, BR, X, SCL>)
 #define O3DML_GEMM_LDS(P, BR, X)                                      \
     do {                                                              \
         if (sscale || pscale) O3DML_GEMM_LDS_SC(P, BR, X, true);      \
         else if (BR && buf_ok) O3DML_GEMM_LDS_BUF(P, X);              \
         else O3DML_GEMM_LDS_SC(P, BR, X, false);                      \
     } while (0)
-#define O3DML_GEMM_LDS_BUF2(P, X, D)                                                                             \
-    implicit_gemm_lds_kernel<P, true, X, false, true, D><<<g, kGemmThreads, 0, st>>>(                            \
-            map, order, order_flag, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, bias, out, ns, part, pre, \
-            residual, counters)
+#define O3DML_GEMM_LDS_BUF2(P, X, D) O3DML_GEMM_LDS_GO(implicit_gemm_lds_kernel<P, true, X, false, true, D>)
 #define O3DML_GEMM_LDS_BUF(P, X)                                 \
     do {                                                         \
         if (depth2) O3DML_GEMM_LDS_BUF2(P, X, 2);                \
@@ -2054,10 +2178,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
             pre.wsplit = reinterpret_cast<const __bf16*>(w3);
             pre.wsplit_bytes = static_cast<uint32_t>(wn * 6);
         }
-#define O3DML_GEMM_LDS_BS(P)                                                                                     \
-    implicit_gemm_lds_kernel<P, true, 6, false, true, 1, true><<<g, kGemmThreads, 0, st>>>(                      \
-            map, order, order_flag, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, bias, out, ns, part, pre, \
-            residual, counters)
+#define O3DML_GEMM_LDS_BS(P) O3DML_GEMM_LDS_GO(implicit_gemm_lds_kernel<P, true, 6, false, true, 1, true>)
         if (nt == 6 && bs) {
             if (pre.scale) O3DML_GEMM_LDS_BS(true); else O3DML_GEMM_LDS_BS(false);
         } else if (nt == 6) {
@@ -2074,6 +2195,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
 #undef O3DML_GEMM_LDS_BUF
 #undef O3DML_GEMM_LDS_BUF2
 #undef O3DML_GEMM_LDS_BS
+#undef O3DML_GEMM_LDS_GO
     } else if (pre.scale) {
         if (vec4) O3DML_GEMM_LAUNCH(true, true); else O3DML_GEMM_LAUNCH(false, true);
     } else {
