@@ -172,8 +172,24 @@ static size_t order_scratch_bytes(int64_t n) {
     return 2 * ws_bytes<uint32_t>(n) + prim::radix_sort_workspace_bytes<uint32_t>(n);
 }
 
-static void build_order(const int32_t* map, int64_t n, int K, int32_t* order, int* flag, Workspace scratch,
-                        hipStream_t st) {
+// The map rows in tile order, tmap[j] = map[order[j]], padded with -1 rows to
+// whole 128-row blocks (the largest GEMM tile): a GEMM wave reads its tile's
+// map rows as one contiguous block, issued at once with (not after) its read
+// of the order.
+constexpr int64_t kTileMapPad = 128;
+static int64_t tile_map_entries(int64_t n, int K) { return ((n + kTileMapPad - 1) & ~(kTileMapPad - 1)) * K; }
+__global__ void tile_map_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, int64_t n, int K,
+                                int32_t* __restrict__ tmap) {
+    const int64_t tot = ((n + kTileMapPad - 1) & ~(kTileMapPad - 1)) * K;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < tot;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t j = e / K;
+        tmap[e] = j < n ? map[static_cast<int64_t>(order[j]) * K + (e - j * K)] : -1;
+    }
+}
+
+static void build_order(const int32_t* map, int64_t n, int K, int32_t* order, int32_t* tmap, int* flag,
+                        Workspace scratch, hipStream_t st) {
     if (!use_order(n, K)) return;
     uint32_t* kin = scratch.take<uint32_t>(n);
     uint32_t* kout = scratch.take<uint32_t>(n);
@@ -185,6 +201,8 @@ static void build_order(const int32_t* map, int64_t n, int K, int32_t* order, in
     const int bits = hb + cb;
     O3DML_REQUIRE(bits <= 32, "tile order: too many row chunks");
     prim::radix_sort_pairs<uint32_t>(kin, nullptr, kout, reinterpret_cast<uint32_t*>(order), n, bits, scratch, st);
+    tile_map_kernel<<<stream_grid(tile_map_entries(n, K), 256), 256, 0, st>>>(map, order, n, K, tmap);
+    O3DML_LAUNCH_CHECK();
 }
 
 // W [K][Cin][Cout] -> Wt [K][Cout][Cin]
@@ -231,6 +249,9 @@ struct GemmPrologue {
     // BS kernels) and the byte size of that copy
     const __bf16* wsplit = nullptr;
     uint32_t wsplit_bytes = 0;
+    // the map rows in tile order (tile_map_kernel; valid with the order):
+    // implicit_gemm_lds_kernel loads its tile's rows from here
+    const int32_t* tmap = nullptr;
     // persistent grid (implicit_gemm_lds_kernel): the column blocks of the
     // work when the grid holds only the resident waves, each looping over
     // (tile, split, column block) items; 0 = one wave per item
@@ -400,6 +421,38 @@ __device__ __forceinline__ void load_map_tile(const int32_t* __restrict__ map, c
         const int e = t + T * it;
         if (e < tot) mtile[e] = v[it];
     }
+}
+
+// A tile from the tile-order map copy (tile_map_kernel): its ROWS x K entries
+// are contiguous at tm, so thread t of T issues all its loads at once without
+// waiting for the order; into LDS as load_map_tile.  Returns the offsets the
+// thread's entries use, OR-reduced over its wave: the same bits as a ballot
+// over the LDS tile, without its LDS round trips.
+template <int ROWS, int T>
+__device__ __forceinline__ unsigned load_map_tile_direct(const int32_t* __restrict__ tm, int K, int t,
+                                                         int32_t* mtile) {
+    constexpr int kIt = (ROWS * 32 + T - 1) / T;
+    const int tot = ROWS * K;
+    const float invk = 1.0f / static_cast<float>(K);  // e / K exact as in load_map_tile
+    int32_t v[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int e = t + T * it;
+        v[it] = tm[e < tot ? e : 0];
+    }
+    unsigned mask = 0u;
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int e = t + T * it;
+        if (e < tot) {
+            mtile[e] = v[it];
+            const int rr = static_cast<int>((static_cast<float>(e) + 0.5f) * invk);
+            mask |= v[it] >= 0 ? 1u << (e - rr * K) : 0u;
+        }
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) mask |= static_cast<unsigned>(__shfl_xor(static_cast<int>(mask), d));
+    return __builtin_amdgcn_readfirstlane(mask);
 }
 
 template <bool VEC4, bool PRE>
@@ -880,25 +933,38 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < 32) {
-        const int64_t oo = o0 + lane;
-        orow[lane] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    O3DML_TRACE(1);
-    load_map_tile<32, 64>(map, orow, K, lane, mtile);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    O3DML_TRACE(2);
     unsigned used = 0u;
-    for (int k = h; k < K; k += 2) {
-        const uint64_t b = __ballot(mtile[i * K + k] >= 0);
-        used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
+    if (order && pre.tmap) {  // tile order with its map copy: map rows and output rows loaded together
+        if (lane < 32) {
+            const int64_t oo = o0 + lane;
+            orow[lane] = oo < n_out ? order[oo] : -1;
+        }
+        used = load_map_tile_direct<32, 64>(pre.tmap + o0 * K, K, lane, mtile);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        O3DML_TRACE(1);
+        O3DML_TRACE(2);
+    } else {
+        if (lane < 32) {
+            const int64_t oo = o0 + lane;
+            orow[lane] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        O3DML_TRACE(1);
+        load_map_tile<32, 64>(map, orow, K, lane, mtile);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        O3DML_TRACE(2);
+        for (int k = h; k < K; k += 2) {
+            const uint64_t b = __ballot(mtile[i * K + k] >= 0);
+            used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
+        }
+        used = __builtin_amdgcn_readlane(used, 32) | __builtin_amdgcn_readlane(used, 0);
     }
-    used = __builtin_amdgcn_readlane(used, 32) | __builtin_amdgcn_readlane(used, 0);
     O3DML_TRACE(3);
     const int64_t o = orow[i] >= 0 ? orow[i] : 0;
     f32x16 acc;
@@ -1216,20 +1282,33 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
     const int i = lane & 31, h = lane >> 5;
     const int col = (blockIdx.y * NW + w) * 32 + i;
     if (order && *order_flag == 0) order = nullptr;
-    for (int t = threadIdx.x; t < R; t += NW * 64) {
-        const int64_t oo = o0 + t;
-        orow[t] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
-    }
-    __syncthreads();
-    load_map_tile<R, NW * 64>(map, orow, K, threadIdx.x, mtile);
-    __syncthreads();
     unsigned used = 0u;  // identical in every wave (same rows)
-    for (int k = h; k < K; k += 2) {
-        bool any = false;
+    if (order && pre.tmap) {  // tile order with its map copy: map rows and output rows loaded together
+        __shared__ unsigned used_w[NW];
+        for (int t = threadIdx.x; t < R; t += NW * 64) {
+            const int64_t oo = o0 + t;
+            orow[t] = oo < n_out ? order[oo] : -1;
+        }
+        const unsigned mw = load_map_tile_direct<R, NW * 64>(pre.tmap + o0 * K, K, threadIdx.x, mtile);
+        if (lane == 0) used_w[w] = mw;
+        __syncthreads();
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) any |= mtile[(32 * rb + i) * K + k] >= 0;
-        const uint64_t b = __ballot(any);
-        used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
+        for (int v = 0; v < NW; ++v) used |= used_w[v];
+    } else {
+        for (int t = threadIdx.x; t < R; t += NW * 64) {
+            const int64_t oo = o0 + t;
+            orow[t] = oo < n_out ? (order ? order[oo] : static_cast<int32_t>(oo)) : -1;
+        }
+        __syncthreads();
+        load_map_tile<R, NW * 64>(map, orow, K, threadIdx.x, mtile);
+        __syncthreads();
+        for (int k = h; k < K; k += 2) {
+            bool any = false;
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) any |= mtile[(32 * rb + i) * K + k] >= 0;
+            const uint64_t b = __ballot(any);
+            used |= ((h ? (b >> 32) : (b & 0xffffffffull)) != 0ull) ? (1u << k) : 0u;
+        }
     }
     used = __builtin_amdgcn_readlane(used, 32) | __builtin_amdgcn_readlane(used, 0);
     int64_t o[RB];
@@ -1969,8 +2048,14 @@ static size_t gemm_ws_bytes(int64_t n_out, int64_t n_src, int K, int cin, int co
 static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, const int* order_flag, int K,
                      int64_t n_out, const float* src, int64_t n_src, const float* sscale, const float* pscale,
                      const float* Wt, int cin, int cout, const float* oscale, const float* bias, float* out,
-                     Workspace ws, GemmPrologue pre = {nullptr, nullptr}, const float* residual = nullptr) {
+                     Workspace ws, GemmPrologue pre = {nullptr, nullptr}, const float* residual = nullptr,
+                     const int32_t* tmap = nullptr) {
     if (n_out == 0 || cout == 0) return;
+    static const bool tile_map = [] {  // O3DML_GEMM_TILE_MAP=0: tiles read the map through the order (A/B)
+        const char* e = std::getenv("O3DML_GEMM_TILE_MAP");
+        return !(e && e[0] == '0');
+    }();
+    pre.tmap = order && tile_map ? tmap : nullptr;
     const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0 &&
                       (reinterpret_cast<uintptr_t>(Wt) % 16) == 0;
     int ns = gemm_splits(n_out, K, cin, cout);
@@ -2467,7 +2552,8 @@ using namespace o3dml;
 O3DML_API size_t o3dml_sparse_conv_map_workspace_size(int64_t n_out, int64_t n_in, int K) {
     return ws_bytes<int32_t>(n_out * K) + ws_bytes<float>(n_out * K) + ws_bytes<float>(n_out) +
            ws_bytes<float>(n_out) + ws_bytes<int32_t>(n_in * K) + ws_bytes<float>(n_in * K) + ws_bytes<int>(4) +
-           ws_bytes<int32_t>(n_out) + ws_bytes<int32_t>(n_in) + order_scratch_bytes(std::max(n_out, n_in));
+           ws_bytes<int32_t>(n_out) + ws_bytes<int32_t>(n_in) + ws_bytes<int32_t>(tile_map_entries(n_out, K)) +
+           ws_bytes<int32_t>(tile_map_entries(n_in, K)) + order_scratch_bytes(std::max(n_out, n_in));
 }
 
 // Tile orders of the map and the inverse map (after the status words) and the
@@ -2475,13 +2561,17 @@ O3DML_API size_t o3dml_sparse_conv_map_workspace_size(int64_t n_out, int64_t n_i
 struct MapOrders {
     int32_t* order;
     int32_t* iorder;
+    int32_t* tmap;   // map rows in tile order
+    int32_t* itmap;  // inverse map rows in tile order
     Workspace scratch;
 };
 
-static MapOrders map_orders(Workspace& ws, int64_t n_out, int64_t n_in) {
+static MapOrders map_orders(Workspace& ws, int64_t n_out, int64_t n_in, int K) {
     int32_t* order = ws.take<int32_t>(n_out);
     int32_t* iorder = ws.take<int32_t>(n_in);
-    return MapOrders{order, iorder, Workspace(ws.base + ws.used, ws.size - ws.used)};
+    int32_t* tmap = ws.take<int32_t>(tile_map_entries(n_out, K));
+    int32_t* itmap = ws.take<int32_t>(tile_map_entries(n_in, K));
+    return MapOrders{order, iorder, tmap, itmap, Workspace(ws.base + ws.used, ws.size - ws.used)};
 }
 
 // Builds the dense kernel map (and, with want_inverse, the inverse map used by
@@ -2669,7 +2759,8 @@ static float* forward_filters(const float* filters, int K, int cin, int cout, Wo
 
 static void map_views(void* workspace, size_t bytes, int64_t n_out, int64_t n_in, int K, int32_t** map,
                       float** pscale, float** oscale, int32_t** inv, float** ipscale, const int32_t** order,
-                      const int32_t** iorder, const int** order_flag, const int** iorder_flag) {
+                      const int32_t** iorder, const int** order_flag, const int** iorder_flag,
+                      const int32_t** tmap = nullptr, const int32_t** itmap = nullptr) {
     Workspace ws(workspace, bytes);
     *map = ws.take<int32_t>(n_out * K);
     *pscale = ws.take<float>(n_out * K);
@@ -2678,10 +2769,12 @@ static void map_views(void* workspace, size_t bytes, int64_t n_out, int64_t n_in
     *inv = ws.take<int32_t>(n_in * K);
     *ipscale = ws.take<float>(n_in * K);
     int* status = ws.take<int>(4);
-    const MapOrders ord = map_orders(ws, n_out, n_in);
+    const MapOrders ord = map_orders(ws, n_out, n_in, K);
     // device flags status[2] / status[3] say whether the orders were built
     *order = use_order(n_out, K) ? ord.order : nullptr;
     *iorder = use_order(n_in, K) ? ord.iorder : nullptr;
+    if (tmap) *tmap = ord.tmap;
+    if (itmap) *itmap = ord.itmap;
     *order_flag = status + 2;
     *iorder_flag = status + 3;
 }
@@ -2700,9 +2793,9 @@ O3DML_API int o3dml_sparse_conv_tile_order(void* map_workspace, size_t map_works
     const int32_t* inv = ws.take<int32_t>(n_in * K);
     ws.take<float>(n_in * K);
     int* status = ws.take<int>(4);
-    MapOrders ord = map_orders(ws, n_out, n_in);
-    build_order(map, n_out, K, ord.order, status + 2, ord.scratch, st);
-    if (inverse) build_order(inv, n_in, K, ord.iorder, status + 3, ord.scratch, st);
+    MapOrders ord = map_orders(ws, n_out, n_in, K);
+    build_order(map, n_out, K, ord.order, ord.tmap, status + 2, ord.scratch, st);
+    if (inverse) build_order(inv, n_in, K, ord.iorder, ord.itmap, status + 3, ord.scratch, st);
     O3DML_GUARD_END
 }
 
@@ -2721,15 +2814,15 @@ O3DML_API int o3dml_sparse_conv_forward_fused(const float* filters_t, int K, int
     O3DML_REQUIRE((pre_scale == nullptr) == (pre_shift == nullptr), "pre_scale and pre_shift go together");
     int32_t *map, *inv;
     float *pscale, *oscale, *ipscale;
-    const int32_t *order, *iorder;
+    const int32_t *order, *iorder, *tmap;
     const int *oflag, *ioflag;
     map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
-              &iorder, &oflag, &ioflag);
+              &iorder, &oflag, &ioflag, &tmap);
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
     ws.take<float>(static_cast<int64_t>(K) * cin * cout);  // (unused Wt slot: filters_t comes transposed)
     run_gemm(st, map, order, oflag, K, n_out, inp_features, n_in, nullptr, nullptr, filters_t, cin, cout, nullptr,
-             bias, out_features, ws, GemmPrologue{pre_scale, pre_shift}, residual);
+             bias, out_features, ws, GemmPrologue{pre_scale, pre_shift}, residual, tmap);
     O3DML_GUARD_END
 }
 
@@ -2750,16 +2843,16 @@ O3DML_API int o3dml_sparse_conv_forward(const float* filters, int K, int cin, in
     O3DML_GUARD_BEGIN
     int32_t *map, *inv;
     float *pscale, *oscale, *ipscale;
-    const int32_t *order, *iorder;
+    const int32_t *order, *iorder, *tmap;
     const int *oflag, *ioflag;
     map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
-              &iorder, &oflag, &ioflag);
+              &iorder, &oflag, &ioflag, &tmap);
     hipStream_t st = as_stream(stream);
     Workspace ws(workspace, workspace_bytes);
     const float* wt = forward_filters(filters, K, cin, cout, ws, st);
     run_gemm(st, map, order, oflag, K, n_out, inp_features, n_in, inp_importance,
              has_neighbors_importance ? pscale : nullptr, wt, cin, cout, use_out_scale ? oscale : nullptr, bias,
-             out_features, ws);
+             out_features, ws, GemmPrologue{nullptr, nullptr}, nullptr, tmap);
     O3DML_GUARD_END
 }
 
@@ -2793,10 +2886,10 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
     hipStream_t st = as_stream(stream);
     int32_t *map, *inv;
     float *pscale, *oscale, *ipscale;
-    const int32_t *order, *iorder;
+    const int32_t *order, *iorder, *itmap;
     const int *oflag, *ioflag;
     map_views(map_workspace, map_workspace_bytes, n_out, n_in, K, &map, &pscale, &oscale, &inv, &ipscale, &order,
-              &iorder, &oflag, &ioflag);
+              &iorder, &oflag, &ioflag, nullptr, &itmap);
     Workspace ws(workspace, workspace_bytes);
     float* wt = ws.take<float>(static_cast<int64_t>(K) * cin * cout);
     float* g = ws.take<float>(n_out * cout);  // unused slot kept for layout stability
@@ -2814,7 +2907,8 @@ O3DML_API int o3dml_sparse_conv_backward(const float* filters, int K, int cin, i
         // fold it in as sscale; pair importance via the inverse pscale.
         (void)wt;
         run_gemm(st, inv, iorder, ioflag, K, n_in, grad_out, n_out, os, has_neighbors_importance ? ipscale : nullptr,
-                 filters, cout, cin, inp_importance, nullptr, grad_inp, gws);
+                 filters, cout, cin, inp_importance, nullptr, grad_inp, gws, GemmPrologue{nullptr, nullptr}, nullptr,
+                 itmap);
     }
     if (grad_filters) {
         const int64_t KC = static_cast<int64_t>(K) * cin * cout;

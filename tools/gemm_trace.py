@@ -49,6 +49,9 @@ def report(t):
     live = t[:, 13] != 0
     t = t[live].astype(np.int64)
     n = t.shape[0]
+    if n == 0:
+        print("  no waves traced (cout >= 64 runs the shared-A kernel, not traced)")
+        return
     t0 = t[:, 0].min()
     span = (t[:, 13].max() - t0) * TICK_NS
     print(f"  waves traced {n}, kernel span {span / 1e3:.1f} us (first entry -> last store)")
