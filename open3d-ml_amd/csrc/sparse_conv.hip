@@ -177,6 +177,14 @@ static size_t order_scratch_bytes(int64_t n) {
 // map rows as one contiguous block, issued at once with (not after) its read
 // of the order.
 constexpr int64_t kTileMapPad = 128;
+// O3DML_GEMM_TILE_MAP=0: no tile-order map copy; tiles read the map through the order (A/B)
+static bool use_tile_map() {
+    static const bool on = [] {
+        const char* e = std::getenv("O3DML_GEMM_TILE_MAP");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 static int64_t tile_map_entries(int64_t n, int K) { return ((n + kTileMapPad - 1) & ~(kTileMapPad - 1)) * K; }
 __global__ void tile_map_kernel(const int32_t* __restrict__ map, const int32_t* __restrict__ order, int64_t n, int K,
                                 int32_t* __restrict__ tmap) {
@@ -201,8 +209,10 @@ static void build_order(const int32_t* map, int64_t n, int K, int32_t* order, in
     const int bits = hb + cb;
     O3DML_REQUIRE(bits <= 32, "tile order: too many row chunks");
     prim::radix_sort_pairs<uint32_t>(kin, nullptr, kout, reinterpret_cast<uint32_t*>(order), n, bits, scratch, st);
-    tile_map_kernel<<<stream_grid(tile_map_entries(n, K), 256), 256, 0, st>>>(map, order, n, K, tmap);
-    O3DML_LAUNCH_CHECK();
+    if (use_tile_map()) {
+        tile_map_kernel<<<stream_grid(tile_map_entries(n, K), 256), 256, 0, st>>>(map, order, n, K, tmap);
+        O3DML_LAUNCH_CHECK();
+    }
 }
 
 // W [K][Cin][Cout] -> Wt [K][Cout][Cin]
@@ -2051,11 +2061,7 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
                      Workspace ws, GemmPrologue pre = {nullptr, nullptr}, const float* residual = nullptr,
                      const int32_t* tmap = nullptr) {
     if (n_out == 0 || cout == 0) return;
-    static const bool tile_map = [] {  // O3DML_GEMM_TILE_MAP=0: tiles read the map through the order (A/B)
-        const char* e = std::getenv("O3DML_GEMM_TILE_MAP");
-        return !(e && e[0] == '0');
-    }();
-    pre.tmap = order && tile_map ? tmap : nullptr;
+    pre.tmap = order && use_tile_map() ? tmap : nullptr;
     const bool vec4 = (cin % 4) == 0 && (reinterpret_cast<uintptr_t>(src) % 16) == 0 &&
                       (reinterpret_cast<uintptr_t>(Wt) % 16) == 0;
     int ns = gemm_splits(n_out, K, cin, cout);
