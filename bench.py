@@ -181,8 +181,9 @@ def cpu_baseline(scenes=64):
     pts, rs = pts.numpy(), rs.numpy()
     one = pts[:N_POINTS]
 
-    def median_rate(fn, n, reps=3):
-        fn()  # warm (first touch, the oracle build if needed)
+    def median_rate(fn, n, warm=3, reps=10):  # BASELINE.md timing protocol: 3 warm-ups, median of 10
+        for _ in range(warm):
+            fn()  # first touch, the oracle build if needed
         times = []
         for _ in range(reps):
             t = time.perf_counter()
@@ -202,7 +203,7 @@ def cpu_baseline(scenes=64):
     return {"value": n_thr, "unit": "Mpoints/s", "cores": threads, "kind": "port",
             "value_1_thread": one_thr, "plain_oracle_value": plain,
             "sample": f"oracle/cpu_frs.c (parallel hash build + one-pass search, AVX2/FMA when the host has "
-                      f"them) on the bench batch ({scenes} x 65,536-pt C1 scenes), median of 3, {threads} OpenMP "
+                      f"them) on the bench batch ({scenes} x 65,536-pt C1 scenes), 3 warm-ups + median of 10, {threads} OpenMP "
                       f"threads; value_1_thread: same code, 1 thread, one scene; plain_oracle_value: the test "
                       f"oracle (serial build, count + fill passes), one scene, {threads} threads"}
 
