@@ -439,17 +439,26 @@ __device__ __forceinline__ void load_map_tile(const int32_t* __restrict__ map, c
 // thread's entries use, OR-reduced over its wave: the same bits as a ballot
 // over the LDS tile, without its LDS round trips.
 template <int ROWS, int T>
-__device__ __forceinline__ unsigned load_map_tile_direct(const int32_t* __restrict__ tm, int K, int t,
-                                                         int32_t* mtile) {
+struct MapTileRegs {
+    int32_t v[(ROWS * 32 + T - 1) / T];
+};
+// the loads only (values land in registers; map_tile_commit stores them)
+template <int ROWS, int T>
+__device__ __forceinline__ void map_tile_fetch(const int32_t* __restrict__ tm, int K, int t, MapTileRegs<ROWS, T>& r) {
     constexpr int kIt = (ROWS * 32 + T - 1) / T;
     const int tot = ROWS * K;
-    const float invk = 1.0f / static_cast<float>(K);  // e / K exact as in load_map_tile
-    int32_t v[kIt];
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
         const int e = t + T * it;
-        v[it] = tm[e < tot ? e : 0];
+        r.v[it] = tm[e < tot ? e : 0];
     }
+}
+template <int ROWS, int T>
+__device__ __forceinline__ unsigned map_tile_commit(const MapTileRegs<ROWS, T>& r, int K, int t, int32_t* mtile) {
+    constexpr int kIt = (ROWS * 32 + T - 1) / T;
+    const int tot = ROWS * K;
+    const float invk = 1.0f / static_cast<float>(K);  // e / K exact as in load_map_tile
+    const int32_t* v = r.v;
     unsigned mask = 0u;
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
@@ -463,6 +472,13 @@ __device__ __forceinline__ unsigned load_map_tile_direct(const int32_t* __restri
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) mask |= static_cast<unsigned>(__shfl_xor(static_cast<int>(mask), d));
     return __builtin_amdgcn_readfirstlane(mask);
+}
+template <int ROWS, int T>
+__device__ __forceinline__ unsigned load_map_tile_direct(const int32_t* __restrict__ tm, int K, int t,
+                                                         int32_t* mtile) {
+    MapTileRegs<ROWS, T> r;
+    map_tile_fetch<ROWS, T>(tm, K, t, r);
+    return map_tile_commit<ROWS, T>(r, K, t, mtile);
 }
 
 template <bool VEC4, bool PRE>
@@ -637,6 +653,11 @@ __device__ __forceinline__ GemmRsrc gemm_rsrc(const float* src, const float* Wt,
                                               static_cast<int>(pre.wsplit_bytes), kBufferFlags)};
 }
 
+// O3DML_GEMM_DIAG (cost-split builds only, results invalid): 1 = the per-wave
+// kernel's buffer path issues no filter loads, 2 = no row gathers
+#ifndef O3DML_GEMM_DIAG
+#define O3DML_GEMM_DIAG 0
+#endif
 template <bool BREG, bool SC = true, bool BUF = false, bool BS = false>
 __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_t* mtile, int K, int k, int c0,
                                           int lane, int64_t o, int i, int col0, const float* __restrict__ src,
@@ -652,6 +673,7 @@ __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_
     if constexpr (BUF) {
         static_assert(BREG && !SC, "buffer addressing: filters in registers, no scales");
         const uint32_t row_bytes = static_cast<uint32_t>(cin) * 4u;
+#if O3DML_GEMM_DIAG != 2  // cost-split diagnostics: 2 = no row gathers
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int r = 8 * q + (lane >> 3);
@@ -659,7 +681,19 @@ __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_
             const uint32_t off = mq[q] >= 0 ? static_cast<uint32_t>(mq[q]) * row_bytes + cb : kNoRow;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs->src, (lds_void_ptr)(abuf + 256 * q), 16, off, 0, 0, 0);
         }
+#else
+        (void)row_bytes;
+#endif
         const int col = col0 + i;
+#if O3DML_GEMM_DIAG == 1  // cost-split diagnostics: 1 = no filter loads
+        if constexpr (!BS) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) st.b[q] = 1.f;
+            st.s1 = st.s2 = 1.f;
+            st.v = mi >= 0 ? 1.f : 0.f;
+            return;
+        }
+#endif
         if constexpr (BS) {  // the lane's 16 channels as two 8-channel blocks of 3 x 16 B
             const uint32_t soff = (live && col < cout)
                                           ? (static_cast<uint32_t>(k * cout + col) * static_cast<uint32_t>(cin) +
@@ -892,7 +926,6 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     int32_t* orow = orow_all[w];
     float* abuf = stage_all[w][0];
     float* bbuf = stage_all[w][BREG ? 0 : 1];  // unused with BREG
-    if (order && *order_flag == 0) order = nullptr;  // map built without a tile order
     // Work items (32-row tile, column block, split).  Default: one wave per
     // item, the grid's (x, y, z).  Persistent grid (pre.pcols > 0): only as
     // many waves as are resident, each looping over items tile-major, so no
@@ -902,9 +935,33 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     const int64_t per_tile = pers ? static_cast<int64_t>(pre.pcols) * nsplit : 1;
     const int64_t n_items = pers ? ntw * per_tile : 1;
     const int64_t it_step = static_cast<int64_t>(gridDim.x) * (kGemmThreads / 64);
+    const int64_t it0 = pers ? static_cast<int64_t>(blockIdx.x) * (kGemmThreads / 64) + w : 0;
+    // With the tile-order map copy, an item's map rows and output rows come
+    // from registers loaded ahead: the wave's first tile before the order
+    // flag is read (the map workspace holds the order and the copy whether
+    // or not they were built, so the loads stay in bounds; their values are
+    // dropped when the flag says no order), each next tile under the current
+    // item's stages (persistent grid).
+    MapTileRegs<32, 64> nxt;
+    int32_t nrow = -1;
+    bool have_next = false;
+    if (order && pre.tmap && it0 < n_items) {
+        const int64_t tw0 = pers ? it0 / per_tile : xcd_block() * (kGemmThreads / 64) + w;
+        const int64_t f0 = tw0 * 32;
+        if (f0 < n_out) {
+            const int ln = threadIdx.x & 63;
+            map_tile_fetch<32, 64>(pre.tmap + f0 * K, K, ln, nxt);
+            nrow = ln < 32 && f0 + ln < n_out ? order[f0 + ln] : -1;
+            have_next = true;
+        }
+    }
+    if (order && *order_flag == 0) {  // map built without a tile order
+        order = nullptr;
+        have_next = false;
+    }
+    const bool prefetch = pers && order && pre.tmap;
 #pragma clang loop unroll(disable)
-    for (int64_t it = pers ? static_cast<int64_t>(blockIdx.x) * (kGemmThreads / 64) + w : 0; it < n_items;
-         it += it_step) {
+    for (int64_t it = it0; it < n_items; it += it_step) {
     // the lane index made opaque per item: otherwise every lane-derived
     // address of the body is hoisted out of the item loop and held live
     // across it (72 -> 161 registers, half the waves)
@@ -945,11 +1002,17 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     unsigned used = 0u;
     if (order && pre.tmap) {  // tile order with its map copy: map rows and output rows loaded together
-        if (lane < 32) {
-            const int64_t oo = o0 + lane;
-            orow[lane] = oo < n_out ? order[oo] : -1;
+        MapTileRegs<32, 64> cur;
+        int32_t orv;
+        if (have_next) {
+            cur = nxt;
+            orv = nrow;
+        } else {
+            map_tile_fetch<32, 64>(pre.tmap + o0 * K, K, lane, cur);
+            orv = lane < 32 && o0 + lane < n_out ? order[o0 + lane] : -1;
         }
-        used = load_map_tile_direct<32, 64>(pre.tmap + o0 * K, K, lane, mtile);
+        if (lane < 32) orow[lane] = orv;
+        used = map_tile_commit<32, 64>(cur, K, lane, mtile);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -984,6 +1047,13 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
     const int j0 = split_stage(used, nch, K, s, nsplit);
     const int j1 = split_stage(used, nch, K, s + 1, nsplit);
     O3DML_TRACE_AT(14, static_cast<uint64_t>(j1 - j0));
+    have_next = false;
+    if (prefetch && it + it_step < n_items) {  // in flight with stage 0's operands
+        const int64_t no0 = (it + it_step) / per_tile * 32;
+        map_tile_fetch<32, 64>(pre.tmap + no0 * K, K, lane, nxt);
+        nrow = lane < 32 && no0 + lane < n_out ? order[no0 + lane] : -1;
+        have_next = true;
+    }
     if (DEPTH == 2 && j0 < j1) {
         static_assert(DEPTH == 1 || (BUF && BREG && !SC), "two stages in flight: buffer path only");
         unsigned u = used;
