@@ -18,7 +18,15 @@ pts = torch.from_numpy(np.random.default_rng(lg).random((n, 3), dtype=np.float32
 rs = torch.tensor([0, n], dtype=torch.int64)
 r = 0.05 * (65536.0 / n) ** (1.0 / 3.0)
 nns = layers.FixedRadiusSearch()
-for _ in range(reps):
-    res = nns(pts, pts, r, rs, rs)
+res = nns(pts, pts, r, rs, rs)  # warm-up
 torch.cuda.synchronize(dev)
-print("pairs", int(res.neighbors_row_splits[-1]))
+times = []
+for _ in range(reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    res = nns(pts, pts, r, rs, rs)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    times.append(e0.elapsed_time(e1))
+ms = float(np.median(times))
+print("pairs", int(res.neighbors_row_splits[-1]), f"median {ms:.3f} ms/call, {n / ms / 1e3:.1f} Mpoints/s")
