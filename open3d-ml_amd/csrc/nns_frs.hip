@@ -763,19 +763,15 @@ __device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 10 bits -> every t
 // in Open3D bucket order (pts, float4), so the sorted payload is a position in
 // pts — the search then reads each query from the same lines its group
 // streams (large self searches); else the raw [M, 3] query array.
-// or_and[0] / [1]: OR of the keys and of their complements (the digits that
-// vary, for the device-planned radix passes; one atomic pair per wave).
 template <bool F4>
 __global__ void __launch_bounds__(256) group_query_keys_kernel(const float* __restrict__ queries, int64_t m,
                                                                float inv2, int n_batch,
                                                                const int64_t* __restrict__ qrs, int cell_bits,
-                                                               uint32_t* __restrict__ keys,
-                                                               unsigned long long* __restrict__ or_and) {
+                                                               uint32_t* __restrict__ keys) {
     __shared__ int64_t s_rs[kLdsSplits];
     const int64_t* rsp = stage_splits(s_rs, qrs, n_batch);
     const uint32_t mask = (1u << cell_bits) - 1u;
     constexpr int W = F4 ? 4 : 3;
-    uint64_t o1 = 0, o0 = 0;
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < m;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int b = batch_of(i, rsp, n_batch);
@@ -790,19 +786,7 @@ __global__ void __launch_bounds__(256) group_query_keys_kernel(const float* __re
         const uint32_t cy = static_cast<uint32_t>(static_cast<int32_t>(floorf(y * inv2))) & mask;
         const uint32_t cz = static_cast<uint32_t>(static_cast<int32_t>(floorf(z * inv2))) & mask;
         const uint32_t mort = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
-        const uint32_t key = (static_cast<uint32_t>(b) << (3 * cell_bits)) | mort;
-        keys[i] = key;
-        o1 |= key;
-        o0 |= ~static_cast<uint64_t>(key);
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        o1 |= static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(o1), d, 64));
-        o0 |= static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(o0), d, 64));
-    }
-    if ((threadIdx.x & 63) == 0 && (o1 | ~o0)) {
-        atomicOr(&or_and[0], static_cast<unsigned long long>(o1));
-        atomicOr(&or_and[1], static_cast<unsigned long long>(o0));
+        keys[i] = (static_cast<uint32_t>(b) << (3 * cell_bits)) | mort;
     }
 }
 
@@ -1189,7 +1173,7 @@ static void launch_group(int metric, bool ignore, bool with_dist, bool rel16, hi
 
 // Workspace kept between _count and _fill (same layout in both entries).
 struct FrsPlan {
-    int64_t* scalars;  // [0] overflow count, [4] / [5] OR of the query keys / of their complements
+    int64_t* scalars;  // [0] overflow count
     float4* pts;       // [2 (N + 1)] points in Open3D bucket order, a far sentinel, the class sub-lists p2
     float4* qpts;      // [M] queries in (batch, Morton) order
     uint32_t* keys;    // [M]
@@ -1209,7 +1193,7 @@ static int64_t dir_bins(int64_t n, int64_t nb) { return n / 32 + 2 * nb + 64; }
 
 static FrsPlan take_plan(Workspace& ws, int64_t n, int64_t m, int64_t nb, bool dist) {
     FrsPlan p;
-    p.scalars = ws.take<int64_t>(8);
+    p.scalars = ws.take<int64_t>(4);
     p.pts = ws.take<float4>(2 * (n + 1));  // + far sentinel + p2
     p.qpts = ws.take<float4>(m);
     p.keys = ws.take<uint32_t>(m);
@@ -1321,7 +1305,7 @@ static bool rel16_rows(int64_t n_batch, const int64_t* prs_host, int64_t n_queri
 }
 
 static size_t plan_bytes(int64_t n, int64_t m, int64_t nb) {
-    return ws_bytes<int64_t>(8) + ws_bytes<float4>(2 * (n + 1)) + ws_bytes<float4>(m) + 3 * ws_bytes<uint32_t>(m) +
+    return ws_bytes<int64_t>(4) + ws_bytes<float4>(2 * (n + 1)) + ws_bytes<float4>(m) + 3 * ws_bytes<uint32_t>(m) +
            2 * ws_bytes<uint32_t>(m) + 2 * ws_bytes<uint32_t>(m * kRowCap) +
            ws_bytes<uint32_t>(dir_bins(n, nb) * kDirWords);
 }
@@ -1352,7 +1336,7 @@ static void frs_count_impl(const float* points, int64_t n_points, const float* q
     Workspace ws(workspace, workspace_bytes);
     FrsPlan pl = take_plan(ws, n_points, n_queries, n_batch, with_distances != 0);
     if (n_queries == 0 || n_points == 0) {
-        fill_async(pl.scalars, 0, sizeof(int64_t) * 8, st);
+        fill_async(pl.scalars, 0, sizeof(int64_t) * 4, st);
         fill_async(neighbors_row_splits, 0, sizeof(int64_t) * (n_queries + 1), st);
         if (totals) frs_totals_kernel<<<1, 64, 0, st>>>(neighbors_row_splits, n_queries, pl.scalars, totals);
         return;
@@ -1372,7 +1356,7 @@ static void frs_count_impl(const float* points, int64_t n_points, const float* q
     bucket_classes_kernel<<<static_cast<unsigned>(std::min<int64_t>(ceil_div(n_points, 64 * 4), 1 << 16)), 256, 0,
                             st>>>(points, hash_table_index, pl.pts, n_points, hash_table_cell_splits,
                                   hash_table_splits, (int)n_batch, inv, 2.0f * radius, pl.dir, pl.dir_cap,
-                                  self_order ? pl.qorder : nullptr, self_order ? pl.keys : nullptr, pl.scalars, 8,
+                                  self_order ? pl.qorder : nullptr, self_order ? pl.keys : nullptr, pl.scalars, 4,
                                   neighbors_row_splits);
     O3DML_LAUNCH_CHECK();
     if (self_order) {
@@ -1384,23 +1368,18 @@ static void frs_count_impl(const float* points, int64_t n_points, const float* q
         const int cell_bits = std::max(1, std::min(8, (24 - batch_bits) / 3));
         // a self search keys the points in bucket order (positions in pl.pts,
         // the batch items' ranges unchanged); other queries key themselves
-        // OR / OR of complements of the keys (scalars [4], [5], zeroed by
-        // bucket_classes_kernel): only the radix passes whose digit varies run
-        // (cell coordinates need fewer bits than cell_bits at most radii)
-        unsigned long long* or_and = reinterpret_cast<unsigned long long*>(pl.scalars + 4);
         if (self_search && frs_self_pts_order())
             group_query_keys_kernel<true><<<stream_grid(n_queries, 256), 256, 0, st>>>(
                     reinterpret_cast<const float*>(pl.pts), n_queries, 2.0f * inv, (int)n_batch, queries_row_splits,
-                    cell_bits, pl.keys, or_and);
+                    cell_bits, pl.keys);
         else
             group_query_keys_kernel<false><<<stream_grid(n_queries, 256), 256, 0, st>>>(
-                    queries, n_queries, 2.0f * inv, (int)n_batch, queries_row_splits, cell_bits, pl.keys, or_and);
+                    queries, n_queries, 2.0f * inv, (int)n_batch, queries_row_splits, cell_bits, pl.keys);
         O3DML_LAUNCH_CHECK();
         {
             Workspace sws = ws;
             prim::radix_sort_pairs<uint32_t>(pl.keys, nullptr, pl.skeys, pl.qorder, n_queries,
-                                             batch_bits + 3 * cell_bits, sws, st, -1,
-                                             reinterpret_cast<const uint64_t*>(or_and));
+                                             batch_bits + 3 * cell_bits, sws, st);
         }
         if (frs_query_gather() && !self_pts) {
             gather_sorted_points_kernel<<<xcd_grid(n_queries, 256), 256, 0, st>>>(queries, pl.qorder, n_queries,

@@ -629,9 +629,13 @@ __global__ void grid_parent_kernel(const float* __restrict__ pos, int64_t n, uin
         o1 |= static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(o1), d, 64));
         o0 |= static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(o0), d, 64));
     }
-    if ((threadIdx.x & 63) == 0 && (o1 | ~o0)) {
-        atomicOr(&or_and[0], static_cast<unsigned long long>(o1));
-        atomicOr(&or_and[1], static_cast<unsigned long long>(o0));
+    // an atomic only for bits not yet recorded: same-address atomics
+    // serialise, and after the first waves nearly every wave adds nothing
+    if ((threadIdx.x & 63) == 0) {
+        const unsigned long long c1 = __hip_atomic_load(&or_and[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long c0 = __hip_atomic_load(&or_and[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (o1 & ~c1) atomicOr(&or_and[0], static_cast<unsigned long long>(o1));
+        if (o0 & ~c0) atomicOr(&or_and[1], static_cast<unsigned long long>(o0));
     }
 }
 
