@@ -514,6 +514,44 @@ def test_split_k_last_wave_finish_bitwise(cuda, tmp_path):
         assert torch.equal(a, b)
 
 
+def test_gemm_schedules_bitwise(cuda, tmp_path):
+    """The GEMM's work schedules change no bits: the persistent grid with the
+    next tile prefetched (O3DML_GEMM_PERSIST, default 1) against one wave per
+    item, and the tile-order map copy (O3DML_GEMM_TILE_MAP, default 1) against
+    reading the map through the order — every row's (offset, Cin) stages and
+    split partition are the same (child processes: the switches are read once).
+    A C4-sized room (88k voxels, cached tile-ordered map, so the persistent grid
+    engages), 32 -> 32 and 32 -> 64 forward, dIn and dW."""
+    import os
+    import subprocess
+    import sys
+    code = ("import sys, torch; sys.path[:0] = ['.', 'open3d-ml_amd']\n"
+            "import bench\n"
+            "from o3dml_amd import layers, sparse_conv as sc\n"
+            "pos = torch.from_numpy(bench.make_room(0)[0]).cuda()\n"
+            "res = []\n"
+            "for cout in (32, 64):\n"
+            "    torch.manual_seed(0)\n"
+            "    conv = layers.SparseConv(32, cout, [3, 3, 3], use_bias=False).cuda()\n"
+            "    x = torch.rand((pos.shape[0], 32), device='cuda', requires_grad=True)\n"
+            "    with sc.rulebook_cache():\n"
+            "        out = conv(x, pos, pos, 1.0)\n"
+            "        out.square().sum().backward()\n"
+            "    res += [out.detach().cpu(), x.grad.cpu(), conv.kernel.grad.cpu()]\n"
+            "torch.save(res, sys.argv[1])\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for i, extra in enumerate(({}, {"O3DML_GEMM_PERSIST": "0"}, {"O3DML_GEMM_TILE_MAP": "0"})):
+        path = str(tmp_path / f"sched_{i}.pt")
+        env = dict(os.environ, **extra)
+        subprocess.run([sys.executable, "-c", code, path], check=True, env=env, cwd=root, timeout=180)
+        outs.append(torch.load(path, weights_only=True))
+    for other in outs[1:]:
+        assert len(other) == len(outs[0]) == 6
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
+
+
 def test_transposed_conv_normalize(cuda):
     """layers.SparseConvTranspose(normalize=True): every input's contribution
     divided by its number of output neighbours (ops.sparse_conv_transpose's
