@@ -658,18 +658,35 @@ __device__ __forceinline__ GemmRsrc gemm_rsrc(const float* src, const float* Wt,
 #ifndef O3DML_GEMM_DIAG
 #define O3DML_GEMM_DIAG 0
 #endif
-template <bool BREG, bool SC = true, bool BUF = false, bool BS = false>
-__device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_t* mtile, int K, int k, int c0,
-                                          int lane, int64_t o, int i, int col0, const float* __restrict__ src,
-                                          const float* __restrict__ sscale, const float* __restrict__ pscale,
-                                          const float* __restrict__ Wt, int cin, int cout, bool live, GemmStage& st,
-                                          const GemmRsrc* rs = nullptr) {
-    const int sl = lane & 7;
-    // all LDS reads of the map first (a DMA in between would order after them)
+// A stage's map entries from the LDS tile: the 4 gathered rows of this lane
+// (rows 8 q + lane / 8) and its own row i; -1 on a dead stage.  The reads are
+// unconditional and then selected: `live` is wave-uniform, and a read under
+// it compiled to one branch per read, each read waited on alone (k stays a
+// valid offset on a dead stage, so the reads are in bounds).
+struct StageMap {
     int32_t mq[4];
+    int32_t mi;
+};
+__device__ __forceinline__ StageMap lds_map(const int32_t* mtile, int K, int k, int lane, int i, bool live) {
+    StageMap m;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) mq[q] = live ? mtile[(8 * q + (lane >> 3)) * K + k] : -1;
-    const int32_t mi = live ? mtile[i * K + k] : -1;
+    for (int q = 0; q < 4; ++q) m.mq[q] = mtile[(8 * q + (lane >> 3)) * K + k];
+    m.mi = mtile[i * K + k];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m.mq[q] = live ? m.mq[q] : -1;
+    m.mi = live ? m.mi : -1;
+    return m;
+}
+
+template <bool BREG, bool SC = true, bool BUF = false, bool BS = false>
+__device__ __forceinline__ void lds_issue_map(float* abuf, float* bbuf, const StageMap& sm, int k, int c0, int lane,
+                                              int64_t o, int i, int col0, const float* __restrict__ src,
+                                              const float* __restrict__ sscale, const float* __restrict__ pscale,
+                                              const float* __restrict__ Wt, int K, int cin, int cout, bool live,
+                                              GemmStage& st, const GemmRsrc* rs) {
+    const int sl = lane & 7;
+    const int32_t* mq = sm.mq;
+    const int32_t mi = sm.mi;
     if constexpr (BUF) {
         static_assert(BREG && !SC, "buffer addressing: filters in registers, no scales");
         const uint32_t row_bytes = static_cast<uint32_t>(cin) * 4u;
@@ -678,7 +695,9 @@ __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_
         for (int q = 0; q < 4; ++q) {
             const int r = 8 * q + (lane >> 3);
             const uint32_t cb = static_cast<uint32_t>(c0 + 4 * (sl ^ (r & 7))) * 4u;
-            const uint32_t off = mq[q] >= 0 ? static_cast<uint32_t>(mq[q]) * row_bytes + cb : kNoRow;
+            // 24-bit multiply (full rate): the host admits the buffer path only when
+            // every byte offset is < 2^31 with cin >= 32, so rows < 2^24
+            const uint32_t off = mq[q] >= 0 ? __umul24(static_cast<uint32_t>(mq[q]), row_bytes) + cb : kNoRow;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs->src, (lds_void_ptr)(abuf + 256 * q), 16, off, 0, 0, 0);
         }
 #else
@@ -704,7 +723,7 @@ __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_
                 st.bs[m] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs->wsp, soff + 16u * m, 0, 0));
         } else {
             const uint32_t boff = (live && col < cout)
-                                          ? (static_cast<uint32_t>(k * cout + col) * static_cast<uint32_t>(cin) +
+                                          ? (__umul24(static_cast<uint32_t>(k * cout + col), static_cast<uint32_t>(cin)) +
                                              static_cast<uint32_t>(c0 + 16 * (lane >> 5))) * 4u
                                           : kNoRow;
 #pragma unroll
@@ -757,6 +776,18 @@ __device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_
         st.s1 = st.s2 = 1.f;
     }
     st.v = valid ? 1.f : 0.f;
+}
+
+template <bool BREG, bool SC = true, bool BUF = false, bool BS = false>
+__device__ __forceinline__ void lds_issue(float* abuf, float* bbuf, const int32_t* mtile, int K, int k, int c0,
+                                          int lane, int64_t o, int i, int col0, const float* __restrict__ src,
+                                          const float* __restrict__ sscale, const float* __restrict__ pscale,
+                                          const float* __restrict__ Wt, int cin, int cout, bool live, GemmStage& st,
+                                          const GemmRsrc* rs = nullptr) {
+    // all LDS reads of the map first (a DMA in between would order after them)
+    const StageMap sm = lds_map(mtile, K, k, lane, i, live);
+    lds_issue_map<BREG, SC, BUF, BS>(abuf, bbuf, sm, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, K, cin, cout,
+                                     live, st, rs);
 }
 
 template <bool BREG>
@@ -1128,7 +1159,18 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
         for (int j = j0; j < j1; ++j) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage j in LDS, its row factors in nx
             if (j - j0 < 8) O3DML_TRACE(4 + j - j0);
+            const int kj = k, cj = c0;
+            c0 += 32;
+            if (c0 >= cin) {
+                c0 = 0;
+                u &= u - 1u;
+                k = u ? __builtin_ctz(u) : 0;
+            }
+            // the next stage's map entries are read beside this stage's rows
+            // (different LDS arrays), so one LDS wait covers both
+            const StageMap sm = lds_map(mtile, K, k, lane, i, j + 1 < j1);
             lds_read<BREG>(abuf, bbuf, i, h, cu);
+            __builtin_amdgcn_sched_barrier(0);  // both read groups issued before any waits on them
             if constexpr (BS) {
 #pragma unroll
                 for (int m = 0; m < 6; ++m) cu.bs[m] = nx.bs[m];
@@ -1139,16 +1181,9 @@ implicit_gemm_lds_kernel(const int32_t* __restrict__ map, const int32_t* __restr
             cu.s1 = nx.s1;
             cu.s2 = nx.s2;
             cu.v = nx.v;
-            const int kj = k, cj = c0;
-            c0 += 32;
-            if (c0 >= cin) {
-                c0 = 0;
-                u &= u - 1u;
-                k = u ? __builtin_ctz(u) : 0;
-            }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // buffer read out before the next DMA
-            lds_issue<BREG, SC, BUF, BS>(abuf, bbuf, mtile, K, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, cin,
-                                         cout, j + 1 < j1, nx, &rs);
+            lds_issue_map<BREG, SC, BUF, BS>(abuf, bbuf, sm, k, c0, lane, o, i, col0, src, sscale, pscale, Wt, K, cin,
+                                             cout, j + 1 < j1, nx, &rs);
             __builtin_amdgcn_sched_barrier(0);
             (void)kj;
             gemm_finish<PRE, SC>(cu, cj, h, lps, lpb);
