@@ -1486,6 +1486,10 @@ implicit_gemm_shared_kernel(const int32_t* __restrict__ map, const int32_t* __re
                                 (PRE ? pre_act(cu.a[rb][r], lps[cbb + r], lpb[cbb + r]) : cu.a[rb][r]) * cu.sc[rb];
             }
             mfma_stage_rb<NT, RB>(cu, acc);
+            // the MFMAs stay above the wait: left to the scheduler, all but one
+            // sank below it, so stage j+1's loads were waited on before stage j
+            // multiplied (no overlap of the gather latency with the MFMAs)
+            __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own share of stage j+1 landed
             __syncthreads();  // every share landed; stage j's buffer free
         }
