@@ -446,9 +446,11 @@ int o3dml_sparse_conv_kernel_index(const float* inp_positions, const float* quer
 /* Tile order of a built kernel map (and of its inverse with inverse = 1): the
  * map rows stably sorted by a hash of their offset mask, so that every
  * 32-row GEMM tile walks (almost) only offsets all its rows use; the GEMMs
- * use it from then on (a device flag in the map workspace).  Optional; pays
- * off when the map serves several convolutions or wide channels.  Results
- * are unchanged (absent offsets only ever added exact zeros). */
+ * use it from then on (a device flag in the map workspace).  It also writes
+ * the map rows in that order (padded to 128-row blocks), so a tile loads its
+ * rows as one contiguous block (map workspace size includes both).  Optional;
+ * pays off when the map serves several convolutions or wide channels.
+ * Results are unchanged (absent offsets only ever added exact zeros). */
 int o3dml_sparse_conv_tile_order(void* map_workspace, size_t map_workspace_bytes, int64_t n_out, int64_t n_in, int K,
                                  int inverse, void* stream);
 size_t o3dml_sparse_conv_lattice_workspace_size(int64_t n_in);
