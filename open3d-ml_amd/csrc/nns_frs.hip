@@ -651,7 +651,7 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
 // MODE 1 re-run.
 __device__ uint32_t g_frs_zero[4];
 #ifndef O3DML_COPY_ROWS
-#define O3DML_COPY_ROWS 32
+#define O3DML_COPY_ROWS 64  // all 64 rows of the wave: copy 218 -> 213 us vs 32 (16: 240; profiles/r05/frs_copy_rows_ab.txt)
 #endif
 constexpr int kCopyRows = O3DML_COPY_ROWS;  // rows whose loads are in flight together
 
