@@ -409,9 +409,16 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
             {
                 const uint32_t vb = static_cast<uint32_t>(bin_lanes<0>(-1, lb));
                 uint32_t s0 = 0, e0 = 0;
+                // the bin's bounds and its class directory entry in flight together
+                // (the directory exists for every bin when `sub`)
+                uint4 w0 = {}, w1 = {}, w2 = {}, w3 = {}, w4 = {}, w5 = {};
                 if (lane < 9) {
                     s0 = cs[vb];
                     e0 = cs[vb + 1];
+                    if (sub) {
+                        const uint4* dp = reinterpret_cast<const uint4*>(dir + static_cast<size_t>(vb) * kDirWords);
+                        w0 = dp[0], w1 = dp[1], w2 = dp[2], w3 = dp[3], w4 = dp[4], w5 = dp[5];
+                    }
                 }
                 // the bins are sorted: a repeat sits right after its first copy
                 const uint32_t prev = static_cast<uint32_t>(
@@ -419,8 +426,6 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                 const bool first = lane < 9 && e0 > s0 && prev != vb;
                 uint32_t st = s0, ln = e0 - s0;
                 if (first && sub) {
-                    const uint4* dp = reinterpret_cast<const uint4*>(dir + static_cast<size_t>(vb) * kDirWords);
-                    const uint4 w0 = dp[0], w1 = dp[1], w2 = dp[2], w3 = dp[3], w4 = dp[4], w5 = dp[5];
                     const uint32_t n0 = w0.x, n1 = w0.y, n2 = ln - n0 - n1;
                     auto f = [](uint32_t u) { return __uint_as_float(u); };
                     const bool r0 = n0 > 0 && box_box_dist<METRIC>(f(w1.x), f(w1.y), f(w1.z), f(w1.w), f(w2.x),
