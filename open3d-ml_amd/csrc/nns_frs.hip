@@ -893,11 +893,23 @@ __global__ void __launch_bounds__(256) O3DML_BC_ATTR bucket_classes_kernel(const
             // bucket = one contiguous 16-B-per-point stream for the search)
             auto load_chunk = [&](uint32_t c0, uint32_t len, bool store) {
                 rows = static_cast<int>((len + 63) >> 6);  // rows past it are skipped (uniform)
+                // every id and point load unconditional (clamped to entry c0,
+                // len >= 1) and issued before any store: under the per-row
+                // conditions each point gather waited for the previous row's
+                // pts store (vmcnt counts stores), four round trips in series
                 uint32_t id[E];
 #pragma unroll
                 for (int h = 0; h < E; ++h) {
                     const uint32_t i = lane + 64 * h;
-                    id[h] = h < rows && i < len ? hti[c0 + i] : 0u;
+                    id[h] = hti[c0 + (i < len ? i : 0u)];
+                }
+                float qx[E], qy[E], qz[E];
+#pragma unroll
+                for (int h = 0; h < E; ++h) {
+                    const float* q = points + 3 * static_cast<int64_t>(id[h]);
+                    qx[h] = q[0];
+                    qy[h] = q[1];
+                    qz[h] = q[2];
                 }
 #pragma unroll
                 for (int h = 0; h < E; ++h) {
@@ -907,8 +919,8 @@ __global__ void __launch_bounds__(256) O3DML_BC_ATTR bucket_classes_kernel(const
                         continue;
                     }
                     const uint32_t i = lane + 64 * h;
-                    const float* q = points + 3 * static_cast<int64_t>(id[h]);
-                    p[h] = i < len ? make_float4(q[0], q[1], q[2], __uint_as_float(id[h])) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    p[h] = i < len ? make_float4(qx[h], qy[h], qz[h], __uint_as_float(id[h]))
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
                     if (store && i < len) pts[c0 + i] = p[h];
                     // the 2r-voxel as the hash build computes it; the octant
                     // (query order only) from the fractional part
