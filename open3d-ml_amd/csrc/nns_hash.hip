@@ -194,10 +194,29 @@ __global__ void __launch_bounds__(256) hash_chunk_hist_kernel(const float* __res
     for (uint32_t i = threadIdx.x; i < tsize; i += 256) h[i] = 0;
     __syncthreads();
     const int64_t p0 = prs[b] + c * chunk, p1 = min(prs[b + 1], p0 + chunk);
-    for (int64_t i = p0 + threadIdx.x; i < p1; i += 256) {
-        const uint32_t bin = point_bin_k(points[3 * i], points[3 * i + 1], points[3 * i + 2], inv, tsize, k64);
-        bins[i] = bin;
-        atomicAdd(&h[bin], 1u);
+    // 8 points per thread loaded before any is binned and stored (clamped to
+    // p0 < p1, unconditional): one point per iteration had each load wait for
+    // the previous iteration's bins store (vmcnt counts stores)
+    constexpr int U = 8;
+    for (int64_t i0 = p0 + threadIdx.x; i0 < p1; i0 += 256 * U) {
+        float px[U], py[U], pz[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + 256 * u;
+            const int64_t j = i < p1 ? i : p0;
+            px[u] = points[3 * j];
+            py[u] = points[3 * j + 1];
+            pz[u] = points[3 * j + 2];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + 256 * u;
+            if (i < p1) {
+                const uint32_t bin = point_bin_k(px[u], py[u], pz[u], inv, tsize, k64);
+                bins[i] = bin;
+                atomicAdd(&h[bin], 1u);
+            }
+        }
     }
     __syncthreads();
     uint32_t* out = hist + hist_off_[b] + c * tsize;
@@ -327,11 +346,18 @@ __global__ void __launch_bounds__(NWV * 64) hash_chunk_scatter_kernel(int nb, co
     const int nbits = tsize > 1 ? 32 - __builtin_clz(tsize - 1) : 0;
     const uint64_t lt = lanemask_lt();
     uint32_t dig[kRows], loff[kRows];
+    // every row's bin loaded up front (clamped to p0 < pend, unconditional):
+    // a load under `valid` compiled to one wait per row
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+        const int64_t i = p0 + (static_cast<int64_t>(w) * kRows + r) * 64 + lane;
+        dig[r] = bins[i < pend ? i : p0];
+    }
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
         const int64_t i = p0 + (static_cast<int64_t>(w) * kRows + r) * 64 + lane;
         const bool valid = i < pend;
-        const uint32_t d = valid ? bins[i] : 0u;
+        const uint32_t d = valid ? dig[r] : 0u;
         dig[r] = d;
         uint64_t peers = __builtin_amdgcn_ballot_w64(valid);
         for (int bit = 0; bit < nbits; ++bit) {
