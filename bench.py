@@ -150,22 +150,28 @@ def load_traffic(kernel):
     return load_pmc(kernel).get("hbm_bytes_per_launch")
 
 
-SIMDS, CLOCK_GHZ = 1024, 2.4  # MI355X: 256 CUs x 4 SIMDs
+SIMDS, CLOCK_GHZ, XCDS = 1024, 2.4, 8  # MI355X: 256 CUs x 4 SIMDs in 8 XCDs; 2.4 GHz peak clock
+VALU_CYC = 4  # issue cost of a wave64 v_add_f32 / v_fma_f32 (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost')
 
 
 def issue_bound(kernel):
     """The bound the search kernel actually sits on: VALU issue.
-    From the committed PMC counters: wave64 VALU instructions x 2 cycles each
-    over SIMD-cycles of the measured launch duration, and the same for the one
-    scalar unit per CU (SALU, 1 cycle each).  None without a PMC summary."""
+    From the committed PMC counters: wave64 VALU instructions x 4 cycles each
+    (the guide's issue cost) over the SIMD-cycles of the measured launch, at the
+    clock the same pass ran at (GRBM_GUI_ACTIVE over the 8 XCDs / duration; the
+    2.4 GHz peak without it); SALU per CU, 1 cycle each.
+    None without a PMC summary."""
     c = load_pmc(kernel).get("counters_per_launch") or {}
     if not c.get("SQ_INSTS_VALU") or not c.get("dur_us_mean"):
         return None
-    cyc = c["dur_us_mean"] * 1e3 * CLOCK_GHZ
-    return {"valu_instr": int(c["SQ_INSTS_VALU"]), "salu_instr": int(c.get("SQ_INSTS_SALU", 0)),
-            "valu_issue_frac": round(2 * c["SQ_INSTS_VALU"] / (SIMDS * cyc), 4),
-            "salu_issue_frac": round(c.get("SQ_INSTS_SALU", 0) / (SIMDS / 4 * cyc), 4),
-            "source": "profiles/*/pmc_%s.json (PMC pass duration %.1f us)" % (kernel, c["dur_us_mean"])}
+    ghz = c["GRBM_GUI_ACTIVE"] / XCDS / (c["dur_us_mean"] * 1e3) if c.get("GRBM_GUI_ACTIVE") else CLOCK_GHZ
+    cyc = c["dur_us_mean"] * 1e3 * ghz
+    out = {"valu_instr": int(c["SQ_INSTS_VALU"]), "salu_instr": int(c.get("SQ_INSTS_SALU", 0)),
+           "clock_ghz": round(ghz, 3),
+           "valu_issue_frac": round(VALU_CYC * c["SQ_INSTS_VALU"] / (SIMDS * cyc), 4),
+           "salu_issue_frac": round(c.get("SQ_INSTS_SALU", 0) / (SIMDS / 4 * cyc), 4),
+           "source": "profiles/*/pmc_%s.json (PMC pass duration %.1f us)" % (kernel, c["dur_us_mean"])}
+    return out
 
 
 def cpu_baseline(scenes=64):
