@@ -223,6 +223,14 @@ __device__ __forceinline__ float box_box_dist(float alx, float aly, float alz, f
     }
 }
 
+// Rank of this lane among the kept lanes of km (mbcnt with a zero accumulator,
+// an inline constant: the list position nc is then added in the address
+// computation, one v_add_lshl, instead of moved into a VGPR for mbcnt).
+__device__ __forceinline__ int keep_slot(uint64_t km) {
+    return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(km >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(km), 0u)));
+}
+
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
@@ -261,6 +269,11 @@ __device__ __forceinline__ int bin_lanes(int v, const uint32_t* lb) {
 // Not with distances (those builds would spill VGPRs to scratch).
 #ifndef O3DML_FRS_WAVES
 #define O3DML_FRS_WAVES 8
+#endif
+// REL16 temp rows hold the low 16 bits of the absolute id (the copy recovers
+// the id from the item base), so the stream stores candidates unchanged
+#ifndef O3DML_FRS_ABS16
+#define O3DML_FRS_ABS16 1
 #endif
 #define O3DML_FRS_ATTR \
     __attribute__((amdgpu_num_sgpr(O3DML_FRS_NUM_SGPR), amdgpu_waves_per_eu(DIST ? 1 : O3DML_FRS_WAVES, 8)))
@@ -532,11 +545,9 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                             float4 c = cand[nc0 + 64 * u + lane];
                             const bool keep = box_dist<METRIC>(c, lx, ly, lz, hx, hy, hz) <= thr;
                             const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
-                            if constexpr (REL16) c.w = __uint_as_float(__float_as_uint(c.w) - gbase);
+                            if constexpr (REL16 && !O3DML_FRS_ABS16) c.w = __uint_as_float(__float_as_uint(c.w) - gbase);
                             if (keep)
-                                cand[__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(km >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(km),
-                                                                                         static_cast<uint32_t>(nc)))] = c;
+                                (cand + nc)[keep_slot(km)] = c;
                             nc += __popcll(km);
                         }
                     }
@@ -551,12 +562,10 @@ frs_group_kernel(const float4* __restrict__ pts, uint32_t n_pts, const uint32_t*
                     for (int u = 0; u < kStreamU; ++u) {
                         const bool keep = box_dist<METRIC>(c[u], lx, ly, lz, hx, hy, hz) <= thr;
                         const uint64_t km = __builtin_amdgcn_ballot_w64(keep);
-                        if constexpr (REL16)  // ids relative to the batch item, as the temp rows store them
+                        if constexpr (REL16 && !O3DML_FRS_ABS16)  // ids relative to the batch item
                             c[u].w = __uint_as_float(__float_as_uint(c[u].w) - gbase);
                         if (keep)
-                            cand[__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(km >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(km),
-                                                                                     static_cast<uint32_t>(nc)))] = c[u];
+                            (cand + nc)[keep_slot(km)] = c[u];
                         nc += __popcll(km);
                     }
                 }
@@ -713,7 +722,10 @@ __global__ void __launch_bounds__(256) group_rows_copy_kernel(int64_t m, const u
                         static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(o), k + u)));
                 const uint32_t pbu = REL16 ? static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(pb), k + u)) : 0u;
                 if (lane < nu) {
-                    idx[ou + lane] = static_cast<TIdx>(v[u] + pbu);
+                    // ABS16: the low 16 bits of the id; the id is pbu + ((v - pbu) mod 2^16),
+                    // as every id of the item lies in [pbu, pbu + 2^16)
+                    idx[ou + lane] = static_cast<TIdx>(O3DML_FRS_ABS16 && REL16 ? pbu + ((v[u] - pbu) & 0xffffu)
+                                                                                 : v[u] + pbu);
                     if constexpr (DIST) dist[ou + lane] = dv[u];
                 }
             }
@@ -742,7 +754,9 @@ __global__ void __launch_bounds__(256) group_rows_dense_kernel(int64_t m, const 
         int32_t* row = out + t * width;
         for (int64_t j = lane; j < width; j += 64) {
             if (j < n)
-                row[j] = static_cast<int32_t>(REL16 ? t16[t * kRowCap + j] + pb : tidx[t * kRowCap + j]);
+                row[j] = static_cast<int32_t>(REL16 ? (O3DML_FRS_ABS16 ? pb + ((t16[t * kRowCap + j] - pb) & 0xffffu)
+                                                                       : t16[t * kRowCap + j] + pb)
+                                                    : tidx[t * kRowCap + j]);
             else if (j >= n_all)
                 row[j] = pad;
         }
