@@ -77,14 +77,21 @@ __global__ void build_kernel_map_kernel(const int32_t* __restrict__ nbr, const i
     }
 }
 
+// inv [n_in, K]: an entry i >= n_in (a map built for other sizes than the
+// caller states, e.g. a transpose_map partner) is dropped and flagged as
+// build_map does (status bit 8), never written past the inverse map
 __global__ void build_inverse_map_kernel(const int32_t* __restrict__ map, const float* __restrict__ pscale,
-                                         int64_t n_out, int K, int32_t* __restrict__ inv,
+                                         int64_t n_out, int K, int64_t n_in, int32_t* __restrict__ inv,
                                          float* __restrict__ ipscale, int* __restrict__ dup) {
     const int64_t total = n_out * K;
     for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int32_t i = map[e];
         if (i < 0) continue;
+        if (i >= n_in) {
+            atomicOr(dup, 8);
+            continue;
+        }
         const int64_t o = e / K;
         const int k = static_cast<int>(e - o * K);
         const int32_t prev = atomicCAS(inv + static_cast<int64_t>(i) * K + k, -1, static_cast<int32_t>(o));
@@ -2727,7 +2734,7 @@ O3DML_API int o3dml_sparse_conv_build_map(const int32_t* neighbors_index, const 
         fill_async(inv, 0xff, sizeof(int32_t) * n_in * K, st);
         if (n_out > 0) {
             build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(
-                    map, neighbors_importance ? pscale : nullptr, n_out, K, inv,
+                    map, neighbors_importance ? pscale : nullptr, n_out, K, n_in, inv,
                     neighbors_importance ? ipscale : nullptr, status);
             O3DML_LAUNCH_CHECK();
         }
@@ -2814,8 +2821,8 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     }
     if (want_inverse) {
         fill_async(inv, 0xff, sizeof(int32_t) * n_in * K, st);
-        build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, nullptr, n_out, K, inv, nullptr,
-                                                                            status);
+        build_inverse_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(map, nullptr, n_out, K, n_in, inv,
+                                                                            nullptr, status);
         O3DML_LAUNCH_CHECK();
     }
     if (defer_status) return 0;  // status stays on the device (o3dml_sparse_conv_map_status_offset)
@@ -2855,7 +2862,7 @@ O3DML_API int o3dml_sparse_conv_transpose_map(const void* conv_workspace, size_t
     fill_async(status + 1, 0, 3 * sizeof(int), st);  // [2], [3]: no tile orders yet
     if (n_fine > 0) fill_async(map, 0xff, sizeof(int32_t) * n_fine * K, st);
     if (n_coarse > 0 && n_fine > 0) {
-        build_inverse_map_kernel<<<stream_grid(n_coarse * K, 256), 256, 0, st>>>(cmap, nullptr, n_coarse, K, map,
+        build_inverse_map_kernel<<<stream_grid(n_coarse * K, 256), 256, 0, st>>>(cmap, nullptr, n_coarse, K, n_fine, map,
                                                                                 nullptr, status);
         O3DML_LAUNCH_CHECK();
     }

@@ -299,6 +299,7 @@ class _RulebookScope:
         self.maps = {}
         self.defer = defer_checks
         self.pending = []
+        self.derived = 0  # transpose maps derived from their convolution partner (_transpose_of_cached)
 
     def check(self):
         """One host round trip for every deferred lattice check of the scope:
@@ -444,6 +445,10 @@ def _transpose_of_cached(scope, key, cache_key, ks, n_in, n_out, want_grad, dev)
     mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_fine, n_coarse, K), dev)
     _lib.call("o3dml_sparse_conv_transpose_map", ptr(cmws), cmws.numel(), n_coarse, n_fine, K, int(bool(want_grad)),
               ptr(mws), mws.numel(), stream_handle(dev))
+    if K > 8:  # a scope map, as conv_lattice's own-built ones: GEMM tiles sorted by offset mask once
+        _lib.call("o3dml_sparse_conv_tile_order", ptr(mws), mws.numel(), n_fine, n_coarse, K, int(bool(want_grad)),
+                  stream_handle(dev))
+    scope.derived += 1
     if scope.defer:
         off = lib.o3dml_sparse_conv_map_status_offset(n_fine, n_coarse, K)
         scope.pending.append(mws[off:off + 4].view(torch.int32))

@@ -40,25 +40,49 @@ def ml3d_available():
         return False
 
 
+def target_of(fullname):
+    """The ml3d module an ``open3d.ml[.torch].<name>[.<rest>]`` name stands
+    for (whole subtrees: ``open3d.ml.torch.models.randlanet`` is
+    ``ml3d.torch.models.randlanet``), or None."""
+    for alias, target in ALIASES.items():
+        if fullname == alias or fullname.startswith(alias + "."):
+            return target + fullname[len(alias):]
+    return None
+
+
 class _Ml3dAlias(importlib.abc.MetaPathFinder, importlib.abc.Loader):
-    """Resolves ``open3d.ml[.torch].<name>`` to the ``ml3d`` module itself
-    (the same module object: no second copy, registries shared)."""
+    """Resolves ``open3d.ml[.torch].<name>`` and every module below it to the
+    ``ml3d`` module itself (the same module object: no second copy, class
+    registries shared).  The module keeps its own ``__spec__`` (importlib
+    sets the alias spec on it; exec_module puts the original back)."""
 
     def find_spec(self, fullname, path=None, target=None):
-        if fullname not in ALIASES or not ml3d_available():
+        if not fullname.startswith("open3d.ml.") or target_of(fullname) is None or not ml3d_available():
             return None
         return importlib.util.spec_from_loader(fullname, self)
 
+    def __init__(self):
+        self._orig = {}  # id(module) -> its own (__spec__, __loader__)
+
     def create_module(self, spec):
-        return importlib.import_module(ALIASES[spec.name])
+        module = importlib.import_module(target_of(spec.name))
+        self._orig[id(module)] = (module.__spec__, getattr(module, "__loader__", None))
+        return module
 
     def exec_module(self, module):
-        pass  # already executed as ml3d.*
+        # already executed as ml3d.*; importlib has just set the alias spec
+        # (no origin, no search locations) on it: put its own back
+        orig = self._orig.pop(id(module), None)
+        if orig is not None:
+            module.__spec__, module.__loader__ = orig
 
 
 def install():
+    # ahead of the path finders: a submodule of an aliased package (whose
+    # __path__ is the ml3d directory) would otherwise be loaded a second time
+    # under the open3d name
     if not any(isinstance(f, _Ml3dAlias) for f in sys.meta_path):
-        sys.meta_path.append(_Ml3dAlias())
+        sys.meta_path.insert(0, _Ml3dAlias())
 
 
 def module_getattr(namespace, name):

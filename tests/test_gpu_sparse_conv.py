@@ -625,20 +625,24 @@ def test_out_of_range_neighbour_index_and_map_entry(cuda):
     assert not torch.equal(outs[0][11], outs[2][11]) and torch.equal(outs[0][12:], outs[2][12:])
 
 
+@pytest.mark.parametrize("ks", [2, 3])
 @pytest.mark.parametrize("want_grad", [False, True])
-def test_transpose_map_derived_from_conv_map(cuda, want_grad):
+def test_transpose_map_derived_from_conv_map(cuda, want_grad, ks):
     """In a rulebook_cache scope a SparseConvTranspose whose SparseConv
     partner (positions swapped, same kernel / offset) is cached takes the
     partner's map inverted (o3dml_sparse_conv_transpose_map) instead of
     building its own: forward (and, with gradients, dIn / dW) bit-identical
-    to the transpose built on its own."""
+    to the transpose built on its own.  The derivation is counted by the
+    scope (scope.derived), so a silent fallback to an own-built map fails;
+    3^3 also runs the tile order on the derived map."""
     from o3dml_amd import layers, ops, sparse_conv as sc
     pos = _voxels(6000, 30, 41)
     p = torch.from_numpy(pos).to(cuda)
     outs = ops.calculate_grid(p)
     torch.manual_seed(0)
-    conv = layers.SparseConv(16, 32, [2, 2, 2], use_bias=False, offset=torch.full((3,), -0.5)).to(cuda)
-    deconv = layers.SparseConvTranspose(32, 16, [2, 2, 2], use_bias=False, offset=torch.full((3,), -0.5)).to(cuda)
+    off = torch.full((3,), -0.5) if ks == 2 else torch.zeros(3)
+    conv = layers.SparseConv(16, 32, [ks] * 3, use_bias=False, offset=off).to(cuda)
+    deconv = layers.SparseConvTranspose(32, 16, [ks] * 3, use_bias=False, offset=off).to(cuda)
     x = torch.randn(len(pos), 16, device=cuda)
     y = torch.randn(len(outs), 32, device=cuda)
     g = torch.randn(len(pos), 16, device=cuda)
@@ -648,16 +652,16 @@ def test_transpose_map_derived_from_conv_map(cuda, want_grad):
         with torch.set_grad_enabled(want_grad), sc.rulebook_cache() as scope:
             if derive:
                 conv(x, p, outs, 1.0)
-            n_maps = len(scope.maps)
+            n_maps, n_derived = len(scope.maps), scope.derived
             out = deconv(yy, outs, p, 1.0)
-            derived = len(scope.maps) - n_maps == 1 and derive
+            derived = len(scope.maps) - n_maps == 1 and scope.derived - n_derived == 1
             if want_grad:
                 out.backward(g)
         return out.detach(), (yy.grad if want_grad else None), derived
 
-    own, gown, _ = run(False)
+    own, gown, own_derived = run(False)
     der, gder, derived = run(True)
-    assert derived
+    assert derived and not own_derived
     assert torch.equal(own, der)
     if want_grad:
         assert torch.equal(gown, gder)

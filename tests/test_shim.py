@@ -47,6 +47,7 @@ _FAKE_ML3D = {
         "    bound = (knn_search, FixedRadiusSearch, subsample, o3c.nns.NearestNeighborSearch)\n"
         "    def __init__(self, **kw):\n"
         "        self.cfg = kw\n"),
+    "ml3d/torch/models/extra.py": "from . import RandLANet\nclass Extra(RandLANet):\n    pass\n",
     "ml3d/torch/pipelines/__init__.py": "class SemanticSegmentation:\n    pass\n",
     "ml3d/torch/dataloaders/__init__.py": "class TorchDataloader:\n    pass\n",
     "ml3d/torch/modules/__init__.py": "class SemSegLoss:\n    pass\n",
@@ -77,6 +78,16 @@ assert open3d.ml.datasets.SemanticKITTI is ml3d.datasets.SemanticKITTI
 assert open3d.ml.utils.MODEL == {} and open3d.ml.configs
 assert ml3d.ops.knn_search is o3dml_amd.ops.knn_search and ml3d.layers.SparseConv is o3dml_amd.layers.SparseConv
 assert "ml3d.vis" not in sys.modules
+# a submodule below an aliased package is the ml3d module itself (one copy,
+# one class object), and aliased modules keep their own spec
+import open3d.ml.torch.models.extra as E
+from open3d.ml.torch.models.extra import Extra
+assert E is sys.modules["ml3d.torch.models.extra"] and Extra is E.Extra
+assert issubclass(Extra, ml3d.models.RandLANet)
+for name in ("ml3d.torch.models", "ml3d.torch.pipelines", "ml3d.torch.models.extra"):
+    sp = sys.modules[name].__spec__
+    assert sp.name == name and sp.origin and sp.origin.endswith(".py"), (name, sp)
+assert list(sys.modules["ml3d.torch.models"].__spec__.submodule_search_locations)
 print("NAMESPACE OK")
 """
 
