@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--scenes", type=int, default=64, help="C1-shaped scenes per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5)
+    ap.add_argument("--op-reps", type=int, default=20, help="per-op roofline reps: kNN, grid subsample, voxelize "
+                    "(0: skip)")
     ap.add_argument("--randla-frames", type=int, default=6, help="RandLA-Net frames timed (0: skip)")
     ap.add_argument("--kpconv-steps", type=int, default=10, help="C3 KPFCNN training steps timed (0: skip)")
     ap.add_argument("--pointpillars-steps", type=int, default=5,
@@ -151,13 +153,21 @@ def load_traffic(kernel):
 
 
 SIMDS, CLOCK_GHZ, XCDS = 1024, 2.4, 8  # MI355X: 256 CUs x 4 SIMDs in 8 XCDs; 2.4 GHz peak clock
-VALU_CYC = 4  # issue cost of a wave64 v_add_f32 / v_fma_f32 (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost')
+# Measured SIMD issue cost per wave64 VALU instruction at 8 waves per SIMD
+# (tools/valu_rate.hip on the box, profiles/r06/valu_rate.jsonl): the search's
+# own candidate-test mix (distance, compare into VCC, group mask, mbcnt rank,
+# clamped row address, running bcnt count: 17 VALU) issues at 2.62 cycles per
+# instruction; v_add_f32 / v_fma_f32 / v_and_b32 alone 2.3, while VOPC into an
+# SGPR, v_mbcnt, v_bcnt, v_min_u32, v_lshl_or, v_cndmask and DPP moves are
+# ~4.1 each.  (The guide's 4 is ONE wave's issue rate, not the SIMD's.)
+VALU_CYC = 2.62
+VALU_CYC_SOURCE = "profiles/r06/valu_rate.jsonl (FRS candidate-test mix, 8 waves/SIMD)"
 
 
 def issue_bound(kernel):
-    """The bound the search kernel actually sits on: VALU issue.
-    From the committed PMC counters: wave64 VALU instructions x 4 cycles each
-    (the guide's issue cost) over the SIMD-cycles of the measured launch, at the
+    """How close the search kernel is to its VALU issue ceiling.
+    From the committed PMC counters: wave64 VALU instructions x VALU_CYC cycles
+    each (measured, see above) over the SIMD-cycles of the measured launch, at the
     clock the same pass ran at (GRBM_GUI_ACTIVE over the 8 XCDs / duration; the
     2.4 GHz peak without it); SALU per CU, 1 cycle each.
     None without a PMC summary."""
@@ -168,6 +178,7 @@ def issue_bound(kernel):
     cyc = c["dur_us_mean"] * 1e3 * ghz
     out = {"valu_instr": int(c["SQ_INSTS_VALU"]), "salu_instr": int(c.get("SQ_INSTS_SALU", 0)),
            "clock_ghz": round(ghz, 3),
+           "valu_cyc": VALU_CYC, "valu_cyc_source": VALU_CYC_SOURCE,
            "valu_issue_frac": round(VALU_CYC * c["SQ_INSTS_VALU"] / (SIMDS * cyc), 4),
            "salu_issue_frac": round(c.get("SQ_INSTS_SALU", 0) / (SIMDS / 4 * cyc), 4),
            "source": "profiles/*/pmc_%s.json (PMC pass duration %.1f us)" % (kernel, c["dur_us_mean"])}
@@ -296,6 +307,86 @@ def randla_frames(dev, frames, cpu=False, world=1, rank=0):
         out["cpu_baseline"] = randla_cpu_baseline(model, make_scan(0)[0], patches[0] / len(scans))
         out["cpu_baseline"]["gpu_speedup"] = round(out["cpu_baseline"]["value"] / (dt / len(scans)), 1)
     return out
+
+
+def op_rooflines(dev, reps=20):
+    """SURVEY §8(d) per-op rooflines for the ops that dominate C2 / C4 besides
+    the FRS search: device time from the library's HIP events (recorded on the
+    launch stream around the kernel or phase, o3dml_timing_*), algorithmic
+    bytes by §8(d)'s formulas, HBM peak; issue counts from the committed PMC
+    summary where one exists (profiles/*/pmc_<kernel>.json).
+      knn: the k = 16 self-kNN of one RandLA patch (its 5 levels in one
+        batched call, randlanet.py:218-229 <- dataprocessing.py:87-103), the
+        search kernel alone; bytes 24 + 4k per query (query xyz, point xyz,
+        row split; int32 ids).
+      grid_subsample: contrib.subsample of the C2 scan (120,000 pts, dl 0.06;
+        randlanet.py:133-139): count + fill phases; bytes per point 12 x 2 +
+        8 + 8, per output point 12 + 8.
+      voxelize: ops.voxelize of the C4 room at vs = 1 (SparseConvUnet's
+        InputLayer, sparseconvnet.py:296-331): count + fill; same formula."""
+    from o3dml_amd import _lib, ops
+    lib = _lib.load()
+
+    def timed(fn, names):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize(dev)
+        lib.o3dml_timing_reset()
+        lib.o3dml_timing_enable(1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        t = _lib.kernel_times(names)
+        lib.o3dml_timing_enable(0)
+        return {k: (ms / c if c else 0.0) for k, (ms, c) in t.items()}, e0.elapsed_time(e1) / reps
+
+    def entry(kernel_ms, alg_bytes, call_ms, pmc=None, **extra):
+        gbs = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+        out = {"bound": "hbm", "kernel_ms": round(kernel_ms, 5), "alg_bytes": int(alg_bytes),
+               "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
+               "call_ms": round(call_ms, 5)}
+        if pmc:
+            out["issue"] = issue_bound(pmc)
+            out["traffic"] = load_traffic(pmc)
+        out.update(extra)
+        return out
+
+    res = {}
+    scan = torch.from_numpy(make_scan(0)[0]).to(dev)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    center = scan[torch.randint(0, scan.shape[0], (1,), generator=g)]
+    d = ((scan - center) ** 2).sum(1)
+    lvl = [scan[d.topk(45056, largest=False).indices]]
+    for _ in range(4):
+        prev = lvl[-1]
+        lvl.append(prev[torch.randperm(prev.shape[0], generator=g)[: prev.shape[0] // 4].to(dev)])
+    cat = torch.cat(lvl).contiguous()
+    krs = torch.tensor(np.cumsum([0] + [x.shape[0] for x in lvl]), dtype=torch.int64)
+    m, k = cat.shape[0], 16
+    t, call = timed(lambda: ops.knn_search(cat, cat, k, krs, krs), ("knn_search",))
+    res["knn"] = entry(t["knn_search"], m * (24 + 4 * k), call, pmc="knn_group",
+                       queries=m, k=k, kernel="knn_group_kernel<16, 8, L2>",
+                       note="call_ms: the whole knn_search call (grid build, search, row splits, compaction)")
+    n = scan.shape[0]
+    sub = ops.grid_subsample(scan, [n], 0.06)
+    s_n = int(sub[0].shape[0])
+    t, call = timed(lambda: ops.grid_subsample(scan, [n], 0.06), ("grid_subsample_count", "grid_subsample_fill"))
+    res["grid_subsample"] = entry(t["grid_subsample_count"] + t["grid_subsample_fill"], n * 40 + s_n * 20, call,
+                                  points=n, out_points=s_n, dl=0.06,
+                                  note="kernel_ms: count + fill phases (keys, segment sort, caps, scan, fill)")
+    pos = torch.from_numpy(make_room(0)[0]).to(dev)
+    vs = torch.ones(3)
+    lo, hi = torch.zeros(3), torch.full((3,), 40960.0)
+    vrs = torch.tensor([0, pos.shape[0]], dtype=torch.int64)
+    nv = int(ops.voxelize(pos, vrs, vs, lo, hi).voxel_coords.shape[0])
+    t, call = timed(lambda: ops.voxelize(pos, vrs, vs, lo, hi), ("voxelize_count", "voxelize_fill"))
+    res["voxelize"] = entry(t["voxelize_count"] + t["voxelize_fill"], pos.shape[0] * 40 + nv * 20, call,
+                            points=int(pos.shape[0]), voxels=nv,
+                            note="kernel_ms: count + fill phases; C4 InputLayer shape")
+    return res
 
 
 def randla_cpu_baseline(model, scan, patches_per_frame, budget_s=30.0):
@@ -809,6 +900,11 @@ def run(args):
             out["kpconv"] = kpconv_bench(dev, args.kpconv_steps)
         if world == 1 and args.randla_frames > 0:
             out["randlanet"] = randla_frames(dev, args.randla_frames, cpu=not args.no_cpu_baseline)
+        if world == 1 and args.op_reps > 0:
+            ops_rl = op_rooflines(dev, args.op_reps)
+            out["ops_roofline"] = ops_rl
+            if "randlanet" in out:
+                out["randlanet"]["roofline"] = dict(ops_rl["knn"], op="knn (C2 dominant kernel)")
         if rl_multi is not None:
             out["randlanet"] = rl_multi
         print(json.dumps(out), flush=True)

@@ -139,52 +139,136 @@ __global__ void __launch_bounds__(256) knn_grid_kernel(const float4* __restrict_
 
 
 // ---------------------------------------------------------------------------
-// k <= 16: G = 8 lanes per query (8 queries per wave).  A lane-per-query walk
-// leaves the chip nearly idle on the sizes RandLA-Net searches (60 k queries
-// = < 1 wave per SIMD, each lane a chain of dependent loads); here the group
-// walks the same rings together, lanes taking every G-th point of each cell
-// into their own sorted top-K.  After each ring the group merges its lists
-// with a butterfly (xor 1, 2, 4): per round a lane takes the K smallest of its
-// list and its partner's as min(a[i], b[K-1-i]) — a bitonic sequence — and
-// sorts it with a register bitonic network; after the last round every lane
-// holds the group's exact top-K, whose k-th entry both prunes the next ring
-// and decides termination.  Lane 0 keeps the merged list, the others restart
-// empty, so no entry is counted twice.  Order: (distance, index) ascending.
+// k <= 16: G lanes per query (64 / G queries per wave; G = 8 by default,
+// O3DML_KNN_G = 4 / 8 / 16).  A lane-per-query walk leaves the chip nearly
+// idle on the sizes RandLA-Net searches (60 k queries = < 1 wave per SIMD,
+// each lane a chain of dependent loads); here the group walks the same rings
+// together, lanes taking every G-th point of each cell into their own sorted
+// top-K.  After each ring the group merges its lists with a butterfly: per
+// round a lane takes the K smallest of its list and its partner's as
+// min(a[i], b[K-1-i]) — a bitonic sequence — and sorts it with a register
+// bitonic network; after the last round every lane holds the group's exact
+// top-K, whose k-th entry both prunes the next ring and decides termination.
+// Lane 0 keeps the merged list, the others restart empty, so no entry is
+// counted twice.  Order: (distance, index) ascending.
+//
+// Keys as doubles (O3DML_KNN_F64, default): the 64-bit key (bits(d) << 32 |
+// index) of a distance d >= +0 whose bits are clamped to <= 0x7FC00000 (every
+// NaN becomes the canonical one, which still sorts after +inf and the empty
+// entry) is, read as an IEEE double, a finite non-negative double whose order
+// is the key's unsigned order (exponent field <= 0x7FC, never 0x7FF; f64
+// denormals are kept: the kernel's f64 denormal mode is IEEE).  So a
+// compare-exchange is v_min_f64 + v_max_f64 — no VOPC into an SGPR mask (a
+// 4-cycle issue, then a hazard nop before the v_cndmask pair that reads it) —
+// and an insertion is branch-free in the list:
+//   new[0] = min(key, old[0]),  new[r] = min(max(key, old[r-1]), old[r]),
+// every position from the old list at once (no carried chain).  The butterfly
+// partners are DPP lane moves (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror,
+// row_mirror: partner i^1, i^2, 7-i, 15-i — each pairs the two halves of the
+// next larger group, which is all a butterfly needs) instead of ds_bpermute.
 // ---------------------------------------------------------------------------
-constexpr int kKnnG = 8;
+#ifndef O3DML_KNN_F64
+#define O3DML_KNN_F64 1
+#endif
+
+struct KnnKey {
+#if O3DML_KNN_F64
+    double v;
+    __device__ __forceinline__ static KnnKey from_bits(uint64_t b) { return {__builtin_bit_cast(double, b)}; }
+    __device__ __forceinline__ uint64_t bits() const { return __builtin_bit_cast(uint64_t, v); }
+    // plain v_min_f64 / v_max_f64: fmin / fmax would first canonicalise both
+    // operands (one v_max_f64 x, x each: the signalling-NaN rule), and these
+    // keys are never NaN
+    __device__ __forceinline__ friend KnnKey kmin(KnnKey a, KnnKey b) {
+        double r;
+        asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a.v), "v"(b.v));
+        return {r};
+    }
+    __device__ __forceinline__ friend KnnKey kmax(KnnKey a, KnnKey b) {
+        double r;
+        asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a.v), "v"(b.v));
+        return {r};
+    }
+    __device__ __forceinline__ friend bool operator<(KnnKey a, KnnKey b) { return a.v < b.v; }
+#else
+    uint64_t v;
+    __device__ __forceinline__ static KnnKey from_bits(uint64_t b) { return {b}; }
+    __device__ __forceinline__ uint64_t bits() const { return v; }
+    __device__ __forceinline__ friend KnnKey kmin(KnnKey a, KnnKey b) { return {b.v < a.v ? b.v : a.v}; }
+    __device__ __forceinline__ friend KnnKey kmax(KnnKey a, KnnKey b) { return {b.v < a.v ? a.v : b.v}; }
+    __device__ __forceinline__ friend bool operator<(KnnKey a, KnnKey b) { return a.v < b.v; }
+#endif
+};
+
+__device__ __forceinline__ KnnKey knn_key_g(float d, uint32_t id) {
+    const uint32_t db = min(__float_as_uint(d), 0x7fc00000u);  // every NaN -> the canonical one (see above)
+    return KnnKey::from_bits((static_cast<uint64_t>(db) << 32) | id);
+}
+
+// partner of round `round` of the butterfly (see above), as a DPP control
+template <int ROUND>
+__device__ __forceinline__ uint32_t dpp_partner(uint32_t v) {
+    constexpr int ctrl = ROUND == 0 ? 0xB1 : ROUND == 1 ? 0x4E : ROUND == 2 ? 0x141 : 0x140;
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), ctrl, 0xF, 0xF, false));
+}
+
+template <int ROUND>
+__device__ __forceinline__ KnnKey dpp_partner_key(KnnKey k) {
+    const uint64_t b = k.bits();
+    const uint32_t lo = dpp_partner<ROUND>(static_cast<uint32_t>(b));
+    const uint32_t hi = dpp_partner<ROUND>(static_cast<uint32_t>(b >> 32));
+    return KnnKey::from_bits((static_cast<uint64_t>(hi) << 32) | lo);
+}
 
 template <int K>
-__device__ __forceinline__ void cas_key(uint64_t (&a)[K], int i, int j) {
-    const uint64_t lo = a[j] < a[i] ? a[j] : a[i];
-    const uint64_t hi = a[j] < a[i] ? a[i] : a[j];
+__device__ __forceinline__ void cas_kkey(KnnKey (&a)[K], int i, int j) {
+    const KnnKey lo = kmin(a[i], a[j]), hi = kmax(a[i], a[j]);
     a[i] = lo;
     a[j] = hi;
 }
 
-template <int K>
-__device__ __forceinline__ void group_merge(uint64_t (&a)[K]) {
+template <int K, int G, int ROUND = 0>
+__device__ __forceinline__ void group_merge_g(KnnKey (&a)[K]) {
+    if constexpr ((1 << ROUND) < G) {
+        // a[i] = min(a[i], partner[K-1-i]): the K smallest of both lists,
+        // bitonic; in place, pair (i, K-1-i) at a time (both partner entries
+        // fetched before either is overwritten)
 #pragma unroll
-    for (int mask = 1; mask < kKnnG; mask <<= 1) {
-        uint64_t o[K];
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-            const uint32_t lo = __shfl_xor(static_cast<uint32_t>(a[i]), mask, 64);
-            const uint32_t hi = __shfl_xor(static_cast<uint32_t>(a[i] >> 32), mask, 64);
-            o[i] = (static_cast<uint64_t>(hi) << 32) | lo;
+        for (int i = 0; i < K / 2; ++i) {
+            const KnnKey p_hi = dpp_partner_key<ROUND>(a[K - 1 - i]);
+            const KnnKey p_lo = dpp_partner_key<ROUND>(a[i]);
+            a[i] = kmin(a[i], p_hi);
+            a[K - 1 - i] = kmin(a[K - 1 - i], p_lo);
         }
-#pragma unroll
-        for (int i = 0; i < K; ++i) a[i] = o[K - 1 - i] < a[i] ? o[K - 1 - i] : a[i];
+        if constexpr (K == 1) a[0] = kmin(a[0], dpp_partner_key<ROUND>(a[0]));
 #pragma unroll
         for (int st = K / 2; st >= 1; st >>= 1) {
 #pragma unroll
             for (int i = 0; i < K; ++i)
-                if ((i & st) == 0) cas_key<K>(a, i, i + st);
+                if ((i & st) == 0) cas_kkey<K>(a, i, i + st);
         }
+        group_merge_g<K, G, ROUND + 1>(a);
     }
 }
 
-template <int K, int METRIC, bool IGNORE>
-__global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict__ sorted,
+template <int G, int ROUND = 0>
+__device__ __forceinline__ uint32_t group_sum_g(uint32_t v) {
+    if constexpr ((1 << ROUND) < G) return group_sum_g<G, ROUND + 1>(v + dpp_partner<ROUND>(v));
+    return v;
+}
+
+// waves per SIMD asked of the register allocator (A/B builds; 0 = the
+// compiler's choice: 89 VGPRs -> 5 waves)
+#ifndef O3DML_KNN_WAVES
+#define O3DML_KNN_WAVES 0
+#endif
+#if O3DML_KNN_WAVES
+#define O3DML_KNN_ATTR __attribute__((amdgpu_waves_per_eu(O3DML_KNN_WAVES, 8)))
+#else
+#define O3DML_KNN_ATTR
+#endif
+template <int K, int G, int METRIC, bool IGNORE>
+__global__ void __launch_bounds__(256) O3DML_KNN_ATTR knn_group_kernel(const float4* __restrict__ sorted,
                                                         const uint32_t* __restrict__ splits,
                                                         const GridBatch* __restrict__ grids,
                                                         const float* __restrict__ queries, int64_t m,
@@ -192,9 +276,11 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
                                                         const int64_t* __restrict__ qrs, int nb, int k,
                                                         int32_t* __restrict__ out_idx, float* __restrict__ out_dist,
                                                         int64_t* __restrict__ counts) {
-    const int gl = threadIdx.x & (kKnnG - 1);
-    const int64_t groups = static_cast<int64_t>(gridDim.x) * (blockDim.x / kKnnG);
-    for (int64_t t = (blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x) / kKnnG; t < m + 0;
+    static_assert(G == 4 || G == 8 || G == 16, "group of 4, 8 or 16 lanes (DPP partners within a row)");
+    const int gl = threadIdx.x & (G - 1);
+    const KnnKey empty = KnnKey::from_bits(kKnnEmpty);
+    const int64_t groups = static_cast<int64_t>(gridDim.x) * (blockDim.x / G);
+    for (int64_t t = (blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x) / G; t < m + 0;
          t += groups) {
         const int64_t q = qorder ? static_cast<int64_t>(qorder[t]) : t;
         const GridBatch g = grids[batch_of(q, qrs, nb)];
@@ -202,22 +288,23 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
         const int cx = grid_axis(qx, g.ox, g.inv_h, g.dx);
         const int cy = grid_axis(qy, g.oy, g.inv_h, g.dy);
         const int cz = grid_axis(qz, g.oz, g.inv_h, g.dz);
-        uint64_t bk[K];  // this lane's sorted top-K keys (knn_key)
+        KnnKey bk[K];  // this lane's sorted top-K keys
 #pragma unroll
-        for (int j = 0; j < K; ++j) bk[j] = kKnnEmpty;
-        uint64_t kk = kKnnEmpty;  // group k-th best after the last merge (pruning bound)
+        for (int j = 0; j < K; ++j) bk[j] = empty;
+        KnnKey kk = empty;  // group k-th best after the last merge (pruning bound)
+        KnnKey thr = empty;  // min(kk, bk[K-1]): a candidate enters only below it
         bool full = false;
         auto consider = [&](const float4& p) {
             if (IGNORE && p.x == qx && p.y == qy && p.z == qz) return;
             const float d = dist_metric<METRIC>(p.x, p.y, p.z, qx, qy, qz);
-            const uint64_t key = knn_key(d, __float_as_uint(p.w));
-            if (!(key < kk) || !(key < bk[K - 1])) return;
+            const KnnKey key = knn_key_g(d, __float_as_uint(p.w));
+            if (!(key < thr)) return;
+            // branch-free insertion, every position from the old list; in
+            // place from the top (position r reads old r - 1 and old r)
 #pragma unroll
-            for (int r = K - 1; r >= 0; --r) {  // insertion: shift the larger entries up
-                const bool lt_prev = r > 0 && key < bk[r > 0 ? r - 1 : 0];
-                const bool lt_cur = key < bk[r];
-                bk[r] = lt_prev ? bk[r > 0 ? r - 1 : 0] : (lt_cur ? key : bk[r]);
-            }
+            for (int r = K - 1; r >= 1; --r) bk[r] = kmin(kmax(key, bk[r - 1]), bk[r]);
+            bk[0] = kmin(key, bk[0]);
+            thr = kmin(kk, bk[K - 1]);
         };
         // cells xa..xb of one (y, z) row are adjacent in the cell order (x
         // fastest), so their points are one contiguous run of `sorted`: one
@@ -227,8 +314,8 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
             const uint32_t c = g.offset + static_cast<uint32_t>(g.dx * (y + g.dy * z));
             const uint32_t s = splits[c + xa], e = splits[c + xb + 1];
             uint32_t j = s + gl;
-            for (; j + kKnnG < e; j += 2 * kKnnG) {  // two loads in flight per lane
-                const float4 p0 = sorted[j], p1 = sorted[j + kKnnG];
+            for (; j + G < e; j += 2 * G) {  // two loads in flight per lane
+                const float4 p0 = sorted[j], p1 = sorted[j + G];
                 consider(p0);
                 consider(p1);
             }
@@ -251,20 +338,19 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
             }
             // merging only pays once the group holds k candidates (it can then
             // prune and terminate); before that the lists keep accumulating
-            int have = 0;
+            uint32_t have = 0;
 #pragma unroll
-            for (int r = 0; r < K; ++r) have += static_cast<uint32_t>(bk[r]) != 0xffffffffu ? 1 : 0;
-#pragma unroll
-            for (int mask = 1; mask < kKnnG; mask <<= 1) have += __shfl_xor(have, mask, 64);
+            for (int r = 0; r < K; ++r) have += static_cast<uint32_t>(bk[r].bits()) != 0xffffffffu ? 1u : 0u;
+            have = group_sum_g<G>(have);
             const bool last_ring = x0 <= 0 && x1 >= g.dx - 1 && y0 <= 0 && y1 >= g.dy - 1 && z0 <= 0 &&
                                    z1 >= g.dz - 1;
-            if (have < k && !last_ring) continue;
-            group_merge<K>(bk);
+            if (have < static_cast<uint32_t>(k) && !last_ring) continue;
+            group_merge_g<K, G>(bk);
 #pragma unroll
             for (int r = 0; r < K; ++r)
                 if (r == k - 1) kk = bk[r];
-            full = static_cast<uint32_t>(kk) != 0xffffffffu;
-            const float kd = __uint_as_float(static_cast<uint32_t>(kk >> 32));
+            full = static_cast<uint32_t>(kk.bits()) != 0xffffffffu;
+            const float kd = __uint_as_float(static_cast<uint32_t>(kk.bits() >> 32));
             const bool lo_x = x0 <= 0, hi_x = x1 >= g.dx - 1, lo_y = y0 <= 0, hi_y = y1 >= g.dy - 1;
             const bool lo_z = z0 <= 0, hi_z = z1 >= g.dz - 1;
             if (lo_x && hi_x && lo_y && hi_y && lo_z && hi_z) break;  // every cell visited
@@ -284,35 +370,52 @@ __global__ void __launch_bounds__(256) knn_group_kernel(const float4* __restrict
             }
             if (gl != 0) {  // lane 0 carries the merged list into the next ring
 #pragma unroll
-                for (int j = 0; j < K; ++j) bk[j] = kKnnEmpty;
+                for (int j = 0; j < K; ++j) bk[j] = empty;
             }
+            thr = kmin(kk, bk[K - 1]);
         }
         int c = 0;
 #pragma unroll
-        for (int r = 0; r < K; ++r) c += (r < k && static_cast<uint32_t>(bk[r]) != 0xffffffffu) ? 1 : 0;
+        for (int r = 0; r < K; ++r) c += (r < k && static_cast<uint32_t>(bk[r].bits()) != 0xffffffffu) ? 1 : 0;
         if (gl == 0) counts[q] = c;
         int32_t* oi = out_idx + q * static_cast<int64_t>(k);
         float* od = out_dist + q * static_cast<int64_t>(k);
 #pragma unroll
         for (int r = 0; r < K; ++r) {
-            if (r < c && (r & (kKnnG - 1)) == gl) {
-                oi[r] = static_cast<int32_t>(static_cast<uint32_t>(bk[r]));
-                od[r] = __uint_as_float(static_cast<uint32_t>(bk[r] >> 32));
+            if (r < c && (r & (G - 1)) == gl) {
+                const uint64_t b = bk[r].bits();
+                oi[r] = static_cast<int32_t>(static_cast<uint32_t>(b));
+                od[r] = __uint_as_float(static_cast<uint32_t>(b >> 32));
             }
         }
     }
+}
+
+// lanes per query of the group kernel (A/B knob O3DML_KNN_G: 4, 8 or 16)
+static int knn_group_lanes() {
+    static const int g = [] {
+        const char* e = std::getenv("O3DML_KNN_G");
+        const int v = e ? std::atoi(e) : 8;
+        return v == 4 || v == 16 ? v : 8;
+    }();
+    return g;
 }
 
 template <int K>
 static void launch_knn_k(int metric, bool ignore, unsigned grid, hipStream_t st, const GridIndex& gi, const float* q,
                          int64_t m, const uint32_t* qorder, const int64_t* qrs, int nb, int k, int32_t* oi, float* od,
                          int64_t* counts) {
+#define O3DML_KNN_G(M, I, G)                                                                                     \
+    knn_group_kernel<K, G, M, I><<<stream_grid(m * G, 256, 1 << 20), 256, 0, st>>>(                              \
+            gi.sorted, gi.splits, gi.params, q, m, qorder, qrs, nb, k, oi, od, counts)
 #define O3DML_KNN(M, I)                                                                                          \
     do {                                                                                                         \
-        if constexpr (K <= 16)                                                                                   \
-            knn_group_kernel<K, M, I><<<stream_grid(m * kKnnG, 256, 1 << 20), 256, 0, st>>>(                      \
-                    gi.sorted, gi.splits, gi.params, q, m, qorder, qrs, nb, k, oi, od, counts);                  \
-        else                                                                                                     \
+        if constexpr (K <= 16) {                                                                                 \
+            const int G = knn_group_lanes();                                                                     \
+            if (G == 4) O3DML_KNN_G(M, I, 4);                                                                    \
+            else if (G == 16) O3DML_KNN_G(M, I, 16);                                                             \
+            else O3DML_KNN_G(M, I, 8);                                                                           \
+        } else                                                                                                   \
             knn_grid_kernel<K, M, I><<<grid, 256, 0, st>>>(gi.sorted, gi.splits, gi.params, q, m, qorder, qrs, nb, \
                                                            k, oi, od, counts);                                   \
     } while (0)
@@ -324,6 +427,7 @@ static void launch_knn_k(int metric, bool ignore, unsigned grid, hipStream_t st,
         if (ignore) O3DML_KNN(kLinf, true); else O3DML_KNN(kLinf, false);
     }
 #undef O3DML_KNN
+#undef O3DML_KNN_G
     O3DML_LAUNCH_CHECK();
 }
 
@@ -413,7 +517,15 @@ static int knn_bucket(int64_t k) {
     return 0;
 }
 
-static constexpr double kKnnCapFactor = 2.0;
+// cells per point at most (grid_cells_cap): O3DML_KNN_CAP (A/B), default 2
+static double knn_cap_factor() {
+    static const double v = [] {
+        const char* e = std::getenv("O3DML_KNN_CAP");
+        const double x = e ? std::atof(e) : 2.0;
+        return x > 0.0 ? x : 2.0;
+    }();
+    return v;
+}
 // points per cell of the uniform-fill grid plan = max(min_target, k * factor)
 static double knn_target_factor() {
     const char* e = std::getenv("O3DML_KNN_TARGET");
@@ -430,7 +542,7 @@ O3DML_API size_t o3dml_knn_search_workspace_size(int64_t n_points, int64_t n_que
         return std::max(topk_bigk_workspace_bytes(n_points, k),
                         ws_bytes<int64_t>(n_queries) + prim::scan_workspace_bytes(n_queries));
     }
-    return grid_workspace_bytes(n_points, static_cast<int>(n_batch), kKnnCapFactor) +
+    return grid_workspace_bytes(n_points, static_cast<int>(n_batch), knn_cap_factor()) +
            3 * ws_bytes<uint32_t>(n_queries) + prim::radix_sort_workspace_bytes<uint32_t>(n_queries) +
            ws_bytes<int32_t>(n_queries * k) + ws_bytes<float>(n_queries * k) + ws_bytes<int64_t>(n_queries) +
            prim::scan_workspace_bytes(n_queries);
@@ -480,7 +592,7 @@ O3DML_API int o3dml_knn_search_count(const float* points, int64_t n_points, cons
     float* sd = ws.take<float>(n_queries * k);
     int64_t* counts = ws.take<int64_t>(n_queries);
     GridIndex gi = build_grid(points, n_points, points_row_splits, nb, std::max(knn_min_target(), k * knn_target_factor()),
-                              kKnnCapFactor, ws, st);
+                              knn_cap_factor(), ws, st);
     uint32_t* qkeys = ws.take<uint32_t>(n_queries);
     uint32_t* qskeys = ws.take<uint32_t>(n_queries);
     uint32_t* qorder = ws.take<uint32_t>(n_queries);
@@ -502,6 +614,7 @@ O3DML_API int o3dml_knn_search_count(const float* points, int64_t n_points, cons
     }
     const unsigned grid = stream_grid(n_queries, 256, 1 << 20);
     const bool ig = ignore_query_point != 0;
+    TimedRegion tr("knn_search", st);  // the search kernel alone (bench op roofline)
     switch (K) {
         case 1: launch_knn_k<1>(metric, ig, grid, st, gi, queries, n_queries, order, queries_row_splits, nb, (int)k, si, sd, counts); break;
         case 4: launch_knn_k<4>(metric, ig, grid, st, gi, queries, n_queries, order, queries_row_splits, nb, (int)k, si, sd, counts); break;
@@ -510,6 +623,7 @@ O3DML_API int o3dml_knn_search_count(const float* points, int64_t n_points, cons
         case 32: launch_knn_k<32>(metric, ig, grid, st, gi, queries, n_queries, order, queries_row_splits, nb, (int)k, si, sd, counts); break;
         default: launch_knn_k<64>(metric, ig, grid, st, gi, queries, n_queries, order, queries_row_splits, nb, (int)k, si, sd, counts); break;
     }
+    tr.end();
     prim::scan<int64_t, int64_t>(counts, neighbors_row_splits + 1, n_queries, true, ws, st);
     O3DML_GUARD_END
 }

@@ -400,6 +400,7 @@ O3DML_API int o3dml_voxelize_count(const float* points, int64_t n_points, int nd
     SegState s = take_seg_state(ws, n_points, nb);
     uint64_t* keys = ws.take<uint64_t>(n_points);
     const unsigned g = stream_grid(n_points > 0 ? n_points : 1, 256);
+    TimedRegion tr("voxelize_count", st);  // device time of the phase (bench op roofline)
     if (n_points > 0) {
         vox_keys_kernel<<<g, 256, 0, st>>>(points, n_points, row_splits, vp, keys);
         O3DML_LAUNCH_CHECK();
@@ -418,6 +419,7 @@ O3DML_API int o3dml_voxelize_count(const float* points, int64_t n_points, int nd
     }
     vox_totals_kernel<<<1, 64, 0, st>>>(s.incl, n_points, s.keep_incl, s.npts_incl, s.scalars + 1);
     O3DML_LAUNCH_CHECK();
+    tr.end();
     int64_t* tot = pinned_scratch();
     O3DML_CHECK_HIP(hipMemcpyAsync(tot, s.scalars + 1, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
@@ -437,6 +439,7 @@ O3DML_API int o3dml_voxelize_fill(int64_t n_points, int ndim, int64_t n_batch, c
     const int nb = static_cast<int>(n_batch);
     VoxParams vp = make_vox_params(ndim, nb, voxel_size_host, range_min_host, range_max_host);
     SegState s = take_seg_state(ws, n_points, nb);
+    TimedRegion tr("voxelize_fill", st);
     if (n_points > 0) {
         vox_fill_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(s.sk, s.sidx, s.start, s.incl, n_points, s.keep,
                                                                    s.keep_incl, s.npts, s.npts_incl, vp, voxel_coords,
@@ -516,6 +519,7 @@ O3DML_API int o3dml_grid_subsample_count_async(const float* points, int64_t n_po
     uint64_t* keys = ws.take<uint64_t>(n_points);
     SubBatch* sb_d = ws.take<SubBatch>(nb);
     float* bbox_d = ws.take<float>(6 * nb);
+    TimedRegion tr("grid_subsample_count", st);  // device time of the phase (bench op roofline)
     launch_bbox(points, row_splits, nb, bbox_d, st);
     O3DML_LAUNCH_CHECK();
     sub_grid_kernel<<<1, 256, 0, st>>>(bbox_d, row_splits, nb, dl, sb_d, out);
@@ -568,6 +572,7 @@ O3DML_API int o3dml_grid_subsample_fill(const float* points, int64_t n_points, i
     Workspace ws(workspace, workspace_bytes);
     const int nb = static_cast<int>(n_batch);
     SegState s = take_seg_state(ws, n_points, nb);
+    TimedRegion tr("grid_subsample_fill", st);
     if (n_points > 0) {
         sub_fill_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(points, features, fdim, classes, ldim, s.sidx,
                                                                    s.start, s.incl, n_points, s.keep, s.keep_incl,

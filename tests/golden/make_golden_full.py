@@ -146,6 +146,28 @@ def make_c2(out):
     out["c2_logit_rows"] = logits[::11]
     out["c2_logit_colsum"] = logits.astype(np.float64).sum(0)
     print("c2 logits", logits.shape, float(np.abs(logits).mean()))
+    # the same reference model in float64 (same neighbours, same weights): the
+    # truth the per-element C2 check holds fp32 results to, and the
+    # reference's own fp32 error against it (as C3 / C4)
+    model64 = RandLANet(num_points=C2_K, num_classes=19, in_channels=3)  # (its Config defeats deepcopy)
+    model64.load_state_dict(model.state_dict())
+    model64 = model64.double().eval()
+    model64.device = torch.device("cpu")
+    t64 = lambda a: torch.from_numpy(a)[None].double()  # noqa: E731
+    inputs64 = dict(inputs, coords=[t64(c) for c in coords], features=t64(pc))
+    with torch.no_grad():
+        logits64 = model64(inputs64)[0].numpy()
+    out["c2_f64_logit_rows"] = logits64[::11]
+    out["c2_f64_logit_colsum"] = logits64.sum(0)
+    err = np.abs(logits.astype(np.float64) - logits64)
+    out["c2_ref32_abs_err"] = np.float64(err.max())
+    out["c2_ref32_rel_err"] = np.float64((err / np.maximum(np.abs(logits64), 1e-300)).max())
+    # per-row scale of the logits (max |logit| of the row): the floor of the
+    # per-element check is a multiple of the reference's own fp32 error
+    # relative to it
+    out["c2_ref32_err_vs_rowmax"] = np.float64((err / np.abs(logits64).max(1, keepdims=True)).max())
+    print("c2 ref fp32 vs fp64: max abs", float(out["c2_ref32_abs_err"]), "max rel", float(out["c2_ref32_rel_err"]),
+          "vs row max", float(out["c2_ref32_err_vs_rowmax"]), "max |f64|", float(np.abs(logits64).max()))
 
 
 def make_c3(out):

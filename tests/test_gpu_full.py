@@ -125,6 +125,21 @@ def test_c2_randla_full_patch_vs_reference(c2):
         out = m(inputs)[0].cpu().numpy()
     np.testing.assert_allclose(out[::11], F["c2_logit_rows"], rtol=0, atol=2e-4)
     np.testing.assert_allclose(out.astype(np.float64).sum(0), F["c2_logit_colsum"], rtol=0, atol=1e-5 * C2_K)
+    # per element against the float64 run of the reference model (same
+    # neighbours and weights; make_golden_full.py): |a - b| <= 1e-4 |b| + a
+    # floor, the floor = 10x the reference's OWN fp32 error (max over the
+    # patch of |ref32 - ref64| / max |row|, ~1.1e-6) times the row's max |b| —
+    # it only matters where the logit is small against its row (the
+    # reference's own fp32 logits reach 0.3 relative error there)
+    b = F["c2_f64_logit_rows"]
+    a = out[::11].astype(np.float64)
+    floor = 10.0 * float(F["c2_ref32_err_vs_rowmax"]) * np.abs(b).max(1, keepdims=True)
+    excess = np.abs(a - b) - (1e-4 * np.abs(b) + floor)
+    worst = np.unravel_index(np.argmax(excess), excess.shape)
+    assert excess.max() <= 0, (f"element {worst}: |a-b| {abs(a[worst] - b[worst]):.3g} vs bound "
+                               f"{1e-4 * abs(b[worst]) + floor[worst[0], 0]:.3g} (b {b[worst]:.4g})")
+    np.testing.assert_allclose(out.astype(np.float64).sum(0), F["c2_f64_logit_colsum"], rtol=1e-5,
+                               atol=1e-6 * C2_K)
 
 
 @pytest.fixture(scope="module")

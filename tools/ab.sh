@@ -11,7 +11,7 @@
 #   knn     batched k = 16 kNN at RandLA-Net's shapes (tools/knn_probe.py)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 KIND=$1; shift
-NOSEC="--no-cpu-baseline --sweep-reps 0"
+NOSEC="--no-cpu-baseline --sweep-reps 0 --op-reps 0"
 run() {
   case "$KIND" in
     frs)

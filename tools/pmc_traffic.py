@@ -18,7 +18,8 @@ def main(src, dst, match, name):
     stats = glob.glob(os.path.join(src, "stats", "**", "run_kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(dst, f"{name}_kernel_stats.csv"))
-    shutil.copy(os.path.join(src, "bench.log"), os.path.join(dst, f"{name}_bench.log"))
+    if os.path.exists(os.path.join(src, "bench.log")):  # (PMC passes over a probe have none)
+        shutil.copy(os.path.join(src, "bench.log"), os.path.join(dst, f"{name}_bench.log"))
     res = load(src, match)
     assert len(res) == 1, list(res)
     (kname, c), = res.items()
