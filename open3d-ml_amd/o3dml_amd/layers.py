@@ -132,6 +132,7 @@ class SparseConv(torch.nn.Module):
         self.lattice_rulebook = True  # False forces the fixed-radius-search rulebook
 
     def _rulebook(self, inp_positions, out_positions, voxel_size, hash_table, mirror, sign):
+        sc.note_search_rulebook()
         vs = _voxel_size_scalar(voxel_size, inp_positions)
         queries = (out_positions - sign * self.offset.to(out_positions.device) * vs).contiguous()
         radius = 0.5 * vs * self.kernel_size[0]

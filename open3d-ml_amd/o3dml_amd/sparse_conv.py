@@ -300,6 +300,7 @@ class _RulebookScope:
         self.defer = defer_checks
         self.pending = []
         self.derived = 0  # transpose maps derived from their convolution partner (_transpose_of_cached)
+        self.searches = 0  # layers that built the search rulebook (host round trips: not graph-capturable)
 
     def check(self):
         """One host round trip for every deferred lattice check of the scope:
@@ -314,6 +315,14 @@ class _RulebookScope:
 
 
 _SCOPE = None  # the active rulebook_cache() scope
+
+
+def note_search_rulebook():
+    """A layer built its rulebook with the fixed-radius search (not the lattice
+    map): counted in the active scope (sparseconvnet._ScnBody then does not
+    capture the body: the search reads sizes back to the host)."""
+    if _SCOPE is not None:
+        _SCOPE.searches += 1
 
 
 @contextlib.contextmanager

@@ -9,6 +9,8 @@ round-trips the voxel maps through numpy, sparseconvnet.py:302-315).  One
 forward runs inside a rulebook-cache scope, so all submanifold convolutions of
 one level share one kernel map instead of rebuilding it per layer.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -297,6 +299,82 @@ class _LevelGrids:
         return outs, half
 
 
+class _FixedGrids:
+    """_LevelGrids' interface over the per-level grids of a captured body:
+    level l's Convolution output grid, the next level's positions = grid / 2
+    computed in the body (one kernel, no extra graph input)."""
+
+    def __init__(self, outs_per_level):
+        self.levels = list(outs_per_level)
+
+    def next(self, pos_list):
+        outs = self.levels.pop(0)
+        return outs, [o / 2 for o in outs]
+
+
+def _graph_mode():
+    """O3DML_SCN_GRAPH: "1" (default) replays the eval body as a HIP graph
+    per size signature, "0" runs it eagerly (A/B)."""
+    return os.environ.get("O3DML_SCN_GRAPH", "1") != "0"
+
+
+class _ScnBody:
+    """The eval forward after the InputLayer and the level grids — every
+    convolution with its lattice kernel map, the folded BatchNorm / ReLU
+    prologues, the residual epilogues, the head — captured once per size
+    signature (voxels and grid points of every level) as a HIP graph and
+    replayed per frame: ~330 launches and their host cost become one replay.
+    The frame's inputs (voxel positions, averaged features, the level grids)
+    are copied into the graph's static buffers first; the lattice status
+    words the body leaves on the device are read once after the replay (the
+    eager path's scope.check)."""
+
+    def __init__(self, model, pos_list, feat_list, outs_per_level):
+        dev = pos_list[0].device
+        self.pos = [p.clone() for p in pos_list]
+        self.feat = [f.clone() for f in feat_list]
+        self.outs = [[o.clone() for o in outs] for outs in outs_per_level]
+        main = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):  # warm-up: lazy caches and library state outside the capture
+            with rulebook_cache(defer_checks=True) as scope:
+                model._body(self.pos, self.feat, _FixedGrids(self.outs))
+                ok = scope.check()
+                searches = scope.searches
+        main.wait_stream(side)
+        self.lattice = ok
+        self.graph = None
+        # off-lattice input, or a layer on the search rulebook (e.g. an empty
+        # level): the caller takes the eager path
+        if not ok or searches:
+            return
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            with rulebook_cache(defer_checks=True) as scope:
+                self.out = model._body(self.pos, self.feat, _FixedGrids(self.outs))
+                self.status = torch.cat(scope.pending) if scope.pending else None
+                scope.pending.clear()
+
+    def run(self, pos_list, feat_list, outs_per_level):
+        """Replay on this frame's inputs; None when a level is off the lattice."""
+        for dst, src in zip(self.pos, pos_list):
+            dst.copy_(src)
+        for dst, src in zip(self.feat, feat_list):
+            dst.copy_(src)
+        for dl, sl in zip(self.outs, outs_per_level):
+            for dst, src in zip(dl, sl):
+                dst.copy_(src)
+        self.graph.replay()
+        if self.status is not None:
+            st = self.status.cpu()
+            if bool((st & 1).any()):
+                raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index")
+            if bool((st & 4).any()):
+                return None
+        return self.out
+
+
 class UNet(nn.Module):
     """sparseconvnet.py:568-653."""
 
@@ -383,7 +461,14 @@ class SparseConvUnet(nn.Module):
         self.linear = LinearBlock(multiplier, num_classes)
         self.output_layer = OutputLayer()
 
+    _MAX_GRAPHS = 4  # captured bodies kept per model (size signatures, LRU)
+
     def forward(self, inputs):
+        if _graph_mode() and not self.training and not torch.is_grad_enabled() and len(inputs.point) and \
+                inputs.point[0].is_cuda:
+            out = self._forward_graph(inputs)
+            if out is not None:
+                return out
         # lattice checks of all levels are read back once at the end; a
         # non-lattice input (never produced by the reference preprocess) is
         # recomputed with per-layer checks and the search rulebook
@@ -394,6 +479,64 @@ class SparseConvUnet(nn.Module):
             return out
         with rulebook_cache():
             return self._forward(inputs)
+
+    def _inputs(self, inputs):
+        pos_list, feat_list, index_maps = [], [], []
+        for i in range(len(inputs.batch_lengths)):
+            f, p, m = self.input_layer(inputs.feat[i], inputs.point[i])
+            pos_list.append(p)
+            feat_list.append(f)
+            index_maps.append(m)
+        return pos_list, feat_list, index_maps
+
+    def _body(self, pos_list, feat_list, grids):
+        """Everything between the InputLayer (+ level grids) and the OutputLayer."""
+        feat_list = self.sub_sparse_conv(feat_list, pos_list, voxel_size=1.0)
+        feat_list = self.unet(pos_list, feat_list, grids=grids)
+        feat_list = self.relu(self.batch_norm(feat_list))
+        return self.linear(feat_list)
+
+    def _param_key(self):
+        """(address, version) of every parameter and buffer: a captured body
+        is only replayed on the weights it was captured with.  The tensor list
+        is kept (walking the module tree costs ~1 ms per frame) and dropped by
+        _apply (.to / .cuda / .float replace the tensors)."""
+        ts = self.__dict__.get("_o3dml_state_tensors")
+        if ts is None:
+            ts = self.__dict__["_o3dml_state_tensors"] = list(self.parameters()) + list(self.buffers())
+        return tuple((t.data_ptr(), t._version) for t in ts)
+
+    def _apply(self, fn, *args, **kwargs):
+        self.__dict__.pop("_o3dml_state_tensors", None)
+        self.__dict__.pop("_o3dml_scn_bodies", None)
+        return super()._apply(fn, *args, **kwargs)
+
+    def _forward_graph(self, inputs):
+        """Eval forward with the body replayed from a captured graph (_ScnBody):
+        the InputLayer and the level grids (whose sizes the host reads) run
+        eagerly, then the body of their size signature replays.  None when the
+        input is off the voxel lattice (the caller recomputes eagerly)."""
+        pos_list, feat_list, index_maps = self._inputs(inputs)
+        outs_per_level, p = [], pos_list
+        for _ in range(self.unet.n_down()):
+            outs = [ops.calculate_grid(x) for x in p]
+            outs_per_level.append(outs)
+            p = [o / 2 for o in outs]
+        key = (str(pos_list[0].device), tuple(int(x.shape[0]) for x in pos_list),
+               tuple(tuple(int(o.shape[0]) for o in outs) for outs in outs_per_level), self._param_key())
+        bodies = self.__dict__.setdefault("_o3dml_scn_bodies", {})
+        body = bodies.pop(key, None)
+        if body is None:
+            body = _ScnBody(self, pos_list, feat_list, outs_per_level)
+            while len(bodies) >= self._MAX_GRAPHS:
+                bodies.pop(next(iter(bodies)))  # least recently used first
+        bodies[key] = body  # most recently used last
+        if body.graph is None:
+            return None
+        out = body.run(pos_list, feat_list, outs_per_level)
+        if out is None:
+            return None
+        return self.output_layer(out, index_maps)
 
     def _forward(self, inputs):
         pos_list, feat_list, index_maps = [], [], []

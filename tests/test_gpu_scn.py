@@ -101,3 +101,38 @@ def test_scn_fused_eval_matches_unfused(cuda, residual):
     b = m(inp).detach()
     err = ((a - b).abs().max() / b.abs().max()).item()
     assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("residual", [True, False])
+def test_scn_graph_replay_equals_eager(cuda, residual, monkeypatch):
+    """The eval body captured as a HIP graph per size signature
+    (sparseconvnet._ScnBody, O3DML_SCN_GRAPH=1) gives the eager forward's
+    logits bit for bit: on the capture frame, on replays with new features,
+    after a second room (second signature) was captured in between, and after
+    the weights change (a new capture keyed on the parameter versions)."""
+    from o3dml_amd import sparseconvnet as S
+    m = _model(residual, cuda)
+    inp = _inputs(cuda)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    n = inp.point[0].shape[0]
+    keep = torch.randperm(n, generator=g)[: n * 2 // 3].to(cuda)
+    room2 = types.SimpleNamespace(point=[inp.point[0][keep].contiguous()], feat=[inp.feat[0][keep].contiguous()],
+                                  batch_lengths=[keep.shape[0]])
+
+    def run(x, graph):
+        monkeypatch.setenv("O3DML_SCN_GRAPH", "1" if graph else "0")
+        with torch.no_grad():
+            return m(x).clone()
+
+    frames = [inp, types.SimpleNamespace(point=inp.point, feat=[torch.rand_like(inp.feat[0])], batch_lengths=[n]),
+              room2, inp]
+    for x in frames:
+        assert torch.equal(run(x, True), run(x, False))
+    bodies = m.__dict__["_o3dml_scn_bodies"]
+    assert len(bodies) == 2 and all(b.graph is not None for b in bodies.values())
+    with torch.no_grad():
+        for p in m.parameters():
+            p.mul_(0.5)
+    assert torch.equal(run(inp, True), run(inp, False))
+    assert len(bodies) == 3
+    assert isinstance(next(iter(bodies.values())), S._ScnBody)
