@@ -1151,7 +1151,7 @@ static int frs_qlog(int64_t m) {
         const char* e = std::getenv("O3DML_FRS_QLOG");
         return e ? std::atoi(e) : 0;
     }();
-    if (env >= 4 && env <= 6) return env;
+    if (env >= 2 && env <= 6) return env;
     if (m >= 4096 * 64) return 6;
     return m >= 4096 * 32 ? 5 : 4;
 }

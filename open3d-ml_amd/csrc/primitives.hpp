@@ -317,7 +317,23 @@ __global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* kin, const ui
         // tile digit offsets: exclusive scan of this tile's histogram
         const uint32_t c = hist[static_cast<int64_t>(t) * tiles + blockIdx.x];
         const uint32_t inc = wave_inclusive_scan(c);
-        const uint32_t dt = dtot[t];
+        // digit total and this tile's base within its digit: from
+        // radix_digit_scan, or (offsets == nullptr: few tiles) summed here
+        // over the digit's histogram row — the same counts, one launch fewer
+        uint32_t dt, tbase;
+        if (offsets) {
+            dt = dtot[t];
+            tbase = offsets[static_cast<int64_t>(t) * tiles + blockIdx.x];
+        } else {
+            dt = 0u;
+            tbase = 0u;
+            const uint32_t* hr = hist + static_cast<int64_t>(t) * tiles;
+            for (int64_t j = 0; j < tiles; ++j) {
+                const uint32_t v = hr[j];
+                dt += v;
+                tbase += j < static_cast<int64_t>(blockIdx.x) ? v : 0u;
+            }
+        }
         const uint32_t dinc = wave_inclusive_scan(dt);  // digit bases: scan of the digit totals
         if (lane == 63) {
             wsum[w] = inc;
@@ -332,7 +348,7 @@ __global__ void __launch_bounds__(kRsBlock) radix_scatter(const K* kin, const ui
             dbefore += dsum[ww];
         }
         toff[t] = before + inc - c;
-        goff[t] = static_cast<int64_t>(dbefore + dinc - dt) + offsets[static_cast<int64_t>(t) * tiles + blockIdx.x];
+        goff[t] = static_cast<int64_t>(dbefore + dinc - dt) + tbase;
     }
     // phase 1: each wave ranks its rows in order, counts per digit in LDS
     const uint64_t lt = lanemask_lt();
@@ -650,6 +666,17 @@ inline int64_t block_sort_max() {
     return v;
 }
 
+// Largest tile count whose scatter sums its own digit bases (no
+// radix_digit_scan launch): O3DML_RS_FUSED_TILES (A/B; 0 = never), default 64
+// (n <= 131,072 keys: every block reads the 256 x tiles histogram, <= 64 KiB)
+inline int64_t rs_fused_tiles() {
+    static const int64_t v = [] {
+        const char* e = std::getenv("O3DML_RS_FUSED_TILES");
+        return e ? std::atoll(e) : 64;
+    }();
+    return v;
+}
+
 inline int bits_needed(uint64_t max_key) {
     int b = 0;
     while (b < 64 && (max_key >> b) != 0) ++b;
@@ -708,6 +735,9 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
         return;
     }
     const int64_t tiles = ceil_div(n, kRsTile);
+    // up to kRsFusedTiles tiles the scatter sums its digit bases from the
+    // histogram itself (radix_digit_scan skipped: 2 launches per pass, not 3)
+    const bool fused = tiles <= rs_fused_tiles();
     K* ktmp = ws.take<K>(n);
     uint32_t* vtmp = ws.take<uint32_t>(n);
     uint32_t* hist = ws.take<uint32_t>(256 * tiles);
@@ -719,11 +749,13 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
             radix_hist<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(keys_in, n, shift, hist, tiles, or_and,
                                                                              passes, ktmp, keys_out);
             O3DML_LAUNCH_CHECK();
-            radix_digit_scan<<<256, kRsBlock, 0, st>>>(hist, tiles, offs, dtot, or_and, p);
-            O3DML_LAUNCH_CHECK();
+            if (!fused) {
+                radix_digit_scan<<<256, kRsBlock, 0, st>>>(hist, tiles, offs, dtot, or_and, p);
+                O3DML_LAUNCH_CHECK();
+            }
             radix_scatter<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(
-                    keys_in, vals_in, nullptr, nullptr, n, shift, offs, dtot, hist, tiles, or_and, passes, ktmp, vtmp,
-                    keys_out, vals_out);
+                    keys_in, vals_in, nullptr, nullptr, n, shift, fused ? nullptr : offs, dtot, hist, tiles, or_and,
+                    passes, ktmp, vtmp, keys_out, vals_out);
             O3DML_LAUNCH_CHECK();
         }
         return;
@@ -737,10 +769,12 @@ void radix_sort_pairs(const K* keys_in, const uint32_t* vals_in, K* keys_out, ui
         const int shift = 8 * p;
         radix_hist<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(ksrc, n, shift, hist, tiles);
         O3DML_LAUNCH_CHECK();
-        radix_digit_scan<<<256, kRsBlock, 0, st>>>(hist, tiles, offs, dtot);
-        O3DML_LAUNCH_CHECK();
+        if (!fused) {
+            radix_digit_scan<<<256, kRsBlock, 0, st>>>(hist, tiles, offs, dtot);
+            O3DML_LAUNCH_CHECK();
+        }
         radix_scatter<K><<<static_cast<unsigned>(tiles), kRsBlock, 0, st>>>(ksrc, vsrc, kdst, vdst, n, shift,
-                                                                          offs, dtot, hist, tiles);
+                                                                          fused ? nullptr : offs, dtot, hist, tiles);
         O3DML_LAUNCH_CHECK();
         ksrc = kdst;
         vsrc = vdst;
