@@ -319,10 +319,29 @@ _SCOPE = None  # the active rulebook_cache() scope
 
 def note_search_rulebook():
     """A layer built its rulebook with the fixed-radius search (not the lattice
-    map): counted in the active scope (sparseconvnet._ScnBody then does not
+    map): counted in the active scope (sparseconvnet._ScnHead / _ScnTail then do not
     capture the body: the search reads sizes back to the host)."""
     if _SCOPE is not None:
         _SCOPE.searches += 1
+
+
+@contextlib.contextmanager
+def rulebook_scope(scope):
+    """Make an existing _RulebookScope the active one (a graph captured in
+    parts continues one scope: the later part finds the earlier part's maps)."""
+    global _SCOPE
+    prev, _SCOPE = _SCOPE, scope
+    try:
+        yield scope
+    finally:
+        _SCOPE = prev
+
+
+def scope_from(maps, defer_checks=True):
+    """A fresh scope that starts with the given kernel maps."""
+    sc_ = _RulebookScope(defer_checks)
+    sc_.maps = dict(maps)
+    return sc_
 
 
 @contextlib.contextmanager

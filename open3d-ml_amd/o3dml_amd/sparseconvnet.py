@@ -16,7 +16,7 @@ import torch.nn as nn
 
 from . import ops
 from .layers import SparseConv, SparseConvTranspose
-from .sparse_conv import rulebook_cache
+from .sparse_conv import rulebook_cache, rulebook_scope, scope_from
 
 
 class BatchNormBlock(nn.Module):
@@ -313,9 +313,17 @@ class _FixedGrids:
 
 
 def _graph_mode():
-    """O3DML_SCN_GRAPH: "1" (default) replays the eval body as a HIP graph
-    per size signature, "0" runs it eagerly (A/B)."""
-    return os.environ.get("O3DML_SCN_GRAPH", "1") != "0"
+    """O3DML_SCN_GRAPH: "1" (default) replays the eval body as ONE HIP graph
+    per size signature (_ScnBody), "2" as a head + tail pair with the deeper
+    level grids computed on a side stream while the head replays
+    (_ScnHead / _ScnTail), "0" runs it eagerly (A/B)."""
+    return os.environ.get("O3DML_SCN_GRAPH", "1")
+
+
+def _copy_into(dst_lists, src_lists):
+    for dl, sl in zip(dst_lists, src_lists):
+        for dst, src in zip(dl, sl):
+            dst.copy_(src)
 
 
 class _ScnBody:
@@ -375,6 +383,116 @@ class _ScnBody:
         return self.out
 
 
+class _ScnTail:
+    """The eval body from the second Convolution on (needs level grids 1..),
+    captured per grid-size signature under one _ScnHead, continuing the
+    head's rulebook scope (the level-0 map the decoder's last block reuses is
+    the head's); its graph also concatenates every lattice status word."""
+
+    def __init__(self, model, head, rest):
+        dev = head.pos[0].device
+        self.outs = [[o.clone() for o in outs] for outs in rest]
+        main = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):  # warm-up on the head's outputs of this frame, in a scratch scope
+            import copy
+            with rulebook_scope(scope_from(head.maps)) as scope:
+                model._body_tail(copy.copy(head.state), _FixedGrids(self.outs), fresh=True)
+                scope.pending[:0] = head.pending
+                ok = scope.check()
+                searches = scope.searches
+        main.wait_stream(side)
+        self.graph = None
+        if not ok or searches:  # off-lattice, or a layer on the search rulebook: eager path
+            return
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            with rulebook_scope(scope_from(head.maps)) as scope:
+                self.out = model._body_tail(copy.copy(head.state), _FixedGrids(self.outs), fresh=True)
+                pending = head.pending + scope.pending
+                self.status = torch.cat(pending) if pending else None
+
+
+class _ScnHead:
+    """The eval body up to the second Convolution — the input convolution,
+    the level-0 block, the first stride-2 Convolution (level-0 grid) and the
+    level-1 block — captured once per (voxels, level-0 grid points) as a HIP
+    graph.  Its replay runs while the host computes the deeper level grids
+    on a side stream (each calculate_grid reads its size back: those reads
+    then wait only for the grid kernels, not for the convolutions); the tail
+    (_ScnTail, per deeper grid sizes) replays after them.  Inputs are copied
+    into the graphs' static buffers; the lattice status words are read once
+    per frame, after the tail (the eager path's scope.check)."""
+
+    _MAX_TAILS = 4
+
+    def __init__(self, model, pos_list, feat_list, outs0, rest):
+        dev = pos_list[0].device
+        self.pos = [p.clone() for p in pos_list]
+        self.feat = [f.clone() for f in feat_list]
+        self.outs0 = [[o.clone() for o in outs0]]
+        self.tails = {}
+        main = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):  # warm-up of the whole body: lazy caches and library state
+            with rulebook_cache(defer_checks=True) as scope:
+                st = model._body_head(self.pos, self.feat, self.outs0)
+                model._body_tail(st, _FixedGrids([[o.clone() for o in outs] for outs in rest]))
+                ok = scope.check()
+                searches = scope.searches
+        main.wait_stream(side)
+        self.graph = None
+        if not ok or searches:
+            return
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            with rulebook_cache(defer_checks=True) as scope:
+                self.state = model._body_head(self.pos, self.feat, self.outs0)
+                self.maps = dict(scope.maps)
+                self.pending = list(scope.pending)
+
+    def replay(self, pos_list, feat_list, outs0):
+        _copy_into([self.pos, self.feat], [pos_list, feat_list])
+        _copy_into(self.outs0, [outs0])
+        self.graph.replay()
+
+    def tail(self, model, rest):
+        key = tuple(tuple(int(o.shape[0]) for o in outs) for outs in rest)
+        t = self.tails.pop(key, None)
+        if t is None:
+            t = _ScnTail(model, self, rest)
+            while len(self.tails) >= self._MAX_TAILS:
+                self.tails.pop(next(iter(self.tails)))
+        self.tails[key] = t
+        return t
+
+
+_GRID_STREAMS = {}
+
+
+def _grid_stream(dev):
+    """One side stream per device for the deeper level grids (created once;
+    O3DML_SCN_SIDE_PRIO=1: at the highest stream priority, A/B)."""
+    st = _GRID_STREAMS.get(str(dev))
+    if st is None:
+        prio = 0
+        if os.environ.get("O3DML_SCN_SIDE_PRIO", "0") == "1":
+            prio = torch.cuda.Stream.priority_range()[1]
+        st = _GRID_STREAMS[str(dev)] = torch.cuda.Stream(dev, priority=prio)
+    return st
+
+
+def _status_ok(status):
+    if status is None:
+        return True
+    st = status.cpu()
+    if bool((st & 1).any()):
+        raise RuntimeError("sparse_conv: two neighbours of one output share a kernel index")
+    return not bool((st & 4).any())
+
+
 class UNet(nn.Module):
     """sparseconvnet.py:568-653."""
 
@@ -386,18 +504,44 @@ class UNet(nn.Module):
     def n_down(self):
         return sum(isinstance(m, Convolution) for m in self.net)
 
+    def split_index(self, k):
+        """Index in self.net of the k-th Convolution (1-based; len(net) if
+        there are fewer): a run stopped there needs only the first k - 1
+        level grids."""
+        seen = 0
+        for j, m in enumerate(self.net):
+            if isinstance(m, Convolution):
+                seen += 1
+                if seen == k:
+                    return j
+        return len(self.net)
+
+    def begin(self, pos_list, feat_list):
+        """State of a (resumable) forward: run(state, grids, stop) advances it."""
+        import types
+        return types.SimpleNamespace(j=0, pos_list=pos_list, feat_list=feat_list, conv_pos=[], conv_out=[],
+                                     concat_feat=[], pre=None)
+
     def forward(self, pos_list, feat_list, grids=None):
+        if grids is None:
+            grids = _LevelGrids(pos_list, self.n_down())
+        st = self.begin(pos_list, feat_list)
+        self.run(st, grids)
+        return st.feat_list
+
+    def run(self, st, grids, stop=None):
         # conv_out: each Convolution's output grid in the fine level's units —
         # the DeConvolution's input positions (= 2 x the coarse positions,
         # exactly), the same tensor, so the DeConvolution's kernel map is
         # derived from the Convolution's (sparse_conv._transpose_of_cached)
-        conv_pos, conv_out, concat_feat = [], [], []
         mods = list(self.net)
+        stop = len(mods) if stop is None else stop
         fuse = _fusable(self)
-        if grids is None:
-            grids = _LevelGrids(pos_list, self.n_down())
-        pre = None  # pending folded BN + ReLU (eval): applied by the next conv's gather
-        for j, m in enumerate(mods):
+        conv_pos, conv_out, concat_feat = st.conv_pos, st.conv_out, st.concat_feat
+        pos_list, feat_list, pre = st.pos_list, st.feat_list, st.pre
+        # pending folded BN + ReLU (eval): applied by the next conv's gather
+        for j in range(st.j, stop):
+            m = mods[j]
             if fuse and isinstance(m, BatchNormBlock) and j + 2 < len(mods) and \
                     isinstance(mods[j + 1], ReLUBlock) and \
                     isinstance(mods[j + 2], (SubmanifoldSparseConv, Convolution, DeConvolution)):
@@ -440,7 +584,8 @@ class UNet(nn.Module):
                 feat_list = m(concat_feat.pop(), feat_list)
             else:
                 raise Exception("Unknown module {}".format(m))
-        return feat_list
+        st.j, st.pos_list, st.feat_list, st.pre = stop, pos_list, feat_list, pre
+        return st
 
 
 class SparseConvUnet(nn.Module):
@@ -464,9 +609,10 @@ class SparseConvUnet(nn.Module):
     _MAX_GRAPHS = 4  # captured bodies kept per model (size signatures, LRU)
 
     def forward(self, inputs):
-        if _graph_mode() and not self.training and not torch.is_grad_enabled() and len(inputs.point) and \
+        mode = _graph_mode()
+        if mode != "0" and not self.training and not torch.is_grad_enabled() and len(inputs.point) and \
                 inputs.point[0].is_cuda:
-            out = self._forward_graph(inputs)
+            out = self._forward_graph(inputs) if mode == "2" else self._forward_graph_single(inputs)
             if out is not None:
                 return out
         # lattice checks of all levels are read back once at the end; a
@@ -496,6 +642,21 @@ class SparseConvUnet(nn.Module):
         feat_list = self.relu(self.batch_norm(feat_list))
         return self.linear(feat_list)
 
+    def _body_head(self, pos_list, feat_list, outs0):
+        """The body up to the second Convolution (needs the level-0 grid only)."""
+        feat_list = self.sub_sparse_conv(feat_list, pos_list, voxel_size=1.0)
+        st = self.unet.begin(pos_list, feat_list)
+        return self.unet.run(st, _FixedGrids(outs0), stop=self.unet.split_index(2))
+
+    def _body_tail(self, st, grids, fresh=False):
+        """The rest of the body from a _body_head state.  fresh: st is a
+        shallow copy whose lists must not be shared with the head's."""
+        if fresh:
+            st.conv_pos, st.conv_out, st.concat_feat = list(st.conv_pos), list(st.conv_out), list(st.concat_feat)
+        self.unet.run(st, grids)
+        feat_list = self.relu(self.batch_norm(st.feat_list))
+        return self.linear(feat_list)
+
     def _param_key(self):
         """(address, version) of every parameter and buffer: a captured body
         is only replayed on the weights it was captured with.  The tensor list
@@ -509,9 +670,68 @@ class SparseConvUnet(nn.Module):
     def _apply(self, fn, *args, **kwargs):
         self.__dict__.pop("_o3dml_state_tensors", None)
         self.__dict__.pop("_o3dml_scn_bodies", None)
+        self.__dict__.pop("_o3dml_scn_single", None)
         return super()._apply(fn, *args, **kwargs)
 
     def _forward_graph(self, inputs):
+        """Eval forward with the body replayed from captured graphs (_ScnHead /
+        _ScnTail): the InputLayer and the level-0 grid run eagerly, the head
+        replays while the deeper grids are computed on a side stream, then the
+        tail.  None when the input is off the voxel lattice (the caller
+        recomputes eagerly)."""
+        pos_list, feat_list, index_maps = self._inputs(inputs)
+        n_down = self.unet.n_down()
+        if n_down < 2:
+            return None
+        outs0 = [ops.calculate_grid(x) for x in pos_list]
+        dev = pos_list[0].device
+        key = (str(dev), tuple(int(x.shape[0]) for x in pos_list), tuple(int(o.shape[0]) for o in outs0),
+               self._param_key())
+        heads = self.__dict__.setdefault("_o3dml_scn_bodies", {})
+        head = heads.pop(key, None)
+        fresh = head is None
+
+        def deeper(outs):
+            rest, p = [], [o / 2 for o in outs]
+            for _ in range(n_down - 1):
+                o = [ops.calculate_grid(x) for x in p]
+                rest.append(o)
+                p = [x / 2 for x in o]
+            return rest
+
+        if fresh:  # first frame of this signature: grids first, then the captures
+            rest = deeper(outs0)
+            head = _ScnHead(self, pos_list, feat_list, outs0, rest)
+            while len(heads) >= self._MAX_GRAPHS:
+                heads.pop(next(iter(heads)))
+        heads[key] = head
+        if head.graph is None:
+            return None
+        main = torch.cuda.current_stream(dev)
+        grids_in = torch.cuda.Event()
+        grids_in.record(main)  # the level-0 grid is ready (before the head's replay is queued)
+        head.replay(pos_list, feat_list, outs0)
+        if not fresh:
+            # the deeper grids on a side stream while the head replays: each
+            # size read waits only for the grid kernels
+            side = _grid_stream(dev)
+            side.wait_event(grids_in)
+            with torch.cuda.stream(side):
+                rest = deeper(outs0)
+            for outs in rest:
+                for t in outs:
+                    t.record_stream(main)
+            main.wait_stream(side)
+        tail = head.tail(self, rest)
+        if tail.graph is None:
+            return None
+        _copy_into(tail.outs, rest)
+        tail.graph.replay()
+        if not _status_ok(tail.status):
+            return None
+        return self.output_layer(tail.out, index_maps)
+
+    def _forward_graph_single(self, inputs):
         """Eval forward with the body replayed from a captured graph (_ScnBody):
         the InputLayer and the level grids (whose sizes the host reads) run
         eagerly, then the body of their size signature replays.  None when the
@@ -524,7 +744,7 @@ class SparseConvUnet(nn.Module):
             p = [o / 2 for o in outs]
         key = (str(pos_list[0].device), tuple(int(x.shape[0]) for x in pos_list),
                tuple(tuple(int(o.shape[0]) for o in outs) for outs in outs_per_level), self._param_key())
-        bodies = self.__dict__.setdefault("_o3dml_scn_bodies", {})
+        bodies = self.__dict__.setdefault("_o3dml_scn_single", {})
         body = bodies.pop(key, None)
         if body is None:
             body = _ScnBody(self, pos_list, feat_list, outs_per_level)

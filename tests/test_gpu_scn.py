@@ -103,13 +103,17 @@ def test_scn_fused_eval_matches_unfused(cuda, residual):
     assert err < 1e-5, err
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("residual", [True, False])
-def test_scn_graph_replay_equals_eager(cuda, residual, monkeypatch):
-    """The eval body captured as a HIP graph per size signature
-    (sparseconvnet._ScnBody, O3DML_SCN_GRAPH=1) gives the eager forward's
-    logits bit for bit: on the capture frame, on replays with new features,
-    after a second room (second signature) was captured in between, and after
-    the weights change (a new capture keyed on the parameter versions)."""
+def test_scn_graph_replay_equals_eager(cuda, residual, mode, monkeypatch):
+    """The eval body replayed from HIP graphs gives the eager forward's logits
+    bit for bit — mode "1": one graph per size signature
+    (sparseconvnet._ScnBody); mode "2": _ScnHead up to the second Convolution,
+    replayed while the deeper level grids are computed on a side stream, then
+    _ScnTail per deeper grid sizes — on the capture frame, on replays with new
+    features, after a second room (second signature) was captured in between,
+    and after the weights change (a new capture keyed on the parameter
+    versions)."""
     from o3dml_amd import sparseconvnet as S
     m = _model(residual, cuda)
     inp = _inputs(cuda)
@@ -120,7 +124,7 @@ def test_scn_graph_replay_equals_eager(cuda, residual, monkeypatch):
                                   batch_lengths=[keep.shape[0]])
 
     def run(x, graph):
-        monkeypatch.setenv("O3DML_SCN_GRAPH", "1" if graph else "0")
+        monkeypatch.setenv("O3DML_SCN_GRAPH", mode if graph else "0")
         with torch.no_grad():
             return m(x).clone()
 
@@ -128,11 +132,15 @@ def test_scn_graph_replay_equals_eager(cuda, residual, monkeypatch):
               room2, inp]
     for x in frames:
         assert torch.equal(run(x, True), run(x, False))
-    bodies = m.__dict__["_o3dml_scn_bodies"]
-    assert len(bodies) == 2 and all(b.graph is not None for b in bodies.values())
+    cache = m.__dict__["_o3dml_scn_single" if mode == "1" else "_o3dml_scn_bodies"]
+    assert len(cache) == 2 and all(b.graph is not None for b in cache.values())
+    if mode == "2":
+        assert all(isinstance(h, S._ScnHead) and len(h.tails) == 1 and
+                   all(t.graph is not None for t in h.tails.values()) for h in cache.values())
+    else:
+        assert all(isinstance(b, S._ScnBody) for b in cache.values())
     with torch.no_grad():
         for p in m.parameters():
             p.mul_(0.5)
     assert torch.equal(run(inp, True), run(inp, False))
-    assert len(bodies) == 3
-    assert isinstance(next(iter(bodies.values())), S._ScnBody)
+    assert len(cache) == 3
