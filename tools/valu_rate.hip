@@ -21,7 +21,8 @@
 
 constexpr int kUnroll = 16;  // step8 blocks per loop iteration (loop overhead < 3 %)
 enum Kind { FMA = 0, ADD = 1, AND = 2, CMP_CND = 3, CMP_S = 4, MBCNT = 5, BCNT = 6, MBCNT_HI = 7, MIN_U32 = 8,
-            LSHL_OR = 9, CNDMASK = 10, DPP_MOV = 11, MIN_F64 = 12, CMP_U64 = 13, FRS_TEST = 14 };
+            LSHL_OR = 9, CNDMASK = 10, DPP_MOV = 11, MIN_F64 = 12, CMP_U64 = 13, FRS_TEST = 14,
+            S_ADD = 15, EXEC_MASK = 16 };
 
 template <int KIND>
 __device__ __forceinline__ void step8(float (&a)[8], float b, float c) {
@@ -66,6 +67,26 @@ __device__ __forceinline__ void step8(float (&a)[8], float b, float c) {
             unsigned long long u = __builtin_bit_cast(unsigned long long, make_float2(a[j], a[j + 1]));
             asm volatile("v_cmp_lt_u64 %0, %1, %2" : "=s"(m) : "v"(u), "v"(0x3f80000012345678ull));
             asm volatile("v_cmp_gt_u64 %0, %1, %2" : "=s"(m) : "v"(u), "v"(0x3f80000012345678ull));
+        } else if constexpr (KIND == S_ADD) {
+            // scalar ALU, 16 instructions on 8 SGPRs in one block (no compiler
+            // padding between them): the CU's one scalar unit serves four SIMDs
+            if (j != 0) continue;
+            asm volatile(
+                    "s_add_u32 s20, s20, 1\n\ts_add_u32 s21, s21, 1\n\ts_add_u32 s22, s22, 1\n\ts_add_u32 s23, s23, 1\n\t"
+                    "s_add_u32 s24, s24, 1\n\ts_add_u32 s25, s25, 1\n\ts_add_u32 s26, s26, 1\n\ts_add_u32 s27, s27, 1\n\t"
+                    "s_add_u32 s20, s20, 1\n\ts_add_u32 s21, s21, 1\n\ts_add_u32 s22, s22, 1\n\ts_add_u32 s23, s23, 1\n\t"
+                    "s_add_u32 s24, s24, 1\n\ts_add_u32 s25, s25, 1\n\ts_add_u32 s26, s26, 1\n\ts_add_u32 s27, s27, 1"
+                    ::: "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "scc");
+        } else if constexpr (KIND == EXEC_MASK) {
+            // the exec-mask pattern around each FRS hit store, 4 times: VOPC
+            // into VCC, s_and_saveexec, s_or_b64 exec (12 instructions, 4 VALU)
+            if (j != 0) continue;
+            asm volatile(
+                    "v_cmp_lt_f32 vcc, %0, %1\n\ts_and_saveexec_b64 s[20:21], vcc\n\ts_or_b64 exec, exec, s[20:21]\n\t"
+                    "v_cmp_lt_f32 vcc, %2, %1\n\ts_and_saveexec_b64 s[20:21], vcc\n\ts_or_b64 exec, exec, s[20:21]\n\t"
+                    "v_cmp_lt_f32 vcc, %3, %1\n\ts_and_saveexec_b64 s[20:21], vcc\n\ts_or_b64 exec, exec, s[20:21]\n\t"
+                    "v_cmp_lt_f32 vcc, %4, %1\n\ts_and_saveexec_b64 s[20:21], vcc\n\ts_or_b64 exec, exec, s[20:21]"
+                    :: "v"(a[0]), "v"(b), "v"(a[1]), "v"(a[2]), "v"(a[3]) : "vcc", "s20", "s21", "exec", "scc");
         } else if constexpr (KIND == FRS_TEST) {
             // one candidate test of nns_frs.hip's search loop as compiled (distance,
             // compare into VCC, group mask, rank of the hit, clamped row address,
@@ -148,6 +169,8 @@ static const char* kname(int k) {
         case MIN_F64: return "v_min_f64+v_max_f64";
         case CMP_U64: return "v_cmp_lt_u64 (SGPR dst)";
         case FRS_TEST: return "FRS candidate test (17 VALU)";
+        case S_ADD: return "s_add_u32 (per SIMD-stream; the scalar unit is per CU)";
+        case EXEC_MASK: return "v_cmp vcc + s_and_saveexec + s_or exec (12 per step)";
         default: return "v_cmp_lt_f32+v_cndmask_b32";
     }
 }
@@ -181,7 +204,7 @@ static void run(int cus, int w, int iters, float* sink, unsigned long long* d_st
     double cyc_mean = cyc_sum / waves;
     double clk_ghz = cyc_sum / (wall_sum / (wall_mhz * 1e-3)) ;  // shader cycles per ns
     // VALU-pipe instructions per step8
-    const int per_step = KIND == CMP_CND ? 16 : KIND == FRS_TEST ? 17 : 8;
+    const int per_step = KIND == CMP_CND ? 16 : KIND == FRS_TEST ? 17 : KIND == S_ADD ? 16 : KIND == EXEC_MASK ? 12 : 8;
     double valu_per_wave = double(iters) * kUnroll * per_step;
     // per SIMD: w waves overlap, each issuing valu_per_wave
     double cyc_per_valu_simd_wave = cyc_mean / (w * valu_per_wave);
@@ -223,6 +246,8 @@ int main(int argc, char** argv) {
     for (int w : {1, 2, 8}) run<MIN_F64>(cus, w, iters, sink, st, wall_mhz);
     for (int w : {1, 8}) run<CMP_U64>(cus, w, iters, sink, st, wall_mhz);
     for (int w : {1, 2, 4, 8}) run<FRS_TEST>(cus, w, iters, sink, st, wall_mhz);
+    for (int w : {1, 2, 8}) run<S_ADD>(cus, w, iters, sink, st, wall_mhz);
+    for (int w : {1, 2, 8}) run<EXEC_MASK>(cus, w, iters, sink, st, wall_mhz);
     CHECK(hipFree(sink));
     CHECK(hipFree(st));
     return 0;
