@@ -2303,9 +2303,16 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
         const char* e = std::getenv("O3DML_GEMM_SHARED_BUF");
         return e ? std::atoi(e) != 0 : false;
     }();
-    if (vec4 && lds_path && shared_path && cout >= 64) {
+    // O3DML_GEMM_NW1=1 (A/B): narrow outputs (cout < 64) on the shared-A
+    // kernel with ONE wave per workgroup — with O3DML_GEMM_RB=2 a wave of 64
+    // rows whose filter fragment feeds two accumulators
+    static const bool nw1 = [] {
+        const char* e = std::getenv("O3DML_GEMM_NW1");
+        return e ? std::atoi(e) != 0 : false;
+    }();
+    if (vec4 && lds_path && shared_path && (cout >= 64 || nw1)) {
         // A tile shared by NW column-block waves (implicit_gemm_shared_kernel)
-        const int nw = (cout % 128 == 0) ? 4 : 2;
+        const int nw = cout < 64 ? 1 : ((cout % 128 == 0) ? 4 : 2);
         static const int rb = [] {
             const char* e = std::getenv("O3DML_GEMM_RB");  // 2 row blocks per wave: measured slower
             return (e && std::atoi(e) == 2) ? 2 : 1;
@@ -2337,6 +2344,8 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
     }
         if (nw == 4) {
             if (pre.scale) { O3DML_GEMM_SH_NT(true, 4) } else { O3DML_GEMM_SH_NT(false, 4) }
+        } else if (nw == 1) {
+            if (pre.scale) { O3DML_GEMM_SH_NT(true, 1) } else { O3DML_GEMM_SH_NT(false, 1) }
         } else {
             if (pre.scale) { O3DML_GEMM_SH_NT(true, 2) } else { O3DML_GEMM_SH_NT(false, 2) }
         }
