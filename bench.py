@@ -728,10 +728,23 @@ def scn_bench(dev, pos, reps, world=1, rank=0):
     feat = torch.rand((pos.shape[0], 3), device=dev)
     inp = types.SimpleNamespace(point=[pos], feat=[feat], batch_lengths=[pos.shape[0]])
     with torch.no_grad():
-        dt, _ = timed_run(lambda: m(inp), reps, 1, world, lambda: torch.cuda.synchronize(dev))
+        # two warmups: the body graph is captured on a size signature's second sighting
+        dt, _ = timed_run(lambda: m(inp), reps, 2, world, lambda: torch.cuda.synchronize(dev))
+        # the same frames with the body eager (O3DML_SCN_GRAPH=0): the rate of a
+        # stream whose scans never repeat a size signature (nothing captured)
+        prev = os.environ.get("O3DML_SCN_GRAPH")
+        os.environ["O3DML_SCN_GRAPH"] = "0"
+        try:
+            dt_eager, _ = timed_run(lambda: m(inp), reps, 1, world, lambda: torch.cuda.synchronize(dev))
+        finally:
+            if prev is None:
+                os.environ.pop("O3DML_SCN_GRAPH")
+            else:
+                os.environ["O3DML_SCN_GRAPH"] = prev
     counts, total, fps = frames_over_ranks(reps, dt, world)
     voxels = sum(gather_units(int(pos.shape[0]) * reps, world))
     return {"ms_per_frame": round(dt / reps * 1e3, 3), "frames_per_s": round(fps, 2),
+            "eager_ms_per_frame": round(dt_eager / reps * 1e3, 3),
             "mvoxels_per_s": round(voxels / dt / 1e6, 3), "n_gpus": world, "frames": total,
             "frames_per_rank": counts,
             "config": "SparseConvUnet m=32 residual reps=1 (sparseconvunet_scannet.yml), fp32 (exact f32 MFMA "

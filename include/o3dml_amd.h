@@ -304,6 +304,20 @@ int o3dml_calculate_grid_count(const float* positions, int64_t n_points, int64_t
 int o3dml_calculate_grid_fill(int64_t n_points, float* out_positions, void* workspace, size_t workspace_bytes,
                               void* stream);
 
+/* ---- SparseConvUnet eval plan: the reference InputLayer
+ * (ml3d/torch/models/sparseconvnet.py:296-331: voxelize at vs = 1 in
+ * [0, 40960)^3, per voxel its first point's position and its points' mean
+ * features, every point's voxel) and calculate_grid of every level
+ * (:388-401; level l's input = level l-1's grid / 2) in one call.
+ * points f32 [n,3], features f32 [n,fdim]; outputs in caller buffers of
+ * cap >= n rows per level: vox_pos f32 [cap,3], vox_feat f32 [cap,fdim],
+ * index_map int64 [cap], grids f32 [n_levels][cap][3]; sizes_host int64
+ * [1 + n_levels] = voxels, then each level's grid points. -------------- */
+size_t o3dml_scn_plan_workspace_size(int64_t n_points);
+int o3dml_scn_plan(const float* points, const float* features, int64_t n_points, int64_t cap, int fdim, int n_levels,
+                   float* vox_pos, float* vox_feat, int64_t* index_map, float* grids, int64_t* sizes_host,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- grid subsampling: replaces open3d.ml.contrib.subsample / subsample_batch
  * (ml3d/datasets/utils/dataprocessing.py:33-49 <- randlanet.py:133-139;
  * kpconv.py:2099-2155 <- dataloaders/concat_batcher.py:245-247).  KPConv

@@ -9,6 +9,7 @@
 // cell in input order, so per-cell sums run left to right exactly as the
 // oracle's and the results are bit-identical.  All HBM-streaming, integer/byte
 // work (no MFMA).
+#include <limits>
 #include <cmath>
 #include <vector>
 
@@ -604,7 +605,9 @@ constexpr int64_t kGridMax = int64_t(1) << 21;
 // or_and[0] / [1]: OR of the keys and of their complements (the bits that
 // vary among them, for the device-planned radix passes): one atomic pair per
 // wave.
-__global__ void grid_parent_kernel(const float* __restrict__ pos, int64_t n, uint64_t* __restrict__ keys,
+constexpr int kGridBlock = 256;  // grid_parent_kernel block (its LDS partials are sized for it)
+
+__global__ void __launch_bounds__(kGridBlock) grid_parent_kernel(const float* __restrict__ pos, int64_t n, uint64_t* __restrict__ keys,
                                    int64_t* __restrict__ flags, unsigned long long* __restrict__ or_and) {
     uint64_t o1 = 0, o0 = 0;
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
@@ -634,9 +637,21 @@ __global__ void grid_parent_kernel(const float* __restrict__ pos, int64_t n, uin
         o1 |= static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(o1), d, 64));
         o0 |= static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(o0), d, 64));
     }
-    // an atomic only for bits not yet recorded: same-address atomics
-    // serialise, and after the first waves nearly every wave adds nothing
+    // the block's waves combined in LDS, then one atomic pair per block and
+    // only for bits not yet recorded: same-address atomics serialise (one
+    // pair per wave cost a 88k-voxel level ~30 us)
+    __shared__ unsigned long long part[2][kGridBlock / 64];
+    const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
+        part[0][w] = o1;
+        part[1][w] = o0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < static_cast<int>(blockDim.x >> 6); ++k) {
+            o1 |= part[0][k];
+            o0 |= part[1][k];
+        }
         const unsigned long long c1 = __hip_atomic_load(&or_and[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long c0 = __hip_atomic_load(&or_and[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (o1 & ~c1) atomicOr(&or_and[0], static_cast<unsigned long long>(o1));
@@ -704,7 +719,9 @@ O3DML_API int o3dml_calculate_grid_count(const float* positions, int64_t n_point
         fill_async(g.flags, 0, 6 * sizeof(int64_t), st);
         const unsigned gr = stream_grid(n_points, 256);
         unsigned long long* or_and = reinterpret_cast<unsigned long long*>(g.flags + 4);
-        grid_parent_kernel<<<gr, 256, 0, st>>>(positions, n_points, g.keys, g.flags, or_and);
+        // one block per CU at most: fewer blocks, fewer same-address atomics
+        grid_parent_kernel<<<stream_grid(n_points, kGridBlock, 256), kGridBlock, 0, st>>>(positions, n_points,
+                                                                                          g.keys, g.flags, or_and);
         O3DML_LAUNCH_CHECK();
         Workspace sws = ws;
         // three 20-bit fields, 8 passes planned on the host; only the digits
@@ -737,6 +754,126 @@ O3DML_API int o3dml_calculate_grid_fill(int64_t n_points, float* out_positions, 
     if (n_points > 0) {
         grid_unique_write_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(g.sk, g.incl, n_points, out_positions);
         O3DML_LAUNCH_CHECK();
+    }
+    O3DML_GUARD_END
+}
+
+// ---------------------------------------------------------------------------
+// SparseConvUnet eval plan in ONE call (sparseconvnet.py:296-331 InputLayer,
+// :388-401 calculate_grid per level): voxelize at vs = 1 in [0, 40960)^3,
+// per voxel its first point's position and the mean of its points' features
+// (summed in point order, as reduce_subarrays_sum over the voxel-sorted
+// features, then divided by the count), the voxel of every input point (0 for
+// points outside the range, as the reference's zero-initialised reverse map),
+// and the stride-2 grid of every level (level l's input = level l-1's grid
+// / 2, exactly).  The host reads each size once (voxel count, one per level),
+// with no Python between the launches.  Outputs go to caller buffers sized
+// for n_points rows per level (every level has at most as many points as
+// the one before), at fixed offsets, so a captured body can read them in place.
+// ---------------------------------------------------------------------------
+namespace o3dml {
+namespace {
+__global__ void scn_splits_kernel(int64_t n, int64_t* __restrict__ rs) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        rs[0] = 0;
+        rs[1] = n;
+    }
+}
+
+__global__ void scn_input_kernel(const float* __restrict__ points, const float* __restrict__ features, int fdim,
+                                 const int64_t* __restrict__ pidx, const int64_t* __restrict__ prs, int64_t nvox,
+                                 float* __restrict__ vpos, float* __restrict__ vfeat,
+                                 int64_t* __restrict__ index_map) {
+    for (int64_t v = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; v < nvox;
+         v += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t s = prs[v], e = prs[v + 1];
+        const int64_t p0 = pidx[s];
+        vpos[3 * v] = points[3 * p0];
+        vpos[3 * v + 1] = points[3 * p0 + 1];
+        vpos[3 * v + 2] = points[3 * p0 + 2];
+        const float cnt = static_cast<float>(e - s);
+        for (int c = 0; c < fdim; ++c) {
+            float acc = 0.f;
+            for (int64_t j = s; j < e; ++j) acc += features[pidx[j] * fdim + c];
+            vfeat[v * fdim + c] = acc / cnt;
+        }
+        for (int64_t j = s; j < e; ++j) index_map[pidx[j]] = v;
+    }
+}
+
+__global__ void scn_half_kernel(const float* __restrict__ in, int64_t n3, float* __restrict__ out) {
+    for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n3;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+        out[i] = in[i] / 2.f;
+}
+}  // namespace
+}  // namespace o3dml
+
+O3DML_API size_t o3dml_scn_plan_workspace_size(int64_t n_points) {
+    const int64_t n = std::max<int64_t>(n_points, 1);
+    return ws_bytes<int64_t>(2) + ws_bytes<int32_t>(3 * n) + ws_bytes<int64_t>(n) + ws_bytes<int64_t>(n + 1) +
+           ws_bytes<int64_t>(2) + ws_bytes<float>(3 * n) +
+           std::max(o3dml_voxelize_workspace_size(n, 1), o3dml_calculate_grid_workspace_size(n));
+}
+
+// points / features: f32 [n, 3] / [n, fdim]; buffers of cap >= n rows: vox_pos
+// [cap, 3], vox_feat [cap, fdim], index_map int64 [cap], grids f32
+// [n_levels][cap][3] (level l's grid at row l * cap); sizes_host int64
+// [1 + n_levels] = voxels, then each level's grid points.
+O3DML_API int o3dml_scn_plan(const float* points, const float* features, int64_t n_points, int64_t cap, int fdim,
+                             int n_levels,
+                             float* vox_pos, float* vox_feat, int64_t* index_map, float* grids, int64_t* sizes_host,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+    O3DML_GUARD_BEGIN
+    O3DML_REQUIRE(fdim >= 1 && fdim <= 64 && n_levels >= 0, "scn_plan: bad fdim / n_levels");
+    O3DML_REQUIRE(cap >= n_points, "scn_plan: capacity %lld < %lld points", (long long)cap, (long long)n_points);
+    O3DML_REQUIRE(workspace_bytes >= o3dml_scn_plan_workspace_size(n_points), "scn_plan: workspace too small");
+    hipStream_t st = as_stream(stream);
+    const int64_t n = std::max<int64_t>(n_points, 1);
+    Workspace ws(workspace, workspace_bytes);
+    int64_t* rs = ws.take<int64_t>(2);
+    int32_t* coords = ws.take<int32_t>(3 * n);
+    int64_t* pidx = ws.take<int64_t>(n);
+    int64_t* prs = ws.take<int64_t>(n + 1);
+    int64_t* bsp = ws.take<int64_t>(2);
+    float* half = ws.take<float>(3 * n);
+    void* sub = ws.base + ws.used;
+    const size_t sub_bytes = ws.size - ws.used;
+    for (int l = 0; l <= n_levels; ++l) sizes_host[l] = 0;
+    fill_async(index_map, 0, sizeof(int64_t) * n_points, st);
+    if (n_points == 0) return 0;
+    scn_splits_kernel<<<1, 64, 0, st>>>(n_points, rs);
+    O3DML_LAUNCH_CHECK();
+    const float vs[3] = {1.f, 1.f, 1.f}, mn[3] = {0.f, 0.f, 0.f}, mx[3] = {40960.f, 40960.f, 40960.f};
+    const int64_t big = std::numeric_limits<int64_t>::max();
+    int64_t counts[2] = {0, 0};
+    int rc = o3dml_voxelize_count(points, n_points, 3, 1, rs, vs, mn, mx, big, big, counts, sub, sub_bytes, stream);
+    if (rc) return rc;
+    const int64_t nvox = counts[0];
+    rc = o3dml_voxelize_fill(n_points, 3, 1, vs, mn, mx, nvox, coords, pidx, prs, bsp, sub, sub_bytes, stream);
+    if (rc) return rc;
+    sizes_host[0] = nvox;
+    if (nvox > 0) {
+        scn_input_kernel<<<stream_grid(nvox, 256), 256, 0, st>>>(points, features, fdim, pidx, prs, nvox, vox_pos,
+                                                                  vox_feat, index_map);
+        O3DML_LAUNCH_CHECK();
+    }
+    const float* in = vox_pos;
+    int64_t m = nvox;
+    for (int l = 0; l < n_levels && m > 0; ++l) {
+        int64_t m_out = 0;
+        rc = o3dml_calculate_grid_count(in, m, &m_out, sub, sub_bytes, stream);
+        if (rc) return rc;
+        float* out = grids + static_cast<int64_t>(l) * cap * 3;
+        rc = o3dml_calculate_grid_fill(m, out, sub, sub_bytes, stream);
+        if (rc) return rc;
+        sizes_host[1 + l] = m_out;
+        if (l + 1 < n_levels && m_out > 0) {
+            scn_half_kernel<<<stream_grid(3 * m_out, 256), 256, 0, st>>>(out, 3 * m_out, half);
+            O3DML_LAUNCH_CHECK();
+        }
+        in = half;
+        m = m_out;
     }
     O3DML_GUARD_END
 }

@@ -139,6 +139,8 @@ SIGNATURES = {
     "o3dml_calculate_grid_workspace_size": (c_sz, [c_i64]),
     "o3dml_calculate_grid_count": (c_i32, [c_p, c_i64, c_p, c_p, c_sz, c_p]),
     "o3dml_calculate_grid_fill": (c_i32, [c_i64, c_p, c_p, c_sz, c_p]),
+    "o3dml_scn_plan_workspace_size": (c_sz, [c_i64]),
+    "o3dml_scn_plan": (c_i32, [c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "o3dml_grid_subsample_workspace_size": (c_sz, [c_i64, c_i64]),
     "o3dml_grid_subsample_count": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_f32, c_i64, c_p, c_p, c_sz, c_p]),
     "o3dml_grid_subsample_count_async": (c_i32, [c_p, c_i64, c_i64, c_p, c_f32, c_i64, c_p, c_p, c_sz, c_p]),

@@ -103,17 +103,20 @@ def test_scn_fused_eval_matches_unfused(cuda, residual):
     assert err < 1e-5, err
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["1", "2", "3"])
 @pytest.mark.parametrize("residual", [True, False])
 def test_scn_graph_replay_equals_eager(cuda, residual, mode, monkeypatch):
     """The eval body replayed from HIP graphs gives the eager forward's logits
     bit for bit — mode "1": one graph per size signature
     (sparseconvnet._ScnBody); mode "2": _ScnHead up to the second Convolution,
     replayed while the deeper level grids are computed on a side stream, then
-    _ScnTail per deeper grid sizes — on the capture frame, on replays with new
-    features, after a second room (second signature) was captured in between,
-    and after the weights change (a new capture keyed on the parameter
-    versions)."""
+    _ScnTail per deeper grid sizes; mode "3": the InputLayer and every level
+    grid as one library call (o3dml_scn_plan) into persistent buffers the
+    captured body reads in place — on the first sighting of a size signature
+    (eager, nothing captured in modes 1 / 3), on the capture frame, on replays
+    with new features, after a second room (second signature) was captured in
+    between, and after the weights change (a new capture keyed on the
+    parameter versions)."""
     from o3dml_amd import sparseconvnet as S
     m = _model(residual, cuda)
     inp = _inputs(cuda)
@@ -128,13 +131,19 @@ def test_scn_graph_replay_equals_eager(cuda, residual, mode, monkeypatch):
         with torch.no_grad():
             return m(x).clone()
 
-    frames = [inp, types.SimpleNamespace(point=inp.point, feat=[torch.rand_like(inp.feat[0])], batch_lengths=[n]),
-              room2, inp]
+    name = {"1": "_o3dml_scn_single", "2": "_o3dml_scn_bodies", "3": "_o3dml_scn_plan_bodies"}[mode]
+    assert torch.equal(run(inp, True), run(inp, False))
+    if mode != "2":  # captured on the second sighting of a size signature
+        assert len(m.__dict__.get(name, {})) == 0
+    frames = [types.SimpleNamespace(point=inp.point, feat=[torch.rand_like(inp.feat[0])], batch_lengths=[n]),
+              room2, room2, inp]
     for x in frames:
         assert torch.equal(run(x, True), run(x, False))
-    cache = m.__dict__["_o3dml_scn_single" if mode == "1" else "_o3dml_scn_bodies"]
+    cache = m.__dict__[name]
     assert len(cache) == 2 and all(b.graph is not None for b in cache.values())
-    if mode == "2":
+    if mode == "3":
+        assert all(isinstance(b, S._ScnPlanBody) for b in cache.values())
+    elif mode == "2":
         assert all(isinstance(h, S._ScnHead) and len(h.tails) == 1 and
                    all(t.graph is not None for t in h.tails.values()) for h in cache.values())
     else:
@@ -142,5 +151,25 @@ def test_scn_graph_replay_equals_eager(cuda, residual, mode, monkeypatch):
     with torch.no_grad():
         for p in m.parameters():
             p.mul_(0.5)
-    assert torch.equal(run(inp, True), run(inp, False))
+    for _ in range(2):
+        assert torch.equal(run(inp, True), run(inp, False))
     assert len(cache) == 3
+
+
+def test_scn_plan_matches_input_layer_and_grids(cuda):
+    """o3dml_scn_plan (one call) gives the InputLayer's voxel positions, mean
+    features and point -> voxel map and every level's calculate_grid bit for
+    bit (the eager path's torch / ops composition)."""
+    from o3dml_amd import ops
+    from o3dml_amd.sparseconvnet import InputLayer, _ScnPlan
+    inp = _inputs(cuda)
+    pts, feat = inp.point[0], inp.feat[0]
+    plan = _ScnPlan(8192 * (1 + pts.shape[0] // 8192), 3, 6, cuda)
+    n, pos, vf, imap, outs = plan.run(pts, feat)
+    avg, vpos, m = InputLayer()(feat, pts)
+    assert n == pts.shape[0] and torch.equal(pos, vpos) and torch.equal(vf, avg) and torch.equal(imap, m)
+    p = vpos
+    for lvl in outs:
+        ref = ops.calculate_grid(p)
+        assert torch.equal(lvl, ref)
+        p = ref / 2
