@@ -311,12 +311,14 @@ int o3dml_calculate_grid_fill(int64_t n_points, float* out_positions, void* work
  * (:388-401; level l's input = level l-1's grid / 2) in one call.
  * points f32 [n,3], features f32 [n,fdim]; outputs in caller buffers of
  * cap >= n rows per level: vox_pos f32 [cap,3], vox_feat f32 [cap,fdim],
- * index_map int64 [cap], grids f32 [n_levels][cap][3]; sizes_host int64
- * [1 + n_levels] = voxels, then each level's grid points. -------------- */
+ * index_map int64 [cap], grids f32 [n_levels][cap][3], halves f32
+ * [n_levels][cap][3] or NULL (each grid / 2, the next level's positions);
+ * sizes_host int64 [1 + n_levels] = voxels, then each level's grid
+ * points. -------------- */
 size_t o3dml_scn_plan_workspace_size(int64_t n_points);
 int o3dml_scn_plan(const float* points, const float* features, int64_t n_points, int64_t cap, int fdim, int n_levels,
-                   float* vox_pos, float* vox_feat, int64_t* index_map, float* grids, int64_t* sizes_host,
-                   void* workspace, size_t workspace_bytes, void* stream);
+                   float* vox_pos, float* vox_feat, int64_t* index_map, float* grids, float* halves,
+                   int64_t* sizes_host, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- grid subsampling: replaces open3d.ml.contrib.subsample / subsample_batch
  * (ml3d/datasets/utils/dataprocessing.py:33-49 <- randlanet.py:133-139;
@@ -474,6 +476,15 @@ int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, const floa
                                   int want_inverse, int defer_status, int* status_host, void* workspace,
                                   size_t workspace_bytes, void* lattice_workspace, size_t lattice_workspace_bytes,
                                   void* stream);
+/* o3dml_sparse_conv_lattice_map with the queries query_pos - query_shift
+ * (host float[3], or NULL): the layer's out_pos - offset * voxel_size
+ * (sparseconvnet.py:363-370 queries) subtracted in f32 inside the map
+ * kernels, bit-identical to materialising it. */
+int o3dml_sparse_conv_lattice_map_shifted(const float* inp_pos, int64_t n_in, const float* query_pos,
+                                          const float* query_shift, int64_t n_out, float voxel_size, int ksize,
+                                          int mirror, int normalize, const float* out_importance, int want_inverse,
+                                          int defer_status, int* status_host, void* workspace, size_t workspace_bytes,
+                                          void* lattice_workspace, size_t lattice_workspace_bytes, void* stream);
 /* The kernel map of the SparseConvTranspose that undoes a built SparseConv
  * map (same positions swapped, same kernel size, voxel size and offset: a
  * pair (coarse c, fine f) of the convolution at kernel index k is the pair

@@ -139,6 +139,23 @@ inline size_t ws_bytes(int64_t count) {
 // ---------------------------------------------------------------------------
 // device helpers
 // ---------------------------------------------------------------------------
+// sum over split-K slabs of element e, in slab order (0.f + p0 + p1 + ...),
+// the loads issued 16 at a time so a deep split is not one L2 round trip per
+// slab; the same bits as the plain loop
+__device__ __forceinline__ float sum_slabs(const float* __restrict__ part, int nsplit, int64_t total, int64_t e) {
+    float v = 0.f;
+    int s = 0;
+    for (; s + 16 <= nsplit; s += 16) {
+        float t[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t[j] = part[(s + j) * total + e];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v += t[j];
+    }
+    for (; s < nsplit; ++s) v += part[s * total + e];
+    return v;
+}
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 

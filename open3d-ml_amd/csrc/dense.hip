@@ -164,8 +164,7 @@ __global__ void dense_split_reduce_kernel(const float* __restrict__ part, int sp
     const int64_t total = n * m;
     for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        float v = 0.f;
-        for (int s = 0; s < splits; ++s) v += part[s * total + e];
+        float v = sum_slabs(part, splits, total, e);
         v += bias ? bias[e % m] : 0.f;
         if (act) v = v >= 0.f ? v : v * slope;
         out[e] = v;

@@ -2039,6 +2039,108 @@ __global__ void kernel_index_kernel(const float* __restrict__ inp_pos, const flo
     }
 }
 
+// Narrow inputs (cin <= 4: the network's first convolution on raw point
+// features, 3 -> m channels): an MFMA tile would spend 29 of its 32 reduction
+// lanes on zeros, so one lane per output row walks the K offsets with FMAs on
+// the VALU instead — the filter words are wave-uniform (scalar loads), the
+// map entries and then the gathered rows of 9 offsets are issued before their
+// FMAs (packed v_pk_fma_f32, two columns per instruction).  COLS output channels per lane
+// (cout % COLS == 0: no per-column guards, the filter words of an offset are
+// one contiguous run of scalar loads); SC: row / pair scales.
+// Per row: K map words + <= K*CIN*4 B gathered + COLS*4 B written.
+template <int CIN, int COLS, bool SC>
+__global__ void __launch_bounds__(256) small_cin_gemm_kernel(const int32_t* __restrict__ map, int K, int64_t n_out,
+                                                             const float* __restrict__ src,
+                                                             const float* __restrict__ sscale,
+                                                             const float* __restrict__ pscale,
+                                                             const float* __restrict__ Wt, int cout,
+                                                             const float* __restrict__ oscale,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ residual, float* __restrict__ out) {
+    const int64_t o = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+    const int cb = blockIdx.y * COLS;
+    const int64_t orow = o < n_out ? o : 0;  // lanes past the end compute row 0 and store nothing
+    const int32_t* mrow = map + orow * K;
+    float acc[COLS];
+#pragma unroll
+    for (int j = 0; j < COLS; ++j) acc[j] = 0.f;
+    constexpr int KB = 9;  // offsets whose loads are in flight together (a 3^3 kernel: 3 blocks)
+    for (int k0 = 0; k0 < K; k0 += KB) {
+        int32_t m[KB];
+#pragma unroll
+        for (int t = 0; t < KB; ++t) m[t] = k0 + t < K ? mrow[k0 + t] : -1;
+        float x[KB][CIN];
+#pragma unroll
+        for (int t = 0; t < KB; ++t) {
+            const bool valid = m[t] >= 0;
+            const int64_t mr = valid ? m[t] : 0;
+            const float* row = valid ? src + mr * CIN : g_zero_page;
+#pragma unroll
+            for (int c = 0; c < CIN; ++c) x[t][c] = row[c];
+            if constexpr (SC) {
+                const float f = valid ? *(sscale ? sscale + mr : g_one_page) *
+                                                *(pscale ? pscale + orow * K + k0 + t : g_one_page)
+                                      : 0.f;
+#pragma unroll
+                for (int c = 0; c < CIN; ++c) x[t][c] *= f;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < KB; ++t) {
+            if (k0 + t >= K) break;
+            const float* w = Wt + (static_cast<int64_t>(k0 + t) * cout + cb) * CIN;
+#pragma unroll
+            for (int j = 0; j < COLS; ++j) {
+#pragma unroll
+                for (int c = 0; c < CIN; ++c) acc[j] = fmaf(x[t][c], w[j * CIN + c], acc[j]);
+            }
+        }
+    }
+    if (o >= n_out) return;
+#pragma unroll
+    for (int j = 0; j < COLS; ++j) {
+        const int col = cb + j;
+        float v = acc[j];
+        if (oscale) v *= oscale[o];
+        if (bias) v += bias[col];
+        if (residual) v += residual[o * cout + col];
+        out[o * cout + col] = v;
+    }
+}
+
+// O3DML_GEMM_SMALL_CIN=0: cin <= 4 on the generic MFMA kernel (A/B)
+constexpr int kSmallCols = 16;
+static bool use_small_cin(int cin, int cout) {
+    static const bool on = [] {
+        const char* e = std::getenv("O3DML_GEMM_SMALL_CIN");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return on && cin >= 1 && cin <= 4 && cout % kSmallCols == 0;
+}
+
+static void launch_small_cin(hipStream_t st, const int32_t* map, int K, int64_t n_out, const float* src,
+                             const float* sscale, const float* pscale, const float* Wt, int cin, int cout,
+                             const float* oscale, const float* bias, const float* residual, float* out) {
+    const dim3 g(static_cast<unsigned>(ceil_div(n_out, 256)), static_cast<unsigned>(cout / kSmallCols));
+#define O3DML_SMALL(C, S)                                                                                    \
+    small_cin_gemm_kernel<C, kSmallCols, S><<<g, 256, 0, st>>>(map, K, n_out, src, sscale, pscale, Wt, cout, \
+                                                               oscale, bias, residual, out)
+#define O3DML_SMALL_K(C)                              \
+    do {                                              \
+        if (sscale || pscale) O3DML_SMALL(C, true);   \
+        else O3DML_SMALL(C, false);                   \
+    } while (0)
+    switch (cin) {
+        case 1: O3DML_SMALL_K(1); break;
+        case 2: O3DML_SMALL_K(2); break;
+        case 3: O3DML_SMALL_K(3); break;
+        default: O3DML_SMALL_K(4); break;
+    }
+#undef O3DML_SMALL_K
+#undef O3DML_SMALL
+    O3DML_LAUNCH_CHECK();
+}
+
 // out[o, c] = (sum_s part[s][o, c]) * oscale[o] + bias[c], splits in order
 __global__ void split_reduce_kernel(const float* __restrict__ part, int nsplit, int64_t n_out, int cout,
                                     const float* __restrict__ oscale, const float* __restrict__ bias,
@@ -2046,8 +2148,7 @@ __global__ void split_reduce_kernel(const float* __restrict__ part, int nsplit, 
     const int64_t total = n_out * cout;
     for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < total;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        float v = 0.f;
-        for (int s = 0; s < nsplit; ++s) v += part[s * total + e];
+        float v = sum_slabs(part, nsplit, total, e);
         const int64_t o = e / cout;
         if (oscale) v *= oscale[o];
         if (bias) v += bias[e - o * cout];
@@ -2275,6 +2376,10 @@ static void run_gemm(hipStream_t st, const int32_t* map, const int32_t* order, c
         return e ? std::atoi(e) != 0 : true;
     }();
     TimedRegion tr("sparse_conv_gemm", st);  // the GEMM kernel alone (bench roofline)
+    if (use_small_cin(cin, cout) && !pre.scale) {  // no split: tile counters (if any) stay untouched
+        launch_small_cin(st, map, K, n_out, src, sscale, pscale, Wt, cin, cout, oscale, bias, residual, out);
+        return;
+    }
     static const bool breg = [] {
         const char* e = std::getenv("O3DML_GEMM_BREG");
         return e ? std::atoi(e) != 0 : true;
@@ -2469,9 +2574,16 @@ __device__ __forceinline__ void lat_stat_init(int* v) {
 
 __device__ __forceinline__ int lat_stat_merge(int j, int a, int b) { return (j & 1) ? max(a, b) : min(a, b); }
 
+// Queries are qpos - qsh (the layer's offset * voxel size, subtracted here in
+// f32 as the torch expression out_pos - offset * vs would: same bits, no
+// elementwise launches); qsh = 0 for plain queries.
+struct QueryShift {
+    float d[3];
+};
+
 __global__ void __launch_bounds__(256) lattice_stats_kernel(const float* __restrict__ inp_pos, int64_t n_in,
                                                             const float* __restrict__ qpos, int64_t n_q,
-                                                            float inv_vs, int* __restrict__ part,
+                                                            QueryShift qsh, float inv_vs, int* __restrict__ part,
                                                             uint64_t* __restrict__ keys, int64_t cap,
                                                             int* __restrict__ status) {
     __shared__ int red[12][256];
@@ -2482,13 +2594,14 @@ __global__ void __launch_bounds__(256) lattice_stats_kernel(const float* __restr
         keys[e] = kLatEmpty;
     const float* pos = blockIdx.y ? qpos : inp_pos;
     const int64_t n = blockIdx.y ? n_q : n_in;
+    const QueryShift sh = blockIdx.y ? qsh : QueryShift{{0.f, 0.f, 0.f}};
     int v[12];
     lat_stat_init(v);
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            const float u = pos[3 * i + d] * inv_vs;
+            const float u = (pos[3 * i + d] - sh.d[d]) * inv_vs;
             const float fl = floorf(u);
             const float fr = u - fl;  // >= 0, so int ordering of the bits is float ordering
             const int key = fabsf(fl) < 1.0e6f ? static_cast<int>(fl) : 0x7fffffff;
@@ -2621,7 +2734,8 @@ __global__ void __launch_bounds__(256) lattice_insert_kernel(const float* __rest
 
 // map[o*K + k] for k = (kz*ks + ky)*ks + kx: one thread per (output, offset)
 __global__ void __launch_bounds__(256) lattice_map_kernel(const float* __restrict__ inp_pos,
-                                                          const float* __restrict__ qpos, int64_t n_out, float inv_vs,
+                                                          const float* __restrict__ qpos, QueryShift qsh,
+                                                          int64_t n_out, float inv_vs,
                                                           float radius, int ks, const LatticeOffsets* __restrict__ lop,
                                                           const uint64_t* __restrict__ keys,
                                                           const int32_t* __restrict__ vals, uint32_t mask,
@@ -2638,7 +2752,7 @@ __global__ void __launch_bounds__(256) lattice_map_kernel(const float* __restric
         }
         const int64_t o = e / K;
         const int k = static_cast<int>(e - o * K);
-        const float qx = qpos[3 * o], qy = qpos[3 * o + 1], qz = qpos[3 * o + 2];
+        const float qx = qpos[3 * o] - qsh.d[0], qy = qpos[3 * o + 1] - qsh.d[1], qz = qpos[3 * o + 2] - qsh.d[2];
         const int ix = k % ks, iy = (k / ks) % ks, iz = k / (ks * ks);
         const uint64_t key = lat_key(static_cast<int>(floorf(qx * inv_vs)) + lo.off[0][ix],
                                      static_cast<int>(floorf(qy * inv_vs)) + lo.off[1][iy],
@@ -2777,7 +2891,24 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
                                             const float* out_importance, int want_inverse, int defer_status,
                                             int* status_host, void* workspace, size_t workspace_bytes,
                                             void* lattice_workspace, size_t lattice_workspace_bytes, void* stream) {
+    return o3dml_sparse_conv_lattice_map_shifted(inp_pos, n_in, query_pos, nullptr, n_out, voxel_size, ksize, mirror,
+                                                 normalize, out_importance, want_inverse, defer_status, status_host,
+                                                 workspace, workspace_bytes, lattice_workspace,
+                                                 lattice_workspace_bytes, stream);
+}
+
+// The same with the queries given as query_pos - query_shift (host float[3],
+// or null for none): the layer's out_pos - offset * voxel_size without
+// materialising it.
+O3DML_API int o3dml_sparse_conv_lattice_map_shifted(const float* inp_pos, int64_t n_in, const float* query_pos,
+                                                    const float* query_shift, int64_t n_out, float voxel_size,
+                                                    int ksize, int mirror, int normalize, const float* out_importance,
+                                                    int want_inverse, int defer_status, int* status_host,
+                                                    void* workspace, size_t workspace_bytes, void* lattice_workspace,
+                                                    size_t lattice_workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
+    const QueryShift qsh = query_shift ? QueryShift{{query_shift[0], query_shift[1], query_shift[2]}}
+                                       : QueryShift{{0.f, 0.f, 0.f}};
     O3DML_REQUIRE(ksize >= 1 && ksize <= 3, "lattice rulebook: kernel size must be 1..3");
     const int K = ksize * ksize * ksize;
     hipStream_t st = as_stream(stream);
@@ -2808,15 +2939,15 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     // from them by every block of the next two kernels: no host round trip,
     // no finalize launch), 2. hash the input voxels, 3. K lookups per output
     const int nblk = static_cast<int>(std::min<int64_t>(kLatStatBlocks, ceil_div(std::max(n_in, n_out), 256)));
-    lattice_stats_kernel<<<dim3(nblk, 2), 256, 0, st>>>(inp_pos, n_in, query_pos, n_out, inv_vs, part, keys, cap,
-                                                         status);
+    lattice_stats_kernel<<<dim3(nblk, 2), 256, 0, st>>>(inp_pos, n_in, query_pos, n_out, qsh, inv_vs, part, keys,
+                                                         cap, status);
     O3DML_LAUNCH_CHECK();
     lattice_insert_kernel<<<stream_grid(n_in, 256) + 1, 256, 0, st>>>(inp_pos, n_in, inv_vs, keys, vals,
                                                                      static_cast<uint32_t>(cap - 1), part, nblk, ksize,
                                                                      mirror, lo, status);
     O3DML_LAUNCH_CHECK();
     lattice_map_kernel<<<stream_grid(n_out * K, 256), 256, 0, st>>>(
-            inp_pos, query_pos, n_out, inv_vs, 0.5f * voxel_size * static_cast<float>(ksize), ksize, lo, keys, vals,
+            inp_pos, query_pos, qsh, n_out, inv_vs, 0.5f * voxel_size * static_cast<float>(ksize), ksize, lo, keys, vals,
             static_cast<uint32_t>(cap - 1), status, map);
     O3DML_LAUNCH_CHECK();
     if (normalize) {
@@ -2838,6 +2969,14 @@ O3DML_API int o3dml_sparse_conv_lattice_map(const float* inp_pos, int64_t n_in, 
     O3DML_CHECK_HIP(hipMemcpyAsync(status_host, status, sizeof(int), hipMemcpyDeviceToHost, st));
     O3DML_CHECK_HIP(hipStreamSynchronize(st));
     O3DML_GUARD_END
+}
+
+__global__ void transpose_prep_kernel(int32_t* __restrict__ map, int64_t n, int* __restrict__ status,
+                                      const int* __restrict__ cstatus) {
+    if (blockIdx.x == 0 && threadIdx.x < 4) status[threadIdx.x] = threadIdx.x == 0 ? cstatus[0] : 0;
+    for (int64_t e = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; e < n;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x)
+        map[e] = -1;
 }
 
 O3DML_API int o3dml_sparse_conv_transpose_map(const void* conv_workspace, size_t conv_workspace_bytes,
@@ -2867,9 +3006,11 @@ O3DML_API int o3dml_sparse_conv_transpose_map(const void* conv_workspace, size_t
     int32_t* inv = ws.take<int32_t>(n_coarse * K);
     ws.take<float>(n_coarse * K);
     int* status = ws.take<int>(4);
-    copy_async(status, cstatus, sizeof(int), st);  // the partner's lattice / duplicate status
-    fill_async(status + 1, 0, 3 * sizeof(int), st);  // [2], [3]: no tile orders yet
-    if (n_fine > 0) fill_async(map, 0xff, sizeof(int32_t) * n_fine * K, st);
+    // the partner's lattice / duplicate status, [2], [3]: no tile orders yet,
+    // and the empty map: one launch
+    transpose_prep_kernel<<<stream_grid(std::max<int64_t>(n_fine * K, 1), 256), 256, 0, st>>>(map, n_fine * K, status,
+                                                                                             cstatus);
+    O3DML_LAUNCH_CHECK();
     if (n_coarse > 0 && n_fine > 0) {
         build_inverse_map_kernel<<<stream_grid(n_coarse * K, 256), 256, 0, st>>>(cmap, nullptr, n_coarse, K, n_fine, map,
                                                                                 nullptr, status);

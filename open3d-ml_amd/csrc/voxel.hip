@@ -822,8 +822,8 @@ O3DML_API size_t o3dml_scn_plan_workspace_size(int64_t n_points) {
 // [1 + n_levels] = voxels, then each level's grid points.
 O3DML_API int o3dml_scn_plan(const float* points, const float* features, int64_t n_points, int64_t cap, int fdim,
                              int n_levels,
-                             float* vox_pos, float* vox_feat, int64_t* index_map, float* grids, int64_t* sizes_host,
-                             void* workspace, size_t workspace_bytes, void* stream) {
+                             float* vox_pos, float* vox_feat, int64_t* index_map, float* grids, float* halves,
+                             int64_t* sizes_host, void* workspace, size_t workspace_bytes, void* stream) {
     O3DML_GUARD_BEGIN
     O3DML_REQUIRE(fdim >= 1 && fdim <= 64 && n_levels >= 0, "scn_plan: bad fdim / n_levels");
     O3DML_REQUIRE(cap >= n_points, "scn_plan: capacity %lld < %lld points", (long long)cap, (long long)n_points);
@@ -868,11 +868,14 @@ O3DML_API int o3dml_scn_plan(const float* points, const float* features, int64_t
         rc = o3dml_calculate_grid_fill(m, out, sub, sub_bytes, stream);
         if (rc) return rc;
         sizes_host[1 + l] = m_out;
-        if (l + 1 < n_levels && m_out > 0) {
-            scn_half_kernel<<<stream_grid(3 * m_out, 256), 256, 0, st>>>(out, 3 * m_out, half);
+        // the next level's positions: into `halves` at the level's offset when
+        // given (the body reads them in place), else a workspace temp
+        float* hl = halves ? halves + static_cast<int64_t>(l) * cap * 3 : half;
+        if ((l + 1 < n_levels || halves) && m_out > 0) {
+            scn_half_kernel<<<stream_grid(3 * m_out, 256), 256, 0, st>>>(out, 3 * m_out, hl);
             O3DML_LAUNCH_CHECK();
         }
-        in = half;
+        in = hl;
         m = m_out;
     }
     O3DML_GUARD_END

@@ -76,6 +76,8 @@ SIGNATURES = {
     "o3dml_sparse_conv_lattice_workspace_size": (c_sz, [c_i64]),
     "o3dml_sparse_conv_lattice_map": (c_i32, [c_p, c_i64, c_p, c_i64, c_f32, c_i32, c_i32, c_i32, c_p, c_i32, c_i32,
                                               c_p, c_p, c_sz, c_p, c_sz, c_p]),
+    "o3dml_sparse_conv_lattice_map_shifted": (c_i32, [c_p, c_i64, c_p, c_p, c_i64, c_f32, c_i32, c_i32, c_i32, c_p,
+                                                      c_i32, c_i32, c_p, c_p, c_sz, c_p, c_sz, c_p]),
     "o3dml_sparse_conv_map_status_offset": (c_sz, [c_i64, c_i64, c_i32]),
     "o3dml_sparse_conv_tile_order": (c_i32, [c_p, c_sz, c_i64, c_i64, c_i32, c_i32, c_p]),
     "o3dml_sparse_conv_transpose_map": (c_i32, [c_p, c_sz, c_i64, c_i64, c_i32, c_i32, c_p, c_sz, c_p]),
@@ -140,7 +142,7 @@ SIGNATURES = {
     "o3dml_calculate_grid_count": (c_i32, [c_p, c_i64, c_p, c_p, c_sz, c_p]),
     "o3dml_calculate_grid_fill": (c_i32, [c_i64, c_p, c_p, c_sz, c_p]),
     "o3dml_scn_plan_workspace_size": (c_sz, [c_i64]),
-    "o3dml_scn_plan": (c_i32, [c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
+    "o3dml_scn_plan": (c_i32, [c_p, c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_sz, c_p]),
     "o3dml_grid_subsample_workspace_size": (c_sz, [c_i64, c_i64]),
     "o3dml_grid_subsample_count": (c_i32, [c_p, c_i64, c_i64, c_p, c_p, c_f32, c_i64, c_p, c_p, c_sz, c_p]),
     "o3dml_grid_subsample_count_async": (c_i32, [c_p, c_i64, c_i64, c_p, c_f32, c_i64, c_p, c_p, c_sz, c_p]),

@@ -1,4 +1,5 @@
 """Drop-in for ``open3d.ml.torch.layers`` on the hot path."""
+import numpy as np
 import torch
 
 from . import ops
@@ -152,13 +153,12 @@ class SparseConv(torch.nn.Module):
             self._off_host = tuple(float(v) for v in self.offset.detach().cpu())  # one read per load
             self._off_ver = (self.offset._version, self.offset.device)
         off = self._off_host
-        if not any(off):
-            queries = out_positions
-        else:  # built only when the map is not cached already
-            def queries():
-                return (out_positions - (sign * vs) * self.offset.to(out_positions.device)).contiguous()
-        return sc.conv_lattice(self.kernel, kw.pop("bias", self.bias), inp_features, inp_positions, queries, vs,
-                               mirror=mirror, cache_key=(inp_positions, out_positions, sign) + off, **kw)
+        # queries out_positions - (sign * vs) * offset: the f32 product here,
+        # the f32 subtraction inside the map kernels (the torch expression's bits)
+        shift = None if not any(off) else tuple(float(np.float32(sign * vs) * np.float32(o)) for o in off)
+        return sc.conv_lattice(self.kernel, kw.pop("bias", self.bias), inp_features, inp_positions, out_positions, vs,
+                               mirror=mirror, cache_key=(inp_positions, out_positions, sign) + off, query_shift=shift,
+                               **kw)
 
     def forward_fused(self, inp_features, inp_positions, out_positions, voxel_size, pre=None, residual=None):
         """Inference form used by SparseConvUnet in eval mode:

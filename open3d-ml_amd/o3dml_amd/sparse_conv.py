@@ -364,11 +364,15 @@ def rulebook_cache(defer_checks=False):
 
 
 def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, voxel_size, mirror=False,
-                 inp_importance=None, normalize=False, out_importance=None, cache_key=None, pre=None, residual=None):
+                 inp_importance=None, normalize=False, out_importance=None, cache_key=None, pre=None, residual=None,
+                 query_shift=None):
     """Layer forward with the lattice rulebook (dense kernel map straight from a
     voxel hash; csrc/sparse_conv.hip o3dml_sparse_conv_lattice_map).  Returns
     None when the positions are not on one voxel lattice — the caller then
-    builds the rulebook with the Linf fixed-radius search (same map)."""
+    builds the rulebook with the Linf fixed-radius search (same map).
+    query_shift: 3 floats (f32 values) the map kernels subtract from
+    query_positions (the layer's offset * voxel size, same bits as the torch
+    expression)."""
     dev = gpu_device(inp_features, filters)
     ks = int(filters.shape[0])
     if tuple(filters.shape[:3]) != (ks, ks, ks) or ks > 3:
@@ -407,7 +411,9 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
         mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
         lws = workspace(lib.o3dml_sparse_conv_lattice_workspace_size(n_in), dev)
         status = np.zeros(1, np.int32)
-        _lib.call("o3dml_sparse_conv_lattice_map", ptr(ip), n_in, ptr(qp), n_out, float(voxel_size), ks,
+        qsh = None if query_shift is None else np.asarray(query_shift, np.float32).reshape(3)
+        _lib.call("o3dml_sparse_conv_lattice_map_shifted", ptr(ip), n_in, ptr(qp),
+                  None if qsh is None else qsh.ctypes.data, n_out, float(voxel_size), ks,
                   int(bool(mirror)), int(bool(normalize)), ptr(oimp), int(bool(want_grad)), int(defer),
                   status.ctypes.data, ptr(mws), mws.numel(), ptr(lws), lws.numel(), stream_handle(dev))
         status0 = int(status[0])

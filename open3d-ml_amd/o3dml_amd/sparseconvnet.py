@@ -303,13 +303,17 @@ class _LevelGrids:
 class _FixedGrids:
     """_LevelGrids' interface over the per-level grids of a captured body:
     level l's Convolution output grid, the next level's positions = grid / 2
-    computed in the body (one kernel, no extra graph input)."""
+    computed in the body (one kernel, no extra graph input) unless given
+    (halves_per_level: the plan's, same bits)."""
 
-    def __init__(self, outs_per_level):
+    def __init__(self, outs_per_level, halves_per_level=None):
         self.levels = list(outs_per_level)
+        self.halves = None if halves_per_level is None else list(halves_per_level)
 
     def next(self, pos_list):
         outs = self.levels.pop(0)
+        if self.halves is not None:
+            return outs, self.halves.pop(0)
         return outs, [o / 2 for o in outs]
 
 
@@ -346,6 +350,7 @@ class _ScnPlan:
         self.vfeat = torch.empty((cap, fdim), dtype=torch.float32, device=dev)
         self.imap = torch.empty(cap, dtype=torch.int64, device=dev)
         self.grids = torch.empty((n_levels, cap, 3), dtype=torch.float32, device=dev)
+        self.halves = torch.empty((n_levels, cap, 3), dtype=torch.float32, device=dev)
         self.ws = workspace(_lib.load().o3dml_scn_plan_workspace_size(cap), dev)
         self.sizes = np.zeros(1 + n_levels, np.int64)
 
@@ -356,11 +361,12 @@ class _ScnPlan:
         if n > self.cap:
             raise RuntimeError(f"scn plan: {n} points > capacity {self.cap}")
         _lib.call("o3dml_scn_plan", ptr(points), ptr(features), n, self.cap, self.fdim, self.n_levels, ptr(self.vpos),
-                  ptr(self.vfeat), ptr(self.imap), ptr(self.grids), self.sizes.ctypes.data, ptr(self.ws),
-                  self.ws.numel(), stream_handle(points.device))
+                  ptr(self.vfeat), ptr(self.imap), ptr(self.grids), ptr(self.halves), self.sizes.ctypes.data,
+                  ptr(self.ws), self.ws.numel(), stream_handle(points.device))
         nv = int(self.sizes[0])
         outs = [self.grids[l, :int(self.sizes[1 + l])] for l in range(self.n_levels)]
-        return n, self.vpos[:nv], self.vfeat[:nv], self.imap[:n], outs
+        halves = [self.halves[l, :int(self.sizes[1 + l])] for l in range(self.n_levels)]
+        return n, self.vpos[:nv], self.vfeat[:nv], self.imap[:n], (outs, halves)
 
 
 class _ScnPlanBody:
@@ -368,14 +374,14 @@ class _ScnPlanBody:
     gather) captured per size signature on a _ScnPlan's buffers and replayed
     per frame right after the one-call plan — no input copies."""
 
-    def __init__(self, model, pos, feat, imap, outs):
+    def __init__(self, model, pos, feat, imap, grids):
         dev = pos.device
         main = torch.cuda.current_stream(dev)
         side = torch.cuda.Stream(dev)
         side.wait_stream(main)
         with torch.cuda.stream(side):  # warm-up: lazy caches and library state outside the capture
             with rulebook_cache(defer_checks=True) as scope:
-                model._plan_body(pos, feat, imap, outs)
+                model._plan_body(pos, feat, imap, grids)
                 ok = scope.check()
                 searches = scope.searches
         main.wait_stream(side)
@@ -385,7 +391,7 @@ class _ScnPlanBody:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             with rulebook_cache(defer_checks=True) as scope:
-                self.out = model._plan_body(pos, feat, imap, outs)
+                self.out = model._plan_body(pos, feat, imap, grids)
                 self.status = torch.cat(scope.pending) if scope.pending else None
                 scope.pending.clear()
 
@@ -815,8 +821,9 @@ class SparseConvUnet(nn.Module):
             return None
         return self.output_layer(tail.out, index_maps)
 
-    def _plan_body(self, pos, feat, imap, outs):
-        out = self._body([pos], [feat], _FixedGrids([[o] for o in outs]))
+    def _plan_body(self, pos, feat, imap, grids):
+        outs, halves = grids
+        out = self._body([pos], [feat], _FixedGrids([[o] for o in outs], [[h] for h in halves]))
         return self.output_layer(out, [imap])
 
     _PLAN_STEP = 8192  # plan buffer capacity granularity (points)
@@ -844,7 +851,8 @@ class SparseConvUnet(nn.Module):
             self.__dict__["_o3dml_scn_plan"] = plan
             self.__dict__.pop("_o3dml_scn_plan_bodies", None)  # they read the old buffers
         plan = plan[1]
-        n, pos, feat, imap, outs = plan.run(pts, feats)
+        n, pos, feat, imap, grids = plan.run(pts, feats)
+        outs = grids[0]
         if any(o.shape[0] == 0 for o in outs):
             return None  # an empty level: the eager path (search rulebook)
         key = (n, pos.shape[0], tuple(o.shape[0] for o in outs), self._param_key())
@@ -853,9 +861,9 @@ class SparseConvUnet(nn.Module):
         if body is None:
             if not self._seen_before(("plan",) + key):  # first sighting: the body eagerly on the plan's buffers
                 with rulebook_cache(defer_checks=True) as scope:
-                    out = self._plan_body(pos, feat, imap, outs)
+                    out = self._plan_body(pos, feat, imap, grids)
                     return out if scope.check() else None
-            body = _ScnPlanBody(self, pos, feat, imap, outs)
+            body = _ScnPlanBody(self, pos, feat, imap, grids)
             while len(bodies) >= self._MAX_GRAPHS:
                 bodies.pop(next(iter(bodies)))
         bodies[key] = body

@@ -165,11 +165,12 @@ def test_scn_plan_matches_input_layer_and_grids(cuda):
     inp = _inputs(cuda)
     pts, feat = inp.point[0], inp.feat[0]
     plan = _ScnPlan(8192 * (1 + pts.shape[0] // 8192), 3, 6, cuda)
-    n, pos, vf, imap, outs = plan.run(pts, feat)
+    n, pos, vf, imap, (outs, halves) = plan.run(pts, feat)
     avg, vpos, m = InputLayer()(feat, pts)
     assert n == pts.shape[0] and torch.equal(pos, vpos) and torch.equal(vf, avg) and torch.equal(imap, m)
     p = vpos
-    for lvl in outs:
+    for lvl, half in zip(outs, halves):
         ref = ops.calculate_grid(p)
         assert torch.equal(lvl, ref)
         p = ref / 2
+        assert torch.equal(half, p)

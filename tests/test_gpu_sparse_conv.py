@@ -61,7 +61,8 @@ def _close(a, b, rtol=RTOL):
     assert np.abs(a - b).max() <= rtol * scale, f"max err {np.abs(a - b).max() / scale:.3e} (rel to max)"
 
 
-@pytest.mark.parametrize("cin,cout", [(32, 32), (3, 16), (64, 96), (96, 224), (64, 128)])
+@pytest.mark.parametrize("cin,cout", [(32, 32), (3, 16), (64, 96), (96, 224), (64, 128), (1, 32), (2, 16),
+                                      (4, 64), (3, 24)])
 def test_submanifold_conv_forward(cuda, cin, cout):
     from o3dml_amd import layers
     pos = _voxels(4000, 24, cin)
@@ -334,25 +335,27 @@ def test_bf16_split_large_and_nonfinite_inputs(cuda):
     assert np.abs(res[0][~hit] - res[1][~hit]).max() <= 1e-6 * scale
 
 
+@pytest.mark.parametrize("cin", [8, 3])
 @pytest.mark.parametrize("normalize,importance", [(False, False), (True, False), (True, True)])
-def test_duplicate_kernel_indices(cuda, normalize, importance):
+def test_duplicate_kernel_indices(cuda, normalize, importance, cin):
     """Off-lattice positions: several neighbours of one output share a kernel
     index (Open3D sums every pair).  The pairs are split into dense-map layers
     (sparse_conv._conv_layers); forward vs the oracle (which sums the CSR pairs
     directly), filter and feature gradients vs float64 autograd of the CSR
-    convolution, through layers.SparseConv's search rulebook."""
+    convolution, through layers.SparseConv's search rulebook.  cin 3: the
+    narrow-input VALU kernel (small_cin_gemm_kernel) with row / pair scales."""
     from o3dml_amd import layers, ops
     rng = np.random.default_rng(31)
     pos = (rng.random((1500, 3)) * 12).astype(np.float32)  # continuous positions: ~1.7 points per voxel
     inp = torch.from_numpy(pos).to(cuda)
-    conv = layers.SparseConv(8, 16, [3, 3, 3], use_bias=True, normalize=normalize).to(cuda)
+    conv = layers.SparseConv(cin, 16, [3, 3, 3], use_bias=True, normalize=normalize).to(cuda)
     torch.nn.init.normal_(conv.bias)
     conv.lattice_rulebook = False
     nb, kidx = conv._rulebook(inp, inp, 1.0, None, False, 1.0)
     idx, rs, kid = (nb.neighbors_index.cpu().numpy(), nb.neighbors_row_splits.cpu().numpy(), kidx.cpu().numpy())
     o = np.repeat(np.arange(len(rs) - 1), np.diff(rs))
     assert len(np.unique(o * 27 + kid)) < len(kid)  # duplicates present
-    x = torch.randn((1500, 8), device=cuda, requires_grad=True)
+    x = torch.randn((1500, cin), device=cuda, requires_grad=True)
     # per-input-point importance, gathered per pair (the layer's inp_importance)
     pimp = torch.rand(1500, device=cuda) if importance else None
     nimp = pimp[nb.neighbors_index.long()] if importance else None
@@ -372,7 +375,7 @@ def test_duplicate_kernel_indices(cuda, normalize, importance):
     gW, gx = torch.autograd.grad(out, (W, x), go)
     W64 = W.detach().cpu().double().requires_grad_(True)
     x64 = x.detach().cpu().double().requires_grad_(True)
-    Wf = W64.reshape(27, 8, 16)
+    Wf = W64.reshape(27, cin, 16)
     contrib = torch.einsum("pc,pcd->pd", x64[torch.from_numpy(idx).long()], Wf[torch.from_numpy(kid).long()])
     if importance:
         contrib = contrib * nimp.cpu().double()[:, None]
