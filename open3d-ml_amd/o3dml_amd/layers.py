@@ -143,19 +143,34 @@ class SparseConv(torch.nn.Module):
         self._avg_neighbors = nb.neighbors_index.shape[0] / max(1, out_positions.shape[0])
         return nb, kidx
 
+    def _offset_shift(self, vs, sign):
+        """(offset as host floats, query shift or None): queries are
+        out_positions - (sign * vs) * offset — the f32 product here, the f32
+        subtraction inside the map kernels (the torch expression's bits)."""
+        if getattr(self, "_off_ver", None) != (self.offset._version, self.offset.device):
+            self._off_host = tuple(float(v) for v in self.offset.detach().cpu())  # one read per load
+            self._off_ver = (self.offset._version, self.offset.device)
+        off = self._off_host
+        return off, (None if not any(off) else tuple(float(np.float32(sign * vs) * np.float32(o)) for o in off))
+
+    def prefetch_map(self, inp_positions, out_positions, voxel_size):
+        """Builds this layer's eval-mode lattice map for (inp -> out) on the
+        current stream ahead of the layer (sparse_conv.prefetch_lattice_map)."""
+        if not self.lattice_rulebook or self.normalize:
+            return False
+        mirror, sign = (True, -1.0) if isinstance(self, SparseConvTranspose) else (False, 1.0)
+        vs = _voxel_size_scalar(voxel_size, inp_positions)
+        off, shift = self._offset_shift(vs, sign)
+        return sc.prefetch_lattice_map(self.kernel_size[0], inp_positions, out_positions, vs, mirror, sign, off,
+                                       shift)
+
     def _lattice(self, inp_features, inp_positions, out_positions, voxel_size, hash_table, mirror, sign, **kw):
         """Lattice rulebook (same dense map as the Linf search, see
         sparse_conv.conv_lattice) unless a prebuilt search hash table is given."""
         if hash_table is not None or not self.lattice_rulebook:
             return None
         vs = _voxel_size_scalar(voxel_size, inp_positions)
-        if getattr(self, "_off_ver", None) != (self.offset._version, self.offset.device):
-            self._off_host = tuple(float(v) for v in self.offset.detach().cpu())  # one read per load
-            self._off_ver = (self.offset._version, self.offset.device)
-        off = self._off_host
-        # queries out_positions - (sign * vs) * offset: the f32 product here,
-        # the f32 subtraction inside the map kernels (the torch expression's bits)
-        shift = None if not any(off) else tuple(float(np.float32(sign * vs) * np.float32(o)) for o in off)
+        off, shift = self._offset_shift(vs, sign)
         return sc.conv_lattice(self.kernel, kw.pop("bias", self.bias), inp_features, inp_positions, out_positions, vs,
                                mirror=mirror, cache_key=(inp_positions, out_positions, sign) + off, query_shift=shift,
                                **kw)

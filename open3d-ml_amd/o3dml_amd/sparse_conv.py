@@ -5,6 +5,7 @@ The neighbourhood arrives as CSR pairs over OUTPUT points (neighbors_index,
 neighbors_kernel_index, neighbors_row_splits); the HIP library turns it into a
 dense kernel map and runs the MFMA implicit GEMM (forward), the inverse-map
 GEMM with W^T (input gradient) and split-K slabs (filter gradient)."""
+import collections
 import contextlib
 
 import numpy as np
@@ -301,6 +302,21 @@ class _RulebookScope:
         self.pending = []
         self.derived = 0  # transpose maps derived from their convolution partner (_transpose_of_cached)
         self.searches = 0  # layers that built the search rulebook (host round trips: not graph-capturable)
+        self.ready = {}  # key -> event of a map built on another stream (prefetch_lattice_map)
+        # maps still to be built ahead on `ahead_stream`: callables, one per map,
+        # returning True when they launched work; pump() runs the next one
+        self.ahead = collections.deque()
+        self.ahead_stream = None
+
+    def pump(self):
+        """Builds the next queued map on the ahead stream (called after every
+        lattice convolution's GEMM launch, so the map builds interleave with the
+        GEMMs in launch order — and in a captured graph's node order)."""
+        while self.ahead:
+            job = self.ahead.popleft()
+            with torch.cuda.stream(self.ahead_stream):
+                if job():
+                    return
 
     def check(self):
         """One host round trip for every deferred lattice check of the scope:
@@ -315,6 +331,11 @@ class _RulebookScope:
 
 
 _SCOPE = None  # the active rulebook_cache() scope
+
+
+def active_scope():
+    """The active rulebook_cache() scope, or None."""
+    return _SCOPE
 
 
 def note_search_rulebook():
@@ -363,6 +384,75 @@ def rulebook_cache(defer_checks=False):
         _SCOPE = prev
 
 
+def _build_lattice_map(scope, key, cache_key, ip, qp, query_shift, n_in, n_out, ks, voxel_size, mirror, normalize,
+                       oimp, want_grad, chans, dev):
+    """Builds (on the current stream) and, with a key, caches in the scope one
+    lattice kernel map: (map workspace, host status, late status word)."""
+    lib = _lib.load()
+    K = ks ** 3
+    late = None
+    # the lattice test stays on the device in a deferring scope and in a
+    # standalone call; the latter reads it once after the GEMM (a failed
+    # test leaves an all-empty, safe map, and the caller recomputes with the
+    # search rulebook), so no host round trip sits between map and GEMM
+    defer = (scope is None or scope.defer) and n_in > 0 and n_out > 0
+    mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
+    lws = workspace(lib.o3dml_sparse_conv_lattice_workspace_size(n_in), dev)
+    status = np.zeros(1, np.int32)
+    qsh = None if query_shift is None else np.asarray(query_shift, np.float32).reshape(3)
+    _lib.call("o3dml_sparse_conv_lattice_map_shifted", ptr(ip), n_in, ptr(qp),
+              None if qsh is None else qsh.ctypes.data, n_out, float(voxel_size), ks,
+              int(bool(mirror)), int(bool(normalize)), ptr(oimp), int(bool(want_grad)), int(defer),
+              status.ctypes.data, ptr(mws), mws.numel(), ptr(lws), lws.numel(), stream_handle(dev))
+    status0 = int(status[0])
+    if K > 8 and (scope is not None or chans >= TILE_ORDER_MIN_CHANNELS) and not status0 & 4:
+        # (no tile orders for K <= 8, csrc use_order) cached maps serve several
+        # convolutions: sort the GEMM tiles by offset mask once
+        _lib.call("o3dml_sparse_conv_tile_order", ptr(mws), mws.numel(), n_out, n_in, K, int(bool(want_grad)),
+                  stream_handle(dev))
+    if defer:
+        off = lib.o3dml_sparse_conv_map_status_offset(n_out, n_in, K)
+        if scope is None:
+            late = mws[off:off + 4].view(torch.int32)
+        else:
+            scope.pending.append(mws[off:off + 4].view(torch.int32))
+    if key is not None:
+        scope.maps[key] = (mws, status0, cache_key[0], cache_key[1])
+    return mws, status0, late
+
+
+def _scope_key(ks, mirror, normalize, want_grad, voxel_size, cache_key):
+    key = (ks, bool(mirror), bool(normalize), bool(want_grad), float(voxel_size)) + tuple(cache_key[2:])
+    return key + (id(cache_key[0]), cache_key[0]._version, id(cache_key[1]), cache_key[1]._version)
+
+
+def prefetch_lattice_map(ks, inp_positions, out_positions, voxel_size, mirror, sign, offset, query_shift):
+    """Builds, on the CURRENT stream, the eval-mode lattice map a layer of
+    kernel size ks, offset (host floats) and direction (mirror, sign) would
+    build for (inp_positions -> out_positions) in the active scope, and records
+    an event the layer's stream waits for when it finds the map
+    (conv_lattice).  A SparseConvTranspose whose SparseConv partner is in the
+    scope is derived from it, as conv_lattice does.  No-op outside a scope or
+    when the map is there already."""
+    scope = _SCOPE
+    if scope is None:
+        return False
+    dev = out_positions.device
+    cache_key = (inp_positions, out_positions, sign) + tuple(offset)
+    key = _scope_key(ks, mirror, False, False, voxel_size, cache_key)
+    if key in scope.maps:
+        return False
+    n_in, n_out = int(inp_positions.shape[0]), int(out_positions.shape[0])
+    hit = _transpose_of_cached(scope, key, cache_key, ks, n_in, n_out, False, dev) if mirror else None
+    if hit is None:
+        _build_lattice_map(scope, key, cache_key, inp_positions, out_positions, query_shift, n_in, n_out, ks,
+                           voxel_size, mirror, False, None, False, 0, dev)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    scope.ready[key] = ev
+    return True
+
+
 def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, voxel_size, mirror=False,
                  inp_importance=None, normalize=False, out_importance=None, cache_key=None, pre=None, residual=None,
                  query_shift=None):
@@ -392,44 +482,22 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
     key = None
     scope = _SCOPE
     if scope is not None and cache_key is not None and out_importance is None:
-        key = (ks, bool(mirror), bool(normalize), bool(want_grad), float(voxel_size)) + tuple(cache_key[2:])
-        key = key + (id(cache_key[0]), cache_key[0]._version, id(cache_key[1]), cache_key[1]._version)
+        key = _scope_key(ks, mirror, normalize, want_grad, voxel_size, cache_key)
     hit = scope.maps.get(key) if key is not None else None
     if hit is None and key is not None and mirror:
         hit = _transpose_of_cached(scope, key, cache_key, ks, n_in, n_out, want_grad, dev)
     late = None  # status word read after the GEMM (standalone call, no scope)
     if hit is not None:
         mws, status0 = hit[0], hit[1]
+        ev = scope.ready.pop(key, None)
+        if ev is not None:  # built on the scope's map stream (prefetch_lattice_map)
+            torch.cuda.current_stream(dev).wait_event(ev)
     else:
         if lazy_q:
             qp = to_dev(query_positions(), dev, torch.float32)
-        # the lattice test stays on the device in a deferring scope and in a
-        # standalone call; the latter reads it once after the GEMM (a failed
-        # test leaves an all-empty, safe map, and the caller recomputes with the
-        # search rulebook), so no host round trip sits between map and GEMM
-        defer = (scope is None or scope.defer) and n_in > 0 and n_out > 0
-        mws = workspace(lib.o3dml_sparse_conv_map_workspace_size(n_out, n_in, K), dev)
-        lws = workspace(lib.o3dml_sparse_conv_lattice_workspace_size(n_in), dev)
-        status = np.zeros(1, np.int32)
-        qsh = None if query_shift is None else np.asarray(query_shift, np.float32).reshape(3)
-        _lib.call("o3dml_sparse_conv_lattice_map_shifted", ptr(ip), n_in, ptr(qp),
-                  None if qsh is None else qsh.ctypes.data, n_out, float(voxel_size), ks,
-                  int(bool(mirror)), int(bool(normalize)), ptr(oimp), int(bool(want_grad)), int(defer),
-                  status.ctypes.data, ptr(mws), mws.numel(), ptr(lws), lws.numel(), stream_handle(dev))
-        status0 = int(status[0])
-        if K > 8 and (scope is not None or int(filters.shape[3]) * int(filters.shape[4]) >= TILE_ORDER_MIN_CHANNELS) \
-                and not status0 & 4:  # (no tile orders for K <= 8, csrc use_order)
-            # cached maps serve several convolutions: sort the GEMM tiles by offset mask once
-            _lib.call("o3dml_sparse_conv_tile_order", ptr(mws), mws.numel(), n_out, n_in, K, int(bool(want_grad)),
-                      stream_handle(dev))
-        if defer:
-            off = lib.o3dml_sparse_conv_map_status_offset(n_out, n_in, K)
-            if scope is None:
-                late = mws[off:off + 4].view(torch.int32)
-            else:
-                scope.pending.append(mws[off:off + 4].view(torch.int32))
-        if key is not None:
-            scope.maps[key] = (mws, status0, cache_key[0], cache_key[1])
+        mws, status0, late = _build_lattice_map(scope, key, cache_key, ip, qp, query_shift, n_in, n_out, ks,
+                                                voxel_size, mirror, normalize, oimp, want_grad,
+                                                int(filters.shape[3]) * int(filters.shape[4]), dev)
     if status0 & 4:
         return None
     if status0 & 1:
@@ -451,10 +519,14 @@ def conv_lattice(filters, bias, inp_features, inp_positions, query_positions, vo
                   ptr(x_c), n_in, ptr(ps), ptr(pb), ptr(res),
                   ptr(b_c), n_out, ptr(out), ptr(mws), mws.numel(),
                   ptr(fws), fws.numel(), stream_handle(dev))
+        if scope is not None and scope.ahead:
+            scope.pump()  # after this GEMM's launch: the next map build follows it in launch order
         return out if _late_ok(late) else None
     empty = torch.empty(0, dtype=torch.int64, device=dev)
     out = _ConvFn.apply(f, x, b, empty, empty, None, empty, _opt(inp_importance, dev), bool(normalize), oimp,
                         want_grad, (mws, n_out))
+    if scope is not None and scope.ahead:
+        scope.pump()
     if not _late_ok(late):
         return None
     return out if inp_features.is_cuda else out.cpu()

@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
+from . import sparse_conv as sc
 from .layers import SparseConv, SparseConvTranspose
 from .sparse_conv import rulebook_cache, rulebook_scope, scope_from
 
@@ -329,6 +330,22 @@ def _graph_mode():
     return os.environ.get("O3DML_SCN_GRAPH", "3")
 
 
+def _map_stream_on():
+    """O3DML_SCN_MAP_STREAM: "1" (default) builds the eval plan body's kernel
+    maps on a second stream (SparseConvUnet._plan_body), "0" in line (A/B)."""
+    return os.environ.get("O3DML_SCN_MAP_STREAM", "1") != "0"
+
+
+_MAP_STREAMS = {}
+
+
+def _map_stream(dev):
+    s = _MAP_STREAMS.get(dev)
+    if s is None:
+        s = _MAP_STREAMS[dev] = torch.cuda.Stream(dev)
+    return s
+
+
 def _copy_into(dst_lists, src_lists):
     for dl, sl in zip(dst_lists, src_lists):
         for dst, src in zip(dl, sl):
@@ -592,6 +609,28 @@ class UNet(nn.Module):
         return types.SimpleNamespace(j=0, pos_list=pos_list, feat_list=feat_list, conv_pos=[], conv_out=[],
                                      concat_feat=[], pre=None)
 
+    def map_schedule(self, pos, outs, halves):
+        """The (layer, input positions, output positions) of every kernel map
+        the forward builds, in the order it needs them, for one batch element
+        whose level grids and their halves are given (the eval plan's)."""
+        sched, conv_pos, conv_out, p, lvl = [], [], [], pos, 0
+        for m in self.net:
+            if isinstance(m, ResidualBlock):
+                sched.append((m.sub_sparse_conv1.net, p, p))
+                sched.append((m.sub_sparse_conv2.net, p, p))
+            elif isinstance(m, SubmanifoldSparseConv):
+                sched.append((m.net, p, p))
+            elif isinstance(m, Convolution):
+                conv_pos.append(p)
+                conv_out.append(outs[lvl])
+                sched.append((m.net, p, outs[lvl]))
+                p = halves[lvl]
+                lvl += 1
+            elif isinstance(m, DeConvolution):
+                sched.append((m.net, conv_out.pop(), conv_pos[-1]))
+                p = conv_pos.pop()
+        return sched
+
     def forward(self, pos_list, feat_list, grids=None):
         if grids is None:
             grids = _LevelGrids(pos_list, self.n_down())
@@ -822,8 +861,30 @@ class SparseConvUnet(nn.Module):
         return self.output_layer(tail.out, index_maps)
 
     def _plan_body(self, pos, feat, imap, grids):
+        """The eval body on the plan's buffers.  With O3DML_SCN_MAP_STREAM (default
+        1) every kernel map after the first is built ahead on a second stream
+        (sparse_conv.prefetch_lattice_map: the lattice maps, their tile orders,
+        the derived transpose maps), one more after each convolution's GEMM
+        launch (scope.pump), each convolution waiting only for its own map's event:
+        the map builds run beside the GEMM chain, and a captured graph holds the
+        two branches with their nodes interleaved in launch order (a graph is
+        dispatched node by node in that order)."""
         outs, halves = grids
+        dev = pos.device
+        side = None
+        scope = sc.active_scope()
+        if _map_stream_on() and not torch.is_grad_enabled() and scope is not None:
+            sched = [(self.sub_sparse_conv.net, pos, pos)] + self.unet.map_schedule(pos, outs, halves)
+            sched[0][0].prefetch_map(pos, pos, 1.0)  # the first map is needed at once: on this stream
+            main = torch.cuda.current_stream(dev)
+            side = _map_stream(dev)
+            side.wait_stream(main)
+            scope.ahead_stream = side
+            scope.ahead.extend((lambda l=l, i=i, o=o: l.prefetch_map(i, o, 1.0)) for l, i, o in sched[1:])
         out = self._body([pos], [feat], _FixedGrids([[o] for o in outs], [[h] for h in halves]))
+        if side is not None:
+            scope.ahead.clear()
+            torch.cuda.current_stream(dev).wait_stream(side)  # join (a capture must end on one stream)
         return self.output_layer(out, [imap])
 
     _PLAN_STEP = 8192  # plan buffer capacity granularity (points)

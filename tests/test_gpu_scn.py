@@ -103,7 +103,7 @@ def test_scn_fused_eval_matches_unfused(cuda, residual):
     assert err < 1e-5, err
 
 
-@pytest.mark.parametrize("mode", ["1", "2", "3"])
+@pytest.mark.parametrize("mode", ["1", "2", "3", "3-inline-maps"])
 @pytest.mark.parametrize("residual", [True, False])
 def test_scn_graph_replay_equals_eager(cuda, residual, mode, monkeypatch):
     """The eval body replayed from HIP graphs gives the eager forward's logits
@@ -116,8 +116,12 @@ def test_scn_graph_replay_equals_eager(cuda, residual, mode, monkeypatch):
     (eager, nothing captured in modes 1 / 3), on the capture frame, on replays
     with new features, after a second room (second signature) was captured in
     between, and after the weights change (a new capture keyed on the
-    parameter versions)."""
+    parameter versions).  Mode 3 builds the kernel maps on a second stream
+    (O3DML_SCN_MAP_STREAM, default on; "3-inline-maps": off)."""
     from o3dml_amd import sparseconvnet as S
+    if mode == "3-inline-maps":
+        monkeypatch.setenv("O3DML_SCN_MAP_STREAM", "0")
+        mode = "3"
     m = _model(residual, cuda)
     inp = _inputs(cuda)
     g = torch.Generator(device="cpu").manual_seed(1)
