@@ -2197,7 +2197,13 @@ static int gemm_splits(int64_t n_out, int K, int cin, int cout) {
     int64_t ns = ceil_div(target, tiles);
     ns = std::min<int64_t>(ns, std::max<int64_t>(1, (static_cast<int64_t>(K) * ceil_div(cin, 32)) / kGemmMinStages));
     ns = std::min<int64_t>(ns, kGemmSplitBytes / (n_out * cout * static_cast<int64_t>(sizeof(float))));
-    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ns, 64)));
+    // O3DML_GEMM_MAX_SPLITS (A/B): cap on the splits (the reduce reads every slab)
+    static const int64_t cap = [] {
+        const char* e = std::getenv("O3DML_GEMM_MAX_SPLITS");
+        const int64_t v = e ? std::atoll(e) : 64;
+        return v < 1 ? 1 : (v > 64 ? 64 : v);
+    }();
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(ns, cap)));
 }
 
 // Persistent grid of implicit_gemm_lds_kernel: O3DML_GEMM_PERSIST = v > 0

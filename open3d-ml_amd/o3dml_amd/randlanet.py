@@ -75,22 +75,26 @@ def concat_rows(a, ia, b, ib):
 
 def dense_act(a1, w, b, slope=None, a2=None, a2_index=None):
     """act([a1 | a2[a2_index]] @ w^T + b) in one launch (csrc/dense.hip):
-    a1 [N, k1], a2 [*, k2] (rows selected by a2_index int64 [N], or a2 [N,
-    k2] itself), w [M, k1 + k2], b [M]; act = LeakyReLU(slope), none if slope
-    is None."""
-    n, k1 = a1.shape
+    a1 [N, k1] (or None: k1 = 0), a2 [*, k2] (rows selected by a2_index int64
+    [N], or a2 [N, k2] itself), w [M, k1 + k2], b [M]; act = LeakyReLU(slope),
+    none if slope is None."""
+    if a1 is None:  # only the gathered operand: rows a2[a2_index] (or a2 itself)
+        n, k1 = (a2_index.shape[0] if a2_index is not None else a2.shape[0]), 0
+    else:
+        n, k1 = a1.shape
     k2 = 0 if a2 is None else a2.shape[1]
     m = w.shape[0]
-    out = torch.empty((n, m), dtype=torch.float32, device=a1.device)
+    dev = (a1 if a1 is not None else a2).device
+    out = torch.empty((n, m), dtype=torch.float32, device=dev)
     nbytes = _lib.load().o3dml_dense_act_workspace_size(n, k1 + k2, m)
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=a1.device) if nbytes else None
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev) if nbytes else None
     # operands bound to names: a temporary freed inside the argument list could
     # be handed to the next temporary by the caching allocator before the launch
-    a1 = a1.contiguous()
+    a1 = None if a1 is None else a1.contiguous()
     a2 = None if a2 is None else a2.contiguous()
     _lib.call("o3dml_dense_act", ptr(a1), k1, ptr(a2), k2,
               ptr(a2_index), ptr(w), ptr(b), n, m, int(slope is not None), float(slope or 0.0), ptr(out), ptr(ws),
-              0 if ws is None else ws.numel(), stream_handle(a1.device))
+              0 if ws is None else ws.numel(), stream_handle(dev))
     return out
 
 

@@ -748,11 +748,26 @@ class SparseConvUnet(nn.Module):
         return pos_list, feat_list, index_maps
 
     def _body(self, pos_list, feat_list, grids):
-        """Everything between the InputLayer (+ level grids) and the OutputLayer."""
+        """Everything between the InputLayer (+ level grids) and the head."""
         feat_list = self.sub_sparse_conv(feat_list, pos_list, voxel_size=1.0)
-        feat_list = self.unet(pos_list, feat_list, grids=grids)
+        return self.unet(pos_list, feat_list, grids=grids)
+
+    def _head(self, feat_list, index_maps):
+        """BatchNorm + ReLU, the Linear and the OutputLayer gather.  Eval
+        without autograd, one batch element: the folded BN + ReLU as one
+        addcmul + relu, then the Linear over the gathered rows in one dense
+        launch (randlanet.dense_act with a row index: logits of every point
+        straight from its voxel's features) — every eval path (eager and
+        captured) runs this same head."""
+        lin = self.linear.linear
+        if _fusable(self) and len(feat_list) == 1 and feat_list[0].is_cuda and isinstance(lin, nn.Linear):
+            from .randlanet import dense_act
+            s, t = _folded_bn(self.batch_norm)
+            y = torch.addcmul(t, feat_list[0], s).relu_()
+            return dense_act(None, lin.weight.detach(), None if lin.bias is None else lin.bias.detach(), a2=y,
+                             a2_index=index_maps[0])
         feat_list = self.relu(self.batch_norm(feat_list))
-        return self.linear(feat_list)
+        return self.output_layer(self.linear(feat_list), index_maps)
 
     def _body_head(self, pos_list, feat_list, outs0):
         """The body up to the second Convolution (needs the level-0 grid only)."""
@@ -766,8 +781,7 @@ class SparseConvUnet(nn.Module):
         if fresh:
             st.conv_pos, st.conv_out, st.concat_feat = list(st.conv_pos), list(st.conv_out), list(st.concat_feat)
         self.unet.run(st, grids)
-        feat_list = self.relu(self.batch_norm(st.feat_list))
-        return self.linear(feat_list)
+        return st.feat_list
 
     def _param_key(self):
         """(address, version) of every parameter and buffer: a captured body
@@ -858,7 +872,7 @@ class SparseConvUnet(nn.Module):
         tail.graph.replay()
         if not _status_ok(tail.status):
             return None
-        return self.output_layer(tail.out, index_maps)
+        return self._head(tail.out, index_maps)
 
     def _plan_body(self, pos, feat, imap, grids):
         """The eval body on the plan's buffers.  With O3DML_SCN_MAP_STREAM (default
@@ -885,7 +899,7 @@ class SparseConvUnet(nn.Module):
         if side is not None:
             scope.ahead.clear()
             torch.cuda.current_stream(dev).wait_stream(side)  # join (a capture must end on one stream)
-        return self.output_layer(out, [imap])
+        return self._head(out, [imap])
 
     _PLAN_STEP = 8192  # plan buffer capacity granularity (points)
 
@@ -956,7 +970,7 @@ class SparseConvUnet(nn.Module):
                     out = self._body(pos_list, feat_list, _FixedGrids(outs_per_level))
                     if not scope.check():
                         return None
-                return self.output_layer(out, index_maps)
+                return self._head(out, index_maps)
             body = _ScnBody(self, pos_list, feat_list, outs_per_level)
             while len(bodies) >= self._MAX_GRAPHS:
                 bodies.pop(next(iter(bodies)))  # least recently used first
@@ -966,7 +980,7 @@ class SparseConvUnet(nn.Module):
         out = body.run(pos_list, feat_list, outs_per_level)
         if out is None:
             return None
-        return self.output_layer(out, index_maps)
+        return self._head(out, index_maps)
 
     def _forward(self, inputs):
         pos_list, feat_list, index_maps = [], [], []
@@ -978,6 +992,4 @@ class SparseConvUnet(nn.Module):
         grids = _LevelGrids(pos_list, self.unet.n_down())  # before the first convolution is queued
         feat_list = self.sub_sparse_conv(feat_list, pos_list, voxel_size=1.0)
         feat_list = self.unet(pos_list, feat_list, grids=grids)
-        feat_list = self.relu(self.batch_norm(feat_list))
-        feat_list = self.linear(feat_list)
-        return self.output_layer(feat_list, index_maps)
+        return self._head(feat_list, index_maps)
