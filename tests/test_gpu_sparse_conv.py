@@ -88,6 +88,36 @@ def test_submanifold_conv_forward(cuda, cin, cout):
     _close_elem(out.detach().cpu().numpy(), t64, mag)
 
 
+@pytest.mark.parametrize("n,ext,cin,cout", [(300, 9, 128, 160), (120, 9, 192, 224), (2000, 14, 64, 64)])
+def test_deep_level_conv_split_k(cuda, n, ext, cin, cout):
+    """Few output rows and wide channels (SparseConvUnet's deep levels): the
+    GEMM splits its (offset, Cin-chunk) stages over 13-40 grid slabs and
+    split_reduce_kernel sums them — per element against the float64 truth,
+    plain and with the fused eval prologue (BN + ReLU gathered) and residual
+    epilogue."""
+    from o3dml_amd import layers
+    pos = _voxels(n, ext, n)
+    torch.manual_seed(1)
+    conv = layers.SparseConv(cin, cout, [3, 3, 3], use_bias=True).to(cuda)
+    torch.nn.init.normal_(conv.bias)
+    feat = torch.randn(len(pos), cin, device=cuda)
+    p = torch.from_numpy(pos).to(cuda)
+    oi, ors, _ = O.fixed_radius_search(pos, pos, 1.5, metric="Linf")
+    ok = O.kernel_index(pos, pos, oi, ors, [3, 3, 3], 1.0)
+    W = conv.kernel.detach().cpu().numpy()
+    with torch.no_grad():
+        out = conv(feat, p, p, 1.0)
+    _close_elem(out.cpu().numpy(), *_truth64(W, feat.cpu().numpy(), oi, ok, ors, conv.bias.detach().cpu().numpy()))
+    scale = torch.rand(cin, device=cuda) + 0.5
+    shift = torch.randn(cin, device=cuda) * 0.1
+    res = torch.randn(len(pos), cout, device=cuda)
+    with torch.no_grad():
+        fused = conv.forward_fused(feat, p, p, 1.0, pre=(scale, shift), residual=res)
+    x = torch.relu(feat * scale + shift).cpu().numpy()
+    t64, mag = _truth64(W, x, oi, ok, ors, conv.bias.detach().cpu().numpy())
+    _close_elem(fused.cpu().numpy(), t64 + res.cpu().numpy(), mag + np.abs(res.cpu().numpy()))
+
+
 def test_strided_and_transposed_conv(cuda):
     """Convolution 2^3 stride 2 (calculate_grid) and its DeConvolution adjoint
     (sparseconvnet.py:388-482)."""
