@@ -30,8 +30,42 @@ struct VoxParams {
     int nb;
 };
 
-__global__ void vox_keys_kernel(const float* __restrict__ pts, int64_t n, const int64_t* __restrict__ rs, VoxParams vp,
-                                uint64_t* __restrict__ keys) {
+// OR of a block's keys and of their complements into or_and[0..1] (zeroed by
+// the caller): one atomic pair per block, only for bits not yet recorded.
+// 256 threads per block.
+__device__ __forceinline__ void or_and_block(uint64_t o1, uint64_t o0, unsigned long long* __restrict__ or_and) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        o1 |= static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(o1), d, 64));
+        o0 |= static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(o0), d, 64));
+    }
+    __shared__ unsigned long long part[2][4];
+    if ((threadIdx.x & 63) == 0) {
+        part[0][threadIdx.x >> 6] = o1;
+        part[1][threadIdx.x >> 6] = o0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < static_cast<int>(blockDim.x >> 6); ++k) {
+            o1 |= part[0][k];
+            o0 |= part[1][k];
+        }
+        const unsigned long long c1 = __hip_atomic_load(&or_and[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long c0 = __hip_atomic_load(&or_and[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (o1 & ~c1) atomicOr(&or_and[0], static_cast<unsigned long long>(o1));
+        if (o0 & ~c0) atomicOr(&or_and[1], static_cast<unsigned long long>(o0));
+    }
+}
+
+// or_and (nullable, zeroed): OR of the keys and of their complements — the
+// bits that vary among them, so the radix sort runs only the digits that do
+// (device-planned passes, as calculate_grid); one atomic pair per block, and
+// only for bits not yet recorded.  256 threads per block.
+__global__ void __launch_bounds__(256) vox_keys_kernel(const float* __restrict__ pts, int64_t n,
+                                                       const int64_t* __restrict__ rs, VoxParams vp,
+                                                       uint64_t* __restrict__ keys,
+                                                       unsigned long long* __restrict__ or_and) {
+    uint64_t o1 = 0, o0 = 0;
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int b = batch_of(i, rs, vp.nb);
@@ -45,8 +79,13 @@ __global__ void vox_keys_kernel(const float* __restrict__ pts, int64_t n, const 
             }
             key += static_cast<int64_t>(c) * vp.stride[d];
         }
-        keys[i] = static_cast<uint64_t>(ok ? key : vp.invalid_key);
+        const uint64_t kv = static_cast<uint64_t>(ok ? key : vp.invalid_key);
+        keys[i] = kv;
+        o1 |= kv;
+        o0 |= ~kv;
     }
+    if (!or_and) return;  // uniform
+    or_and_block(o1, o0, or_and);
 }
 
 // head[j] = 1 where a new valid segment starts; also records n_valid.
@@ -161,8 +200,11 @@ struct SubBatch {
     uint64_t nx, ny;
 };
 
-__global__ void sub_keys_kernel(const float* __restrict__ pts, int64_t n, const int64_t* __restrict__ rs, int nb,
-                                const SubBatch* __restrict__ sb, uint64_t* __restrict__ keys) {
+__global__ void __launch_bounds__(256) sub_keys_kernel(const float* __restrict__ pts, int64_t n,
+                                                       const int64_t* __restrict__ rs, int nb,
+                                                       const SubBatch* __restrict__ sb, uint64_t* __restrict__ keys,
+                                                       unsigned long long* __restrict__ or_and) {
+    uint64_t o1 = 0, o0 = 0;
     for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int b = batch_of(i, rs, nb);
@@ -171,8 +213,12 @@ __global__ void sub_keys_kernel(const float* __restrict__ pts, int64_t n, const 
         const uint64_t iy = static_cast<uint64_t>(floorf((pts[3 * i + 1] - s.oy) / s.dl));
         const uint64_t iz = static_cast<uint64_t>(floorf((pts[3 * i + 2] - s.oz) / s.dl));
         const uint64_t key = ix + s.nx * iy + s.nx * s.ny * iz;
-        keys[i] = (static_cast<uint64_t>(b) << 48) | (key & ((uint64_t(1) << 48) - 1));
+        const uint64_t kv = (static_cast<uint64_t>(b) << 48) | (key & ((uint64_t(1) << 48) - 1));
+        keys[i] = kv;
+        o1 |= kv;
+        o0 |= ~kv;
     }
+    or_and_block(o1, o0, or_and);
 }
 
 __global__ void sub_caps_kernel(const int64_t* __restrict__ start, const int64_t* __restrict__ incl, int64_t n,
@@ -275,6 +321,17 @@ __global__ void sub_grid_kernel(const float* __restrict__ bbox, const int64_t* _
                 x.ny = static_cast<uint64_t>(ey) + 1;
                 const uint64_t nz = static_cast<uint64_t>(ez) + 1;
                 if (static_cast<double>(x.nx) * x.ny * nz >= 2.8e14) bad = 1;
+                // power-of-two row / plane pitches when they fit the 48 key
+                // bits: the same cell order, each coordinate in whole bits, so
+                // the sort runs only the digits the keys vary in (or_and)
+                uint64_t px = 1, py = 1, pz = 1;
+                while (px < x.nx) px <<= 1;
+                while (py < x.ny) py <<= 1;
+                while (pz < nz) pz <<= 1;
+                if (static_cast<double>(px) * py * pz < 2.8e14) {
+                    x.nx = px;
+                    x.ny = py;
+                }
             }
         }
         sb[b] = x;
@@ -332,13 +389,16 @@ inline size_t seg_state_bytes(int64_t n, int nb) {
 }
 
 // keys (unsorted) -> sorted segments, heads, starts, batch firsts.
+// or_and (nullable): the keys' OR / complement-OR pair (vox_keys_kernel), in
+// s.scalars[6..7], which the caller zeroed before the keys (prefilled)
 inline void sort_segments(const uint64_t* keys, int64_t n, int end_bit, uint64_t invalid, int nb, bool batch_shift,
-                          uint64_t batch_div, SegState& s, Workspace& ws, hipStream_t st) {
-    fill_async(s.scalars, 0, sizeof(int64_t) * 8, st);
+                          uint64_t batch_div, SegState& s, Workspace& ws, hipStream_t st,
+                          const uint64_t* or_and = nullptr) {
+    if (!or_and) fill_async(s.scalars, 0, sizeof(int64_t) * 8, st);
     const unsigned g = stream_grid(n > 0 ? n : 1, 256);
     if (n > 0) {
         Workspace sws = ws;
-        prim::radix_sort_pairs<uint64_t>(keys, nullptr, s.sk, s.sidx, n, end_bit, sws, st);
+        prim::radix_sort_pairs<uint64_t>(keys, nullptr, s.sk, s.sidx, n, end_bit, sws, st, -1, or_and);
         int64_t* head = s.keep;  // reuse as scratch before keep is computed
         seg_heads_kernel<<<g, 256, 0, st>>>(s.sk, n, invalid, head, s.scalars);
         O3DML_LAUNCH_CHECK();
@@ -359,7 +419,8 @@ inline VoxParams make_vox_params(int ndim, int nb, const float* vs, const float*
     VoxParams vp{};
     vp.ndim = ndim;
     vp.nb = nb;
-    int64_t h = 1;
+    int64_t h = 1, h2 = 1;
+    int64_t stride2[kMaxVoxDim];
     for (int d = 0; d < ndim; ++d) {
         vp.inv[d] = 1.0 / static_cast<double>(vs[d]);
         vp.mn[d] = static_cast<double>(mn[d]);
@@ -367,6 +428,17 @@ inline VoxParams make_vox_params(int ndim, int nb, const float* vs, const float*
         if (vp.ext[d] < 0) vp.ext[d] = 0;
         vp.stride[d] = h;
         h *= vp.ext[d];
+        // power-of-two strides: the same order of (batch, coordinates) keys,
+        // each coordinate in whole bits, so only the digits its values vary in
+        // need a sort pass (the keys' OR / AND plan the passes)
+        stride2[d] = h2;
+        int64_t p2 = 1;
+        while (p2 < vp.ext[d] && p2 < (int64_t(1) << 40)) p2 <<= 1;
+        h2 = h2 < (int64_t(1) << 56) / p2 ? h2 * p2 : (int64_t(1) << 56);
+    }
+    if (h2 < (int64_t(1) << 56) / (nb + 1)) {  // fits the 64-bit key budget: use it
+        for (int d = 0; d < ndim; ++d) vp.stride[d] = stride2[d];
+        h = h2;
     }
     vp.batch_hash = h > 0 ? h : 1;
     vp.invalid_key = vp.batch_hash * nb;
@@ -402,12 +474,16 @@ O3DML_API int o3dml_voxelize_count(const float* points, int64_t n_points, int nd
     uint64_t* keys = ws.take<uint64_t>(n_points);
     const unsigned g = stream_grid(n_points > 0 ? n_points : 1, 256);
     TimedRegion tr("voxelize_count", st);  // device time of the phase (bench op roofline)
+    // scalars zeroed first: [6..7] collect the keys' OR / complement OR
+    fill_async(s.scalars, 0, sizeof(int64_t) * 8, st);
+    unsigned long long* or_and = reinterpret_cast<unsigned long long*>(s.scalars + 6);
     if (n_points > 0) {
-        vox_keys_kernel<<<g, 256, 0, st>>>(points, n_points, row_splits, vp, keys);
+        vox_keys_kernel<<<g, 256, 0, st>>>(points, n_points, row_splits, vp, keys, or_and);
         O3DML_LAUNCH_CHECK();
     }
     sort_segments(keys, n_points, prim::bits_needed(static_cast<uint64_t>(vp.invalid_key)),
-                  static_cast<uint64_t>(vp.invalid_key), nb, false, static_cast<uint64_t>(vp.batch_hash), s, ws, st);
+                  static_cast<uint64_t>(vp.invalid_key), nb, false, static_cast<uint64_t>(vp.batch_hash), s, ws, st,
+                  reinterpret_cast<const uint64_t*>(or_and));
     if (n_points > 0) {
         vox_caps_kernel<<<g, 256, 0, st>>>(s.sk, s.start, s.incl, s.scalars, n_points, s.bfirst, vp.batch_hash,
                                            max_voxels, max_points_per_voxel, s.keep, s.npts);
@@ -525,11 +601,13 @@ O3DML_API int o3dml_grid_subsample_count_async(const float* points, int64_t n_po
     O3DML_LAUNCH_CHECK();
     sub_grid_kernel<<<1, 256, 0, st>>>(bbox_d, row_splits, nb, dl, sb_d, out);
     O3DML_LAUNCH_CHECK();
-    sub_keys_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(points, n_points, row_splits, nb, sb_d, keys);
+    fill_async(s.scalars, 0, sizeof(int64_t) * 8, st);  // [6..7]: the keys' OR / complement OR
+    unsigned long long* or_and = reinterpret_cast<unsigned long long*>(s.scalars + 6);
+    sub_keys_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(points, n_points, row_splits, nb, sb_d, keys, or_and);
     O3DML_LAUNCH_CHECK();
     const uint64_t invalid = ~uint64_t(0);
     sort_segments(keys, n_points, 48 + prim::bits_needed(static_cast<uint64_t>(nb > 1 ? nb - 1 : 0)), invalid, nb,
-                  true, 48, s, ws, st);
+                  true, 48, s, ws, st, reinterpret_cast<const uint64_t*>(or_and));
     sub_caps_kernel<<<stream_grid(n_points, 256), 256, 0, st>>>(s.start, s.incl, n_points, s.sk, s.bfirst, max_p,
                                                                s.keep);
     O3DML_LAUNCH_CHECK();

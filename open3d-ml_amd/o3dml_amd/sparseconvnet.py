@@ -206,15 +206,13 @@ class ResidualBlock(nn.Module):
         self.sub_sparse_conv2 = SubmanifoldSparseConv(in_channels=nOut, filters=nOut, kernel_size=[3, 3, 3])
 
     def forward(self, feat_list, pos_list):
-        out1 = self.lin(feat_list)
         if _fusable(self):
             pre1, pre2 = _folded_bn(self.batch_norm1), _folded_bn(self.batch_norm2)
             c1, c2 = self.sub_sparse_conv1.net, self.sub_sparse_conv2.net
-            out = []
-            for f, p, r in zip(feat_list, pos_list, out1):
-                h = c1.forward_fused(f, p, p, 1.0, pre=pre1)
-                out.append(c2.forward_fused(h, p, p, 1.0, pre=pre2, residual=r))
-            return out
+            out1 = self.lin(feat_list)
+            hs = [c1.forward_fused(f, p, p, 1.0, pre=pre1) for f, p in zip(feat_list, pos_list)]
+            return [c2.forward_fused(h, p, p, 1.0, pre=pre2, residual=r) for h, p, r in zip(hs, pos_list, out1)]
+        out1 = self.lin(feat_list)
         f = self.relu1(self.batch_norm1(feat_list))
         f = self.sub_sparse_conv1(f, pos_list)
         f = self.relu2(self.batch_norm2(f))
