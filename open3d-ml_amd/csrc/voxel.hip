@@ -887,6 +887,128 @@ __global__ void scn_half_kernel(const float* __restrict__ in, int64_t n3, float*
 }  // namespace
 }  // namespace o3dml
 
+// The deep levels of the eval plan in ONE workgroup: once a level's input has
+// <= kDeepMax points (a room: from level 2 on, ~5k, then ~1.3k, ~400, ~130),
+// every remaining level's calculate_grid runs here — parent keys (grid_parent
+// arithmetic), a bitonic sort in LDS, the unique keys compacted — each
+// level's grid and grid / 2 written at its offset, the counts to sizes_dev;
+// the next level's keys are the unique keys' fields >> 1 (its positions are
+// k + 0.25, whose trunc is k).  Same keys, same order, same floats as
+// calculate_grid level by level, in one launch and one host read instead of
+// ~7 launches and a read per level.
+constexpr int kDeepMax = 8192;
+constexpr int kDeepThreads = 1024;
+
+__device__ __forceinline__ void deep_write(uint64_t k, int64_t o, float* __restrict__ out, float* __restrict__ half) {
+    const uint64_t m = (uint64_t(1) << 20) - 1;
+    const float x = static_cast<float>(static_cast<int64_t>((k >> 40) & m) * 2) + 0.5f;
+    const float y = static_cast<float>(static_cast<int64_t>((k >> 20) & m) * 2) + 0.5f;
+    const float z = static_cast<float>(static_cast<int64_t>(k & m) * 2) + 0.5f;
+    out[3 * o] = x;
+    out[3 * o + 1] = y;
+    out[3 * o + 2] = z;
+    if (half) {
+        half[3 * o] = x / 2.f;
+        half[3 * o + 1] = y / 2.f;
+        half[3 * o + 2] = z / 2.f;
+    }
+}
+
+__global__ void __launch_bounds__(kDeepThreads) scn_deep_levels_kernel(const float* __restrict__ in_pos, int m, int l0,
+                                                                        int n_levels, int64_t cap,
+                                                                        float* __restrict__ grids,
+                                                                        float* __restrict__ halves,
+                                                                        int64_t* __restrict__ sizes_dev) {
+    __shared__ uint64_t a[kDeepMax];
+    __shared__ uint64_t b[kDeepMax];
+    __shared__ int wsum[kDeepThreads / 64];
+    const int t = threadIdx.x;
+    const uint64_t kPad = ~uint64_t(0);  // sorts after every key, kGridInvalid included
+    for (int i = t; i < m; i += kDeepThreads) {  // grid_parent_kernel's keys (in range by construction)
+        uint64_t key = 0;
+        bool valid = true;
+        for (int d = 0; d < 3; ++d) {
+            const float p = in_pos[3 * i + d];
+            if (!(p > -1.0f) || p >= static_cast<float>(kGridMax)) {
+                valid = false;
+                continue;
+            }
+            key = (key << 20) | static_cast<uint64_t>(static_cast<int64_t>(p) >> 1);
+        }
+        a[i] = valid ? key : kGridInvalid;
+    }
+    int n = m;
+    for (int l = l0; l < n_levels; ++l) {
+        if (n == 0) {
+            if (t == 0) sizes_dev[l] = 0;
+            continue;
+        }
+        int P = 1;
+        while (P < n) P <<= 1;
+        for (int i = n + t; i < P; i += kDeepThreads) a[i] = kPad;
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1) {  // bitonic sort, ascending
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = t; i < P; i += kDeepThreads) {
+                    const int ixj = i ^ j;
+                    if (ixj > i) {
+                        const uint64_t x = a[i], y = a[ixj];
+                        if ((x > y) == ((i & k) == 0)) {
+                            a[i] = y;
+                            a[ixj] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // unique: thread t owns the contiguous items [t c, t c + c)
+        const int c = (P + kDeepThreads - 1) / kDeepThreads;
+        const int i0 = t * c;
+        int h = 0;
+        for (int i = i0; i < i0 + c && i < P; ++i) {
+            const uint64_t k = a[i];
+            h += (k != kGridInvalid && k != kPad && (i == 0 || k != a[i - 1])) ? 1 : 0;
+        }
+        const int incl = wave_inclusive_scan(h);
+        if ((t & 63) == 63) wsum[t >> 6] = incl;
+        __syncthreads();
+        int o = incl - h, tot = 0;
+        for (int w = 0; w < kDeepThreads / 64; ++w) {
+            o += w < (t >> 6) ? wsum[w] : 0;
+            tot += wsum[w];
+        }
+        float* out = grids + static_cast<int64_t>(l) * cap * 3;
+        float* hl = halves ? halves + static_cast<int64_t>(l) * cap * 3 : nullptr;
+        for (int i = i0; i < i0 + c && i < P; ++i) {
+            const uint64_t k = a[i];
+            if (k != kGridInvalid && k != kPad && (i == 0 || k != a[i - 1])) {
+                b[o] = k;
+                deep_write(k, o, out, hl);
+                ++o;
+            }
+        }
+        if (t == 0) sizes_dev[l] = tot;
+        __syncthreads();
+        const uint64_t f = (uint64_t(1) << 20) - 1;
+        for (int i = t; i < tot; i += kDeepThreads) {  // next level: the fields >> 1
+            const uint64_t k = b[i];
+            a[i] = ((((k >> 40) & f) >> 1) << 40) | ((((k >> 20) & f) >> 1) << 20) | ((k & f) >> 1);
+        }
+        n = tot;
+        __syncthreads();
+    }
+}
+
+// O3DML_SCN_DEEP=0: every level through calculate_grid (A/B)
+static bool scn_deep_on() {
+    static const bool v = [] {
+        const char* e = std::getenv("O3DML_SCN_DEEP");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 O3DML_API size_t o3dml_scn_plan_workspace_size(int64_t n_points) {
     const int64_t n = std::max<int64_t>(n_points, 1);
     return ws_bytes<int64_t>(2) + ws_bytes<int32_t>(3 * n) + ws_bytes<int64_t>(n) + ws_bytes<int64_t>(n + 1) +
@@ -939,6 +1061,18 @@ O3DML_API int o3dml_scn_plan(const float* points, const float* features, int64_t
     const float* in = vox_pos;
     int64_t m = nvox;
     for (int l = 0; l < n_levels && m > 0; ++l) {
+        if (scn_deep_on() && m <= kDeepMax && n_levels - l <= 8) {  // the rest in one workgroup, one host read
+            int64_t* sizes_dev = reinterpret_cast<int64_t*>(sub);
+            scn_deep_levels_kernel<<<1, kDeepThreads, 0, st>>>(in, static_cast<int>(m), l, n_levels, cap, grids,
+                                                               halves, sizes_dev);
+            O3DML_LAUNCH_CHECK();
+            int64_t* pinned = pinned_scratch();
+            O3DML_CHECK_HIP(hipMemcpyAsync(pinned, sizes_dev + l, (n_levels - l) * sizeof(int64_t),
+                                           hipMemcpyDeviceToHost, st));
+            O3DML_CHECK_HIP(hipStreamSynchronize(st));
+            for (int q = l; q < n_levels; ++q) sizes_host[1 + q] = pinned[q - l];
+            break;
+        }
         int64_t m_out = 0;
         rc = o3dml_calculate_grid_count(in, m, &m_out, sub, sub_bytes, stream);
         if (rc) return rc;

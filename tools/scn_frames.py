@@ -1,5 +1,6 @@
 """SparseConvUnet eval frames (bench.scn_bench's model and input): median
-ms per frame, host time to return vs GPU drain; for rocprofv3 runs."""
+ms per frame, host time to return vs GPU drain; for rocprofv3 runs.
+  python tools/scn_frames.py N [prof | ops | split]"""
 import os
 import sys
 import time
@@ -33,6 +34,26 @@ with torch.no_grad():
         host.append(t1 - t)
         tot.append(t2 - t)
 print(f"SCN frame: {np.median(tot)*1e3:.3f} ms (host return {np.median(host)*1e3:.3f} ms), voxels {pos.shape[0]}")
+
+if len(sys.argv) > 2 and sys.argv[2] == "split":
+    # mode 3: the plan call alone and the body replay alone (each synchronised)
+    plan = m.__dict__["_o3dml_scn_plan"][1]
+    bodies = m.__dict__["_o3dml_scn_plan_bodies"]
+    body = next(iter(bodies.values()))
+    tp, tb = [], []
+    with torch.no_grad():
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            plan.run(inp.point[0], inp.feat[0])
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            body.graph.replay()
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter()
+            tp.append(t1 - t)
+            tb.append(t2 - t1)
+    print(f"SCN plan call {np.median(tp)*1e3:.3f} ms, body replay {np.median(tb)*1e3:.3f} ms")
 
 if len(sys.argv) > 2 and sys.argv[2] == "prof":
     import cProfile
