@@ -2194,6 +2194,13 @@ static int gemm_splits(int64_t n_out, int K, int cin, int cout) {
         return e ? std::max<int64_t>(1, std::atoll(e)) : kGemmTargetWaves;
     }();
     const int64_t tiles = ceil_div(n_out, 32) * ceil_div(cout, 32);
+    // O3DML_GEMM_NOSPLIT_TILES = v > 0 (A/B): no split once the output tiles
+    // number >= v (the partial slabs and the reduce launch vs occupancy)
+    static const int64_t nosplit = [] {
+        const char* e = std::getenv("O3DML_GEMM_NOSPLIT_TILES");
+        return e ? std::atoll(e) : 0;
+    }();
+    if (nosplit > 0 && tiles >= nosplit) return 1;
     int64_t ns = ceil_div(target, tiles);
     ns = std::min<int64_t>(ns, std::max<int64_t>(1, (static_cast<int64_t>(K) * ceil_div(cin, 32)) / kGemmMinStages));
     ns = std::min<int64_t>(ns, kGemmSplitBytes / (n_out * cout * static_cast<int64_t>(sizeof(float))));
